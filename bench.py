@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark of the per-level ibDCF client-key evaluation (BASELINE.json metric:
+"client x prefix key evals/sec (AES blocks/s) + full-crawl wall time").
+
+One step = one full crawl (data_len levels) of the in-process leader + both servers:
+GPU keys already resident in HBM; per level: k_expand for both servers (one launch),
+the plaintext equality count standing in for the GC/OT step, [RCCL all-reduce of the
+per-child partial counts when N > 1], leader keep decision, prune. Workload = configs[1]:
+100k Zipf clients (num_sites 10000, s = 1.03), data_len 512, d = 1, ball 1,
+threshold 0.001; clients are sharded by GPU (weak scaling: --clients per GPU).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+LDS_PEAK_GBPS = 75_000.0       # ds_read_b32 aggregate, MI355X_MICROARCH.md §LDS (≈75 TB/s)
+HBM_PEAK_GBPS = 8_000.0        # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TOPS = 78.64         # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (confirmed by fhh_microbench)
+LDS_BYTES_PER_BLOCK = 160 * 4  # T-table AES-128: 10 rounds x 16 ds_read_b32 lookups
+VALU_OPS_PER_BLOCK = 400       # SURVEY §8d canonical int32 ops per AES block
+HBM_BYTES_PER_BLOCK = 42       # SURVEY §8d algorithmic bytes per AES block
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, n_total):
+    """Oracle restatement (AES-NI, one non-pipelined block per eval_bit, OpenMP over clients)
+    on a bounded sample of the same workload — rank 0, N = 1 only."""
+    from fuzzyheavyhitters_amd import workload
+    from oracle import oracle as O
+    O.build()
+    n_cpu = min(args.clients, args.cpu_sample_clients)
+    wl = workload.zipf_workload(n_cpu, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
+                                ball_size=args.ball, seed=args.seed)
+    k0, k1 = O.gen_keys(wl.left, wl.right, wl.root_seeds)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    t0 = time.perf_counter()
+    res = O.crawl(k0, k1, args.threshold, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds)
+    dt = time.perf_counter() - t0
+    return {
+        "value": res.aes_blocks / dt,
+        "unit": "AES blocks/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{n_cpu} clients of the same Zipf workload, levels 0..{len(res.n_children) - 1} of "
+                   f"{args.data_len}, both servers, {res.aes_blocks} AES blocks in {dt:.2f} s "
+                   f"(oracle/fhh_oracle.c: AES-NI single block per eval_bit, reference child order, "
+                   f"OpenMP {threads} threads; the Rust reference is not buildable here)"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--clients", type=int, default=100_000, help="clients per GPU")
+    ap.add_argument("--data-len", type=int, default=512)
+    ap.add_argument("--dims", type=int, default=1)
+    ap.add_argument("--num-sites", type=int, default=10_000)
+    ap.add_argument("--zipf", type=float, default=1.03)
+    ap.add_argument("--ball", type=int, default=1)
+    ap.add_argument("--threshold", type=float, default=0.001)
+    ap.add_argument("--mode", default="count", choices=["count", "fe"])
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-sample-clients", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+
+    import numpy as np
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+
+    n_local = args.clients
+    n_total = n_local * world
+    t_gen = time.perf_counter()
+    wl = workload.zipf_workload(n_local, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
+                                ball_size=args.ball, seed=args.seed, client_offset=rank * n_local)
+    c0 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
+    c1 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    c0.set_client_base(rank * n_local)
+    c1.set_client_base(rank * n_local)
+    log(f"[rank {rank}] workload+keygen {time.perf_counter() - t_gen:.2f}s "
+        f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
+
+    def step():
+        return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
+                             record=False, distributed=world > 1)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        res = step()
+    barrier()
+    c0.reset_stats()
+    c1.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    s0, s1 = c0.stats(), c1.stats()
+    blocks = s0["aes_blocks"] + s1["aes_blocks"]
+    ref_evals = s0["ref_evals"] + s1["ref_evals"]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        b = torch.tensor([blocks, ref_evals], dtype=torch.int64, device="cuda")
+        dist.all_reduce(b)
+        blocks, ref_evals = int(b[0].item()), int(b[1].item())
+
+    if rank == 0:
+        launches = max(1, s0["expand_launches"])
+        avg_launch_s = s0["expand_ms"] / launches / 1e3
+        blocks_per_launch = s0["expand_blocks_timed"] / launches
+        lds_gbps = blocks_per_launch * LDS_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        valu_tops = blocks_per_launch * VALU_OPS_PER_BLOCK / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
+        hbm_gbps = blocks_per_launch * HBM_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_expand.json")
+        if os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                if pmc.get("config") == f"n{n_local}_L{args.data_len}_d{args.dims}":
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "client x prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients",
+            "value": blocks / elapsed,
+            "unit": "AES blocks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded Zipf workload shaped like leader.rs; random-init keys via GPU keygen)",
+            "config": {
+                "workload": "configs[1]: Zipf clients, data_len 512 ibDCF tree crawl, two in-process servers",
+                "clients_per_gpu": n_local, "clients_total": n_total, "data_len": args.data_len,
+                "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
+                "threshold": args.threshold, "mode": args.mode, "parallelism": f"client-shard x{world}",
+            },
+            "full_crawl_wall_s": elapsed / args.steps,
+            "ref_equiv_evals_per_s": ref_evals / elapsed,
+            "aes_blocks_per_step": blocks / args.steps,
+            "final_heavy_hitters": len(res.final),
+            "levels": int(len(res.level_children)),
+            "children_total": int(res.level_children.sum()),
+            "roofline": {
+                "bound": "lds", "achieved": lds_gbps, "peak": LDS_PEAK_GBPS, "unit": "GB/s",
+                "frac": lds_gbps / LDS_PEAK_GBPS, "traffic": traffic,
+                "kernel": "k_expand", "algorithmic": f"{LDS_BYTES_PER_BLOCK} B of ds_read_b32 T-table lookups per AES block",
+                "avg_launch_us": avg_launch_s * 1e6, "blocks_per_launch": blocks_per_launch,
+            },
+            "roofline_valu": {"achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                              "frac": valu_tops / VALU_PEAK_TOPS,
+                              "algorithmic": f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d)"},
+            "roofline_hbm": {"achieved": hbm_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": hbm_gbps / HBM_PEAK_GBPS,
+                             "algorithmic": f"{HBM_BYTES_PER_BLOCK} B per AES block (SURVEY 8d)"},
+        }
+        if args.microbench:
+            import ctypes
+            r = ctypes.c_double()
+            fhh.lib().fhh_microbench(local_rank, 0, ctypes.byref(r))
+            out["measured_valu_peak_tops"] = r.value / 1e12
+            fhh.lib().fhh_microbench(local_rank, 1, ctypes.byref(r))
+            out["measured_lds_peak_gbps"] = r.value / 1e9
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, n_total)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

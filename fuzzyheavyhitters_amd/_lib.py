@@ -1,0 +1,148 @@
+"""ctypes binding of libfhh.so (C ABI in include/fhh.h).
+
+The product path is the HIP library only: if libfhh.so is missing or fails to load, every
+entry point raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfhh.so")
+_CSRC = os.path.join(_HERE, "csrc")
+_LIB = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, u64p, ctypes.c_uint64, ctypes.c_void_p)
+
+FHH_MAX_DIMS = 4
+
+# every symbol include/fhh.h declares
+EXPORTS = [
+    "fhh_create", "fhh_destroy", "fhh_last_error", "fhh_reset", "fhh_set_client_base",
+    "fhh_add_keys", "fhh_gen_keys_pair", "fhh_num_clients", "fhh_export_keys",
+    "fhh_tree_init", "fhh_tree_crawl", "fhh_tree_crawl_last", "fhh_node_sums_fe",
+    "fhh_node_sums_fe255", "fhh_tree_prune", "fhh_tree_prune_last", "fhh_frontier_size",
+    "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
+    "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
+    "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench",
+]
+
+
+class FhhStats(ctypes.Structure):
+    _fields_ = [
+        ("aes_blocks", ctypes.c_uint64),
+        ("ref_evals", ctypes.c_uint64),
+        ("expand_launches", ctypes.c_uint64),
+        ("expand_ms", ctypes.c_double),
+        ("expand_blocks_timed", ctypes.c_uint64),
+        ("levels", ctypes.c_uint64),
+        ("keygen_ms", ctypes.c_double),
+    ]
+
+
+class FhhSimConfig(ctypes.Structure):
+    _fields_ = [
+        ("threshold", ctypes.c_double),
+        ("nclients_total", ctypes.c_uint64),
+        ("mode", ctypes.c_uint32),
+        ("levels", ctypes.c_uint32),
+        ("prf_seed", ctypes.c_uint64),
+        ("allreduce", ALLREDUCE_FN),
+        ("allreduce_user", ctypes.c_void_p),
+        ("xchg_dev", u64p),
+        ("xchg_capacity", ctypes.c_uint64),
+        ("level_children", u64p),
+        ("level_kept", u64p),
+        ("counts", u64p),
+        ("counts_capacity", ctypes.c_uint64),
+    ]
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box)."""
+    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_microbench.hip", "fhh_host.cpp")]
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           *srcs, "-o", LIB_PATH]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
+    if verbose and (r.stdout or r.stderr):
+        print(r.stdout + r.stderr)
+    return LIB_PATH
+
+
+class FhhError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise FhhError(f"{LIB_PATH} not built: run __graft_entry__.build() (the HIP extension is required; "
+                       "there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    i = ctypes.c_int
+    u32 = ctypes.c_uint32
+    u64 = ctypes.c_uint64
+    P = ctypes.POINTER
+    sig = {
+        "fhh_create": (i, [P(vp), u32, u32, i]),
+        "fhh_destroy": (None, [vp]),
+        "fhh_last_error": (ctypes.c_char_p, [vp]),
+        "fhh_reset": (i, [vp]),
+        "fhh_set_client_base": (i, [vp, u64]),
+        "fhh_add_keys": (i, [vp, u64, u8p, u8p, u8p, u8p]),
+        "fhh_gen_keys_pair": (i, [vp, vp, u64, u8p, u8p, u8p]),
+        "fhh_num_clients": (i, [vp, u64p]),
+        "fhh_export_keys": (i, [vp, u8p, u8p, u8p, u8p]),
+        "fhh_tree_init": (i, [vp]),
+        "fhh_tree_crawl": (i, [vp, u64p, u64p]),
+        "fhh_tree_crawl_last": (i, [vp, u64p, u64p]),
+        "fhh_node_sums_fe": (i, [vp, u64p, u64p]),
+        "fhh_node_sums_fe255": (i, [vp, u32p, u32p, u32p]),
+        "fhh_tree_prune": (i, [vp, u8p, u64]),
+        "fhh_tree_prune_last": (i, [vp, u8p, u64]),
+        "fhh_frontier_size": (i, [vp, u64p, u64p]),
+        "fhh_final_shares": (i, [vp, u64p, u32p, u8p, u32p]),
+        "fhh_export_states": (i, [vp, u64p, u8p, u8p, u8p]),
+        "fhh_keep_values": (i, [u64, u64p, u64p, u64, u8p]),
+        "fhh_keep_values_last": (i, [u32, u32p, u32p, u64, u8p]),
+        "fhh_final_values": (i, [u32p, u32p, u64, u32p]),
+        "fhh_sim_eq_count": (i, [vp, vp, u64p]),
+        "fhh_sim_ot_sums": (i, [vp, vp, u64, vp, vp]),
+        "fhh_sim_crawl": (i, [vp, vp, P(FhhSimConfig)]),
+        "fhh_get_stats": (i, [vp, P(FhhStats)]),
+        "fhh_reset_stats": (i, [vp]),
+        "fhh_set_timing": (i, [vp, i]),
+        "fhh_device_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i)]),
+        "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc: int, ctx=None):
+    if rc != 0:
+        msg = lib().fhh_last_error(ctx)
+        raise FhhError(f"fhh error {rc}: {msg.decode() if msg else ''}")
+
+
+def ptr(a, t=u8p):
+    """Pointer to a C-contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(t)

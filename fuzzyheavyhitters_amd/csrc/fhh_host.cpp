@@ -1,0 +1,1269 @@
+// Host engine of the MI355X evaluator: one fhh_ctx = one server's
+// `KeyCollection<FE, FieldElm>` (src/collect.rs:28-1030) bound to one GPU, exposed through
+// the C ABI declared in include/fhh.h.
+//
+// The frontier of the reference is a Vec<TreeNode> whose nodes carry every client's d
+// (left, right) EvalStates (collect.rs:18-22). Here a node is a tuple of d indices into
+// per-dim prefix tables that live on the GPU (fhh_internal.h); pruning edits index lists
+// on the host and never moves state (the reference does O(F) Vec::remove of whole nodes,
+// collect.rs:918-929).
+#include "fhh_internal.h"
+#include "../../include/fhh.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace fhh;
+
+namespace {
+
+thread_local std::string g_err;
+
+constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    // grow-only; contents are NOT preserved
+    hipError_t ensure(size_t nbytes) {
+        if (nbytes <= bytes && p) return hipSuccess;
+        release();
+        if (nbytes == 0) nbytes = 256;
+        hipError_t e = hipMalloc(&p, nbytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        bytes = nbytes;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t ensure(size_t nbytes) {
+        if (nbytes <= bytes && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (nbytes == 0) nbytes = 256;
+        hipError_t e = hipHostMalloc(&p, nbytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        bytes = nbytes;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct DimTable {
+    DevBuf seed[2], t[2], y[2];
+    size_t cap[2] = {0, 0};       // entries
+    int cur = 0;                  // buffer that holds the frontier's entries
+    std::vector<uint32_t> live;   // frontier entries (indices into buffer `cur`), ordered
+    DevBuf live_dev;
+};
+
+struct Node {
+    uint32_t pos[kMaxDims];       // position of the node's dim-j entry in tab[j].live
+};
+
+enum class Phase { kNoInit, kFrontier, kPending, kPendingLast };
+
+// 320-bit little-endian u32 helpers for FE255 (field.rs)
+using Limbs10 = std::array<uint32_t, 10>;
+
+}  // namespace
+
+struct fhh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t L = 0, d = 0, K = 0;
+    uint64_t n = 0, npad = 0, nw = 0;
+    uint64_t client_base = 0;
+    int grid = 0;
+
+    // host-staged keys (add_key); uploaded at tree_init
+    std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;
+    uint64_t h_n = 0;
+    bool dev_keys = false;        // keys resident on the device (uploaded or generated)
+
+    DevBuf cw_seed, cw_bits, root_seed, key_idx, valid;
+    DimTable tab[kMaxDims];
+
+    Phase phase = Phase::kNoInit;
+    uint32_t level = 0;           // depth of the frontier (= CorWord index of next crawl)
+    std::vector<Node> frontier;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist;   // per depth: (parent, i)
+    uint64_t pending_C = 0;
+    int child_buf[kMaxDims] = {0};
+    DevBuf parent_pos;            // [F][d] u32 for pending children
+
+    // frontier_last (collect.rs:33, 909-914): surviving (parent, i) + values
+    std::vector<std::pair<uint32_t, uint32_t>> last_nodes;
+    std::vector<Limbs10> last_values;
+    uint32_t last_depth = 0;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> last_hist;
+
+    DevBuf scratch, scratch2;
+    std::vector<PinnedBuf*> stage;   // pinned staging for async H2D, recycled at every sync
+    size_t stage_used = 0;
+
+    fhh_stats stats{};
+    bool timing = true;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    std::vector<std::pair<size_t, uint64_t>> ev_pending;   // (pool index, blocks)
+    size_t ev_next = 0;
+
+    std::string err;
+
+    int fail(int code, const std::string& msg) {
+        err = msg;
+        g_err = msg;
+        return code;
+    }
+};
+
+#define CTX_CHECK(ctx)                                              \
+    do {                                                            \
+        if (!(ctx)) {                                               \
+            g_err = "null fhh_ctx";                                 \
+            return FHH_E_ARG;                                       \
+        }                                                           \
+    } while (0)
+
+#define HIP_TRY(ctx, expr)                                                                   \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return (ctx)->fail(e_ == hipErrorOutOfMemory ? FHH_E_NOMEM : FHH_E_HIP,          \
+                               std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+namespace {
+
+// ---- timing -------------------------------------------------------------------------------
+hipError_t timing_begin(fhh_ctx* ctx, size_t* slot) {
+    if (ctx->ev_next >= ctx->ev_pool.size()) {
+        hipEvent_t a, b;
+        hipError_t e = hipEventCreate(&a);
+        if (e != hipSuccess) return e;
+        e = hipEventCreate(&b);
+        if (e != hipSuccess) return e;
+        ctx->ev_pool.emplace_back(a, b);
+    }
+    *slot = ctx->ev_next++;
+    return hipEventRecord(ctx->ev_pool[*slot].first, ctx->stream);
+}
+
+hipError_t timing_end(fhh_ctx* ctx, size_t slot, uint64_t blocks) {
+    ctx->ev_pending.emplace_back(slot, blocks);
+    return hipEventRecord(ctx->ev_pool[slot].second, ctx->stream);
+}
+
+// call after the stream is synchronised
+void timing_resolve(fhh_ctx* ctx) {
+    for (auto& pr : ctx->ev_pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ctx->ev_pool[pr.first].first, ctx->ev_pool[pr.first].second) == hipSuccess) {
+            ctx->stats.expand_ms += ms;
+            ctx->stats.expand_blocks_timed += pr.second;
+        }
+    }
+    ctx->ev_pending.clear();
+    ctx->ev_next = 0;
+}
+
+int sync(fhh_ctx* ctx) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    timing_resolve(ctx);
+    ctx->stage_used = 0;
+    return FHH_OK;
+}
+
+// pinned host staging that stays valid until the next sync(ctx)
+void* stage_bytes(fhh_ctx* ctx, size_t bytes) {
+    if (ctx->stage_used >= ctx->stage.size()) ctx->stage.push_back(new PinnedBuf());
+    PinnedBuf* b = ctx->stage[ctx->stage_used];
+    if (b->ensure(bytes) != hipSuccess) return nullptr;
+    ctx->stage_used++;
+    return b->p;
+}
+
+// ---- FE / FE255 host arithmetic --------------------------------------------------------------
+uint64_t fe_canon_from_limbs(uint64_t lo, uint64_t hi) {
+    // value = lo + hi * 2^32 (< 2^96 for any realistic n), reduced mod p_FE
+    unsigned __int128 v = (unsigned __int128)lo + ((unsigned __int128)hi << 32);
+    return (uint64_t)(v % kFeP);
+}
+
+uint64_t fe_canon(uint64_t v) { return v % kFeP; }
+
+// carry-propagate 8 u64 limb sums (limb k weight 2^(32k)) into 10 u32 limbs
+Limbs10 limbs_from_partials(const uint64_t* p8) {
+    Limbs10 out{};
+    unsigned __int128 carry = 0;
+    for (int k = 0; k < 10; k++) {
+        unsigned __int128 acc = carry + (k < 8 ? p8[k] : 0);
+        out[k] = (uint32_t)acc;
+        carry = acc >> 32;
+    }
+    return out;
+}
+
+// x mod (2^255 - 19) for x given as 10 u32 limbs (< 2^320)
+std::array<uint32_t, 8> fe255_reduce(const Limbs10& x) {
+    // fold: x = hi * 2^255 + lo  ->  lo + 19 * hi, repeated
+    uint64_t w[5] = {0, 0, 0, 0, 0};
+    for (int k = 0; k < 10; k++) w[k / 2] |= (uint64_t)x[k] << (32 * (k % 2));
+    for (int iter = 0; iter < 3; iter++) {
+        uint64_t hi[2] = {(w[3] >> 63) | (w[4] << 1), w[4] >> 63};
+        uint64_t lo[4] = {w[0], w[1], w[2], w[3] & 0x7FFFFFFFFFFFFFFFull};
+        unsigned __int128 acc = (unsigned __int128)lo[0] + (unsigned __int128)hi[0] * 19;
+        w[0] = (uint64_t)acc;
+        acc = (acc >> 64) + lo[1] + (unsigned __int128)hi[1] * 19;
+        w[1] = (uint64_t)acc;
+        acc = (acc >> 64) + lo[2];
+        w[2] = (uint64_t)acc;
+        acc = (acc >> 64) + lo[3];
+        w[3] = (uint64_t)acc;
+        w[4] = (uint64_t)(acc >> 64);
+    }
+    // now w < 2^255 + small; conditional subtract p
+    for (int iter = 0; iter < 2; iter++) {
+        uint64_t t[4];
+        unsigned __int128 acc = (unsigned __int128)w[0] + 19;
+        t[0] = (uint64_t)acc;
+        for (int k = 1; k < 4; k++) {
+            acc = (acc >> 64) + w[k];
+            t[k] = (uint64_t)acc;
+        }
+        if (t[3] >> 63) {   // w >= p
+            w[0] = t[0];
+            w[1] = t[1];
+            w[2] = t[2];
+            w[3] = t[3] & 0x7FFFFFFFFFFFFFFFull;
+        }
+    }
+    std::array<uint32_t, 8> out{};
+    for (int k = 0; k < 8; k++) out[k] = (uint32_t)(w[k / 2] >> (32 * (k % 2)));
+    return out;
+}
+
+// (a - b) mod p255 on canonical values
+std::array<uint32_t, 8> fe255_sub(const std::array<uint32_t, 8>& a, const std::array<uint32_t, 8>& b) {
+    // a + p - b (> 0 for a, b < p), then reduce
+    static const uint32_t P[8] = {0xFFFFFFED, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF,
+                                  0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0x7FFFFFFF};
+    Limbs10 x{};
+    int64_t carry = 0;
+    for (int k = 0; k < 8; k++) {
+        const int64_t v = (int64_t)a[k] + (int64_t)P[k] - (int64_t)b[k] + carry;
+        x[k] = (uint32_t)((uint64_t)v & 0xFFFFFFFFull);
+        carry = (v - (int64_t)x[k]) / ((int64_t)1 << 32);
+    }
+    x[8] = (uint32_t)carry;
+    return fe255_reduce(x);
+}
+
+bool fe255_ge_u32(const std::array<uint32_t, 8>& v, uint32_t t) {
+    for (int k = 7; k >= 1; k--)
+        if (v[k]) return true;
+    return v[0] >= t;
+}
+
+// ---- device key / table management -----------------------------------------------------------
+int alloc_keys(fhh_ctx* ctx, uint64_t n) {
+    ctx->n = n;
+    ctx->nw = (n + 63) / 64;
+    if (ctx->nw == 0) ctx->nw = 1;
+    ctx->npad = ctx->nw * 64;
+    const size_t K = ctx->K, L = ctx->L;
+    HIP_TRY(ctx, ctx->cw_seed.ensure(L * K * ctx->npad * 16));
+    HIP_TRY(ctx, ctx->cw_bits.ensure(L * K * 4 * ctx->nw * 8));
+    HIP_TRY(ctx, ctx->root_seed.ensure(K * ctx->npad * 16));
+    HIP_TRY(ctx, ctx->key_idx.ensure(K * ctx->nw * 8));
+    HIP_TRY(ctx, ctx->valid.ensure(ctx->nw * 8));
+    std::vector<uint64_t> v(ctx->nw, ~0ull);
+    if (n % 64) v[ctx->nw - 1] = (1ull << (n % 64)) - 1;
+    if (n == 0) v[0] = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->valid.p, v.data(), ctx->nw * 8, hipMemcpyHostToDevice, ctx->stream));
+    return sync(ctx);
+}
+
+int upload_staged_keys(fhh_ctx* ctx) {
+    if (ctx->h_n == 0) return FHH_OK;
+    if (ctx->dev_keys) return ctx->fail(FHH_E_STATE, "cannot mix add_keys with device-generated keys");
+    int rc = alloc_keys(ctx, ctx->h_n);
+    if (rc) return rc;
+    const size_t K = ctx->K, L = ctx->L, n = ctx->h_n;
+    DevBuf a, b, c, dd;
+    HIP_TRY(ctx, a.ensure(n * K));
+    HIP_TRY(ctx, b.ensure(n * K * 16));
+    HIP_TRY(ctx, c.ensure(n * K * L * 16));
+    HIP_TRY(ctx, dd.ensure(n * K * L));
+    HIP_TRY(ctx, hipMemcpyAsync(a.p, ctx->h_key_idx.data(), n * K, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(b.p, ctx->h_root.data(), n * K * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(c.p, ctx->h_cws.data(), n * K * L * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dd.p, ctx->h_cwb.data(), n * K * L, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_keys_from_aos(a.as<uint8_t>(), b.as<uint8_t>(), c.as<uint8_t>(), dd.as<uint8_t>(), n,
+                                      ctx->K, ctx->L, (uint32_t)ctx->npad, (uint32_t)ctx->nw, ctx->cw_seed.as<uint4>(),
+                                      ctx->cw_bits.as<uint64_t>(), ctx->root_seed.as<uint4>(),
+                                      ctx->key_idx.as<uint64_t>(), ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    ctx->dev_keys = true;
+    ctx->h_key_idx.clear();
+    ctx->h_root.clear();
+    ctx->h_cws.clear();
+    ctx->h_cwb.clear();
+    ctx->h_key_idx.shrink_to_fit();
+    ctx->h_root.shrink_to_fit();
+    ctx->h_cws.shrink_to_fit();
+    ctx->h_cwb.shrink_to_fit();
+    ctx->h_n = 0;
+    return FHH_OK;
+}
+
+int table_ensure(fhh_ctx* ctx, DimTable& T, int buf, size_t entries) {
+    if (entries <= T.cap[buf] && T.seed[buf].p) return FHH_OK;
+    size_t cap = std::max<size_t>(entries, T.cap[buf] * 2);
+    cap = std::max<size_t>(cap, 4);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, T.seed[buf].ensure(cap * 2 * ctx->npad * 16));
+    HIP_TRY(ctx, T.t[buf].ensure(cap * 2 * ctx->nw * 8));
+    HIP_TRY(ctx, T.y[buf].ensure(cap * 2 * ctx->nw * 8));
+    T.cap[buf] = cap;
+    return FHH_OK;
+}
+
+int upload_u32(fhh_ctx* ctx, DevBuf& dst, const std::vector<uint32_t>& v) {
+    const size_t bytes = std::max<size_t>(v.size() * 4, 4);
+    if (dst.bytes < bytes) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, dst.ensure(bytes * 2));
+    }
+    if (!v.empty()) {
+        void* h = stage_bytes(ctx, v.size() * 4);
+        if (!h) return ctx->fail(FHH_E_NOMEM, "pinned staging allocation failed");
+        std::memcpy(h, v.data(), v.size() * 4);
+        HIP_TRY(ctx, hipMemcpyAsync(dst.p, h, v.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return FHH_OK;
+}
+
+// Prepare expansion jobs for one ctx: dst buffers sized, live lists uploaded.
+int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
+    for (uint32_t j = 0; j < ctx->d; j++) {
+        DimTable& T = ctx->tab[j];
+        const int src = T.cur, dst = 1 - T.cur;
+        int rc = table_ensure(ctx, T, dst, 2 * T.live.size());
+        if (rc) return rc;
+        rc = upload_u32(ctx, T.live_dev, T.live);
+        if (rc) return rc;
+        ExpandJob& J = jobs[(*njobs)++];
+        J.cw_seed = ctx->cw_seed.as<uint4>();
+        J.cw_bits = ctx->cw_bits.as<uint64_t>();
+        J.src_seed = T.seed[src].as<uint4>();
+        J.src_t = T.t[src].as<uint64_t>();
+        J.src_y = T.y[src].as<uint64_t>();
+        J.dst_seed = T.seed[dst].as<uint4>();
+        J.dst_t = T.t[dst].as<uint64_t>();
+        J.dst_y = T.y[dst].as<uint64_t>();
+        J.live = T.live_dev.as<uint32_t>();
+        J.n_live = (uint32_t)T.live.size();
+        J.level = ctx->level;
+        J.dim = j;
+        J.K = ctx->K;
+        J.npad = (uint32_t)ctx->npad;
+        J.nw = (uint32_t)ctx->nw;
+        J.group = 1;
+        J.pad_ = 0;
+        J.item_begin = 0;
+    }
+    return FHH_OK;
+}
+
+void finalize_launch(ExpandLaunch& L, int grid) {
+    uint64_t entry_words = 0;
+    for (uint32_t k = 0; k < L.njobs; k++) entry_words += (uint64_t)L.job[k].n_live * L.job[k].nw;
+    const uint64_t waves = (uint64_t)grid * (kExpandThreads / 64);
+    uint64_t g = entry_words / (2 * waves);
+    if (g < 1) g = 1;
+    if (g > 8) g = 8;
+    uint64_t begin = 0;
+    for (uint32_t k = 0; k < L.njobs; k++) {
+        ExpandJob& J = L.job[k];
+        J.group = (uint32_t)g;
+        J.item_begin = begin;
+        begin += (uint64_t)J.nw * ((J.n_live + g - 1) / g);
+    }
+    L.total_items = begin;
+}
+
+uint64_t launch_blocks(const fhh_ctx* ctx) {
+    uint64_t b = 0;
+    for (uint32_t j = 0; j < ctx->d; j++) b += (uint64_t)ctx->tab[j].live.size() * 4 * ctx->n;
+    return b;
+}
+
+// Record the children created by an expansion of ctx's frontier.
+int post_expand(fhh_ctx* ctx, bool last) {
+    const uint64_t F = ctx->frontier.size();
+    ctx->pending_C = F << ctx->d;
+    std::vector<uint32_t> pp(F * ctx->d);
+    for (uint64_t p = 0; p < F; p++)
+        for (uint32_t j = 0; j < ctx->d; j++) pp[p * ctx->d + j] = ctx->frontier[p].pos[j];
+    int rc = upload_u32(ctx, ctx->parent_pos, pp);
+    if (rc) return rc;
+    for (uint32_t j = 0; j < ctx->d; j++) {
+        DimTable& T = ctx->tab[j];
+        ctx->child_buf[j] = 1 - T.cur;
+        if (!last) T.cur = 1 - T.cur;     // tree_crawl: next_frontier replaces frontier
+    }
+    ctx->stats.aes_blocks += launch_blocks(ctx);
+    ctx->stats.ref_evals += ctx->pending_C * ctx->n * 2 * ctx->d;
+    ctx->stats.levels += 1;
+    if (last) {
+        ctx->phase = Phase::kPendingLast;
+        ctx->last_nodes.clear();
+        for (uint64_t c = 0; c < ctx->pending_C; c++)
+            ctx->last_nodes.emplace_back((uint32_t)(c >> ctx->d), (uint32_t)(c & ((1u << ctx->d) - 1)));
+        ctx->last_values.assign(ctx->pending_C, Limbs10{});
+        ctx->last_depth = ctx->level + 1;
+        ctx->last_hist = ctx->hist;
+    } else {
+        ctx->phase = Phase::kPending;
+    }
+    return FHH_OK;
+}
+
+int prune_impl(fhh_ctx* ctx, const uint8_t* keep, uint64_t n);
+
+int check_can_crawl(fhh_ctx* ctx) {
+    if (ctx->phase == Phase::kNoInit) return ctx->fail(FHH_E_STATE, "tree_crawl before tree_init");
+    if (ctx->phase == Phase::kPending) {
+        // the unpruned children become the frontier (collect.rs:505 `self.frontier = next_frontier`)
+        std::vector<uint8_t> all(ctx->pending_C, 1);
+        int rc = prune_impl(ctx, all.data(), ctx->pending_C);
+        if (rc) return rc;
+    }
+    if (ctx->level >= ctx->L) return ctx->fail(FHH_E_STATE, "crawl past data_len (cor_words index out of bounds)");
+    return FHH_OK;
+}
+
+int crawl_one(fhh_ctx* ctx, bool last) {
+    int rc = check_can_crawl(ctx);
+    if (rc) return rc;
+    ExpandLaunch La{};
+    La.njobs = 0;
+    rc = prepare_expand(ctx, La.job, &La.njobs);
+    if (rc) return rc;
+    finalize_launch(La, ctx->grid);
+    size_t slot = 0;
+    if (ctx->timing) HIP_TRY(ctx, timing_begin(ctx, &slot));
+    HIP_TRY(ctx, launch_expand(La, ctx->grid, ctx->stream));
+    if (ctx->timing) HIP_TRY(ctx, timing_end(ctx, slot, launch_blocks(ctx)));
+    ctx->stats.expand_launches++;
+    return post_expand(ctx, last);
+}
+
+// Both servers' expansions in ONE launch (same device): the in-process harness path.
+int crawl_pair(fhh_ctx* c0, fhh_ctx* c1, bool last) {
+    int rc = check_can_crawl(c0);
+    if (rc) return rc;
+    rc = check_can_crawl(c1);
+    if (rc) return rc;
+    HIP_TRY(c1, hipStreamSynchronize(c1->stream));
+    ExpandLaunch La{};
+    La.njobs = 0;
+    rc = prepare_expand(c0, La.job, &La.njobs);
+    if (rc) return rc;
+    rc = prepare_expand(c1, La.job, &La.njobs);
+    if (rc) return rc;
+    HIP_TRY(c1, hipStreamSynchronize(c1->stream));   // c1's live lists uploaded
+    finalize_launch(La, c0->grid);
+    size_t slot = 0;
+    const uint64_t blocks = launch_blocks(c0) + launch_blocks(c1);
+    if (c0->timing) HIP_TRY(c0, timing_begin(c0, &slot));
+    HIP_TRY(c0, launch_expand(La, c0->grid, c0->stream));
+    if (c0->timing) HIP_TRY(c0, timing_end(c0, slot, blocks));
+    c0->stats.expand_launches++;
+    rc = post_expand(c0, last);
+    if (rc) return rc;
+    return post_expand(c1, last);
+}
+
+ChildArgs child_args(fhh_ctx* c0, fhh_ctx* c1) {
+    ChildArgs a{};
+    for (uint32_t j = 0; j < c0->d; j++) {
+        a.s0.t[j] = c0->tab[j].t[c0->child_buf[j]].as<uint64_t>();
+        a.s0.y[j] = c0->tab[j].y[c0->child_buf[j]].as<uint64_t>();
+        fhh_ctx* o = c1 ? c1 : c0;
+        a.s1.t[j] = o->tab[j].t[o->child_buf[j]].as<uint64_t>();
+        a.s1.y[j] = o->tab[j].y[o->child_buf[j]].as<uint64_t>();
+    }
+    a.parent_pos = c0->parent_pos.as<uint32_t>();
+    a.valid = c0->valid.as<uint64_t>();
+    a.C = c0->pending_C;
+    a.d = c0->d;
+    a.nw = (uint32_t)c0->nw;
+    a.client_base = c0->client_base;
+    a.level = c0->level;
+    a.n = (uint32_t)c0->n;
+    return a;
+}
+
+int share_planes_out(fhh_ctx* ctx, uint64_t* host_out) {
+    if (!host_out || ctx->pending_C == 0) return FHH_OK;
+    const size_t words = ctx->pending_C * 2 * ctx->d * ctx->nw;
+    HIP_TRY(ctx, ctx->scratch.ensure(words * 8));
+    ChildArgs a = child_args(ctx, nullptr);
+    HIP_TRY(ctx, launch_share_planes(a, ctx->scratch.as<uint64_t>(), ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(host_out, ctx->scratch.p, words * 8, hipMemcpyDeviceToHost, ctx->stream));
+    return sync(ctx);
+}
+
+int prune_impl(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
+    if (ctx->phase != Phase::kPending) return ctx->fail(FHH_E_STATE, "tree_prune without a pending tree_crawl");
+    if (n != ctx->pending_C)
+        return ctx->fail(FHH_E_ARG, "tree_prune: keep.len() != frontier.len() (collect.rs:919)");
+    const uint32_t d = ctx->d;
+    std::vector<Node> nf;
+    std::vector<std::pair<uint32_t, uint32_t>> h;
+    std::vector<std::unordered_map<uint32_t, uint32_t>> remap(d);
+    std::vector<std::vector<uint32_t>> new_live(d);
+    for (uint64_t c = 0; c < n; c++) {
+        if (!keep[c]) continue;
+        const uint32_t p = (uint32_t)(c >> d), i = (uint32_t)(c & ((1u << d) - 1));
+        Node node{};
+        for (uint32_t j = 0; j < d; j++) {
+            const uint32_t e = 2 * ctx->frontier[p].pos[j] + ((i >> j) & 1);
+            auto it = remap[j].find(e);
+            if (it == remap[j].end()) {
+                const uint32_t k = (uint32_t)new_live[j].size();
+                remap[j].emplace(e, k);
+                new_live[j].push_back(e);
+                node.pos[j] = k;
+            } else {
+                node.pos[j] = it->second;
+            }
+        }
+        nf.push_back(node);
+        h.emplace_back(p, i);
+    }
+    for (uint32_t j = 0; j < d; j++) ctx->tab[j].live = std::move(new_live[j]);
+    ctx->frontier = std::move(nf);
+    ctx->hist.push_back(std::move(h));
+    ctx->level += 1;
+    ctx->pending_C = 0;
+    ctx->phase = Phase::kFrontier;
+    return FHH_OK;
+}
+
+// path of a frontier node at depth `depth` (hist[0..depth-1]) followed by (p, i)
+void node_path(const std::vector<std::vector<std::pair<uint32_t, uint32_t>>>& hist, uint32_t depth, uint32_t p,
+               uint32_t i, uint32_t d, uint8_t* out /*[d][depth+1]*/) {
+    const uint32_t len = depth + 1;
+    for (uint32_t j = 0; j < d; j++) out[j * len + depth] = (uint8_t)((i >> j) & 1);
+    uint32_t node = p;
+    for (int64_t lv = (int64_t)depth - 1; lv >= 0; lv--) {
+        const auto& pr = hist[(size_t)lv][node];
+        for (uint32_t j = 0; j < d; j++) out[j * len + (uint32_t)lv] = (uint8_t)((pr.second >> j) & 1);
+        node = pr.first;
+    }
+}
+
+int check_pair(fhh_ctx* c0, fhh_ctx* c1) {
+    if (!c0 || !c1) {
+        g_err = "null fhh_ctx";
+        return FHH_E_ARG;
+    }
+    if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim: ctxs on different devices");
+    if (c0->d != c1->d || c0->n != c1->n || c0->L != c1->L)
+        return c0->fail(FHH_E_ARG, "sim: ctx shapes differ");
+    if (c0->phase != c1->phase || (c0->phase != Phase::kPending && c0->phase != Phase::kPendingLast))
+        return c0->fail(FHH_E_STATE, "sim: both ctxs need a pending crawl");
+    if (c0->pending_C != c1->pending_C || c0->frontier.size() != c1->frontier.size())
+        return c0->fail(FHH_E_ARG, "sim: frontiers differ");
+    for (size_t k = 0; k < c0->frontier.size(); k++)
+        for (uint32_t j = 0; j < c0->d; j++)
+            if (c0->frontier[k].pos[j] != c1->frontier[k].pos[j]) return c0->fail(FHH_E_ARG, "sim: frontiers differ");
+    HIP_TRY(c1, hipStreamSynchronize(c1->stream));
+    return FHH_OK;
+}
+
+// partials on device -> (optional all-reduce) -> host
+int fetch_partials(fhh_ctx* ctx, const fhh_sim_config* cfg, uint64_t* dev, uint64_t count, uint64_t* host) {
+    if (count == 0) return FHH_OK;
+    if (cfg && cfg->allreduce) {
+        if (!cfg->xchg_dev || cfg->xchg_capacity < count)
+            return ctx->fail(FHH_E_ARG, "sim: all-reduce exchange buffer too small");
+        HIP_TRY(ctx, hipMemcpyAsync(cfg->xchg_dev, dev, count * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        int rc = sync(ctx);
+        if (rc) return rc;
+        if (cfg->allreduce(cfg->xchg_dev, count, cfg->allreduce_user) != 0)
+            return ctx->fail(FHH_E_CALLBACK, "all-reduce callback failed");
+        HIP_TRY(ctx, hipMemcpyAsync(host, cfg->xchg_dev, count * 8, hipMemcpyDeviceToHost, ctx->stream));
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(host, dev, count * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    return sync(ctx);
+}
+
+int sim_eq_count_impl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, uint64_t* counts) {
+    int rc = check_pair(c0, c1);
+    if (rc) return rc;
+    const uint64_t C = c0->pending_C;
+    HIP_TRY(c0, c0->scratch2.ensure(std::max<uint64_t>(C, 1) * 8 * 16));
+    ChildArgs a = child_args(c0, c1);
+    HIP_TRY(c0, launch_eq_count(a, c0->scratch2.as<uint64_t>(), c0->stream));
+    return fetch_partials(c0, cfg, c0->scratch2.as<uint64_t>(), C, counts);
+}
+
+// mode FE (non-last): sums0/sums1 [C] canonical; FE255 (last): [C][10] unreduced
+int sim_ot_sums_impl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, uint64_t seed, void* s0, void* s1) {
+    int rc = check_pair(c0, c1);
+    if (rc) return rc;
+    const uint64_t C = c0->pending_C;
+    const bool last = c0->phase == Phase::kPendingLast;
+    const uint64_t per = last ? 16 : 4;
+    HIP_TRY(c0, c0->scratch2.ensure(std::max<uint64_t>(C, 1) * 8 * 16));
+    ChildArgs a = child_args(c0, c1);
+    a.prf_seed = seed;
+    if (last) HIP_TRY(c0, launch_sim_ot_fe255(a, c0->scratch2.as<uint64_t>(), c0->stream));
+    else HIP_TRY(c0, launch_sim_ot_fe(a, c0->scratch2.as<uint64_t>(), c0->stream));
+    std::vector<uint64_t> h(C * per);
+    rc = fetch_partials(c0, cfg, c0->scratch2.as<uint64_t>(), C * per, h.data());
+    if (rc) return rc;
+    for (uint64_t c = 0; c < C; c++) {
+        if (!last) {
+            static_cast<uint64_t*>(s0)[c] = fe_canon_from_limbs(h[c * 4 + 0], h[c * 4 + 1]);
+            static_cast<uint64_t*>(s1)[c] = fe_canon_from_limbs(h[c * 4 + 2], h[c * 4 + 3]);
+        } else {
+            Limbs10 v0 = limbs_from_partials(&h[c * 16]);
+            Limbs10 v1 = limbs_from_partials(&h[c * 16 + 8]);
+            std::memcpy(static_cast<uint32_t*>(s0) + c * 10, v0.data(), 40);
+            std::memcpy(static_cast<uint32_t*>(s1) + c * 10, v1.data(), 40);
+            c0->last_values[c] = v0;
+            c1->last_values[c] = v1;
+        }
+    }
+    return FHH_OK;
+}
+
+int set_device(fhh_ctx* ctx) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    return FHH_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+const char* fhh_last_error(const fhh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
+    if (!out) {
+        g_err = "fhh_create: out is NULL";
+        return FHH_E_ARG;
+    }
+    *out = nullptr;
+    if (n_dims < 1 || n_dims > FHH_MAX_DIMS) {
+        g_err = "fhh_create: n_dims must be in [1, " + std::to_string(FHH_MAX_DIMS) + "]";
+        return FHH_E_ARG;
+    }
+    if (data_len < 1) {
+        g_err = "fhh_create: data_len must be >= 1";
+        return FHH_E_ARG;
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        g_err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+        return FHH_E_HIP;
+    }
+    fhh_ctx* ctx = new fhh_ctx();
+    ctx->device = device;
+    ctx->L = data_len;
+    ctx->d = n_dims;
+    ctx->K = 2 * n_dims;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        g_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+        delete ctx;
+        return FHH_E_HIP;
+    }
+    ctx->grid = expand_grid(device);
+    *out = ctx;
+    return FHH_OK;
+}
+
+void fhh_destroy(fhh_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& pr : ctx->ev_pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    (void)hipStreamDestroy(ctx->stream);
+    for (auto* b : ctx->stage) delete b;
+    delete ctx;
+}
+
+int fhh_reset(fhh_ctx* ctx) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->h_key_idx.clear();
+    ctx->h_root.clear();
+    ctx->h_cws.clear();
+    ctx->h_cwb.clear();
+    ctx->h_n = 0;
+    ctx->dev_keys = false;
+    ctx->n = ctx->npad = ctx->nw = 0;
+    ctx->phase = Phase::kNoInit;
+    ctx->frontier.clear();
+    ctx->hist.clear();
+    ctx->last_nodes.clear();
+    ctx->last_values.clear();
+    ctx->last_hist.clear();
+    ctx->pending_C = 0;
+    ctx->level = 0;
+    for (auto& T : ctx->tab) T.live.clear();
+    return FHH_OK;
+}
+
+int fhh_set_client_base(fhh_ctx* ctx, uint64_t client_base) {
+    CTX_CHECK(ctx);
+    ctx->client_base = client_base;
+    return FHH_OK;
+}
+
+int fhh_add_keys(fhh_ctx* ctx, uint64_t n, const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
+                 const uint8_t* cw_bits) {
+    CTX_CHECK(ctx);
+    if (n == 0) return FHH_OK;
+    if (!key_idx || !root_seed || !cw_seed || !cw_bits) return ctx->fail(FHH_E_ARG, "add_keys: NULL buffer");
+    if (ctx->dev_keys) return ctx->fail(FHH_E_STATE, "add_keys after keys were placed on the device");
+    const size_t K = ctx->K, L = ctx->L;
+    ctx->h_key_idx.insert(ctx->h_key_idx.end(), key_idx, key_idx + n * K);
+    ctx->h_root.insert(ctx->h_root.end(), root_seed, root_seed + n * K * 16);
+    ctx->h_cws.insert(ctx->h_cws.end(), cw_seed, cw_seed + n * K * L * 16);
+    ctx->h_cwb.insert(ctx->h_cwb.end(), cw_bits, cw_bits + n * K * L);
+    ctx->h_n += n;
+    return FHH_OK;
+}
+
+int fhh_gen_keys_pair(fhh_ctx* c0, fhh_ctx* c1, uint64_t n, const uint8_t* left_bits, const uint8_t* right_bits,
+                      const uint8_t* root_seeds) {
+    if (!c0 || !c1) {
+        g_err = "null fhh_ctx";
+        return FHH_E_ARG;
+    }
+    if (c0->device != c1->device || c0->d != c1->d || c0->L != c1->L)
+        return c0->fail(FHH_E_ARG, "gen_keys_pair: ctxs differ in device/d/L");
+    if (c0->dev_keys || c1->dev_keys || c0->h_n || c1->h_n)
+        return c0->fail(FHH_E_STATE, "gen_keys_pair: ctxs must be empty");
+    if (!left_bits || !right_bits || !root_seeds) return c0->fail(FHH_E_ARG, "gen_keys_pair: NULL buffer");
+    int rc = set_device(c0);
+    if (rc) return rc;
+    rc = alloc_keys(c0, n);
+    if (rc) return rc;
+    rc = alloc_keys(c1, n);
+    if (rc) return rc;
+    const size_t d = c0->d, L = c0->L;
+    DevBuf lb, rb, rs;
+    HIP_TRY(c0, lb.ensure(n * d * L));
+    HIP_TRY(c0, rb.ensure(n * d * L));
+    HIP_TRY(c0, rs.ensure(n * d * 64));
+    HIP_TRY(c0, hipMemcpyAsync(lb.p, left_bits, n * d * L, hipMemcpyHostToDevice, c0->stream));
+    HIP_TRY(c0, hipMemcpyAsync(rb.p, right_bits, n * d * L, hipMemcpyHostToDevice, c0->stream));
+    HIP_TRY(c0, hipMemcpyAsync(rs.p, root_seeds, n * d * 64, hipMemcpyHostToDevice, c0->stream));
+    KeygenArgs a{};
+    a.left_bits = lb.as<uint8_t>();
+    a.right_bits = rb.as<uint8_t>();
+    a.root_seeds = rs.as<uint8_t>();
+    fhh_ctx* cs[2] = {c0, c1};
+    for (int b = 0; b < 2; b++) {
+        a.cw_seed[b] = cs[b]->cw_seed.as<uint4>();
+        a.cw_bits[b] = cs[b]->cw_bits.as<uint64_t>();
+        a.root[b] = cs[b]->root_seed.as<uint4>();
+        a.key_idx[b] = cs[b]->key_idx.as<uint64_t>();
+    }
+    a.n = n;
+    a.d = (uint32_t)d;
+    a.L = (uint32_t)L;
+    a.K = c0->K;
+    a.npad = (uint32_t)c0->npad;
+    a.nw = (uint32_t)c0->nw;
+    hipEvent_t e0, e1;
+    HIP_TRY(c0, hipEventCreate(&e0));
+    HIP_TRY(c0, hipEventCreate(&e1));
+    HIP_TRY(c0, hipEventRecord(e0, c0->stream));
+    HIP_TRY(c0, launch_keygen(a, c0->stream));
+    HIP_TRY(c0, hipEventRecord(e1, c0->stream));
+    rc = sync(c0);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    c0->stats.keygen_ms += ms;
+    c0->dev_keys = c1->dev_keys = true;
+    return FHH_OK;
+}
+
+int fhh_num_clients(const fhh_ctx* ctx, uint64_t* n) {
+    CTX_CHECK(ctx);
+    if (n) *n = ctx->dev_keys ? ctx->n : ctx->h_n;
+    return FHH_OK;
+}
+
+int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t* cw_seed, uint8_t* cw_bits) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!ctx->dev_keys) {
+        const size_t n = ctx->h_n;
+        if (key_idx) std::memcpy(key_idx, ctx->h_key_idx.data(), ctx->h_key_idx.size());
+        if (root_seed) std::memcpy(root_seed, ctx->h_root.data(), ctx->h_root.size());
+        if (cw_seed) std::memcpy(cw_seed, ctx->h_cws.data(), ctx->h_cws.size());
+        if (cw_bits) std::memcpy(cw_bits, ctx->h_cwb.data(), ctx->h_cwb.size());
+        (void)n;
+        return FHH_OK;
+    }
+    const size_t n = ctx->n, K = ctx->K, L = ctx->L, npad = ctx->npad, nw = ctx->nw;
+    std::vector<uint8_t> cws(L * K * npad * 16), roots(K * npad * 16);
+    std::vector<uint64_t> cwb(L * K * 4 * nw), kidx(K * nw);
+    HIP_TRY(ctx, hipMemcpy(cws.data(), ctx->cw_seed.p, cws.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(roots.data(), ctx->root_seed.p, roots.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(cwb.data(), ctx->cw_bits.p, cwb.size() * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(kidx.data(), ctx->key_idx.p, kidx.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < n; c++)
+        for (size_t kk = 0; kk < K; kk++) {
+            const size_t w = c / 64, bit = c % 64;
+            if (key_idx) key_idx[c * K + kk] = (uint8_t)((kidx[kk * nw + w] >> bit) & 1);
+            if (root_seed) std::memcpy(root_seed + (c * K + kk) * 16, &roots[(kk * npad + c) * 16], 16);
+            for (size_t l = 0; l < L; l++) {
+                const size_t row = l * K + kk;
+                if (cw_seed) std::memcpy(cw_seed + ((c * K + kk) * L + l) * 16, &cws[(row * npad + c) * 16], 16);
+                if (cw_bits) {
+                    uint8_t nib = 0;
+                    for (int b = 0; b < 4; b++) nib |= (uint8_t)(((cwb[(row * 4 + b) * nw + w] >> bit) & 1) << b);
+                    cw_bits[(c * K + kk) * L + l] = nib;
+                }
+            }
+        }
+    return FHH_OK;
+}
+
+int fhh_tree_init(fhh_ctx* ctx) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    rc = upload_staged_keys(ctx);
+    if (rc) return rc;
+    if (!ctx->dev_keys || ctx->n == 0) return ctx->fail(FHH_E_STATE, "tree_init with no keys (collect.rs:83)");
+    for (uint32_t j = 0; j < ctx->d; j++) {
+        DimTable& T = ctx->tab[j];
+        T.cur = 0;
+        rc = table_ensure(ctx, T, 0, 1);
+        if (rc) return rc;
+        HIP_TRY(ctx, launch_init_tables(ctx->root_seed.as<uint4>(), ctx->key_idx.as<uint64_t>(), j, ctx->K,
+                                        (uint32_t)ctx->npad, (uint32_t)ctx->nw, T.seed[0].as<uint4>(),
+                                        T.t[0].as<uint64_t>(), T.y[0].as<uint64_t>(), ctx->stream));
+        T.live.assign(1, 0);
+    }
+    ctx->frontier.assign(1, Node{});
+    ctx->hist.clear();
+    ctx->last_nodes.clear();
+    ctx->last_values.clear();
+    ctx->last_hist.clear();
+    ctx->level = 0;
+    ctx->pending_C = 0;
+    ctx->phase = Phase::kFrontier;
+    return sync(ctx);
+}
+
+int fhh_tree_crawl(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    rc = crawl_one(ctx, false);
+    if (rc) return rc;
+    if (n_children) *n_children = ctx->pending_C;
+    rc = share_planes_out(ctx, share_planes);
+    if (rc) return rc;
+    return sync(ctx);
+}
+
+int fhh_tree_crawl_last(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    rc = crawl_one(ctx, true);
+    if (rc) return rc;
+    if (n_children) *n_children = ctx->pending_C;
+    rc = share_planes_out(ctx, share_planes);
+    if (rc) return rc;
+    return sync(ctx);
+}
+
+int fhh_node_sums_fe(fhh_ctx* ctx, const uint64_t* vals, uint64_t* sums) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
+        return ctx->fail(FHH_E_STATE, "node_sums without a pending crawl");
+    const uint64_t C = ctx->pending_C, n = ctx->n;
+    if (C == 0) return FHH_OK;
+    if (!vals || !sums) return ctx->fail(FHH_E_ARG, "node_sums_fe: NULL buffer");
+    HIP_TRY(ctx, ctx->scratch.ensure(C * n * 8));
+    HIP_TRY(ctx, ctx->scratch2.ensure(C * 2 * 8));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, vals, C * n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_sum_fe(ctx->scratch.as<uint64_t>(), C, n, ctx->scratch2.as<uint64_t>(), ctx->stream));
+    std::vector<uint64_t> h(C * 2);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->scratch2.p, C * 16, hipMemcpyDeviceToHost, ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    for (uint64_t c = 0; c < C; c++) sums[c] = fe_canon_from_limbs(h[2 * c], h[2 * c + 1]);
+    return FHH_OK;
+}
+
+int fhh_node_sums_fe255(fhh_ctx* ctx, const uint32_t* vals, uint32_t* sums_unreduced, uint32_t* sums_canonical) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
+        return ctx->fail(FHH_E_STATE, "node_sums without a pending crawl");
+    const uint64_t C = ctx->pending_C, n = ctx->n;
+    if (C == 0) return FHH_OK;
+    if (!vals) return ctx->fail(FHH_E_ARG, "node_sums_fe255: NULL vals");
+    HIP_TRY(ctx, ctx->scratch.ensure(C * n * 32));
+    HIP_TRY(ctx, ctx->scratch2.ensure(C * 8 * 8));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, vals, C * n * 32, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_sum_fe255(ctx->scratch.as<uint32_t>(), C, n, ctx->scratch2.as<uint64_t>(), ctx->stream));
+    std::vector<uint64_t> h(C * 8);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->scratch2.p, C * 64, hipMemcpyDeviceToHost, ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    for (uint64_t c = 0; c < C; c++) {
+        Limbs10 v = limbs_from_partials(&h[c * 8]);
+        if (sums_unreduced) std::memcpy(sums_unreduced + c * 10, v.data(), 40);
+        if (sums_canonical) {
+            auto r = fe255_reduce(v);
+            std::memcpy(sums_canonical + c * 8, r.data(), 32);
+        }
+        if (ctx->phase == Phase::kPendingLast) ctx->last_values[c] = v;
+    }
+    return FHH_OK;
+}
+
+int fhh_tree_prune(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
+    CTX_CHECK(ctx);
+    if (n && !keep) return ctx->fail(FHH_E_ARG, "tree_prune: NULL keep");
+    return prune_impl(ctx, keep, n);
+}
+
+int fhh_tree_prune_last(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
+    CTX_CHECK(ctx);
+    if (n && !keep) return ctx->fail(FHH_E_ARG, "tree_prune_last: NULL keep");
+    if (ctx->phase != Phase::kPendingLast && ctx->last_nodes.empty() && n != 0)
+        return ctx->fail(FHH_E_STATE, "tree_prune_last without tree_crawl_last");
+    if (n != ctx->last_nodes.size())
+        return ctx->fail(FHH_E_ARG, "tree_prune_last: keep.len() != frontier_last.len() (collect.rs:932)");
+    std::vector<std::pair<uint32_t, uint32_t>> nodes;
+    std::vector<Limbs10> vals;
+    for (uint64_t k = 0; k < n; k++)
+        if (keep[k]) {
+            nodes.push_back(ctx->last_nodes[k]);
+            vals.push_back(ctx->last_values[k]);
+        }
+    ctx->last_nodes = std::move(nodes);
+    ctx->last_values = std::move(vals);
+    if (ctx->phase == Phase::kPendingLast) ctx->phase = Phase::kFrontier;   // frontier unchanged (collect.rs:909-914)
+    ctx->pending_C = 0;
+    return FHH_OK;
+}
+
+int fhh_frontier_size(const fhh_ctx* ctx, uint64_t* n_frontier, uint64_t* n_frontier_last) {
+    CTX_CHECK(ctx);
+    if (n_frontier) *n_frontier = ctx->phase == Phase::kPending ? ctx->pending_C : ctx->frontier.size();
+    if (n_frontier_last) *n_frontier_last = ctx->last_nodes.size();
+    return FHH_OK;
+}
+
+int fhh_final_shares(fhh_ctx* ctx, uint64_t* n_final, uint32_t* levels, uint8_t* paths, uint32_t* values) {
+    CTX_CHECK(ctx);
+    const uint64_t F = ctx->last_nodes.size();
+    if (n_final) *n_final = F;
+    if (levels) *levels = ctx->last_depth;
+    if (F == 0) return FHH_OK;
+    const uint32_t len = ctx->last_depth;
+    for (uint64_t k = 0; k < F; k++) {
+        if (paths) node_path(ctx->last_hist, len - 1, ctx->last_nodes[k].first, ctx->last_nodes[k].second, ctx->d,
+                             paths + k * ctx->d * len);
+        if (values) std::memcpy(values + k * 10, ctx->last_values[k].data(), 40);
+    }
+    return FHH_OK;
+}
+
+int fhh_export_states(fhh_ctx* ctx, uint64_t* n_nodes, uint8_t* seeds, uint8_t* t, uint8_t* y) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (ctx->phase == Phase::kNoInit) return ctx->fail(FHH_E_STATE, "export_states before tree_init");
+    const bool pending = ctx->phase == Phase::kPending || ctx->phase == Phase::kPendingLast;
+    const uint64_t F = pending ? ctx->pending_C : ctx->frontier.size();
+    if (n_nodes) *n_nodes = F;
+    if (!seeds && !t && !y) return FHH_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const size_t n = ctx->n, npad = ctx->npad, nw = ctx->nw, d = ctx->d;
+    for (uint32_t j = 0; j < d; j++) {
+        DimTable& T = ctx->tab[j];
+        const int buf = pending ? ctx->child_buf[j] : T.cur;
+        const size_t E = pending ? 2 * ctx->frontier.size() : T.live.size();
+        (void)E;
+        // copy the whole buffer (tests only)
+        std::vector<uint8_t> hs(T.cap[buf] * 2 * npad * 16);
+        std::vector<uint64_t> ht(T.cap[buf] * 2 * nw), hy(T.cap[buf] * 2 * nw);
+        HIP_TRY(ctx, hipMemcpy(hs.data(), T.seed[buf].p, hs.size(), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(ht.data(), T.t[buf].p, ht.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(hy.data(), T.y[buf].p, hy.size() * 8, hipMemcpyDeviceToHost));
+        for (uint64_t node = 0; node < F; node++) {
+            uint32_t e;
+            if (pending) {
+                const uint64_t p = node >> d;
+                const uint32_t i = (uint32_t)(node & ((1u << d) - 1));
+                e = 2 * ctx->frontier[p].pos[j] + ((i >> j) & 1);
+            } else {
+                e = T.live[ctx->frontier[node].pos[j]];
+            }
+            for (size_t c = 0; c < n; c++)
+                for (int s = 0; s < 2; s++) {
+                    const size_t o = ((node * n + c) * d + j) * 2 + s;
+                    if (seeds) std::memcpy(seeds + o * 16, &hs[(((size_t)e * 2 + s) * npad + c) * 16], 16);
+                    if (t) t[o] = (uint8_t)((ht[((size_t)e * 2 + s) * nw + c / 64] >> (c % 64)) & 1);
+                    if (y) y[o] = (uint8_t)((hy[((size_t)e * 2 + s) * nw + c / 64] >> (c % 64)) & 1);
+                }
+        }
+    }
+    return FHH_OK;
+}
+
+int fhh_keep_values(uint64_t threshold, const uint64_t* vals0, const uint64_t* vals1, uint64_t n, uint8_t* keep) {
+    if (n && (!vals0 || !vals1 || !keep)) {
+        g_err = "keep_values: NULL buffer";
+        return FHH_E_ARG;
+    }
+    const uint64_t t = fe_canon(threshold);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t a = fe_canon(vals0[i]), b = fe_canon(vals1[i]);
+        const uint64_t v = a >= b ? a - b : a + (kFeP - b);
+        keep[i] = v >= t;
+    }
+    return FHH_OK;
+}
+
+int fhh_keep_values_last(uint32_t threshold, const uint32_t* vals0, const uint32_t* vals1, uint64_t n, uint8_t* keep) {
+    if (n && (!vals0 || !vals1 || !keep)) {
+        g_err = "keep_values_last: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        Limbs10 a{}, b{};
+        std::memcpy(a.data(), vals0 + i * 10, 40);
+        std::memcpy(b.data(), vals1 + i * 10, 40);
+        auto v = fe255_sub(fe255_reduce(a), fe255_reduce(b));   // v0.reduce(); v1.reduce(); v0 - v1
+        keep[i] = fe255_ge_u32(v, threshold);
+    }
+    return FHH_OK;
+}
+
+int fhh_final_values(const uint32_t* vals0, const uint32_t* vals1, uint64_t n, uint32_t* out) {
+    if (n && (!vals0 || !vals1 || !out)) {
+        g_err = "final_values: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        Limbs10 a{}, b{};
+        std::memcpy(a.data(), vals0 + i * 10, 40);
+        std::memcpy(b.data(), vals1 + i * 10, 40);
+        auto v = fe255_sub(fe255_reduce(a), fe255_reduce(b));
+        std::memcpy(out + i * 8, v.data(), 32);
+    }
+    return FHH_OK;
+}
+
+int fhh_sim_eq_count(fhh_ctx* c0, fhh_ctx* c1, uint64_t* counts) {
+    if (!c0 || !c1) {
+        g_err = "null fhh_ctx";
+        return FHH_E_ARG;
+    }
+    int rc = set_device(c0);
+    if (rc) return rc;
+    if (!counts) return c0->fail(FHH_E_ARG, "sim_eq_count: NULL counts");
+    return sim_eq_count_impl(c0, c1, nullptr, counts);
+}
+
+int fhh_sim_ot_sums(fhh_ctx* c0, fhh_ctx* c1, uint64_t prf_seed, void* sums0, void* sums1) {
+    if (!c0 || !c1) {
+        g_err = "null fhh_ctx";
+        return FHH_E_ARG;
+    }
+    int rc = set_device(c0);
+    if (rc) return rc;
+    if (!sums0 || !sums1) return c0->fail(FHH_E_ARG, "sim_ot_sums: NULL buffer");
+    return sim_ot_sums_impl(c0, c1, nullptr, prf_seed, sums0, sums1);
+}
+
+int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
+    if (!c0 || !c1 || !cfg) {
+        g_err = "sim_crawl: NULL argument";
+        return FHH_E_ARG;
+    }
+    int rc = set_device(c0);
+    if (rc) return rc;
+    const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
+    if (levels > c0->L) return c0->fail(FHH_E_ARG, "sim_crawl: levels > data_len");
+    if (cfg->mode > 1) return c0->fail(FHH_E_ARG, "sim_crawl: bad mode");
+    rc = fhh_tree_init(c0);
+    if (rc) return rc;
+    rc = fhh_tree_init(c1);
+    if (rc) return rc;
+    // leader.rs:193-194 and 245-246
+    const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
+    const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));
+    uint64_t counts_off = 0;
+    std::vector<uint64_t> vals, s0, s1;
+    std::vector<uint32_t> l0, l1;
+    std::vector<uint8_t> keep;
+    for (uint32_t lv = 0; lv < levels; lv++) {
+        const bool last = lv + 1 == levels;
+        rc = crawl_pair(c0, c1, last);
+        if (rc) return rc;
+        const uint64_t C = c0->pending_C;
+        keep.assign(C, 0);
+        if (cfg->mode == 0) {
+            vals.resize(C);
+            rc = sim_eq_count_impl(c0, c1, cfg, vals.data());
+            if (rc) return rc;
+            for (uint64_t c = 0; c < C; c++) keep[c] = vals[c] >= (last ? (uint64_t)thr_last : thr);
+            if (cfg->counts && counts_off + C <= cfg->counts_capacity)
+                std::memcpy(cfg->counts + counts_off, vals.data(), C * 8);
+            counts_off += C;
+            if (last) {
+                for (uint64_t c = 0; c < C; c++) {
+                    Limbs10 v{};
+                    v[0] = (uint32_t)vals[c];
+                    v[1] = (uint32_t)(vals[c] >> 32);
+                    c0->last_values[c] = v;
+                    c1->last_values[c] = Limbs10{};
+                }
+            }
+        } else if (!last) {
+            s0.resize(C);
+            s1.resize(C);
+            rc = sim_ot_sums_impl(c0, c1, cfg, cfg->prf_seed, s0.data(), s1.data());
+            if (rc) return rc;
+            rc = fhh_keep_values(thr, s0.data(), s1.data(), C, keep.data());
+            if (rc) return rc;
+            if (cfg->counts && counts_off + C <= cfg->counts_capacity)
+                for (uint64_t c = 0; c < C; c++)
+                    cfg->counts[counts_off + c] = s0[c] >= s1[c] ? s0[c] - s1[c] : s0[c] + (kFeP - s1[c]);
+            counts_off += C;
+        } else {
+            l0.resize(C * 10);
+            l1.resize(C * 10);
+            rc = sim_ot_sums_impl(c0, c1, cfg, cfg->prf_seed, l0.data(), l1.data());
+            if (rc) return rc;
+            rc = fhh_keep_values_last(thr_last, l0.data(), l1.data(), C, keep.data());
+            if (rc) return rc;
+            if (cfg->counts && counts_off + C <= cfg->counts_capacity) {
+                std::vector<uint32_t> fv(C * 8);
+                fhh_final_values(l0.data(), l1.data(), C, fv.data());
+                for (uint64_t c = 0; c < C; c++)
+                    cfg->counts[counts_off + c] = (uint64_t)fv[c * 8] | ((uint64_t)fv[c * 8 + 1] << 32);
+            }
+            counts_off += C;
+        }
+        uint64_t kept = 0;
+        for (uint64_t c = 0; c < C; c++) kept += keep[c];
+        if (cfg->level_children) cfg->level_children[lv] = C;
+        if (cfg->level_kept) cfg->level_kept[lv] = kept;
+        if (last) {
+            rc = fhh_tree_prune_last(c0, keep.data(), C);
+            if (rc) return rc;
+            rc = fhh_tree_prune_last(c1, keep.data(), C);
+            if (rc) return rc;
+        } else {
+            rc = prune_impl(c0, keep.data(), C);
+            if (rc) return rc;
+            rc = prune_impl(c1, keep.data(), C);
+            if (rc) return rc;
+        }
+    }
+    return FHH_OK;
+}
+
+int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out) {
+    CTX_CHECK(ctx);
+    if (out) *out = ctx->stats;
+    return FHH_OK;
+}
+
+int fhh_reset_stats(fhh_ctx* ctx) {
+    CTX_CHECK(ctx);
+    ctx->stats = fhh_stats{};
+    return FHH_OK;
+}
+
+int fhh_set_timing(fhh_ctx* ctx, int enabled) {
+    CTX_CHECK(ctx);
+    ctx->timing = enabled != 0;
+    return FHH_OK;
+}
+
+int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus) {
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) {
+        g_err = std::string("hipGetDeviceProperties: ") + hipGetErrorString(e);
+        return FHH_E_HIP;
+    }
+    if (arch_name && cap) {
+        std::snprintf(arch_name, cap, "%s", prop.gcnArchName);
+    }
+    if (num_cus) *num_cus = prop.multiProcessorCount;
+    return FHH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+// Internal interface between the host engine (fhh_host.cpp) and the HIP kernels
+// (fhh_kernels.hip). Not part of the public C ABI (include/fhh.h).
+//
+// Device layout of one server's keys and evaluation states (SoA, lane = client):
+//   npad = 64 * nw clients (padded), K = 2*d keys per client, kk = 2*j + side
+//   cw_seed   [L][K][npad]   uint4      CorWord.seed            (ibDCF.rs:9-14)
+//   cw_bits   [L][K][4][nw]  u64 planes bits.0, bits.1, y.0, y.1
+//   root_seed [K][npad]      uint4      ibDCFKey.root_seed      (ibDCF.rs:16-21)
+//   key_idx   [K][nw]        u64 plane  ibDCFKey.key_idx
+//   per dim j, prefix table (double buffered), entry e = one dim-j prefix:
+//     seed [E][2][npad] uint4, t [E][2][nw] u64, y [E][2][nw] u64   (EvalState, ibDCF.rs:24-30)
+// A frontier node is a tuple of d entries (one per dim); a dim-j prefix shared by several
+// nodes is evaluated once (the reference re-evaluates it per node, collect.rs:94-119).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fhh {
+
+constexpr int kMaxDims = 4;
+constexpr int kMaxJobs = 2 * kMaxDims;      // two servers' ctxs x dims in one launch
+constexpr int kExpandThreads = 512;
+constexpr int kReduceThreads = 256;
+
+struct ExpandJob {
+    const uint4* cw_seed;
+    const uint64_t* cw_bits;
+    const uint4* src_seed;
+    const uint64_t* src_t;
+    const uint64_t* src_y;
+    uint4* dst_seed;
+    uint64_t* dst_t;
+    uint64_t* dst_y;
+    const uint32_t* live;   // [n_live] src entries, in frontier order
+    uint32_t n_live;
+    uint32_t level;
+    uint32_t dim;
+    uint32_t K;
+    uint32_t npad;
+    uint32_t nw;
+    uint32_t group;         // entries per work item (CW reuse factor)
+    uint32_t pad_;
+    uint64_t item_begin;
+};
+
+struct ExpandLaunch {
+    ExpandJob job[kMaxJobs];
+    uint32_t njobs;
+    uint32_t pad_;
+    uint64_t total_items;
+};
+
+// Pending children: child c -> parent p = c >> d, i = c & (2^d - 1); its dim-j entry in
+// the child table is 2 * parent_pos[p*d + j] + ((i >> j) & 1).
+struct PlaneSet {
+    const uint64_t* t[kMaxDims];
+    const uint64_t* y[kMaxDims];
+};
+
+struct ChildArgs {
+    PlaneSet s0, s1;            // server 0 / server 1 child tables (s1 unused for share export)
+    const uint32_t* parent_pos; // [F][d]
+    const uint64_t* valid;      // [nw]
+    uint64_t C;
+    uint32_t d;
+    uint32_t nw;
+    uint64_t client_base;       // global index of client 0 (simulated-OT PRF)
+    uint64_t prf_seed;
+    uint32_t level;
+    uint32_t n;                 // real clients on this ctx
+};
+
+struct KeygenArgs {
+    const uint8_t* left_bits;   // [n][d][L]
+    const uint8_t* right_bits;
+    const uint8_t* root_seeds;  // [n][d][2 side][2 server][16]
+    uint4* cw_seed[2];
+    uint64_t* cw_bits[2];
+    uint4* root[2];
+    uint64_t* key_idx[2];
+    uint64_t n;
+    uint32_t d, L, K, npad, nw;
+};
+
+// ---- launch wrappers (fhh_kernels.hip); all asynchronous on `stream` ----
+hipError_t launch_expand(const ExpandLaunch& a, int grid, hipStream_t stream);
+hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream);
+hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream);
+hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream);
+hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials /*[C][16]*/, hipStream_t stream);
+hipError_t launch_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][2]*/, hipStream_t stream);
+hipError_t launch_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][8]*/, hipStream_t stream);
+hipError_t launch_keygen(const KeygenArgs& a, hipStream_t stream);
+hipError_t launch_init_tables(const uint4* root, const uint64_t* key_idx, uint32_t dim, uint32_t K, uint32_t npad,
+                              uint32_t nw, uint4* seed, uint64_t* t, uint64_t* y, hipStream_t stream);
+hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
+                                const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
+                                uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
+                                hipStream_t stream);
+// occupancy-derived persistent grid for k_expand on the current device
+int expand_grid(int device);
+
+}  // namespace fhh

@@ -1,0 +1,598 @@
+// HIP kernels for gfx950 (MI355X): the per-level ibDCF key evaluation of
+// sks-codes/fuzzyheavyhitters and the kernels around it.
+//
+//   k_expand        ibDCFKey::eval_bit for every (dim-prefix, client, side, dir)
+//                   (ibDCF.rs:208-227, prg.rs:92-122, collect.rs:379-391). Integer/LDS bound.
+//   k_eq_count      plaintext stand-in for the GC equality test: clients whose two share
+//                   strings agree, per child (collect.rs:393-482 replaced)
+//   k_share_planes  share-bit planes for the GC (collect.rs:393-418)
+//   k_sim_ot_fe*    simulated OT share values summed per child (collect.rs:439-501, 846-905)
+//   k_sum_fe*       per-child sums of host-provided FE / FE255 values (collect.rs:487-501)
+//   k_keygen        batched gen_interval keygen (ibDCF.rs:84-173)
+//   k_init_table    eval_init for every key (ibDCF.rs:229-236, collect.rs:67-92)
+//   k_keys_from_aos add_key wire layout -> SoA device layout
+#include "fhh_internal.h"
+#include "aes_ttable.h"
+
+namespace fhh {
+
+__constant__ WordTable c_T0 = T0;
+
+__device__ __forceinline__ uint32_t wave_id_uniform() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ void fill_table(uint32_t* tbl) {
+    for (int i = threadIdx.x; i < kTableWords; i += blockDim.x) tbl[i] = c_T0.v[i / kTableReplicas];
+    __syncthreads();
+}
+
+// --------------------------------------------------------------------------------------
+// k_expand: one wave = 64 consecutive clients of one dim-j prefix group. Per entry and
+// lane: 2 sides x 2 directions = 4 AES blocks in lockstep (ILP for the LDS lookups).
+// CorWords of (level, dim, side, client) are loaded once per work item and reused for
+// `group` entries.
+// --------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kExpandThreads) void k_expand(ExpandLaunch a) {
+    __shared__ uint32_t tbl[kTableWords];
+    fill_table(tbl);
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lanebase = lane * 4;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+
+    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < a.total_items; item += nwaves) {
+        uint32_t ji = 0;
+        while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
+        const ExpandJob& J = a.job[ji];
+        const uint64_t local = item - J.item_begin;
+        const uint32_t w = (uint32_t)(local % J.nw);
+        const uint32_t g = (uint32_t)(local / J.nw);
+        const uint32_t c = w * 64 + lane;
+        const size_t npad = J.npad, nw = J.nw;
+
+        // CorWord for (level, dim, side) — ibDCF.rs:215-217 `cor_words[state.level]`
+        const size_t krow = (size_t)J.level * J.K + 2 * J.dim;
+        uint4 cw[2];
+        uint64_t cwp[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            cw[s] = J.cw_seed[(krow + s) * npad + c];
+#pragma unroll
+            for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
+        }
+
+        const uint32_t e_begin = g * J.group;
+        const uint32_t e_end = min(e_begin + J.group, J.n_live);
+        for (uint32_t e = e_begin; e < e_end; e++) {
+            const uint32_t src = J.live[e];
+            uint32_t blk[4][4];      // index s*2 + dir
+            uint64_t tw[2], yw[2];
+            uint64_t pb[4], py[4];   // PRG control bits (tau.bits / tau.y_bits), ballot planes
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const uint4 sd = J.src_seed[((size_t)src * 2 + s) * npad + c];
+                tw[s] = J.src_t[((size_t)src * 2 + s) * nw + w];
+                yw[s] = J.src_y[((size_t)src * 2 + s) * nw + w];
+                const uint32_t sw[4] = {sd.x, sd.y, sd.z, sd.w};
+#pragma unroll
+                for (int dir = 0; dir < 2; dir++) {
+                    prg_ctr(sw, dir, blk[s * 2 + dir]);
+                    uint32_t bit, ybit;
+                    prg_ctrl_bits(blk[s * 2 + dir][0], dir, bit, ybit);
+                    pb[s * 2 + dir] = __ballot(bit);
+                    py[s * 2 + dir] = __ballot(ybit);
+                }
+            }
+
+            aes0_mmo<DevOps, 4>(blk, tbl, lanebase);
+
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const uint32_t tmask = 0u - (uint32_t)((tw[s] >> lane) & 1);   // if state.bit
+#pragma unroll
+                for (int dir = 0; dir < 2; dir++) {
+                    const uint32_t* o = blk[s * 2 + dir];
+                    uint4 out;
+                    out.x = o[0] ^ (cw[s].x & tmask);
+                    out.y = o[1] ^ (cw[s].y & tmask);
+                    out.z = o[2] ^ (cw[s].z & tmask);
+                    out.w = o[3] ^ (cw[s].w & tmask);
+                    const size_t de = (size_t)(2 * e + dir) * 2 + s;
+                    J.dst_seed[de * npad + c] = out;
+                    if (lane == 0) {
+                        // new_bit = tau.bits[dir] ^ (t & cw.bits[dir]);
+                        // new_y = tau.y_bits[dir] ^ (t & cw.y_bits[dir]) ^ y   (ibDCF.rs:211-219)
+                        J.dst_t[de * nw + w] = pb[s * 2 + dir] ^ (tw[s] & cwp[s][dir]);
+                        J.dst_y[de * nw + w] = py[s * 2 + dir] ^ (tw[s] & cwp[s][2 + dir]) ^ yw[s];
+                    }
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_expand(const ExpandLaunch& a, int grid, hipStream_t stream) {
+    if (a.total_items == 0) return hipSuccess;
+    uint64_t waves_needed = a.total_items;
+    uint64_t blocks_needed = (waves_needed + (kExpandThreads / 64) - 1) / (kExpandThreads / 64);
+    int g = (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
+    hipLaunchKernelGGL(k_expand, dim3(g), dim3(kExpandThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+int expand_grid(int device) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_expand), kExpandThreads,
+                                                     0) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 1;
+    return cus * per_cu;
+}
+
+// --------------------------------------------------------------------------------------
+// Child-level kernels (one block per child, grid-stride).
+// --------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum_u64(uint64_t (&v)[NV], uint64_t* red /*[NV][kReduceThreads/64]*/) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = wave_sum_u64(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; k++) red[k * (kReduceThreads / 64) + wid] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; k++) {
+            uint64_t s = 0;
+            for (int i = 0; i < nwv; i++) s += red[k * (kReduceThreads / 64) + i];
+            v[k] = s;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void child_entries(const ChildArgs& a, uint64_t c, uint32_t (&e)[kMaxDims]) {
+    const uint64_t p = c >> a.d;
+    const uint32_t i = (uint32_t)(c & ((1u << a.d) - 1));
+#pragma unroll
+    for (int j = 0; j < kMaxDims; j++)
+        if (j < (int)a.d) e[j] = 2 * a.parent_pos[p * a.d + j] + ((i >> j) & 1);
+}
+
+// eq word: bit = 1 iff the client's share string is identical on both servers
+__device__ __forceinline__ uint64_t eq_word(const ChildArgs& a, const uint32_t (&e)[kMaxDims], uint32_t w) {
+    uint64_t m = a.valid[w];
+#pragma unroll
+    for (int j = 0; j < kMaxDims; j++) {
+        if (j < (int)a.d) {
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const size_t idx = ((size_t)e[j] * 2 + s) * a.nw + w;
+                const uint64_t e0 = a.s0.t[j][idx] ^ a.s0.y[j][idx];
+                const uint64_t e1 = a.s1.t[j][idx] ^ a.s1.y[j][idx];
+                m &= ~(e0 ^ e1);
+            }
+        }
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kReduceThreads) void k_eq_count(ChildArgs a, uint64_t* counts) {
+    __shared__ uint64_t red[kReduceThreads / 64];
+    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+        uint32_t e[kMaxDims];
+        child_entries(a, c, e);
+        uint64_t v[1] = {0};
+        for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) v[0] += __popcll(eq_word(a, e, w));
+        block_sum_u64<1>(v, red);
+        if (threadIdx.x == 0) counts[c] = v[0];
+    }
+}
+
+static int child_grid(uint64_t C) { return (int)(C < 65535 ? (C ? C : 1) : 65535); }
+
+hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_eq_count, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, counts);
+    return hipGetLastError();
+}
+
+// out [C][2d][nw]: left dims then right dims, E = y ^ t (collect.rs:399-405)
+__global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, uint64_t* out) {
+    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+        uint32_t e[kMaxDims];
+        child_entries(a, c, e);
+        for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) {
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int j = 0; j < kMaxDims; j++)
+                    if (j < (int)a.d) {
+                        const size_t idx = ((size_t)e[j] * 2 + s) * a.nw + w;
+                        out[((size_t)c * 2 * a.d + (size_t)s * a.d + j) * a.nw + w] =
+                            (a.s0.t[j][idx] ^ a.s0.y[j][idx]) & a.valid[w];
+                    }
+        }
+    }
+}
+
+hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_share_planes, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, out);
+    return hipGetLastError();
+}
+
+// ---- simulated OT share values --------------------------------------------------------
+// PRF: mix64 chain (SplitMix64 finaliser) over (seed, level, child, client, word).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;
+
+__global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
+    __shared__ uint64_t red[4 * (kReduceThreads / 64)];
+    const uint64_t base = mix64(a.prf_seed ^ a.level);
+    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+        uint32_t e[kMaxDims];
+        child_entries(a, c, e);
+        const uint64_t bc = mix64(base ^ c);
+        uint64_t v[4] = {0, 0, 0, 0};
+        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
+            const uint64_t eqw = eq_word(a, e, i >> 6);
+            const bool eq = (eqw >> (i & 63)) & 1;
+            uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
+            if (r0 >= kFeP) r0 -= kFeP;
+            const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
+            const uint64_t v1 = eq ? r0 : r1;                    // receiver gets pair[o] (A.5)
+            v[0] += r1 & 0xFFFFFFFFull;
+            v[1] += r1 >> 32;
+            v[2] += v1 & 0xFFFFFFFFull;
+            v[3] += v1 >> 32;
+        }
+        block_sum_u64<4>(v, red);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 4; k++) partials[c * 4 + k] = v[k];
+    }
+}
+
+hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, partials);
+    return hipGetLastError();
+}
+
+// 255-bit helpers on 4 x u64 little-endian
+__device__ __forceinline__ void fe255_canon(uint64_t (&x)[4]) {
+    // x < 2^255; subtract p = 2^255 - 19 when x >= p (i.e. x + 19 carries into bit 255)
+    uint64_t t[4];
+    unsigned __int128 acc = (unsigned __int128)x[0] + 19;
+    t[0] = (uint64_t)acc;
+    acc = (unsigned __int128)x[1] + (uint64_t)(acc >> 64);
+    t[1] = (uint64_t)acc;
+    acc = (unsigned __int128)x[2] + (uint64_t)(acc >> 64);
+    t[2] = (uint64_t)acc;
+    acc = (unsigned __int128)x[3] + (uint64_t)(acc >> 64);
+    t[3] = (uint64_t)acc;
+    if (t[3] >> 63) {
+        x[0] = t[0];
+        x[1] = t[1];
+        x[2] = t[2];
+        x[3] = t[3] & 0x7FFFFFFFFFFFFFFFull;
+    }
+}
+
+__global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
+    __shared__ uint64_t red[16 * (kReduceThreads / 64)];
+    const uint64_t base = mix64(a.prf_seed ^ a.level);
+    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+        uint32_t e[kMaxDims];
+        child_entries(a, c, e);
+        const uint64_t bc = mix64(base ^ c);
+        uint64_t v[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = 0;
+        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
+            const uint64_t eqw = eq_word(a, e, i >> 6);
+            const bool eq = (eqw >> (i & 63)) & 1;
+            const uint64_t bi = mix64(bc ^ (a.client_base + i));
+            uint64_t r0[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) r0[k] = mix64(bi ^ (uint64_t)k);
+            r0[3] &= 0x7FFFFFFFFFFFFFFFull;
+            fe255_canon(r0);
+            // r1 = r0 + 1 mod p
+            uint64_t r1[4];
+            unsigned __int128 acc = (unsigned __int128)r0[0] + 1;
+            r1[0] = (uint64_t)acc;
+#pragma unroll
+            for (int k = 1; k < 4; k++) {
+                acc = (unsigned __int128)r0[k] + (uint64_t)(acc >> 64);
+                r1[k] = (uint64_t)acc;
+            }
+            fe255_canon(r1);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t x1 = eq ? r0[k] : r1[k];
+                v[2 * k] += r1[k] & 0xFFFFFFFFull;
+                v[2 * k + 1] += r1[k] >> 32;
+                v[8 + 2 * k] += x1 & 0xFFFFFFFFull;
+                v[8 + 2 * k + 1] += x1 >> 32;
+            }
+        }
+        block_sum_u64<16>(v, red);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 16; k++) partials[c * 16 + k] = v[k];
+    }
+}
+
+hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sim_ot_fe255, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, partials);
+    return hipGetLastError();
+}
+
+// ---- sums of host-provided OT outputs -------------------------------------------------
+__global__ __launch_bounds__(kReduceThreads) void k_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n,
+                                                          uint64_t* partials) {
+    __shared__ uint64_t red[2 * (kReduceThreads / 64)];
+    for (uint64_t c = blockIdx.x; c < C; c += gridDim.x) {
+        uint64_t v[2] = {0, 0};
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t x = vals[c * n + i];
+            v[0] += x & 0xFFFFFFFFull;
+            v[1] += x >> 32;
+        }
+        block_sum_u64<2>(v, red);
+        if (threadIdx.x == 0) {
+            partials[c * 2] = v[0];
+            partials[c * 2 + 1] = v[1];
+        }
+    }
+}
+
+hipError_t launch_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t* partials, hipStream_t stream) {
+    if (C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sum_fe, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream, vals, C, n, partials);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kReduceThreads) void k_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n,
+                                                             uint64_t* partials) {
+    __shared__ uint64_t red[8 * (kReduceThreads / 64)];
+    for (uint64_t c = blockIdx.x; c < C; c += gridDim.x) {
+        uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint4* p = reinterpret_cast<const uint4*>(vals + (c * n + i) * 8);
+            const uint4 lo = p[0], hi = p[1];
+            v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
+            v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+        }
+        block_sum_u64<8>(v, red);
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 8; k++) partials[c * 8 + k] = v[k];
+    }
+}
+
+hipError_t launch_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n, uint64_t* partials, hipStream_t stream) {
+    if (C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sum_fe255, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream, vals, C, n, partials);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------------
+// k_keygen: one wave = 64 clients of one key (dim j, side). Restates gen_cor_word
+// (ibDCF.rs:84-119) level by level; 4 AES blocks per level per lane (both seeds, both
+// directions). Writes server 0's and server 1's key arrays (shared cor_words).
+// --------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kExpandThreads) void k_keygen(KeygenArgs a) {
+    __shared__ uint32_t tbl[kTableWords];
+    fill_table(tbl);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lanebase = lane * 4;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    const uint64_t items = (uint64_t)a.K * a.nw;
+    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items; item += nwaves) {
+        const uint32_t kk = (uint32_t)(item / a.nw);
+        const uint32_t w = (uint32_t)(item % a.nw);
+        const uint32_t j = kk >> 1, side_idx = kk & 1;
+        const uint32_t side = side_idx == 0 ? 1u : 0u;   // left key: side=true, right: false (ibDCF.rs:170-171)
+        const uint64_t c = (uint64_t)w * 64 + lane;
+        const bool valid = c < a.n;
+        const uint8_t* alpha = (side_idx == 0 ? a.left_bits : a.right_bits) + (valid ? (c * a.d + j) * a.L : 0);
+
+        uint32_t seed[2][4];
+        if (valid) {
+            const uint4* rs = reinterpret_cast<const uint4*>(a.root_seeds + ((c * a.d + j) * 2 + side_idx) * 32);
+            const uint4 r0 = rs[0], r1 = rs[1];
+            seed[0][0] = r0.x; seed[0][1] = r0.y; seed[0][2] = r0.z; seed[0][3] = r0.w;
+            seed[1][0] = r1.x; seed[1][1] = r1.y; seed[1][2] = r1.z; seed[1][3] = r1.w;
+        } else {
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int k = 0; k < 4; k++) seed[b][k] = 0;
+        }
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+            a.root[b][(size_t)kk * a.npad + c] = make_uint4(seed[b][0], seed[b][1], seed[b][2], seed[b][3]);
+        if (lane == 0) {
+            a.key_idx[0][(size_t)kk * a.nw + w] = 0;         // key_idx = false
+            a.key_idx[1][(size_t)kk * a.nw + w] = ~0ull;     // key_idx = true (ibDCF.rs:153-161)
+        }
+        uint32_t t[2] = {0u, 1u};                           // root_bits = (false, true), ibDCF.rs:140
+
+        for (uint32_t l = 0; l < a.L; l++) {
+            const uint32_t bit = valid ? (alpha[l] ? 1u : 0u) : 0u;
+            uint32_t blk[4][4];                             // index b*2 + dir
+            uint32_t pbit[4], pyb[4];
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int dir = 0; dir < 2; dir++) {
+                    prg_ctr(seed[b], dir, blk[b * 2 + dir]);
+                    prg_ctrl_bits(blk[b * 2 + dir][0], dir, pbit[b * 2 + dir], pyb[b * 2 + dir]);
+                }
+            aes0_mmo<DevOps, 4>(blk, tbl, lanebase);
+
+            const uint32_t keep = bit, lose = bit ^ 1u;
+            uint32_t cws[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t l0 = lose ? blk[1][k] : blk[0][k];
+                const uint32_t l1 = lose ? blk[3][k] : blk[2][k];
+                cws[k] = l0 ^ l1;                                   // ibDCF.rs:91
+            }
+            // data.b.bits.k = pbit[b*2+k], data.b.y_bits.k = pyb[b*2+k]
+            const uint32_t cb0 = pbit[0] ^ pbit[2] ^ bit ^ 1u;       // :93
+            const uint32_t cb1 = pbit[1] ^ pbit[3] ^ bit;            // :94
+            const uint32_t cy0 = pyb[0] ^ pyb[2] ^ (bit & (side ^ 1u) & 1u);   // :97 bit & !side
+            const uint32_t cy1 = pyb[1] ^ pyb[3] ^ ((bit ^ 1u) & side);        // :98 !bit & side
+            const uint32_t cwb_keep = keep ? cb1 : cb0;
+#pragma unroll
+            for (int b = 0; b < 2; b++) {                            // :103-116
+                const uint32_t tm = 0u - t[b];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t kept = keep ? blk[b * 2 + 1][k] : blk[b * 2][k];
+                    seed[b][k] = kept ^ (cws[k] & tm);
+                }
+                const uint32_t nb = (keep ? pbit[b * 2 + 1] : pbit[b * 2]) ^ (t[b] & cwb_keep);
+                t[b] = nb;
+            }
+            const size_t row = (size_t)l * a.K + kk;
+            const uint4 cwv = make_uint4(cws[0], cws[1], cws[2], cws[3]);
+            a.cw_seed[0][row * a.npad + c] = cwv;
+            a.cw_seed[1][row * a.npad + c] = cwv;
+            const uint64_t q0 = __ballot(cb0), q1 = __ballot(cb1), q2 = __ballot(cy0), q3 = __ballot(cy1);
+            if (lane == 0) {
+                const uint64_t q[4] = {q0, q1, q2, q3};
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    a.cw_bits[0][(row * 4 + b) * a.nw + w] = q[b];
+                    a.cw_bits[1][(row * 4 + b) * a.nw + w] = q[b];
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_keygen(const KeygenArgs& a, hipStream_t stream) {
+    const uint64_t items = (uint64_t)a.K * a.nw;
+    if (items == 0) return hipSuccess;
+    const uint64_t wpb = kExpandThreads / 64;
+    uint64_t blocks = (items + wpb - 1) / wpb;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_keygen, dim3((unsigned)blocks), dim3(kExpandThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------------
+// eval_init for dim `dim` -> entry 0 of that dim's table: seed = root_seed, t = y = key_idx
+// --------------------------------------------------------------------------------------
+__global__ void k_init_table(const uint4* root, const uint64_t* key_idx, uint32_t dim, uint32_t npad, uint32_t nw,
+                             uint4* seed, uint64_t* t, uint64_t* y) {
+    const uint64_t total = (uint64_t)2 * npad;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(i / npad), c = (uint32_t)(i % npad);
+        seed[(size_t)s * npad + c] = root[((size_t)2 * dim + s) * npad + c];
+        if (c < nw) {
+            const uint64_t k = key_idx[((size_t)2 * dim + s) * nw + c];
+            t[(size_t)s * nw + c] = k;
+            y[(size_t)s * nw + c] = k;
+        }
+    }
+}
+
+hipError_t launch_init_tables(const uint4* root, const uint64_t* key_idx, uint32_t dim, uint32_t K, uint32_t npad,
+                              uint32_t nw, uint4* seed, uint64_t* t, uint64_t* y, hipStream_t stream) {
+    (void)K;
+    const uint64_t total = (uint64_t)2 * npad;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_init_table, dim3(blocks), dim3(256), 0, stream, root, key_idx, dim, npad, nw, seed, t, y);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------------
+// add_key wire layout (AoS, client-major) -> SoA. One wave = 64 clients of one (level, key).
+// --------------------------------------------------------------------------------------
+__global__ void k_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
+                                const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
+                                uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    const uint64_t items = (uint64_t)(L + 1) * K * nw;   // level L = roots / key_idx
+    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items; item += nwaves) {
+        const uint32_t w = (uint32_t)(item % nw);
+        const uint32_t kk = (uint32_t)((item / nw) % K);
+        const uint32_t l = (uint32_t)(item / ((uint64_t)nw * K));
+        const uint64_t c = (uint64_t)w * 64 + lane;
+        const bool valid = c < n;
+        if (l < L) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            uint32_t nib = 0;
+            if (valid) {
+                const uint8_t* p = cw_seed + ((c * K + kk) * L + l) * 16;
+                uint32_t x[4];
+                for (int k = 0; k < 4; k++)
+                    x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+                           ((uint32_t)p[4 * k + 3] << 24);
+                v = make_uint4(x[0], x[1], x[2], x[3]);
+                nib = cw_bits[(c * K + kk) * L + l];
+            }
+            const size_t row = (size_t)l * K + kk;
+            d_cw_seed[row * npad + c] = v;
+            uint64_t q[4];
+            for (int b = 0; b < 4; b++) q[b] = __ballot((nib >> b) & 1);
+            if (lane == 0)
+                for (int b = 0; b < 4; b++) d_cw_bits[(row * 4 + b) * nw + w] = q[b];
+        } else {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            uint32_t ki = 0;
+            if (valid) {
+                const uint8_t* p = root_seed + (c * K + kk) * 16;
+                uint32_t x[4];
+                for (int k = 0; k < 4; k++)
+                    x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+                           ((uint32_t)p[4 * k + 3] << 24);
+                v = make_uint4(x[0], x[1], x[2], x[3]);
+                ki = key_idx[c * K + kk] ? 1u : 0u;
+            }
+            d_root[(size_t)kk * npad + c] = v;
+            const uint64_t q = __ballot(ki);
+            if (lane == 0) d_key_idx[(size_t)kk * nw + w] = q;
+        }
+    }
+}
+
+hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
+                                const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
+                                uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
+                                hipStream_t stream) {
+    const uint64_t items = (uint64_t)(L + 1) * K * nw;
+    uint64_t blocks = (items + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_keys_from_aos, dim3((unsigned)blocks), dim3(256), 0, stream, key_idx, root_seed, cw_seed,
+                       cw_bits, n, K, L, npad, nw, d_cw_seed, d_cw_bits, d_root, d_key_idx);
+    return hipGetLastError();
+}
+
+}  // namespace fhh

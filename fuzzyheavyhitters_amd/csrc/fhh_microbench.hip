@@ -1,0 +1,92 @@
+// Peak-rate microbenchmarks that pin the roofline denominators on the box itself
+// ("confirm P_int with a v_xor_b32 throughput microbenchmark"):
+//   which = 0: v_xor_b32 lane-ops/s, every CU, 8 waves/SIMD, independent chains
+//   which = 1: ds_read_b32 bytes/s with the k_expand access pattern (per-lane replica,
+//              bank-conflict free, data-dependent byte index)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/fhh.h"
+
+namespace fhh {
+
+__global__ __launch_bounds__(256) void k_valu_peak(uint32_t* out, uint32_t iters, uint32_t seed) {
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = seed * (threadIdx.x + 1) + k * 0x9e3779b9u + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) x[k] ^= x[(k + 1 + r) & 15];
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc ^= x[k];
+    if (acc == 0x12345678u) out[0] = acc;   // keep live
+}
+
+__global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters) {
+    __shared__ uint32_t tbl[256 * 64];
+    for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) tbl[i] = (uint32_t)i * 2654435761u;
+    __syncthreads();
+    const uint32_t lb = (threadIdx.x & 63) * 4;
+    uint32_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = threadIdx.x * 31 + k * 77;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t a = __builtin_amdgcn_perm(lb, x[k], 0x0C0C0104u);
+            x[k] = *(const uint32_t*)((const char*)tbl + a);
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc ^= x[k];
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+}  // namespace fhh
+
+extern "C" int fhh_microbench(int device, int which, double* rate) {
+    if (!rate) return FHH_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return FHH_E_HIP;
+    uint32_t* out = nullptr;
+    if (hipMalloc(&out, 4) != hipSuccess) return FHH_E_NOMEM;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const int threads = 256;
+    double ops = 0;
+    float ms = 0.f;
+    for (int rep = 0; rep < 2; rep++) {   // first pass warms clocks
+        if (which == 0) {
+            const int blocks = cus * 8;   // 8 waves/SIMD
+            const uint32_t iters = 4096;
+            (void)hipEventRecord(a, 0);
+            hipLaunchKernelGGL(fhh::k_valu_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            (void)hipEventRecord(b, 0);
+            ops = (double)blocks * threads * iters * 8 * 16;
+        } else {
+            const int blocks = cus * 2;   // 64 KiB LDS -> 2 blocks/CU of 512 threads (as k_expand)
+            const uint32_t iters = 8192;
+            (void)hipEventRecord(a, 0);
+            hipLaunchKernelGGL(fhh::k_lds_peak, dim3(blocks), dim3(512), 0, 0, out, iters);
+            (void)hipEventRecord(b, 0);
+            ops = (double)blocks * 512 * iters * 8 * 4;   // bytes
+        }
+        if (hipEventSynchronize(b) != hipSuccess) {
+            (void)hipFree(out);
+            return FHH_E_HIP;
+        }
+        (void)hipEventElapsedTime(&ms, a, b);
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(out);
+    *rate = ops / (ms * 1e-3);
+    return FHH_OK;
+}

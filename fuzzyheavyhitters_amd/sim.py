@@ -1,0 +1,91 @@
+"""In-process leader + two servers (the reference's leader level loop, leader.rs:417-440),
+with the servers' garbled-circuit equality test + OT (collect.rs:419-482, out of scope)
+replaced by either plaintext equality of the two share strings (mode "count") or simulated
+OT share values (mode "fe": r0 from a fixed PRF, r1 = r0 + 1, v0 = r1, v1 = eq ? r0 : r1).
+
+Clients may be sharded across GPUs (one process per GPU): each rank holds both servers'
+keys for its client range, and the per-child partial sums are all-reduced over RCCL with
+torch.distributed before the leader's keep decision.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import ALLREDUCE_FN, FhhSimConfig, check, lib, u64p
+from .collection import KeyCollection
+
+
+@dataclass
+class SimResult:
+    level_children: np.ndarray
+    level_kept: np.ndarray
+    counts: list = field(default_factory=list)     # per level np.ndarray (mode count: counts; fe: v0-v1)
+    final: list = field(default_factory=list)      # Result(path, value) from server 0's final_shares
+
+
+class _TorchAllReduce:
+    """Sum a device buffer across ranks with torch.distributed (backend nccl = RCCL)."""
+
+    def __init__(self, capacity: int, device: int):
+        import torch
+        import torch.distributed as dist
+        self.torch = torch
+        self.dist = dist
+        self.buf = torch.zeros(capacity, dtype=torch.int64, device=f"cuda:{device}")
+        self.cb = ALLREDUCE_FN(self._call)
+        self.err = None
+
+    def _call(self, ptr, count, user):
+        try:
+            view = self.buf[:count]
+            self.dist.all_reduce(view)                 # u64 partials: sums fit
+            self.torch.cuda.current_stream().synchronize()
+            return 0
+        except Exception as e:  # pragma: no cover - surfaced as FHH_E_CALLBACK
+            self.err = e
+            return 1
+
+
+def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
+              mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
+              distributed: bool = False, xchg_capacity: int = 1 << 16) -> SimResult:
+    L = levels or c0.depth
+    n_local = c0.num_clients()
+    cfg = FhhSimConfig()
+    cfg.threshold = threshold
+    cfg.nclients_total = nclients_total if nclients_total is not None else n_local
+    cfg.mode = {"count": 0, "fe": 1}[mode]
+    cfg.levels = L
+    cfg.prf_seed = prf_seed
+    ar = None
+    if distributed:
+        ar = _TorchAllReduce(xchg_capacity, c0.device)
+        cfg.allreduce = ar.cb
+        cfg.xchg_dev = ctypes.cast(ctypes.c_void_p(ar.buf.data_ptr()), u64p)
+        cfg.xchg_capacity = xchg_capacity
+    else:
+        cfg.allreduce = ALLREDUCE_FN()
+    lc = np.zeros(L, np.uint64)
+    lk = np.zeros(L, np.uint64)
+    cap = 1 << 22 if record else 0
+    counts = np.zeros(max(cap, 1), np.uint64)
+    cfg.level_children = lc.ctypes.data_as(u64p)
+    cfg.level_kept = lk.ctypes.data_as(u64p)
+    if record:
+        cfg.counts = counts.ctypes.data_as(u64p)
+        cfg.counts_capacity = cap
+    rc = lib().fhh_sim_crawl(c0.handle, c1.handle, ctypes.byref(cfg))
+    if ar is not None and ar.err is not None:
+        raise ar.err
+    check(rc, c0.handle)
+    res = SimResult(lc, lk)
+    if record:
+        off = 0
+        for C in lc:
+            res.counts.append(counts[off:off + int(C)].copy())
+            off += int(C)
+    res.final = c0.final_shares()
+    return res

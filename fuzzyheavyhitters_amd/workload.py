@@ -1,0 +1,150 @@
+"""Deterministic synthetic workloads shaped like the reference leader's (src/bin/leader.rs).
+
+The reference draws everything from `thread_rng` (irreproducible); here a seeded numpy
+Generator stands in, with the same shapes:
+  * sites: `num_sites` strings of (data_len - aug_len) bits per dim, each an alphanumeric
+    ASCII string turned into bits LSB-first per byte (`string_to_bits`, lib.rs:90-98;
+    `generate_random_bit_vectors`, leader.rs:45-58; `generate_strings`, leader.rs:60-66);
+  * clients: a Zipf(s) draw over sites (leader.rs:140-147; inverse-CDF here instead of the
+    `zipf` crate's rejection sampler) plus an `aug_len`-bit alphanumeric augmentation per
+    dim (`augment_string`, leader.rs:78-87);
+  * key bounds: l = a - ball, r = a + ball on MSB-first bit strings of width
+    max(len, 32) (`gen_l_inf_ball`, ibDCF.rs:175-188; lib.rs:131-183).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+ALNUM = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
+
+
+def chars_to_bits(chars: np.ndarray) -> np.ndarray:
+    """uint8 ASCII [..., m] -> bits [..., 8m], LSB first per byte (lib.rs:90-98)."""
+    b = (chars[..., None] >> np.arange(8, dtype=np.uint8)) & 1
+    return b.reshape(*chars.shape[:-1], chars.shape[-1] * 8).astype(np.uint8)
+
+
+def random_alnum(rng: np.random.Generator, shape) -> np.ndarray:
+    return ALNUM[rng.integers(0, ALNUM.size, size=shape)]
+
+
+def zipf_indices(rng: np.random.Generator, n: int, num_sites: int, s: float) -> np.ndarray:
+    """P(k) ∝ k^-s for k = 1..num_sites; returns k-1."""
+    w = np.arange(1, num_sites + 1, dtype=np.float64) ** (-s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    u = rng.random(n)
+    return np.minimum(np.searchsorted(cdf, u, side="right"), num_sites - 1)
+
+
+def _add_small(bits: np.ndarray, delta: int, sign: int) -> np.ndarray:
+    """MSB-first bit strings [..., W] +/- delta (< 2^32) with wrap (subtract) or carry check."""
+    W = bits.shape[-1]
+    nwords = (W + 63) // 64
+    pad = nwords * 64 - W
+    b = np.concatenate([np.zeros(bits.shape[:-1] + (pad,), np.uint8), bits], axis=-1)
+    # pack big-endian into u64 words (word 0 most significant)
+    words = np.zeros(bits.shape[:-1] + (nwords,), np.uint64)
+    for k in range(64):
+        words |= b[..., k::64].astype(np.uint64) << np.uint64(63 - k)
+    carry = np.full(bits.shape[:-1], np.uint64(delta), np.uint64)
+    for wi in range(nwords - 1, -1, -1):
+        x = words[..., wi]
+        if sign > 0:
+            nx = x + carry
+            carry = (nx < x).astype(np.uint64)
+        else:
+            nx = x - carry
+            carry = (nx > x).astype(np.uint64)
+        words[..., wi] = nx
+    if sign > 0 and np.any(carry) or (sign > 0 and pad and np.any(words[..., 0] >> np.uint64(64 - pad))):
+        raise ValueError("carry out of add_bitstrings: the reference panics on this input (ibDCF.rs:182)")
+    out = np.zeros_like(b)
+    for k in range(64):
+        out[..., k::64] = ((words >> np.uint64(63 - k)) & np.uint64(1)).astype(np.uint8)
+    return out[..., pad:]
+
+
+def l_inf_ball_bounds(alpha: np.ndarray, ball: int):
+    """alpha [n][d][L] MSB-first bits -> (left, right) [n][d][max(L,32)] (ibDCF.rs:175-188)."""
+    L = alpha.shape[-1]
+    if L < 32:
+        alpha = np.concatenate([np.zeros(alpha.shape[:-1] + (32 - L,), np.uint8), alpha], axis=-1)
+    return _add_small(alpha, ball, -1), _add_small(alpha, ball, +1)
+
+
+def i16_to_bits(v: np.ndarray) -> np.ndarray:
+    """sample_driving_data.rs:25-28: i16 -> 16 bits MSB first (two's complement)."""
+    u = v.astype(np.int64) & 0xFFFF
+    return ((u[..., None] >> np.arange(15, -1, -1)) & 1).astype(np.uint8)
+
+
+@dataclass
+class Workload:
+    alpha: np.ndarray        # [n][d][L] client points (bits)
+    left: np.ndarray         # [n][d][L] interval lower bounds
+    right: np.ndarray        # [n][d][L] interval upper bounds
+    root_seeds: np.ndarray   # [n][d][2 side][2 server][16]
+    site_of_client: np.ndarray
+
+    @property
+    def n(self):
+        return self.alpha.shape[0]
+
+
+def zipf_workload(n: int, data_len: int = 512, n_dims: int = 1, num_sites: int = 10000, zipf_s: float = 1.03,
+                  ball_size: int = 1, aug_len: int = 8, seed: int = 0x5EED, client_offset: int = 0,
+                  sites_seed: int | None = None) -> Workload:
+    """Config 'zipf' of the reference leader (leader.rs:331-365). `client_offset` draws the
+    clients [client_offset, client_offset + n) of one global stream, so shards of a
+    multi-GPU run are slices of the single-GPU population (the site table is shared)."""
+    if data_len < 32:
+        raise ValueError("zipf workload needs data_len >= 32 (gen_l_inf_ball pads to 32 bits, ibDCF.rs:178)")
+    if aug_len % 8 or (data_len - aug_len) % 8:
+        raise ValueError("data_len and aug_len must be multiples of 8 (leader.rs:306)")
+    srng = np.random.default_rng(sites_seed if sites_seed is not None else seed)
+    site_bits = chars_to_bits(random_alnum(srng, (num_sites, n_dims, (data_len - aug_len) // 8)))
+    # per-client draws: generate the global stream up to client_offset + n and slice, so
+    # any client range is reproducible
+    sites = zipf_indices(np.random.default_rng([seed, 1]), client_offset + n, num_sites, zipf_s)[client_offset:]
+    arng = np.random.default_rng([seed, 2])
+    aug = random_alnum(arng, (client_offset + n, n_dims, aug_len // 8))[client_offset:]
+    alpha = np.concatenate([site_bits[sites], chars_to_bits(aug)], axis=-1)
+    left, right = l_inf_ball_bounds(alpha, ball_size)
+    rrng = np.random.default_rng([seed, 3])
+    roots = rrng.integers(0, 256, size=(client_offset + n, n_dims, 2, 2, 16), dtype=np.uint8)[client_offset:]
+    return Workload(alpha, left, right, np.ascontiguousarray(roots), sites)
+
+
+def plaintext_heavy_hitters(alpha_left: np.ndarray, alpha_right: np.ndarray, threshold_count: int):
+    """Brute-force recount (no crypto): heavy prefixes of the full depth whose box is
+    contained in at least `threshold_count` clients' [l, r] boxes, crawled level by level
+    exactly as the leader prunes (keep iff count >= threshold at every level). Returns
+    the sorted list of final paths as tuples of d bit-tuples. For tests only at small n."""
+    n, d, L = alpha_left.shape
+    frontier = [tuple(() for _ in range(d))]
+    for lvl in range(L):
+        children = []
+        for p in frontier:
+            for i in range(1 << d):
+                children.append(tuple(p[j] + ((i >> j) & 1,) for j in range(d)))
+        kept = []
+        for ch in children:
+            k = lvl + 1
+            cnt = 0
+            for c in range(n):
+                ok = True
+                for j in range(d):
+                    pre = ch[j]
+                    lo = tuple(int(x) for x in alpha_left[c, j, :k])
+                    hi = tuple(int(x) for x in alpha_right[c, j, :k])
+                    if not (lo <= pre <= hi):
+                        ok = False
+                        break
+                cnt += ok
+            if cnt >= threshold_count:
+                kept.append(ch)
+        frontier = kept
+    return sorted(frontier)

@@ -1,0 +1,210 @@
+/*
+ * fhh.h — C ABI of the MI355X-native evaluator for the per-level client-key evaluation
+ * of sks-codes/fuzzyheavyhitters (the ibDCF tree crawl).
+ *
+ * Drop-in boundary: `impl KeyCollection<T = FE, U = FieldElm>` (src/collect.rs:45-1030),
+ * called by the tarpc `Collector` handlers (src/bin/server.rs:64-171). One fhh_ctx is one
+ * server's KeyCollection bound to one GPU. Every entry point below names the reference
+ * item it replaces. A reference-side binding (Rust `extern "C"` + build.rs) is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - Return 0 on success, a negative FHH_E* code on error; fhh_last_error(ctx) explains.
+ *    The reference panics (unwrap/assert, collect.rs:83,919,932,946,967,1008,1012); a
+ *    caller that wants that behaviour aborts on nonzero.
+ *  - All buffers are caller-owned HOST memory unless the name ends in `_dev` (device
+ *    pointer on the ctx's GPU). The ctx owns its device memory and its HIP stream.
+ *  - A ctx may be used from any thread, but not concurrently (the reference wraps the
+ *    collection in a Mutex, server.rs:49). Calls are synchronous w.r.t. the host.
+ *  - Key order: client-major, then dim j in [0,d), then (left, right) — the order of
+ *    `add_key(Vec<(ibDCFKey, ibDCFKey)>)` (collect.rs:62) and `gen_l_inf_ball`
+ *    (ibDCF.rs:175-188). K = 2*d keys per client.
+ *  - cw_bits nibble per (key, level): bit0 = bits.0, bit1 = bits.1, bit2 = y_bits.0,
+ *    bit3 = y_bits.1 of `CorWord` (ibDCF.rs:9-14).
+ *  - Child order: parent order, then i in `all_bit_vectors(d)` (lib.rs:125-129): child i
+ *    takes direction (i >> j) & 1 in dim j (collect.rs:379-391).
+ *  - Share bits per (child, client): [left.y^left.t for each dim] ++ [right.y^right.t for
+ *    each dim] (collect.rs:393-418). Exported as bit-planes [child][2d][nw] u64, bit
+ *    (client % 64) of word (client / 64); nw = ceil(n_clients / 64).
+ *  - FE = GF(2^62 - 2^30 - 1) (fastfield.rs:24-28); FE255 = GF(2^255 - 19) (field.rs:19).
+ *    FE values may be passed in any u64 representation (FE::new semantics,
+ *    fastfield.rs:112-118); sums are returned canonical (`value()`, fastfield.rs:147-152).
+ */
+#ifndef FHH_H
+#define FHH_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FHH_OK 0
+#define FHH_E_ARG (-1)      /* bad argument / shape mismatch (reference: assert_eq! panic) */
+#define FHH_E_STATE (-2)    /* call out of protocol order (e.g. prune without crawl)       */
+#define FHH_E_HIP (-3)      /* HIP runtime error                                           */
+#define FHH_E_NOMEM (-4)    /* device allocation failed                                    */
+#define FHH_E_CALLBACK (-5) /* all-reduce callback failed                                  */
+
+#define FHH_MAX_DIMS 4
+
+typedef struct fhh_ctx fhh_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------ */
+
+/* KeyCollection::new(seed, depth) (collect.rs:51-60). data_len = tree depth L (number of
+ * crawl levels); n_dims = d. The PRG seed of `new` only feeds the unused rand_stream. */
+int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device);
+void fhh_destroy(fhh_ctx* ctx);
+/* Thread-local message of the last failure (ctx may be NULL for fhh_create failures). */
+const char* fhh_last_error(const fhh_ctx* ctx);
+/* `reset` RPC (server.rs:64-69): drop keys and frontier. */
+int fhh_reset(fhh_ctx* ctx);
+/* Global index of this ctx's first client (used by the simulated-OT PRF when clients are
+ * sharded across GPUs); default 0. */
+int fhh_set_client_base(fhh_ctx* ctx, uint64_t client_base);
+
+/* ---- keys ----------------------------------------------------------------------------- */
+
+/* KeyCollection::add_key (collect.rs:62-65), batched: append n clients.
+ *   key_idx   [n][d][2]         (ibDCFKey.key_idx, ibDCF.rs:17)
+ *   root_seed [n][d][2][16]     (ibDCFKey.root_seed)
+ *   cw_seed   [n][d][2][L][16]  (CorWord.seed for levels 0..L-1)
+ *   cw_bits   [n][d][2][L]      (nibble, see above)
+ * Keys are staged on the host and transposed to the device layout at tree_init. */
+int fhh_add_keys(fhh_ctx* ctx, uint64_t n, const uint8_t* key_idx, const uint8_t* root_seed,
+                 const uint8_t* cw_seed, const uint8_t* cw_bits);
+
+/* Leader-side batched `gen_l_inf_ball` keygen on the GPU (ibDCF.rs:84-119,138-188),
+ * writing server 0's keys into ctx0 and server 1's into ctx1 (both must be empty and on the
+ * same device). Replaces the leader's per-client `add_fuzzy_keys` loop (leader.rs:130-163).
+ *   left_bits/right_bits [n][d][L] (0/1, MSB first: interval bounds l = a-δ, r = a+δ)
+ *   root_seeds [n][d][2 side][2 server][16] (caller randomness; the reference uses
+ *   thread_rng, prg.rs:153-158). */
+int fhh_gen_keys_pair(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t n, const uint8_t* left_bits,
+                      const uint8_t* right_bits, const uint8_t* root_seeds);
+
+/* Number of clients (len of `keys`). */
+int fhh_num_clients(const fhh_ctx* ctx, uint64_t* n);
+
+/* Copy this ctx's keys back in add_keys layout (for parity checks). Any pointer may be NULL. */
+int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t* cw_seed, uint8_t* cw_bits);
+
+/* ---- crawl ---------------------------------------------------------------------------- */
+
+/* tree_init (collect.rs:67-92) with eval_init per key (ibDCF.rs:229-236). */
+int fhh_tree_init(fhh_ctx* ctx);
+
+/* Frontier expansion of tree_crawl (collect.rs:379-418): evaluates every client's 2d keys
+ * one level for every child of every frontier node. *n_children = C. share_planes (may be
+ * NULL) receives [C][2d][nw] u64 — the GC input of collect.rs:415-418.
+ * If the previous crawl was not pruned, its children become the frontier (as
+ * `self.frontier = next_frontier`, collect.rs:505). */
+int fhh_tree_crawl(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes);
+/* tree_crawl_last (collect.rs:775-823): same expansion; children become frontier_last. */
+int fhh_tree_crawl_last(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes);
+
+/* Per-node sums of the OT outputs (collect.rs:487-501): vals [C][n] (client order),
+ * sums [C] canonical FE. */
+int fhh_node_sums_fe(fhh_ctx* ctx, const uint64_t* vals, uint64_t* sums);
+/* Last level (collect.rs:891-905) in FieldElm: vals [C][n][8] u32 little-endian limbs
+ * (< 2^256). sums_unreduced [C][10] u32 LE = the exact BigUint `add_lazy` sum
+ * (field.rs:337-339); sums_canonical [C][8] = mod 2^255-19. Either may be NULL. The sums
+ * become the frontier_last values (collect.rs:909-914). */
+int fhh_node_sums_fe255(fhh_ctx* ctx, const uint32_t* vals, uint32_t* sums_unreduced, uint32_t* sums_canonical);
+
+/* tree_prune (collect.rs:918-929) / tree_prune_last (collect.rs:931-942). */
+int fhh_tree_prune(fhh_ctx* ctx, const uint8_t* keep, uint64_t n);
+int fhh_tree_prune_last(fhh_ctx* ctx, const uint8_t* keep, uint64_t n);
+
+/* Current frontier size / frontier_last size. */
+int fhh_frontier_size(const fhh_ctx* ctx, uint64_t* n_frontier, uint64_t* n_frontier_last);
+
+/* final_shares (collect.rs:993-1005): paths [F][d][levels] (0/1) and values [F][10] u32
+ * (the unreduced FieldElm sum recorded by fhh_node_sums_fe255 / fhh_sim_ot_sums, zeros if
+ * none). *levels receives the path length. Pass NULL buffers to query F and levels. */
+int fhh_final_shares(fhh_ctx* ctx, uint64_t* n_final, uint32_t* levels, uint8_t* paths, uint32_t* values);
+
+/* Export the seeds/t/y of the current frontier's (or pending children's, if unpruned)
+ * evaluation states in reference layout [node][client][d][2] (seed 16 B, t, y): parity aid
+ * (EvalState, ibDCF.rs:24-30). Returns the node count in *n_nodes; NULL buffers = query. */
+int fhh_export_states(fhh_ctx* ctx, uint64_t* n_nodes, uint8_t* seeds, uint8_t* t, uint8_t* y);
+
+/* ---- leader-side helpers (pure host arithmetic) ----------------------------------------- */
+
+/* keep_values (collect.rs:945-964): v = v0 - v1 mod p_FE; keep iff v >= threshold. */
+int fhh_keep_values(uint64_t threshold, const uint64_t* vals0, const uint64_t* vals1, uint64_t n, uint8_t* keep);
+/* keep_values_last (collect.rs:966-989) on FE255 values given as [n][10] u32 LE limbs. */
+int fhh_keep_values_last(uint32_t threshold, const uint32_t* vals0, const uint32_t* vals1, uint64_t n, uint8_t* keep);
+/* final_values (collect.rs:1007-1029): out [n][8] canonical (v0 - v1 mod p255). */
+int fhh_final_values(const uint32_t* vals0, const uint32_t* vals1, uint64_t n, uint32_t* out);
+
+/* ---- in-process two-server harness ----------------------------------------------------- */
+/* The reference computes the "client inside node" bit with a garbled-circuit equality test
+ * + OT between the servers (equalitytest.rs:25-106, collect.rs:419-482) — out of scope.
+ * These entry points stand in for it when both servers' ctxs live in one process on the
+ * same GPU: plaintext equality of the two share strings (eq = mask ^ out), or simulated OT
+ * share values (r0 from a fixed PRF, r1 = r0 + 1; v0 = r1, v1 = eq ? r0 : r1). */
+
+/* counts [C]: clients whose two share strings are equal, per pending child. */
+int fhh_sim_eq_count(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t* counts);
+/* Simulated OT share sums. Non-last level: sums0/sums1 [C] canonical FE. After
+ * tree_crawl_last: [C][10] u32 unreduced FE255 (also recorded as frontier_last values). */
+int fhh_sim_ot_sums(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t prf_seed, void* sums0, void* sums1);
+
+/* All-reduce hook for client-sharded multi-GPU runs: called with a device buffer of
+ * `count` u64 partial sums (on the ctx's GPU, already complete); must sum it in place
+ * across ranks and return 0 once the result is visible to the device. */
+typedef int (*fhh_allreduce_fn)(uint64_t* buf_dev, uint64_t count, void* user);
+
+typedef struct fhh_sim_config {
+    double threshold;          /* fraction, leader.rs:193-194 / 245-246             */
+    uint64_t nclients_total;   /* nreqs (all ranks)                                   */
+    uint32_t mode;             /* 0 = eq count, 1 = simulated OT shares (FE / FE255) */
+    uint32_t levels;           /* 0 = data_len                                        */
+    uint64_t prf_seed;         /* mode 1                                              */
+    fhh_allreduce_fn allreduce;/* NULL on a single GPU                               */
+    void* allreduce_user;
+    uint64_t* xchg_dev;        /* device buffer handed to allreduce (>= capacity u64) */
+    uint64_t xchg_capacity;
+    /* optional per-level records (NULL to skip) */
+    uint64_t* level_children;  /* [levels] */
+    uint64_t* level_kept;      /* [levels] */
+    uint64_t* counts;          /* concatenated per-level child counts/values (mode 0) */
+    uint64_t counts_capacity;
+} fhh_sim_config;
+
+/* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x
+ * (crawl, count/sums, [allreduce], keep_values, prune), crawl_last, keep_values_last,
+ * prune_last. Heavy hitters are then read with fhh_final_shares(ctx0, ...). */
+int fhh_sim_crawl(fhh_ctx* ctx0, fhh_ctx* ctx1, const fhh_sim_config* cfg);
+
+/* ---- statistics ------------------------------------------------------------------------ */
+
+typedef struct fhh_stats {
+    uint64_t aes_blocks;        /* executed AES-128 blocks (eval_bit PRG calls)          */
+    uint64_t ref_evals;         /* reference-equivalent eval_bit calls (C * n * 2d)      */
+    uint64_t expand_launches;   /* k_expand launches                                     */
+    double expand_ms;           /* summed k_expand duration (HIP events on ctx stream)   */
+    uint64_t expand_blocks_timed; /* AES blocks covered by expand_ms                     */
+    uint64_t levels;            /* crawled levels                                        */
+    double keygen_ms;
+} fhh_stats;
+
+int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);
+int fhh_reset_stats(fhh_ctx* ctx);
+/* 1 to time every k_expand launch with HIP events (default 1). */
+int fhh_set_timing(fhh_ctx* ctx, int enabled);
+
+/* Peak-rate microbenchmarks pinning the roofline denominators on the running device:
+ * which = 0 -> v_xor_b32 lane-ops/s; which = 1 -> ds_read_b32 bytes/s (k_expand pattern). */
+int fhh_microbench(int device, int which, double* rate);
+
+/* Device properties the library targets (gfx950). */
+int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FHH_H */

@@ -1,0 +1,472 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the per-level client-key evaluation of
+ * sks-codes/fuzzyheavyhitters (Rust crate `counttree`, read-only at /root/reference).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library; the product library (fuzzyheavyhitters_amd/libfhh.so) never links it.
+ *
+ * The reference cannot be compiled here (Rust: no cargo/rustc, crates not vendored), so
+ * this file restates it. Parity is pinned by:
+ *   - FIPS-197 AES-128 known answers and OpenSSL's AES_encrypt (tests/test_oracle_kat.py),
+ *   - the ibDCF comparison semantics derived from the algebra, checked exhaustively,
+ *   - fastfield.rs's own known answers (FE tests, recip(999)).
+ * Every function cites the reference file:line it follows.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <omp.h>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#include <cpuid.h>
+#endif
+
+/* ------------------------------------------------------------------ */
+/* AES-128, portable byte-oriented FIPS-197 implementation.           */
+/* Third-party algorithm: crate `aes 0.4.0` / `aesni 0.7.0`           */
+/* (Cargo.lock:17-70), called at src/prg.rs:224 `encrypt_block`.      */
+/* ------------------------------------------------------------------ */
+
+static uint8_t g_sbox[256];
+static uint8_t g_rk0[176];          /* expanded zero key, src/prg.rs:185-197 */
+static int g_init = 0;
+
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    for (int i = 0; i < 8; i++) {
+        if (b & 1) p ^= a;
+        uint8_t hi = a & 0x80;
+        a <<= 1;
+        if (hi) a ^= 0x1b;
+        b >>= 1;
+    }
+    return p;
+}
+
+static uint8_t rotl8(uint8_t x, int s) { return (uint8_t)((x << s) | (x >> (8 - s))); }
+
+static void build_sbox(void) {
+    /* S(x) = affine(inverse(x)), FIPS-197 5.1.1 */
+    for (int x = 0; x < 256; x++) {
+        uint8_t inv = 0;
+        if (x) {
+            for (int y = 1; y < 256; y++)
+                if (gf_mul((uint8_t)x, (uint8_t)y) == 1) { inv = (uint8_t)y; break; }
+        }
+        uint8_t s = inv ^ rotl8(inv, 1) ^ rotl8(inv, 2) ^ rotl8(inv, 3) ^ rotl8(inv, 4) ^ 0x63;
+        g_sbox[x] = s;
+    }
+}
+
+static void key_expand(const uint8_t key[16], uint8_t rk[176]) {
+    memcpy(rk, key, 16);
+    uint8_t rcon = 1;
+    for (int i = 4; i < 44; i++) {
+        uint8_t t[4];
+        memcpy(t, rk + 4 * (i - 1), 4);
+        if (i % 4 == 0) {
+            uint8_t u = t[0];
+            t[0] = g_sbox[t[1]] ^ rcon;
+            t[1] = g_sbox[t[2]];
+            t[2] = g_sbox[t[3]];
+            t[3] = g_sbox[u];
+            rcon = gf_mul(rcon, 2);
+        }
+        for (int k = 0; k < 4; k++) rk[4 * i + k] = rk[4 * (i - 4) + k] ^ t[k];
+    }
+}
+
+static void oracle_init(void) {
+    if (g_init) return;
+#pragma omp critical(fhh_oracle_init)
+    {
+        if (!g_init) {
+            uint8_t zero[16] = {0};
+            build_sbox();
+            key_expand(zero, g_rk0);
+            __atomic_store_n(&g_init, 1, __ATOMIC_RELEASE);
+        }
+    }
+}
+
+static void aes128_encrypt_rk(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) {
+    uint8_t s[16];
+    for (int i = 0; i < 16; i++) s[i] = in[i] ^ rk[i];
+    for (int round = 1; round <= 10; round++) {
+        uint8_t t[16];
+        /* SubBytes + ShiftRows: state byte (r,c) lives at s[4c+r] */
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++)
+                t[4 * c + r] = g_sbox[s[4 * ((c + r) & 3) + r]];
+        if (round != 10) {
+            for (int c = 0; c < 4; c++) {
+                uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                s[4 * c + 0] = gf_mul(a0, 2) ^ gf_mul(a1, 3) ^ a2 ^ a3;
+                s[4 * c + 1] = a0 ^ gf_mul(a1, 2) ^ gf_mul(a2, 3) ^ a3;
+                s[4 * c + 2] = a0 ^ a1 ^ gf_mul(a2, 2) ^ gf_mul(a3, 3);
+                s[4 * c + 3] = gf_mul(a0, 3) ^ a1 ^ a2 ^ gf_mul(a3, 2);
+            }
+        } else {
+            memcpy(s, t, 16);
+        }
+        for (int i = 0; i < 16; i++) s[i] ^= rk[16 * round + i];
+    }
+    memcpy(out, s, 16);
+}
+
+void orc_aes128_encrypt(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+    oracle_init();
+    uint8_t rk[176];
+    key_expand(key, rk);
+    aes128_encrypt_rk(rk, in, out);
+}
+
+/* AES-128 with the fixed all-zero key (src/prg.rs:185-197 `FixedKeyPrgStream::new`). */
+void orc_aes128_zero_encrypt(const uint8_t in[16], uint8_t out[16]) {
+    oracle_init();
+    aes128_encrypt_rk(g_rk0, in, out);
+}
+
+void orc_sbox(uint8_t out[256]) {
+    oracle_init();
+    memcpy(out, g_sbox, 256);
+}
+
+void orc_zero_round_keys(uint8_t out[176]) {
+    oracle_init();
+    memcpy(out, g_rk0, 176);
+}
+
+/* ---------------- AES-NI path (CPU baseline speed) ---------------- */
+#if defined(__x86_64__)
+static __m128i g_ni_rk[11];
+static int g_ni_ready = 0;
+
+int orc_aes_ni_available(void) {
+    unsigned a, b, c, d;
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return 0;
+    return (c & bit_AES) ? 1 : 0;
+}
+
+__attribute__((target("aes,sse4.1"))) static void ni_prepare(void) {
+    oracle_init();
+    for (int i = 0; i < 11; i++) g_ni_rk[i] = _mm_loadu_si128((const __m128i*)(g_rk0 + 16 * i));
+    g_ni_ready = 1;
+}
+
+/* One non-pipelined AES-NI block, like the reference's single-block `encrypt_block`. */
+__attribute__((target("aes,sse4.1"))) static inline __m128i ni_aes0(__m128i x) {
+    x = _mm_xor_si128(x, g_ni_rk[0]);
+    x = _mm_aesenc_si128(x, g_ni_rk[1]);
+    x = _mm_aesenc_si128(x, g_ni_rk[2]);
+    x = _mm_aesenc_si128(x, g_ni_rk[3]);
+    x = _mm_aesenc_si128(x, g_ni_rk[4]);
+    x = _mm_aesenc_si128(x, g_ni_rk[5]);
+    x = _mm_aesenc_si128(x, g_ni_rk[6]);
+    x = _mm_aesenc_si128(x, g_ni_rk[7]);
+    x = _mm_aesenc_si128(x, g_ni_rk[8]);
+    x = _mm_aesenc_si128(x, g_ni_rk[9]);
+    return _mm_aesenclast_si128(x, g_ni_rk[10]);
+}
+
+__attribute__((target("aes,sse4.1"))) void orc_aes128_zero_encrypt_ni(const uint8_t in[16], uint8_t out[16]) {
+    if (!g_ni_ready) ni_prepare();
+    __m128i x = _mm_loadu_si128((const __m128i*)in);
+    _mm_storeu_si128((__m128i*)out, ni_aes0(x));
+}
+#else
+int orc_aes_ni_available(void) { return 0; }
+void orc_aes128_zero_encrypt_ni(const uint8_t in[16], uint8_t out[16]) { orc_aes128_zero_encrypt(in, out); }
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Fixed-key PRG (src/prg.rs)                                          */
+/* ------------------------------------------------------------------ */
+
+/* `inc_be` (src/prg.rs:273-276): _mm_add_epi64(v, _mm_set_epi64x(1, 0)) adds 1 to the
+ * UPPER 64-bit lane (bytes 8..15 as a little-endian u64), no carry into bytes 0..7. */
+static void ctr_inc(uint8_t k[16]) {
+    uint64_t hi;
+    memcpy(&hi, k + 8, 8);
+    hi += 1;
+    memcpy(k + 8, &hi, 8);
+}
+
+/* MMO block: `refill` (src/prg.rs:212-234) = AES_0(ctr) XOR ctr. */
+static void mmo(const uint8_t ctr[16], uint8_t out[16], int use_ni) {
+    uint8_t e[16];
+    if (use_ni) orc_aes128_zero_encrypt_ni(ctr, e);
+    else aes128_encrypt_rk(g_rk0, ctr, e);
+    for (int i = 0; i < 16; i++) out[i] = e[i] ^ ctr[i];
+}
+
+/* `PrgSeed::expand_dir(!dir, dir)` (src/prg.rs:92-122) as called by eval_bit: only the
+ * requested side is encrypted, the other is `skip_block`ed. bits4 receives
+ * (bits.0, bits.1, y_bits.0, y_bits.1) read from the MASKED byte 0 (prg.rs:96-105). */
+static void expand_dir_impl(const uint8_t seed[16], int dir, uint8_t out[16], uint8_t bits4[4], int use_ni) {
+    uint8_t k[16];
+    memcpy(k, seed, 16);
+    k[0] &= 0xF0;                               /* prg.rs:96 */
+    bits4[0] = (k[0] & 0x1) == 0;               /* prg.rs:102 */
+    bits4[1] = (k[0] & 0x2) == 0;
+    bits4[2] = (k[0] & 0x4) == 0;               /* prg.rs:103 */
+    bits4[3] = (k[0] & 0x8) == 0;
+    if (dir) ctr_inc(k);                        /* left block skipped: skip_block, prg.rs:205-210 */
+    mmo(k, out, use_ni);
+}
+
+void orc_expand_dir(const uint8_t seed[16], int dir, uint8_t out[16], uint8_t bits4[4]) {
+    oracle_init();
+    expand_dir_impl(seed, dir, out, bits4, 0);
+}
+
+/* `PrgSeed::expand` (src/prg.rs:124-126): both children. */
+static void expand_both(const uint8_t seed[16], uint8_t left[16], uint8_t right[16], uint8_t bits4[4], int use_ni) {
+    expand_dir_impl(seed, 0, left, bits4, use_ni);
+    expand_dir_impl(seed, 1, right, bits4, use_ni);
+}
+
+/* ------------------------------------------------------------------ */
+/* ibDCF (src/ibDCF.rs)                                                */
+/* cw_bits nibble: bit0 = bits.0, bit1 = bits.1, bit2 = y_bits.0, bit3 = y_bits.1    */
+/* ------------------------------------------------------------------ */
+
+/* `gen_ibDCF` (ibDCF.rs:138-164) with `gen_cor_word` (ibDCF.rs:84-119). Root seeds are
+ * caller-provided (the reference draws them from thread_rng, prg.rs:153-158). */
+static void gen_ibdcf_impl(const uint8_t* alpha, uint32_t L, int side, const uint8_t root0[16],
+                           const uint8_t root1[16], uint8_t* cw_seed, uint8_t* cw_bits, int use_ni) {
+    uint8_t seeds[2][16];
+    int bits[2] = {0, 1};                       /* root_bits = (false, true), ibDCF.rs:140 */
+    memcpy(seeds[0], root0, 16);
+    memcpy(seeds[1], root1, 16);
+    for (uint32_t l = 0; l < L; l++) {
+        int bit = alpha[l] ? 1 : 0;
+        uint8_t ds[2][2][16];                   /* data[b].seeds.{0,1} */
+        uint8_t db[2][4];                       /* data[b].bits / y_bits */
+        for (int b = 0; b < 2; b++) expand_both(seeds[b], ds[b][0], ds[b][1], db[b], use_ni);
+        int keep = bit, lose = !bit;
+        uint8_t cws[16];
+        for (int i = 0; i < 16; i++) cws[i] = ds[0][lose][i] ^ ds[1][lose][i];          /* :91 */
+        int cb0 = db[0][0] ^ db[1][0] ^ bit ^ 1;                                          /* :93 */
+        int cb1 = db[0][1] ^ db[1][1] ^ bit;                                              /* :94 */
+        int cy0 = db[0][2] ^ db[1][2] ^ (bit & !side);                                    /* :97 */
+        int cy1 = db[0][3] ^ db[1][3] ^ ((!bit) & side);                                  /* :98 */
+        int cwb[2] = {cb0, cb1};
+        for (int b = 0; b < 2; b++) {                                                     /* :103-116 */
+            memcpy(seeds[b], ds[b][keep], 16);
+            if (bits[b])
+                for (int i = 0; i < 16; i++) seeds[b][i] ^= cws[i];
+            int nb = db[b][keep];
+            if (bits[b]) nb ^= cwb[keep];
+            bits[b] = nb;
+        }
+        memcpy(cw_seed + 16 * (size_t)l, cws, 16);
+        cw_bits[l] = (uint8_t)(cb0 | (cb1 << 1) | (cy0 << 2) | (cy1 << 3));
+    }
+}
+
+void orc_gen_ibdcf(const uint8_t* alpha, uint32_t L, int side, const uint8_t root0[16],
+                   const uint8_t root1[16], uint8_t* cw_seed, uint8_t* cw_bits) {
+    oracle_init();
+    gen_ibdcf_impl(alpha, L, side, root0, root1, cw_seed, cw_bits, 0);
+}
+
+/* Batched interval keygen, `gen_interval` (ibDCF.rs:166-173) per dim: left key =
+ * gen_ibDCF(l, side=true), right key = gen_ibDCF(r, side=false); both servers' keys share
+ * cor_words (ibDCF.rs:152-163), so cw arrays are produced once.
+ *   left_bits/right_bits: [n][d][L] (0/1)
+ *   root_seeds: [n][d][2 side][2 server][16]
+ *   cw_seed out: [n][d][2 side][L][16], cw_bits out: [n][d][2 side][L]            */
+void orc_gen_keys(uint64_t n, uint32_t d, uint32_t L, const uint8_t* left_bits, const uint8_t* right_bits,
+                  const uint8_t* root_seeds, uint8_t* cw_seed, uint8_t* cw_bits, int nthreads) {
+    oracle_init();
+    int ni = orc_aes_ni_available();
+#if defined(__x86_64__)
+    if (ni && !g_ni_ready) ni_prepare();
+#endif
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+    for (int64_t c = 0; c < (int64_t)n; c++) {
+        for (uint32_t j = 0; j < d; j++) {
+            for (int s = 0; s < 2; s++) {
+                const uint8_t* alpha = (s == 0 ? left_bits : right_bits) + ((size_t)c * d + j) * L;
+                const uint8_t* rs = root_seeds + (((size_t)c * d + j) * 2 + s) * 32;
+                size_t key = ((size_t)c * d + j) * 2 + s;
+                gen_ibdcf_impl(alpha, L, s == 0 ? 1 : 0, rs, rs + 16, cw_seed + key * L * 16,
+                               cw_bits + key * L, ni);
+            }
+        }
+    }
+}
+
+/* `eval_bit` (ibDCF.rs:208-227). */
+static inline void eval_bit_impl(const uint8_t seed[16], int t, int y, const uint8_t cws[16], uint8_t cwb,
+                                 int dir, uint8_t out[16], uint8_t* t_out, uint8_t* y_out, int use_ni) {
+    uint8_t b4[4];
+    expand_dir_impl(seed, dir, out, b4, use_ni);   /* tau = expand_dir(!dir, dir) */
+    int nb = b4[dir];                              /* tau.bits.get(dir) */
+    int ny = b4[2 + dir];                          /* tau.y_bits.get(dir) */
+    if (t) {
+        for (int i = 0; i < 16; i++) out[i] ^= cws[i];
+        nb ^= (cwb >> dir) & 1;
+        ny ^= (cwb >> (2 + dir)) & 1;
+    }
+    ny ^= y;
+    *t_out = (uint8_t)nb;
+    *y_out = (uint8_t)ny;
+}
+
+void orc_eval_bit(const uint8_t seed[16], int t, int y, const uint8_t cw_seed[16], uint8_t cw_bits, int dir,
+                  uint8_t out_seed[16], uint8_t* t_out, uint8_t* y_out) {
+    oracle_init();
+    eval_bit_impl(seed, t, y, cw_seed, cw_bits, dir, out_seed, t_out, y_out, 0);
+}
+
+/* ------------------------------------------------------------------ */
+/* Collection engine (src/collect.rs), reference child order.          */
+/* State arrays are node-major: [node][client][dim][side] -> seed(16), t, y.        */
+/* ------------------------------------------------------------------ */
+
+/* `tree_init` (collect.rs:67-92) + `eval_init` (ibDCF.rs:229-236):
+ * key_idx [n][d][2], root_seed [n][d][2][16]. Output node 0. */
+void orc_tree_init(uint64_t n, uint32_t d, const uint8_t* key_idx, const uint8_t* root_seed,
+                   uint8_t* seeds, uint8_t* t, uint8_t* y) {
+    size_t K = (size_t)n * d * 2;
+    memcpy(seeds, root_seed, K * 16);
+    for (size_t k = 0; k < K; k++) {
+        t[k] = key_idx[k] ? 1 : 0;
+        y[k] = key_idx[k] ? 1 : 0;
+    }
+}
+
+/* One crawl level, `tree_crawl` frontier expansion (collect.rs:379-391) +
+ * `make_tree_node` (collect.rs:94-119) + `eval_str` (ibDCF.rs:120-131).
+ * Children are ordered by parent, then by i in `all_bit_vectors(d)` (lib.rs:125-129):
+ * child i takes direction (i >> j) & 1 in dim j.
+ *   cw_seed [n][d][2][L][16], cw_bits [n][d][2][L]
+ *   parent_idx[F]: rows of the input state arrays that form the frontier (after prune)
+ *   out arrays hold F * 2^d nodes.  Returns the number of AES blocks executed. */
+uint64_t orc_level_expand(uint64_t n, uint32_t d, uint32_t L, uint32_t level, const uint8_t* cw_seed,
+                          const uint8_t* cw_bits, uint64_t F, const uint64_t* parent_idx,
+                          const uint8_t* in_seed, const uint8_t* in_t, const uint8_t* in_y,
+                          uint8_t* out_seed, uint8_t* out_t, uint8_t* out_y, int nthreads, int use_ni) {
+    oracle_init();
+#if defined(__x86_64__)
+    if (use_ni && !orc_aes_ni_available()) use_ni = 0;
+    if (use_ni && !g_ni_ready) ni_prepare();
+#else
+    use_ni = 0;
+#endif
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    const uint32_t nch = 1u << d;
+    const size_t per_node = (size_t)n * d * 2;
+    for (uint64_t p = 0; p < F; p++) {
+        const size_t src = (size_t)parent_idx[p];
+        for (uint32_t i = 0; i < nch; i++) {
+            const size_t dst = (size_t)p * nch + i;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+            for (int64_t c = 0; c < (int64_t)n; c++) {
+                for (uint32_t j = 0; j < d; j++) {
+                    int dir = (i >> j) & 1;
+                    for (int s = 0; s < 2; s++) {
+                        size_t key = ((size_t)c * d + j) * 2 + s;
+                        size_t si = src * per_node + key, di = dst * per_node + key;
+                        eval_bit_impl(in_seed + si * 16, in_t[si], in_y[si], cw_seed + (key * L + level) * 16,
+                                      cw_bits[key * L + level], dir, out_seed + di * 16, out_t + di, out_y + di,
+                                      use_ni);
+                    }
+                }
+            }
+        }
+    }
+    return (uint64_t)F * nch * n * d * 2;
+}
+
+/* Share strings (collect.rs:393-418): per (child, client), [left.y^left.t for each dim]
+ * then [right.y^right.t for each dim]. out [C][n][2d]. */
+void orc_share_bits(uint64_t C, uint64_t n, uint32_t d, const uint8_t* t, const uint8_t* y, uint8_t* out) {
+    for (uint64_t c = 0; c < C; c++)
+        for (uint64_t i = 0; i < n; i++)
+            for (int s = 0; s < 2; s++)
+                for (uint32_t j = 0; j < d; j++) {
+                    size_t k = ((c * n + i) * d + j) * 2 + s;
+                    out[(c * n + i) * 2 * d + (size_t)s * d + j] = t[k] ^ y[k];
+                }
+}
+
+/* Plaintext stand-in for the GC equality test (equalitytest.rs:25-106): count, per child,
+ * the clients whose two servers' share strings are equal (eq = mask ^ out, collect.rs:439-472). */
+void orc_eq_count(uint64_t C, uint64_t n, uint32_t d, const uint8_t* t0, const uint8_t* y0, const uint8_t* t1,
+                  const uint8_t* y1, uint64_t* counts) {
+    const size_t per = (size_t)n * d * 2;
+    for (uint64_t c = 0; c < C; c++) {
+        uint64_t cnt = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            int eq = 1;
+            for (size_t k = 0; k < (size_t)d * 2; k++) {
+                size_t idx = c * per + i * d * 2 + k;
+                if ((t0[idx] ^ y0[idx]) != (t1[idx] ^ y1[idx])) { eq = 0; break; }
+            }
+            cnt += (uint64_t)eq;
+        }
+        counts[c] = cnt;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* FE, p = 2^62 - 2^30 - 1 (src/fastfield.rs)                          */
+/* ------------------------------------------------------------------ */
+#define FE_NBITS 62
+#define FE_OFFSET 30
+#define FE_P ((((uint64_t)1) << FE_NBITS) - (((uint64_t)1) << FE_OFFSET) - 1)
+#define FE_MASK ((((uint64_t)1) << FE_NBITS) - 1)
+
+uint64_t orc_fe_bit_reduce_once(uint64_t v) {       /* fastfield.rs:86-95 */
+    uint64_t excess = v >> FE_NBITS;
+    uint64_t low = v & FE_MASK;
+    return low + excess + (excess << FE_OFFSET);
+}
+static uint64_t fe_reduce_by_p(uint64_t v) {        /* fastfield.rs:100-107 */
+    uint64_t diff = v - FE_P;
+    uint64_t mask = (uint64_t)(((int64_t)(diff & ((uint64_t)1 << 63))) >> 63);
+    return (mask & v) | (~mask & diff);
+}
+uint64_t orc_fe_new(uint64_t v) { return orc_fe_bit_reduce_once(v); }                       /* :112-118 */
+uint64_t orc_fe_value(uint64_t val) { return fe_reduce_by_p(orc_fe_bit_reduce_once(val)); } /* :147-152 */
+uint64_t orc_fe_add(uint64_t a, uint64_t b) { return orc_fe_new(a + b); }                   /* :226-233 */
+uint64_t orc_fe_neg(uint64_t a) { return orc_fe_new(FE_P * 2 - a); }                        /* :235-242 */
+uint64_t orc_fe_sub(uint64_t a, uint64_t b) { return orc_fe_add(a, orc_fe_neg(b)); }        /* :244-249 */
+uint64_t orc_fe_mul(uint64_t a, uint64_t b) {                                               /* :299-328 */
+    unsigned __int128 prod = (unsigned __int128)a * b;
+    for (int r = 0; r < 2; r++) {
+        unsigned __int128 low = prod & FE_MASK;
+        unsigned __int128 high = prod >> FE_NBITS;
+        prod = low + (high << FE_OFFSET) + high;
+    }
+    return orc_fe_new((uint64_t)prod);
+}
+
+/* Node sum with `add_lazy` = `add` for FE (field.rs:219-222; collect.rs:487-501), folded
+ * in client order. Returns the internal (bit-reduced-once) val; compare value(). */
+uint64_t orc_fe_fold_sum(const uint64_t* vals, uint64_t n) {
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; i++) acc = orc_fe_add(acc, orc_fe_new(vals[i]));
+    return acc;
+}
+
+/* ------------------------------------------------------------------ */
+/* Simulated OT share values (harness-defined).         */
+/* The real values come from ALSZ OT (collect.rs:439-472); the        */
+/* reference draws r0 from thread_rng, so any fixed PRF is as faithful. */
+/* ------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+uint64_t orc_sim_prf(uint64_t seed, uint64_t level, uint64_t child, uint64_t client, uint32_t word) {
+    return mix64(mix64(mix64(mix64(seed ^ level) ^ child) ^ client) ^ word);
+}

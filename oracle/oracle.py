@@ -1,0 +1,480 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Python side of the CPU restatement of sks-codes/fuzzyheavyhitters' per-level client-key
+evaluation (reference: Rust crate `counttree`, /root/reference, not compilable here).
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import
+this module; the product package never does.
+
+Parity anchors (see tests/test_oracle_kat.py):
+  * AES-128: FIPS-197 appendix C.1 vector + zero-key vector, and OpenSSL ``AES_encrypt``.
+  * FE (fastfield.rs): the reference's own known answers (fastfield.rs:459-559).
+  * ibDCF: comparison semantics derived from ibDCF.rs:84-119,208-227, checked exhaustively.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def build() -> str:
+    """Compile liboracle.so (Makefile in this directory)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return os.path.join(_HERE, "liboracle.so")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.orc_level_expand.restype = ctypes.c_uint64
+        L.orc_fe_new.restype = ctypes.c_uint64
+        L.orc_fe_new.argtypes = [ctypes.c_uint64]
+        L.orc_fe_value.restype = ctypes.c_uint64
+        L.orc_fe_value.argtypes = [ctypes.c_uint64]
+        for nm in ("orc_fe_add", "orc_fe_sub", "orc_fe_mul"):
+            getattr(L, nm).restype = ctypes.c_uint64
+            getattr(L, nm).argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_fe_neg.restype = ctypes.c_uint64
+        L.orc_fe_neg.argtypes = [ctypes.c_uint64]
+        L.orc_fe_fold_sum.restype = ctypes.c_uint64
+        L.orc_sim_prf.restype = ctypes.c_uint64
+        L.orc_sim_prf.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_uint32]
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray, t=u8p):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(t)
+
+
+# --------------------------------------------------------------------------------------
+# AES / PRG / ibDCF
+# --------------------------------------------------------------------------------------
+
+def aes128_encrypt(key: bytes, block: bytes) -> bytes:
+    k = np.frombuffer(key, np.uint8).copy()
+    i = np.frombuffer(block, np.uint8).copy()
+    o = np.zeros(16, np.uint8)
+    lib().orc_aes128_encrypt(_p(k), _p(i), _p(o))
+    return o.tobytes()
+
+
+def aes0(block: bytes, ni: bool = False) -> bytes:
+    i = np.frombuffer(block, np.uint8).copy()
+    o = np.zeros(16, np.uint8)
+    (lib().orc_aes128_zero_encrypt_ni if ni else lib().orc_aes128_zero_encrypt)(_p(i), _p(o))
+    return o.tobytes()
+
+
+def aes_ni_available() -> bool:
+    return bool(lib().orc_aes_ni_available())
+
+
+def sbox() -> np.ndarray:
+    o = np.zeros(256, np.uint8)
+    lib().orc_sbox(_p(o))
+    return o
+
+
+def zero_round_keys() -> np.ndarray:
+    o = np.zeros(176, np.uint8)
+    lib().orc_zero_round_keys(_p(o))
+    return o
+
+
+def expand_dir(seed: bytes, direction: int):
+    """prg.rs:92-122 (as called from eval_bit). Returns (child_seed, (b0,b1,y0,y1))."""
+    s = np.frombuffer(seed, np.uint8).copy()
+    o = np.zeros(16, np.uint8)
+    b = np.zeros(4, np.uint8)
+    lib().orc_expand_dir(_p(s), ctypes.c_int(direction), _p(o), _p(b))
+    return o.tobytes(), tuple(int(x) for x in b)
+
+
+def gen_ibdcf(alpha_bits, side: bool, root0: bytes, root1: bytes):
+    """ibDCF.rs:138-164. Returns (cw_seed [L][16] u8, cw_bits [L] nibble)."""
+    a = np.asarray(alpha_bits, np.uint8).copy()
+    L = a.size
+    r0 = np.frombuffer(root0, np.uint8).copy()
+    r1 = np.frombuffer(root1, np.uint8).copy()
+    cs = np.zeros((L, 16), np.uint8)
+    cb = np.zeros(L, np.uint8)
+    lib().orc_gen_ibdcf(_p(a), ctypes.c_uint32(L), ctypes.c_int(int(side)), _p(r0), _p(r1), _p(cs), _p(cb))
+    return cs, cb
+
+
+def eval_bit(seed: bytes, t: int, y: int, cw_seed: bytes, cw_bits: int, direction: int):
+    """ibDCF.rs:208-227."""
+    s = np.frombuffer(seed, np.uint8).copy()
+    c = np.frombuffer(cw_seed, np.uint8).copy()
+    o = np.zeros(16, np.uint8)
+    to = ctypes.c_uint8()
+    yo = ctypes.c_uint8()
+    lib().orc_eval_bit(_p(s), ctypes.c_int(t), ctypes.c_int(y), _p(c), ctypes.c_uint8(cw_bits),
+                       ctypes.c_int(direction), _p(o), ctypes.byref(to), ctypes.byref(yo))
+    return o.tobytes(), to.value, yo.value
+
+
+def eval_ibdcf(key_idx: int, root_seed: bytes, cw_seed, cw_bits, idx_bits):
+    """ibDCF.rs:238-250: returns y_bit ^ bit after evaluating the prefix idx_bits."""
+    seed, t, y = root_seed, key_idx, key_idx
+    for lvl, b in enumerate(idx_bits):
+        seed, t, y = eval_bit(seed, t, y, bytes(cw_seed[lvl]), int(cw_bits[lvl]), int(b))
+    return y ^ t
+
+
+@dataclass
+class ServerKeys:
+    """One server's keys, client-major then dim then (left,right) — the order of
+    ``add_key(Vec<(ibDCFKey, ibDCFKey)>)`` (collect.rs:62)."""
+    key_idx: np.ndarray   # [n][d][2] u8
+    root_seed: np.ndarray  # [n][d][2][16] u8
+    cw_seed: np.ndarray    # [n][d][2][L][16] u8 (shared by both servers)
+    cw_bits: np.ndarray    # [n][d][2][L] u8 nibble
+
+    @property
+    def n(self):
+        return self.key_idx.shape[0]
+
+
+def gen_keys(left_bits: np.ndarray, right_bits: np.ndarray, root_seeds: np.ndarray, nthreads: int = 0):
+    """Batched ``gen_interval`` per (client, dim) — ibDCF.rs:166-173.
+
+    left_bits/right_bits: [n][d][L] (0/1); root_seeds: [n][d][2 side][2 server][16].
+    Returns (ServerKeys server0, ServerKeys server1)."""
+    n, d, L = left_bits.shape
+    lb = np.ascontiguousarray(left_bits, np.uint8)
+    rb = np.ascontiguousarray(right_bits, np.uint8)
+    rs = np.ascontiguousarray(root_seeds, np.uint8)
+    cws = np.zeros((n, d, 2, L, 16), np.uint8)
+    cwb = np.zeros((n, d, 2, L), np.uint8)
+    lib().orc_gen_keys(ctypes.c_uint64(n), ctypes.c_uint32(d), ctypes.c_uint32(L), _p(lb), _p(rb), _p(rs),
+                       _p(cws), _p(cwb), ctypes.c_int(nthreads))
+    k0 = ServerKeys(np.zeros((n, d, 2), np.uint8), np.ascontiguousarray(rs[:, :, :, 0, :]), cws, cwb)
+    k1 = ServerKeys(np.ones((n, d, 2), np.uint8), np.ascontiguousarray(rs[:, :, :, 1, :]), cws, cwb)
+    return k0, k1
+
+
+# --------------------------------------------------------------------------------------
+# Collection engine restatement (collect.rs), reference order, no dedup.
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class States:
+    seed: np.ndarray  # [F][n][d][2][16]
+    t: np.ndarray     # [F][n][d][2]
+    y: np.ndarray
+
+
+def tree_init(keys: ServerKeys) -> States:
+    n, d = keys.key_idx.shape[:2]
+    seed = np.zeros((1, n, d, 2, 16), np.uint8)
+    t = np.zeros((1, n, d, 2), np.uint8)
+    y = np.zeros((1, n, d, 2), np.uint8)
+    lib().orc_tree_init(ctypes.c_uint64(n), ctypes.c_uint32(d), _p(np.ascontiguousarray(keys.key_idx)),
+                        _p(np.ascontiguousarray(keys.root_seed)), _p(seed), _p(t), _p(y))
+    return States(seed, t, y)
+
+
+def level_expand(keys: ServerKeys, st: States, parent_idx, level: int, nthreads: int = 0, use_ni: bool = True):
+    """collect.rs:379-391 for one server. Returns (States of F*2^d children, aes_blocks)."""
+    n, d, _, L = keys.cw_bits.shape
+    pidx = np.ascontiguousarray(np.asarray(parent_idx, np.uint64))
+    F = pidx.size
+    C = F << d
+    out = States(np.zeros((C, n, d, 2, 16), np.uint8), np.zeros((C, n, d, 2), np.uint8),
+                 np.zeros((C, n, d, 2), np.uint8))
+    blocks = lib().orc_level_expand(
+        ctypes.c_uint64(n), ctypes.c_uint32(d), ctypes.c_uint32(L), ctypes.c_uint32(level),
+        _p(keys.cw_seed), _p(keys.cw_bits), ctypes.c_uint64(F), _p(pidx, u64p),
+        _p(st.seed), _p(st.t), _p(st.y), _p(out.seed), _p(out.t), _p(out.y),
+        ctypes.c_int(nthreads), ctypes.c_int(int(use_ni)))
+    return out, int(blocks)
+
+
+def share_bits(st: States) -> np.ndarray:
+    """collect.rs:393-418: [C][n][2d], left dims then right dims."""
+    e = st.t ^ st.y                       # [C][n][d][2]
+    return np.ascontiguousarray(np.concatenate([e[..., 0], e[..., 1]], axis=-1))
+
+
+def eq_counts(s0: States, s1: States) -> np.ndarray:
+    e0 = share_bits(s0)
+    e1 = share_bits(s1)
+    return np.all(e0 == e1, axis=-1).sum(axis=1).astype(np.uint64)
+
+
+# --------------------------------------------------------------------------------------
+# Fields (fastfield.rs / field.rs) — exact Python-int restatements.
+# --------------------------------------------------------------------------------------
+FE_P = (1 << 62) - (1 << 30) - 1           # fastfield.rs:24-28
+FE255_P = (1 << 255) - 19                  # field.rs:19 (MODULUS_STR)
+FE_MASK = (1 << 62) - 1
+
+
+def fe_new(v: int) -> int:                 # internal (bit-reduced-once) val
+    return int(lib().orc_fe_new(v & ((1 << 64) - 1)))
+
+
+def fe_value(val: int) -> int:
+    return int(lib().orc_fe_value(val))
+
+
+def fe_fold_sum(vals: np.ndarray) -> int:
+    """collect.rs:487-501 with FE add_lazy (field.rs:219-222): internal val."""
+    v = np.ascontiguousarray(vals, np.uint64)
+    return int(lib().orc_fe_fold_sum(_p(v, u64p), ctypes.c_uint64(v.size)))
+
+
+def _mix64(z):
+    z = (z + np.uint64(0x9E3779B97F4A7C15))
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def sim_prf(seed: int, level: int, child, client, word: int):
+    """Harness-defined PRF for simulated OT shares (vectorised over child/client)."""
+    with np.errstate(over="ignore"):
+        a = _mix64(np.uint64(seed) ^ np.uint64(level))
+        b = _mix64(a ^ np.asarray(child, np.uint64))
+        c = _mix64(b ^ np.asarray(client, np.uint64))
+        return _mix64(c ^ np.uint64(word))
+
+
+def sim_r0_fe(seed: int, level: int, C: int, n: int) -> np.ndarray:
+    """r0 per (child, client), canonical FE: prf & (2^62-1), minus p if >= p."""
+    ch = np.arange(C, dtype=np.uint64)[:, None]
+    cl = np.arange(n, dtype=np.uint64)[None, :]
+    r = sim_prf(seed, level, ch, cl, 0) & np.uint64(FE_MASK)
+    return np.where(r >= np.uint64(FE_P), r - np.uint64(FE_P), r)
+
+
+def sim_r0_fe255(seed: int, level: int, C: int, n: int):
+    """r0 per (child, client) as Python ints < p255 (4 prf words, LE, masked to 255 bits)."""
+    ch = np.arange(C, dtype=np.uint64)[:, None]
+    cl = np.arange(n, dtype=np.uint64)[None, :]
+    words = [sim_prf(seed, level, ch, cl, w) for w in range(4)]
+    out = np.empty((C, n), dtype=object)
+    for c in range(C):
+        for i in range(n):
+            v = sum(int(words[w][c, i]) << (64 * w) for w in range(4)) & ((1 << 255) - 1)
+            out[c, i] = v - FE255_P if v >= FE255_P else v
+    return out
+
+
+def sim_ot_sums_fe(eq: np.ndarray, seed: int, level: int):
+    """Server sums of simulated OT outputs (collect.rs:439-501): v0 = r1 = r0+1,
+    v1 = r0 if eq else r1. Returns canonical (sum0, sum1) per child."""
+    C, n = eq.shape
+    r0 = sim_r0_fe(seed, level, C, n)
+    s0, s1 = [], []
+    for c in range(C):
+        r0c = [int(x) for x in r0[c]]
+        r1c = [(x + 1) % FE_P for x in r0c]
+        s0.append(sum(r1c) % FE_P)
+        s1.append(sum(r0c[i] if eq[c, i] else r1c[i] for i in range(n)) % FE_P)
+    return s0, s1
+
+
+def sim_ot_sums_fe255(eq: np.ndarray, seed: int, level: int):
+    """As sim_ot_sums_fe for FieldElm; returns the UNREDUCED sums (add_lazy, field.rs:337-339)."""
+    C, n = eq.shape
+    r0 = sim_r0_fe255(seed, level, C, n)
+    s0, s1 = [], []
+    for c in range(C):
+        r0c = list(r0[c])
+        r1c = [(x + 1) % FE255_P for x in r0c]
+        s0.append(sum(r1c))
+        s1.append(sum(r0c[i] if eq[c, i] else r1c[i] for i in range(n)))
+    return s0, s1
+
+
+def keep_values(threshold: int, v0, v1, p=FE_P):
+    """collect.rs:945-964 / 966-989: v = v0 - v1 mod p, keep iff v >= threshold."""
+    return [((a % p) - (b % p)) % p >= threshold for a, b in zip(v0, v1)]
+
+
+# --------------------------------------------------------------------------------------
+# In-process two-server crawl (leader.rs:417-440 level loop), GC/OT replaced by plaintext
+# equality (mode "count") or simulated OT shares (mode "fe").
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class CrawlResult:
+    n_children: list = field(default_factory=list)  # per level
+    counts: list = field(default_factory=list)      # per level: np.ndarray[C]
+    keeps: list = field(default_factory=list)       # per level: np.ndarray[C] bool
+    sums: list = field(default_factory=list)        # per level (fe mode): (s0, s1)
+    final_paths: list = field(default_factory=list)  # [(tuple of d bit-tuples)]
+    final_values: list = field(default_factory=list)
+    aes_blocks: int = 0
+    states0: list = field(default_factory=list)     # optional: per level States
+    states1: list = field(default_factory=list)
+
+
+def thresholds(frac: float, nclients: int):
+    """leader.rs:193-194 (FE, u64) and leader.rs:245-246 (FieldElm, u32)."""
+    t = max(1, int(frac * nclients))
+    tl = max(1, int(frac * nclients) & 0xFFFFFFFF)
+    return t, tl
+
+
+def crawl(keys0: ServerKeys, keys1: ServerKeys, threshold: float, mode: str = "count", sim_seed: int = 0,
+          nthreads: int = 0, keep_states: bool = False, levels: int | None = None,
+          max_seconds: float | None = None) -> CrawlResult:
+    """max_seconds bounds the run (CPU-baseline sampling): stops after the level that
+    crosses it; res.n_children then covers only the levels done."""
+    import time
+    t_start = time.perf_counter()
+    n, d, _, L = keys0.cw_bits.shape
+    if levels is None:
+        levels = L
+    thr, thr_last = thresholds(threshold, n)
+    res = CrawlResult()
+    s0, s1 = tree_init(keys0), tree_init(keys1)
+    parents = np.zeros(1, np.uint64)
+    paths = [tuple(() for _ in range(d))]
+    for level in range(levels):
+        last = level == levels - 1
+        c0, b0 = level_expand(keys0, s0, parents, level, nthreads)
+        c1, b1 = level_expand(keys1, s1, parents, level, nthreads)
+        res.aes_blocks += b0 + b1
+        C = c0.t.shape[0]
+        eqm = np.all(share_bits(c0) == share_bits(c1), axis=-1)   # [C][n]
+        counts = eqm.sum(axis=1).astype(np.uint64)
+        if mode == "count":
+            keep = counts >= (thr_last if last else thr)
+            vals = [int(x) for x in counts]
+        elif mode == "fe":
+            if last:
+                sv0, sv1 = sim_ot_sums_fe255(eqm, sim_seed, level)
+                keep = np.array(keep_values(thr_last, sv0, sv1, FE255_P), bool)
+                vals = [((a % FE255_P) - (b % FE255_P)) % FE255_P for a, b in zip(sv0, sv1)]
+            else:
+                sv0, sv1 = sim_ot_sums_fe(eqm, sim_seed, level)
+                keep = np.array(keep_values(thr, sv0, sv1, FE_P), bool)
+                vals = [(a - b) % FE_P for a, b in zip(sv0, sv1)]
+            res.sums.append((sv0, sv1))
+        else:
+            raise ValueError(mode)
+        res.n_children.append(C)
+        res.counts.append(counts)
+        res.keeps.append(np.asarray(keep, bool))
+        if keep_states:
+            res.states0.append(c0)
+            res.states1.append(c1)
+        child_paths = []
+        for p in paths:
+            for i in range(1 << d):
+                child_paths.append(tuple(p[j] + (bool((i >> j) & 1),) for j in range(d)))
+        kept = np.nonzero(np.asarray(keep, bool))[0]
+        if last:
+            res.final_paths = [child_paths[k] for k in kept]
+            res.final_values = [vals[k] for k in kept]
+        paths = [child_paths[k] for k in kept]
+        parents = kept.astype(np.uint64)
+        s0, s1 = c0, c1
+        if max_seconds is not None and time.perf_counter() - t_start > max_seconds:
+            break
+        if parents.size == 0 and not last:
+            # reference: an empty frontier makes every later level produce no children
+            res.final_paths, res.final_values = [], []
+            for _ in range(level + 1, levels):
+                res.n_children.append(0)
+                res.counts.append(np.zeros(0, np.uint64))
+                res.keeps.append(np.zeros(0, bool))
+            break
+    return res
+
+
+# --------------------------------------------------------------------------------------
+# Bit-string utilities (lib.rs) — restated for the oracle's own key generation.
+# --------------------------------------------------------------------------------------
+
+def u32_to_bits(nbits: int, x: int):           # lib.rs:56-65 (LSB first)
+    return [bool((x >> i) & 1) for i in range(nbits)]
+
+
+def msb_u32_to_bits(nbits: int, x: int):       # lib.rs:67-76
+    return [bool((x >> i) & 1) for i in reversed(range(nbits))]
+
+
+def bits_to_u32(bits) -> int:                  # lib.rs:78-88 (MSB first)
+    r = 0
+    for b in bits:
+        r = (r << 1) | int(bool(b))
+    return r
+
+
+def string_to_bits(s: bytes):                  # lib.rs:90-98
+    out = []
+    for byte in s:
+        out += u32_to_bits(8, byte)
+    return out
+
+
+def all_bit_vectors(dim: int):                 # lib.rs:125-129
+    return [[bool((i >> j) & 1) for j in range(dim)] for i in range(1 << dim)]
+
+
+def add_bitstrings(a, b):                      # lib.rs:131-151
+    m = max(len(a), len(b))
+    a = [False] * (m - len(a)) + list(a)
+    b = [False] * (m - len(b)) + list(b)
+    out, carry = [], False
+    for x, y in zip(reversed(a), reversed(b)):
+        s = x ^ y ^ carry
+        carry = (x and y) or (y and carry) or (x and carry)
+        out.append(s)
+    if carry:
+        out.append(True)
+    return list(reversed(out))
+
+
+def subtract_bitstrings(a, b):                 # lib.rs:153-183
+    m = max(len(a), len(b))
+    a = [False] * (m - len(a)) + list(a)
+    b = [False] * (m - len(b)) + list(b)
+    bt = [not x for x in b]
+    carry = True
+    for i in reversed(range(m)):
+        s = bt[i] ^ carry
+        carry = bt[i] and carry
+        bt[i] = s
+        if not carry:
+            break
+    out, carry = [], False
+    for x, y in zip(reversed(a), reversed(bt)):
+        s = x ^ y ^ carry
+        carry = (x and y) or (y and carry) or (x and carry)
+        out.append(s)
+    return list(reversed(out))
+
+
+def l_inf_ball_bounds(alpha, size: int):
+    """ibDCF.rs:175-188: (alpha - size, alpha + size) MSB-first, width max(len, 32)."""
+    delta = msb_u32_to_bits(32, size)
+    left = subtract_bitstrings(alpha, delta)
+    right = add_bitstrings(alpha, delta)
+    assert len(left) == len(right), "carry out of add_bitstrings (reference panics, ibDCF.rs:182)"
+    return left, right
+
+
+def i16_to_bitvec(v: int):                     # sample_driving_data.rs:25-28
+    u = v & 0xFFFF
+    return [bool((u >> (15 - i)) & 1) for i in range(16)]

@@ -1,0 +1,51 @@
+"""The C-ABI library loads and exports every symbol include/fhh.h declares (no GPU calls)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "fhh.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    names = set(re.findall(r"\b(fhh_[a-z0-9_]+)\s*\(", hdr))
+    return sorted(n for n in names if n not in ("fhh_allreduce_fn",))
+
+
+def test_library_exports_header(fhh):
+    lib = fhh.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"libfhh.so does not export {s}"
+    from fuzzyheavyhitters_amd._lib import EXPORTS
+    assert sorted(EXPORTS) == syms
+
+
+def test_host_only_entry_points(fhh):
+    """Pure-host helpers run without a GPU: keep_values / final_values arithmetic."""
+    import numpy as np
+    from fuzzyheavyhitters_amd.collection import KeyCollection
+    P = fhh.FE_P
+    keep = KeyCollection.keep_values(10, 3, [5, 2 + P, 7], [1, 0, 5])
+    assert list(keep) == [True, False, False]
+    P2 = fhh.FE255_P
+    k2 = KeyCollection.keep_values_last(10, 2, [P2 + 5, 3 * P2 + 1, 7], [2, P2 + 0, 6])
+    assert list(k2) == [True, False, False]
+    from fuzzyheavyhitters_amd.collection import Result
+    fv = KeyCollection.final_values([Result([[True]], 2 * P2 + 9)], [Result([[True]], 4)])
+    assert fv[0].value == 5
+    fv = KeyCollection.final_values([Result([[True]], 1)], [Result([[True]], 4)])
+    assert fv[0].value == P2 - 3
+
+
+def test_create_fails_cleanly_without_gpu(fhh):
+    import torch
+    if torch.cuda.is_available():
+        return
+    lib = fhh.lib()
+    h = ctypes.c_void_p()
+    rc = lib.fhh_create(ctypes.byref(h), 8, 1, 0)
+    assert rc != 0
+    assert lib.fhh_last_error(None)

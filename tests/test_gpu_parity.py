@@ -1,0 +1,248 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden
+fixtures — bit-exact for keys, seeds, control bits, share bits, counts and field sums."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+
+
+def load(path):
+    z = np.load(path, allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def kc():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    from fuzzyheavyhitters_amd import KeyCollection, gen_keys_pair
+    return KeyCollection, gen_keys_pair
+
+
+def make_pair(kc, left, right, roots):
+    KeyCollection, gen_keys_pair = kc
+    n, d, L = left.shape
+    c0, c1 = KeyCollection(L, d), KeyCollection(L, d)
+    gen_keys_pair(c0, c1, left, right, roots)
+    return c0, c1
+
+
+def add_pair(kc, k0, k1):
+    KeyCollection, _ = kc
+    n, d, _, L = k0.cw_bits.shape
+    c0, c1 = KeyCollection(L, d), KeyCollection(L, d)
+    c0.add_keys(k0.key_idx, k0.root_seed, k0.cw_seed, k0.cw_bits)
+    c1.add_keys(k1.key_idx, k1.root_seed, k1.cw_seed, k1.cw_bits)
+    return c0, c1
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
+def test_gpu_keygen_bit_exact(kc, oracle, path):
+    g = load(path)
+    k0, k1 = oracle.gen_keys(g["left"], g["right"], g["root_seeds"])
+    c0, c1 = make_pair(kc, g["left"], g["right"], g["root_seeds"])
+    for c, k in ((c0, k0), (c1, k1)):
+        ki, rs, cs, cb = c.export_keys()
+        assert np.array_equal(ki, k.key_idx)
+        assert np.array_equal(rs, k.root_seed)
+        assert np.array_equal(cs, k.cw_seed), "cor_words seeds differ"
+        assert np.array_equal(cb, k.cw_bits), "cor_words bits differ"
+    assert np.array_equal(cs, g["cw_seed"]) and np.array_equal(cb, g["cw_bits"])
+
+
+def test_keygen_ragged_and_tiny(kc, oracle):
+    from fuzzyheavyhitters_amd import workload
+    for n in (1, 63, 64, 65, 130):
+        wl = workload.zipf_workload(n, 32, 1, num_sites=3, seed=n)
+        k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+        c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+        _, _, cs, cb = c1.export_keys()
+        assert np.array_equal(cs, k1.cw_seed) and np.array_equal(cb, k1.cw_bits)
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
+def test_level_states_bit_exact(kc, oracle, path):
+    """Every level: EvalState seeds/t/y of all children, share planes and equality counts
+    equal the oracle's (reference child order), pruning with the oracle's keep masks."""
+    g = load(path)
+    n, d, L, _, _ = [int(x) for x in g["meta"]]
+    k0, k1 = oracle.gen_keys(g["left"], g["right"], g["root_seeds"])
+    for build in ("gen", "add"):
+        c0, c1 = make_pair(kc, g["left"], g["right"], g["root_seeds"]) if build == "gen" else add_pair(kc, k0, k1)
+        c0.tree_init()
+        c1.tree_init()
+        s0, s1 = oracle.tree_init(k0), oracle.tree_init(k1)
+        seeds, t, y = c0.export_states()
+        assert np.array_equal(seeds, s0.seed) and np.array_equal(t, s0.t) and np.array_equal(y, s0.y)
+        parents = np.zeros(1, np.uint64)
+        thr = max(1, int(float(g["threshold"][0]) * n))
+        from fuzzyheavyhitters_amd.collection import sim_eq_count
+        for lvl in range(min(L, 12 if build == "add" else L)):
+            o0, _ = oracle.level_expand(k0, s0, parents, lvl)
+            o1, _ = oracle.level_expand(k1, s1, parents, lvl)
+            C, planes = c0.tree_crawl(share_planes=True)
+            C1, _ = c1.tree_crawl()
+            assert C == C1 == o0.t.shape[0]
+            gs, gt, gy = c0.export_states()
+            assert np.array_equal(gt, o0.t), f"t bits level {lvl}"
+            assert np.array_equal(gy, o0.y), f"y bits level {lvl}"
+            assert np.array_equal(gs, o0.seed), f"seeds level {lvl}"
+            gs1, gt1, gy1 = c1.export_states()
+            assert np.array_equal(gs1, o1.seed) and np.array_equal(gt1, o1.t) and np.array_equal(gy1, o1.y)
+            # share planes: [C][2d][nw] bit (client % 64)
+            sb = oracle.share_bits(o0)           # [C][n][2d]
+            if C:
+                bits = ((planes[:, :, np.arange(n) // 64] >> (np.arange(n, dtype=np.uint64) % 64)) & 1)
+                assert np.array_equal(bits.transpose(0, 2, 1).astype(np.uint8), sb)
+            cnt = sim_eq_count(c0, c1, C)
+            assert np.array_equal(cnt, oracle.eq_counts(o0, o1))
+            keep = cnt >= thr
+            c0.tree_prune(keep)
+            c1.tree_prune(keep)
+            parents = np.nonzero(keep)[0].astype(np.uint64)
+            s0, s1 = o0, o1
+            if parents.size == 0:
+                break
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
+def test_sim_crawl_matches_golden(kc, path):
+    from fuzzyheavyhitters_amd import sim_crawl
+    g = load(path)
+    n, d, L, _, _ = [int(x) for x in g["meta"]]
+    mode = str(g["mode"][0])
+    c0, c1 = make_pair(kc, g["left"], g["right"], g["root_seeds"])
+    res = sim_crawl(c0, c1, float(g["threshold"][0]), mode=mode, prf_seed=77)
+    assert np.array_equal(res.level_children, g["level_children"])
+    counts = np.concatenate(res.counts) if res.counts else np.zeros(0, np.uint64)
+    assert np.array_equal(counts, g["counts"])
+    paths = np.array([r.path for r in res.final], np.uint8).reshape(-1, d, L)
+    assert np.array_equal(paths, g["final_paths"])
+    if mode == "count":
+        assert [r.value for r in res.final] == [int(x) for x in g["final_values"]]
+    else:
+        # final_shares values are server 0's unreduced FieldElm sums; leader's final_values
+        from fuzzyheavyhitters_amd import KeyCollection
+        r1 = c1.final_shares()
+        fv = KeyCollection.final_values(res.final, r1)
+        assert [r.value for r in fv] == [int(x) for x in g["final_values"]]
+    st = c0.stats()
+    assert st["levels"] == L
+
+
+def test_sim_ot_sums_match_oracle(kc, oracle):
+    from fuzzyheavyhitters_amd import workload
+    from fuzzyheavyhitters_amd.collection import sim_ot_sums
+    wl = workload.zipf_workload(150, 40, 1, num_sites=4, seed=3)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    c0.tree_init(); c1.tree_init()
+    s0, s1 = oracle.tree_init(k0), oracle.tree_init(k1)
+    parents = np.zeros(1, np.uint64)
+    for lvl in range(6):
+        o0, _ = oracle.level_expand(k0, s0, parents, lvl)
+        o1, _ = oracle.level_expand(k1, s1, parents, lvl)
+        C, _ = c0.tree_crawl(); c1.tree_crawl()
+        eqm = np.all(oracle.share_bits(o0) == oracle.share_bits(o1), axis=-1)
+        a, b = sim_ot_sums(c0, c1, C, 1234, last=False)
+        ea, eb = oracle.sim_ot_sums_fe(eqm, 1234, lvl)
+        assert a == ea and b == eb
+        keep = np.ones(C, bool)
+        c0.tree_prune(keep); c1.tree_prune(keep)
+        parents = np.arange(C, dtype=np.uint64)
+        s0, s1 = o0, o1
+    o0, _ = oracle.level_expand(k0, s0, parents, 6)
+    o1, _ = oracle.level_expand(k1, s1, parents, 6)
+    C, _ = c0.tree_crawl_last(); c1.tree_crawl_last()
+    eqm = np.all(oracle.share_bits(o0) == oracle.share_bits(o1), axis=-1)
+    a, b = sim_ot_sums(c0, c1, C, 99, last=True)
+    ea, eb = oracle.sim_ot_sums_fe255(eqm, 99, 6)
+    assert a == ea and b == eb
+
+
+def test_node_sums_host_values(kc, oracle):
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(200, 32, 1, num_sites=3, seed=8)
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    c0.tree_init()
+    C, _ = c0.tree_crawl()
+    rng = np.random.default_rng(5)
+    vals = rng.integers(0, 2 ** 64, size=(C, 200), dtype=np.uint64)
+    vals[0, :5] = 2 ** 64 - 1
+    got = c0.node_sums_fe(vals)
+    for c in range(C):
+        assert int(got[c]) == oracle.fe_value(oracle.fe_fold_sum(vals[c]))
+        assert int(got[c]) == sum(int(x) for x in vals[c]) % oracle.FE_P
+    c0.tree_prune(np.ones(C, bool))
+    C, _ = c0.tree_crawl_last()
+    v8 = rng.integers(0, 2 ** 32, size=(C, 200, 8), dtype=np.uint32)
+    v8[:, :, 7] &= 0x7FFFFFFF
+    unr, can = c0.node_sums_fe255(v8)
+    for c in range(C):
+        exact = sum(sum(int(v8[c, i, k]) << (32 * k) for k in range(8)) for i in range(200))
+        assert unr[c] == exact
+        assert can[c] == exact % oracle.FE255_P
+    res = c0.final_shares()
+    assert [r.value for r in res] == unr
+
+
+def test_protocol_edges(kc, oracle):
+    """Unpruned double crawl (children become the frontier), crawl_last keeps the frontier,
+    prune length mismatches raise, empty frontier yields zero children."""
+    from fuzzyheavyhitters_amd import FhhError, workload
+    wl = workload.zipf_workload(70, 32, 1, num_sites=3, seed=21)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    c0.tree_init()
+    C1, _ = c0.tree_crawl()
+    C2, _ = c0.tree_crawl()          # no prune in between
+    assert (C1, C2) == (2, 4)
+    s = oracle.tree_init(k0)
+    o1, _ = oracle.level_expand(k0, s, np.zeros(1, np.uint64), 0)
+    o2, _ = oracle.level_expand(k0, o1, np.arange(2, dtype=np.uint64), 1)
+    seeds, t, y = c0.export_states()
+    assert np.array_equal(seeds, o2.seed) and np.array_equal(t, o2.t)
+    with pytest.raises(FhhError):
+        c0.tree_prune(np.ones(3, bool))
+    c0.tree_prune(np.array([True, False, False, False]))
+    C3, _ = c0.tree_crawl_last()
+    assert C3 == 2
+    c0.tree_prune_last([False, True])
+    assert c0.frontier_size() == (1, 1)
+    C4, _ = c0.tree_crawl_last()     # frontier unchanged by crawl_last (collect.rs:909-914)
+    assert C4 == 2
+    # empty frontier
+    c0.tree_prune_last([False, False])
+    c0.tree_crawl(); c0.tree_prune([False, False])
+    C5, _ = c0.tree_crawl()
+    assert C5 == 0
+    with pytest.raises(FhhError):
+        c1.tree_crawl()              # before tree_init
+
+
+@pytest.mark.parametrize("d,n,L,sites,thr", [(1, 3000, 512, 40, 0.01), (2, 500, 40, 6, 0.004)])
+def test_sim_crawl_matches_oracle_crawl(kc, oracle, d, n, L, sites, thr):
+    """Moderate-size end-to-end parity (reference data_len 512 for d = 1)."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(n, L, d, num_sites=sites, seed=1000 + n)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    ores = oracle.crawl(k0, k1, thr, mode="count")
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    res = sim_crawl(c0, c1, thr, mode="count")
+    assert list(res.level_children) == list(ores.n_children)
+    assert np.array_equal(np.concatenate(res.counts), np.concatenate(ores.counts))
+    got = sorted(tuple(tuple(p) for p in r.path) for r in res.final)
+    exp = sorted(tuple(tuple(p) for p in fp) for fp in ores.final_paths)
+    assert got == exp
+    st = c0.stats()
+    if d == 1:
+        assert st["aes_blocks"] * 2 == ores.aes_blocks
+    else:
+        assert st["aes_blocks"] * 2 <= ores.aes_blocks
+        assert st["ref_evals"] * 2 == ores.aes_blocks

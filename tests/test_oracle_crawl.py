@@ -1,0 +1,95 @@
+"""Oracle crawl (CPU restatement of collect.rs + leader level loop) against (a) the committed
+golden fixtures and (b) a brute-force plaintext recount of every child at every level."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+
+
+def load(path):
+    z = np.load(path, allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def prefix_ints(bits, k):
+    """bits [..., L] MSB first -> int of the first k bits (k <= 62)."""
+    w = (1 << np.arange(k - 1, -1, -1, dtype=np.int64))
+    return (bits[..., :k].astype(np.int64) * w).sum(-1)
+
+
+def plaintext_counts(left, right, paths_k):
+    """paths_k: [C][d] ints of length-k prefixes -> per child number of clients whose
+    [l, r] prefix box contains it."""
+    k = paths_k["k"]
+    lo = prefix_ints(left, k)     # [n][d]
+    hi = prefix_ints(right, k)
+    p = paths_k["p"]              # [C][d]
+    inside = (lo[None] <= p[:, None]) & (p[:, None] <= hi[None])   # [C][n][d]
+    return inside.all(-1).sum(-1)
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
+def test_oracle_matches_golden_and_plaintext(oracle, path):
+    g = load(path)
+    n, d, L, _, _ = [int(x) for x in g["meta"]]
+    thr = float(g["threshold"][0])
+    mode = str(g["mode"][0])
+    k0, k1 = oracle.gen_keys(g["left"], g["right"], g["root_seeds"])
+    assert np.array_equal(k0.cw_seed, g["cw_seed"]) and np.array_equal(k0.cw_bits, g["cw_bits"])
+    res = oracle.crawl(k0, k1, thr, mode=mode, sim_seed=77)
+    assert np.array_equal(np.array(res.n_children, np.uint64), g["level_children"])
+    counts = np.concatenate([np.asarray(c, np.uint64) for c in res.counts])
+    assert np.array_equal(counts, g["counts"])
+    keeps = np.concatenate([np.asarray(k, np.uint8) for k in res.keeps])
+    assert np.array_equal(keeps, g["keeps"])
+
+    # brute-force recount, level by level, following the same pruning
+    left, right = g["left"], g["right"]
+    tcount = max(1, int(thr * n))
+    frontier = np.zeros((1, d), np.int64)
+    off = 0
+    for lvl in range(L):
+        kids = []
+        for p in frontier:
+            for i in range(1 << d):
+                kids.append([(p[j] << 1) | ((i >> j) & 1) for j in range(d)])
+        kids = np.array(kids, np.int64).reshape(-1, d)
+        C = kids.shape[0]
+        pc = plaintext_counts(left, right, {"k": lvl + 1, "p": kids})
+        assert np.array_equal(pc.astype(np.uint64), counts[off:off + C]), f"level {lvl}"
+        keep = pc >= tcount
+        assert np.array_equal(keep.astype(np.uint8), keeps[off:off + C])
+        off += C
+        frontier = kids[keep]
+    fp = np.array([[list(map(int, p[j])) for j in range(d)] for p in res.final_paths], np.uint8).reshape(-1, d, L)
+    assert np.array_equal(fp, g["final_paths"])
+    if mode == "count":
+        assert [int(v) for v in res.final_values] == [int(x) for x in g["final_values"]]
+    else:
+        # FieldElm final values (v0 - v1 mod p) equal the plaintext counts
+        assert [int(v) for v in res.final_values] == [int(x) for x in g["final_values"]]
+        last_counts = counts[-len(res.keeps[-1]):][res.keeps[-1]]
+        assert [int(v) for v in res.final_values] == [int(x) for x in last_counts]
+
+
+def test_workload_bounds_match_oracle_bitstrings(oracle):
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(64, 40, 2, num_sites=7, ball_size=3, seed=5)
+    for c in range(64):
+        for j in range(2):
+            l, r = oracle.l_inf_ball_bounds([bool(b) for b in wl.alpha[c, j]], 3)
+            assert list(map(int, l)) == list(wl.left[c, j])
+            assert list(map(int, r)) == list(wl.right[c, j])
+
+
+def test_workload_shard_slices_are_consistent():
+    from fuzzyheavyhitters_amd import workload
+    full = workload.zipf_workload(300, 64, 1, num_sites=50, seed=11)
+    a = workload.zipf_workload(120, 64, 1, num_sites=50, seed=11, client_offset=0)
+    b = workload.zipf_workload(180, 64, 1, num_sites=50, seed=11, client_offset=120)
+    assert np.array_equal(np.concatenate([a.alpha, b.alpha]), full.alpha)
+    assert np.array_equal(np.concatenate([a.root_seeds, b.root_seeds]), full.root_seeds)

@@ -41,7 +41,12 @@ class _TorchAllReduce:
     def _call(self, ptr, count, user):
         try:
             view = self.buf[:count]
-            self.dist.all_reduce(view)                 # u64 partials: sums fit
+            if self.dist.get_backend() == "gloo":      # CPU rehearsal path: gloo reduces host tensors
+                host = view.cpu()
+                self.dist.all_reduce(host)
+                view.copy_(host)
+            else:
+                self.dist.all_reduce(view)             # RCCL over xGMI; u64 partials fit
             self.torch.cuda.current_stream().synchronize()
             return 0
         except Exception as e:  # pragma: no cover - surfaced as FHH_E_CALLBACK

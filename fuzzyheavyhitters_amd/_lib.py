@@ -32,6 +32,7 @@ EXPORTS = [
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
     "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench",
+    "fhh_set_variant", "fhh_variant_info",
 ]
 
 
@@ -125,6 +126,8 @@ def lib():
         "fhh_set_timing": (i, [vp, i]),
         "fhh_device_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i)]),
         "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
+        "fhh_set_variant": (i, [vp, i]),
+        "fhh_variant_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i), P(i)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -165,6 +165,10 @@ class KeyCollection:
         self._chk(lib().fhh_get_stats(self._h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in FhhStats._fields_}
 
+    def set_variant(self, variant: int):
+        """Select the k_expand variant (bit-identical outputs, different speed)."""
+        self._chk(lib().fhh_set_variant(self._h, variant))
+
     def reset_stats(self):
         self._chk(lib().fhh_reset_stats(self._h))
 

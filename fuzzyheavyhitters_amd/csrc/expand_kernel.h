@@ -1,0 +1,169 @@
+// k_expand — the hot path: ibDCFKey::eval_bit (ibDCF.rs:208-227) for every
+// (dim-prefix entry, client, side, direction), with the PRG expand_dir (prg.rs:92-122) as an
+// LDS T-table AES-128 and the MMO feed-forward.
+//
+// The kernel is a template over
+//   Tab   — the LDS T-table layout (how a byte of state becomes a conflict-free ds_read_b32),
+//   NB    — AES blocks per lane kept in flight (4: both sides x both dirs; 2: one side),
+//   THR   — workgroup size,
+// plus a runtime choice of static (grid-stride) or dynamic (atomic work counter) item
+// distribution. fhh_kernels.hip instantiates the variants; fhh_set_variant selects one.
+//
+// Every Tab is generic over Ops (perm/load/bfe) so tests/host/aes_ttable_host_test.cpp can
+// instantiate the exact same lookup code on the CPU with emulated v_perm_b32.
+#pragma once
+#include "aes_ttable.h"
+#include "fhh_internal.h"
+
+namespace fhh {
+
+template <int k> __host__ __device__ __forceinline__ uint32_t rotk(uint32_t v) {
+    if constexpr (k == 0) return v;
+    else return rotl32(v, 8 * k);
+}
+
+// ---- layouts ----------------------------------------------------------------------------
+// A: T0 only, one replica per lane (64), entry stride 256 B (64 KiB). addr = 1 v_perm.
+template <class Ops> struct TabT0R64 {
+    static constexpr int kWords = 256 * 64;
+    static constexpr const char* kName = "T0/64rep/64KiB";
+    __host__ __device__ static uint32_t word(const uint32_t* t0, int i) { return t0[i >> 6]; }
+    __host__ __device__ static void bases(uint32_t lane, uint32_t& b0, uint32_t& b1) { b0 = lane * 4; b1 = 0; }
+    template <int k>
+    __host__ __device__ static uint32_t term(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        return rotk<k>(Ops::load(t, Ops::perm(b0, x, lookup_sel(k))));
+    }
+    template <int k>
+    __host__ __device__ static uint32_t last(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        return Ops::load(t, Ops::perm(b0, x, lookup_sel(k)));
+    }
+    static constexpr int spos(int) { return 1; }
+};
+
+// B: four tables T0..T3, 32 replicas each (lanes l and l+32 share a replica: they are in
+// different ds_read_b32 lane groups), 128 KiB. Region m (64 KiB) holds T_{2m} in bytes
+// [0,128) and T_{2m+1} in [128,256) of each 256-B entry row. No rotations.
+template <class Ops> struct Tab4T32 {
+    static constexpr int kWords = 2 * 256 * 64;
+    static constexpr const char* kName = "T0..T3/32rep/128KiB";
+    __host__ __device__ static uint32_t word(const uint32_t* t0, int i) {
+        const int region = i >> 14, within = i & 16383, x = within >> 6, slot = within & 63;
+        const int tab = 2 * region + (slot >= 32 ? 1 : 0);
+        const uint32_t v = t0[x];
+        return tab == 0 ? v : rotl32(v, 8 * tab);
+    }
+    __host__ __device__ static void bases(uint32_t lane, uint32_t& b0, uint32_t& b1) {
+        b0 = (lane & 31) * 4;
+        b1 = b0 | (1u << 16);
+    }
+    template <int tab>
+    __host__ __device__ static uint32_t look(const uint32_t* t, uint32_t b0, uint32_t b1, uint32_t x, int k) {
+        // {lb.byte0, x.byte[k], lb.byte2, 0}
+        const uint32_t sel = 0x0C060004u | ((uint32_t)k << 8);
+        const uint32_t a = Ops::perm((tab >> 1) ? b1 : b0, x, sel) + 128u * (tab & 1);
+        return Ops::load(t, a);
+    }
+    template <int k>
+    __host__ __device__ static uint32_t term(const uint32_t* t, uint32_t b0, uint32_t b1, uint32_t x) {
+        return look<k>(t, b0, b1, x, k);
+    }
+    // final round: take S[x] at byte k from T_{(k+3)&3}
+    template <int k>
+    __host__ __device__ static uint32_t last(const uint32_t* t, uint32_t b0, uint32_t b1, uint32_t x) {
+        return look<(k + 3) & 3>(t, b0, b1, x, k);
+    }
+    static constexpr int spos(int k) { return k; }
+};
+
+// C: T0 only, 32 replicas, entry stride 128 B (32 KiB). addr = bfe + lshl_or (2 VALU).
+template <class Ops> struct TabT0R32 {
+    static constexpr int kWords = 256 * 32;
+    static constexpr const char* kName = "T0/32rep/32KiB";
+    __host__ __device__ static uint32_t word(const uint32_t* t0, int i) { return t0[i >> 5]; }
+    __host__ __device__ static void bases(uint32_t lane, uint32_t& b0, uint32_t& b1) { b0 = (lane & 31) * 4; b1 = 0; }
+    template <int k>
+    __host__ __device__ static uint32_t addr(uint32_t b0, uint32_t x) {
+        return (Ops::bfe(x, 8 * k, 8) << 7) | b0;
+    }
+    template <int k>
+    __host__ __device__ static uint32_t term(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        return rotk<k>(Ops::load(t, addr<k>(b0, x)));
+    }
+    template <int k>
+    __host__ __device__ static uint32_t last(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        return Ops::load(t, addr<k>(b0, x));
+    }
+    static constexpr int spos(int) { return 1; }
+};
+
+// D: T0 and T1 interleaved (32 replicas each, 64 KiB); T2 = rotl16(T0), T3 = rotl16(T1).
+template <class Ops> struct TabT01R32 {
+    static constexpr int kWords = 256 * 64;
+    static constexpr const char* kName = "T0,T1/32rep/64KiB";
+    __host__ __device__ static uint32_t word(const uint32_t* t0, int i) {
+        const uint32_t v = t0[i >> 6];
+        return (i & 63) >= 32 ? rotl32(v, 8) : v;
+    }
+    __host__ __device__ static void bases(uint32_t lane, uint32_t& b0, uint32_t& b1) { b0 = (lane & 31) * 4; b1 = 0; }
+    template <int k>
+    __host__ __device__ static uint32_t term(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        const uint32_t v = Ops::load(t, Ops::perm(b0, x, lookup_sel(k)) + 128u * (k & 1));
+        return (k >= 2) ? rotl32(v, 16) : v;
+    }
+    template <int k>
+    __host__ __device__ static uint32_t last(const uint32_t* t, uint32_t b0, uint32_t, uint32_t x) {
+        return Ops::load(t, Ops::perm(b0, x, lookup_sel(k)));
+    }
+    static constexpr int spos(int) { return 1; }
+};
+
+// ---- AES-128 (zero key) + MMO over a table layout ----------------------------------------
+template <class Ops, class Tab, int NB>
+__host__ __device__ __forceinline__ void aes0_mmo_tab(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0,
+                                                      uint32_t b1) {
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[b][c] = s[b][c];   // rk0 = 0
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                y[b][c] = Tab::template term<0>(tbl, b0, b1, x[b][c]) ^
+                          Tab::template term<1>(tbl, b0, b1, x[b][(c + 1) & 3]) ^
+                          Tab::template term<2>(tbl, b0, b1, x[b][(c + 2) & 3]) ^
+                          Tab::template term<3>(tbl, b0, b1, x[b][(c + 3) & 3]) ^ ZERO_RK.w[r][c];
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[b][c] = y[b][c];
+    }
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[b][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[b][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[b][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[b][(c + 3) & 3]);
+            o[c] = Ops::perm(a1, a0, sel_lo) ^ Ops::perm(a3, a2, sel_hi) ^ ZERO_RK.w[10][c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) s[b][c] ^= o[c];
+    }
+}
+
+struct DevOpsX : DevOps {
+    static __device__ __forceinline__ uint32_t bfe(uint32_t x, uint32_t off, uint32_t w) {
+        return (x >> off) & ((1u << w) - 1u);
+    }
+};
+
+}  // namespace fhh

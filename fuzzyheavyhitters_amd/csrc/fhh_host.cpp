@@ -26,6 +26,8 @@ namespace {
 
 thread_local std::string g_err;
 
+constexpr int kDefaultVariant = 0;
+
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
 
 struct DevBuf {
@@ -104,7 +106,9 @@ struct fhh_ctx {
     uint32_t L = 0, d = 0, K = 0;
     uint64_t n = 0, npad = 0, nw = 0;
     uint64_t client_base = 0;
+    int variant = 0;              // k_expand variant (fhh_set_variant)
     int grid = 0;
+    DevBuf work_counter;          // dynamic item distribution
 
     // host-staged keys (add_key); uploaded at tree_init
     std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;
@@ -407,10 +411,10 @@ int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
     return FHH_OK;
 }
 
-void finalize_launch(ExpandLaunch& L, int grid) {
+void finalize_launch(ExpandLaunch& L, int grid, int variant) {
     uint64_t entry_words = 0;
     for (uint32_t k = 0; k < L.njobs; k++) entry_words += (uint64_t)L.job[k].n_live * L.job[k].nw;
-    const uint64_t waves = (uint64_t)grid * (kExpandThreads / 64);
+    const uint64_t waves = (uint64_t)grid * (expand_threads(variant) / 64);
     uint64_t g = entry_words / (2 * waves);
     if (g < 1) g = 1;
     if (g > 8) g = 8;
@@ -482,10 +486,10 @@ int crawl_one(fhh_ctx* ctx, bool last) {
     La.njobs = 0;
     rc = prepare_expand(ctx, La.job, &La.njobs);
     if (rc) return rc;
-    finalize_launch(La, ctx->grid);
+    finalize_launch(La, ctx->grid, ctx->variant);
     size_t slot = 0;
     if (ctx->timing) HIP_TRY(ctx, timing_begin(ctx, &slot));
-    HIP_TRY(ctx, launch_expand(La, ctx->grid, ctx->stream));
+    HIP_TRY(ctx, launch_expand(La, ctx->variant, ctx->grid, ctx->work_counter.as<uint32_t>(), ctx->stream));
     if (ctx->timing) HIP_TRY(ctx, timing_end(ctx, slot, launch_blocks(ctx)));
     ctx->stats.expand_launches++;
     return post_expand(ctx, last);
@@ -505,11 +509,11 @@ int crawl_pair(fhh_ctx* c0, fhh_ctx* c1, bool last) {
     rc = prepare_expand(c1, La.job, &La.njobs);
     if (rc) return rc;
     HIP_TRY(c1, hipStreamSynchronize(c1->stream));   // c1's live lists uploaded
-    finalize_launch(La, c0->grid);
+    finalize_launch(La, c0->grid, c0->variant);
     size_t slot = 0;
     const uint64_t blocks = launch_blocks(c0) + launch_blocks(c1);
     if (c0->timing) HIP_TRY(c0, timing_begin(c0, &slot));
-    HIP_TRY(c0, launch_expand(La, c0->grid, c0->stream));
+    HIP_TRY(c0, launch_expand(La, c0->variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
     if (c0->timing) HIP_TRY(c0, timing_end(c0, slot, blocks));
     c0->stats.expand_launches++;
     rc = post_expand(c0, last);
@@ -719,7 +723,14 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
         delete ctx;
         return FHH_E_HIP;
     }
-    ctx->grid = expand_grid(device);
+    ctx->variant = kDefaultVariant;
+    ctx->grid = expand_grid(device, ctx->variant);
+    if (ctx->work_counter.ensure(256) != hipSuccess) {
+        g_err = "work counter allocation failed";
+        (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return FHH_E_NOMEM;
+    }
     *out = ctx;
     return FHH_OK;
 }
@@ -1230,6 +1241,29 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
             rc = prune_impl(c1, keep.data(), C);
             if (rc) return rc;
         }
+    }
+    return FHH_OK;
+}
+
+int fhh_set_variant(fhh_ctx* ctx, int variant) {
+    CTX_CHECK(ctx);
+    if (variant < 0 || variant >= expand_variant_count()) return ctx->fail(FHH_E_ARG, "set_variant: no such variant");
+    ctx->variant = variant;
+    ctx->grid = expand_grid(ctx->device, variant);
+    return FHH_OK;
+}
+
+int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* grid_per_device) {
+    if (variant < 0 || variant >= expand_variant_count()) {
+        g_err = "variant_info: no such variant";
+        return FHH_E_ARG;
+    }
+    if (name && cap) std::snprintf(name, cap, "%s", expand_variant_name(variant));
+    if (threads) *threads = expand_threads(variant);
+    if (grid_per_device) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        *grid_per_device = expand_grid(dev, variant);
     }
     return FHH_OK;
 }

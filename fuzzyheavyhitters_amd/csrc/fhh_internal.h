@@ -83,7 +83,10 @@ struct KeygenArgs {
 };
 
 // ---- launch wrappers (fhh_kernels.hip); all asynchronous on `stream` ----
-hipError_t launch_expand(const ExpandLaunch& a, int grid, hipStream_t stream);
+hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream);
+int expand_variant_count();
+const char* expand_variant_name(int variant);
+int expand_threads(int variant);
 hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream);
 hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream);
 hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream);
@@ -97,7 +100,7 @@ hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
                                 const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
                                 uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
                                 hipStream_t stream);
-// occupancy-derived persistent grid for k_expand on the current device
-int expand_grid(int device);
+// occupancy-derived persistent grid for k_expand variant on `device`
+int expand_grid(int device, int variant);
 
 }  // namespace fhh

@@ -12,7 +12,7 @@
 //   k_init_table    eval_init for every key (ibDCF.rs:229-236, collect.rs:67-92)
 //   k_keys_from_aos add_key wire layout -> SoA device layout
 #include "fhh_internal.h"
-#include "aes_ttable.h"
+#include "expand_kernel.h"
 
 namespace fhh {
 
@@ -29,71 +29,64 @@ __device__ __forceinline__ void fill_table(uint32_t* tbl) {
 
 // --------------------------------------------------------------------------------------
 // k_expand: one wave = 64 consecutive clients of one dim-j prefix group. Per entry and
-// lane: 2 sides x 2 directions = 4 AES blocks in lockstep (ILP for the LDS lookups).
+// lane: 2 sides x 2 directions = 4 AES blocks (NB = 4 in lockstep, or NB = 2 per side).
 // CorWords of (level, dim, side, client) are loaded once per work item and reused for
-// `group` entries.
+// `group` entries. Work items are dealt grid-stride (static) or from an atomic counter.
 // --------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kExpandThreads) void k_expand(ExpandLaunch a) {
-    __shared__ uint32_t tbl[kTableWords];
-    fill_table(tbl);
+template <class Tab, int NB>
+__device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
+                                            uint32_t b0, uint32_t b1) {
+    const uint32_t w = (uint32_t)(local % J.nw);
+    const uint32_t g = (uint32_t)(local / J.nw);
+    const uint32_t c = w * 64 + lane;
+    const size_t npad = J.npad, nw = J.nw;
 
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t lanebase = lane * 4;
-    const uint64_t wpb = blockDim.x >> 6;
-    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
-
-    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < a.total_items; item += nwaves) {
-        uint32_t ji = 0;
-        while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
-        const ExpandJob& J = a.job[ji];
-        const uint64_t local = item - J.item_begin;
-        const uint32_t w = (uint32_t)(local % J.nw);
-        const uint32_t g = (uint32_t)(local / J.nw);
-        const uint32_t c = w * 64 + lane;
-        const size_t npad = J.npad, nw = J.nw;
-
-        // CorWord for (level, dim, side) — ibDCF.rs:215-217 `cor_words[state.level]`
-        const size_t krow = (size_t)J.level * J.K + 2 * J.dim;
-        uint4 cw[2];
-        uint64_t cwp[2][4];
+    // CorWord for (level, dim, side) — ibDCF.rs:215-217 `cor_words[state.level]`
+    const size_t krow = (size_t)J.level * J.K + 2 * J.dim;
+    uint4 cw[2];
+    uint64_t cwp[2][4];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            cw[s] = J.cw_seed[(krow + s) * npad + c];
+    for (int s = 0; s < 2; s++) {
+        cw[s] = J.cw_seed[(krow + s) * npad + c];
 #pragma unroll
-            for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
-        }
+        for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
+    }
 
-        const uint32_t e_begin = g * J.group;
-        const uint32_t e_end = min(e_begin + J.group, J.n_live);
-        for (uint32_t e = e_begin; e < e_end; e++) {
-            const uint32_t src = J.live[e];
-            uint32_t blk[4][4];      // index s*2 + dir
-            uint64_t tw[2], yw[2];
-            uint64_t pb[4], py[4];   // PRG control bits (tau.bits / tau.y_bits), ballot planes
+    const uint32_t e_begin = g * J.group;
+    const uint32_t e_end = min(e_begin + J.group, J.n_live);
+    for (uint32_t e = e_begin; e < e_end; e++) {
+        const uint32_t src = J.live[e];
 #pragma unroll
-            for (int s = 0; s < 2; s++) {
+        for (int s0 = 0; s0 < 2; s0 += NB / 2) {
+            uint32_t blk[NB][4];      // index (s - s0)*2 + dir
+            uint64_t tw[NB / 2], yw[NB / 2];
+            uint64_t pb[NB], py[NB];  // PRG control bits (tau.bits / tau.y_bits) as ballot planes
+#pragma unroll
+            for (int q = 0; q < NB / 2; q++) {
+                const int s = s0 + q;
                 const uint4 sd = J.src_seed[((size_t)src * 2 + s) * npad + c];
-                tw[s] = J.src_t[((size_t)src * 2 + s) * nw + w];
-                yw[s] = J.src_y[((size_t)src * 2 + s) * nw + w];
+                tw[q] = J.src_t[((size_t)src * 2 + s) * nw + w];
+                yw[q] = J.src_y[((size_t)src * 2 + s) * nw + w];
                 const uint32_t sw[4] = {sd.x, sd.y, sd.z, sd.w};
 #pragma unroll
                 for (int dir = 0; dir < 2; dir++) {
-                    prg_ctr(sw, dir, blk[s * 2 + dir]);
+                    prg_ctr(sw, dir, blk[q * 2 + dir]);
                     uint32_t bit, ybit;
-                    prg_ctrl_bits(blk[s * 2 + dir][0], dir, bit, ybit);
-                    pb[s * 2 + dir] = __ballot(bit);
-                    py[s * 2 + dir] = __ballot(ybit);
+                    prg_ctrl_bits(blk[q * 2 + dir][0], dir, bit, ybit);
+                    pb[q * 2 + dir] = __ballot(bit);
+                    py[q * 2 + dir] = __ballot(ybit);
                 }
             }
 
-            aes0_mmo<DevOps, 4>(blk, tbl, lanebase);
+            aes0_mmo_tab<DevOpsX, Tab, NB>(blk, tbl, b0, b1);
 
 #pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const uint32_t tmask = 0u - (uint32_t)((tw[s] >> lane) & 1);   // if state.bit
+            for (int q = 0; q < NB / 2; q++) {
+                const int s = s0 + q;
+                const uint32_t tmask = 0u - (uint32_t)((tw[q] >> lane) & 1);   // if state.bit
 #pragma unroll
                 for (int dir = 0; dir < 2; dir++) {
-                    const uint32_t* o = blk[s * 2 + dir];
+                    const uint32_t* o = blk[q * 2 + dir];
                     uint4 out;
                     out.x = o[0] ^ (cw[s].x & tmask);
                     out.y = o[1] ^ (cw[s].y & tmask);
@@ -104,8 +97,8 @@ __global__ __launch_bounds__(kExpandThreads) void k_expand(ExpandLaunch a) {
                     if (lane == 0) {
                         // new_bit = tau.bits[dir] ^ (t & cw.bits[dir]);
                         // new_y = tau.y_bits[dir] ^ (t & cw.y_bits[dir]) ^ y   (ibDCF.rs:211-219)
-                        J.dst_t[de * nw + w] = pb[s * 2 + dir] ^ (tw[s] & cwp[s][dir]);
-                        J.dst_y[de * nw + w] = py[s * 2 + dir] ^ (tw[s] & cwp[s][2 + dir]) ^ yw[s];
+                        J.dst_t[de * nw + w] = pb[q * 2 + dir] ^ (tw[q] & cwp[s][dir]);
+                        J.dst_y[de * nw + w] = py[q * 2 + dir] ^ (tw[q] & cwp[s][2 + dir]) ^ yw[q];
                     }
                 }
             }
@@ -113,25 +106,108 @@ __global__ __launch_bounds__(kExpandThreads) void k_expand(ExpandLaunch a) {
     }
 }
 
-hipError_t launch_expand(const ExpandLaunch& a, int grid, hipStream_t stream) {
+template <class Tab, int NB, int THR, int MINW>
+__global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
+    __shared__ uint32_t tbl[Tab::kWords];
+    for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t b0, b1;
+    Tab::bases(lane, b0, b1);
+    const uint64_t wpb = THR / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    uint64_t item = work_counter ? 0 : (uint64_t)blockIdx.x * wpb + wave_id_uniform();
+    if (work_counter) {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(work_counter, 1u);
+        item = __builtin_amdgcn_readfirstlane(v);
+    }
+    while (item < a.total_items) {
+        uint32_t ji = 0;
+        while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
+        expand_item<Tab, NB>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
+        if (work_counter) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(work_counter, 1u);
+            item = __builtin_amdgcn_readfirstlane(v);
+        } else {
+            item += nwaves;
+        }
+    }
+}
+
+// Variant table (fhh_set_variant). Order matters: index = variant id.
+#define FHH_EXPAND_VARIANTS(X)                          \
+    X(0, TabT0R64<DevOpsX>, 4, 512, 1, false)           \
+    X(1, TabT0R64<DevOpsX>, 4, 512, 1, true)            \
+    X(2, Tab4T32<DevOpsX>, 4, 1024, 1, false)           \
+    X(3, Tab4T32<DevOpsX>, 4, 1024, 1, true)            \
+    X(4, TabT0R32<DevOpsX>, 2, 256, 1, false)           \
+    X(5, TabT01R32<DevOpsX>, 4, 512, 1, false)          \
+    X(6, TabT0R64<DevOpsX>, 2, 768, 1, false)           \
+    X(7, Tab4T32<DevOpsX>, 2, 1024, 1, false)           \
+    X(8, TabT0R32<DevOpsX>, 2, 384, 1, false)           \
+    X(9, TabT0R32<DevOpsX>, 2, 512, 8, false)           \
+    X(10, TabT0R64<DevOpsX>, 2, 1024, 8, false)         \
+    X(11, TabT0R64<DevOpsX>, 2, 768, 1, true)
+
+struct VariantInfo {
+    const void* fn;
+    int threads;
+    bool dynamic;
+    const char* name;
+};
+
+static VariantInfo variant_info(int v) {
+    switch (v) {
+#define FHH_CASE(id, TAB, NB, THR, MINW, DYN) \
+    case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW>), THR, DYN, TAB::kName};
+        FHH_EXPAND_VARIANTS(FHH_CASE)
+#undef FHH_CASE
+        default: return VariantInfo{nullptr, 0, false, ""};
+    }
+}
+
+int expand_variant_count() { return 12; }
+
+const char* expand_variant_name(int v) { return variant_info(v).name; }
+
+hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream) {
     if (a.total_items == 0) return hipSuccess;
-    uint64_t waves_needed = a.total_items;
-    uint64_t blocks_needed = (waves_needed + (kExpandThreads / 64) - 1) / (kExpandThreads / 64);
-    int g = (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
-    hipLaunchKernelGGL(k_expand, dim3(g), dim3(kExpandThreads), 0, stream, a);
+    const VariantInfo vi = variant_info(variant);
+    if (!vi.fn) return hipErrorInvalidValue;
+    const uint64_t wpb = vi.threads / 64;
+    const uint64_t blocks_needed = (a.total_items + wpb - 1) / wpb;
+    const int g = (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
+    uint32_t* ctr = nullptr;
+    if (vi.dynamic) {
+        hipError_t e = hipMemsetAsync(work_counter, 0, 4, stream);
+        if (e != hipSuccess) return e;
+        ctr = work_counter;
+    }
+    switch (variant) {
+#define FHH_CASE(id, TAB, NB, THR, MINW, DYN) \
+    case id: hipLaunchKernelGGL((k_expand<TAB, NB, THR, MINW>), dim3(g), dim3(THR), 0, stream, a, ctr); break;
+        FHH_EXPAND_VARIANTS(FHH_CASE)
+#undef FHH_CASE
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-int expand_grid(int device) {
+int expand_grid(int device, int variant) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    const VariantInfo vi = variant_info(variant);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_expand), kExpandThreads,
-                                                     0) != hipSuccess ||
+    if (!vi.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vi.fn, vi.threads, 0) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
     return cus * per_cu;
 }
+
+int expand_threads(int variant) { return variant_info(variant).threads; }
 
 // --------------------------------------------------------------------------------------
 // Child-level kernels (one block per child, grid-stride).

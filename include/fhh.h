@@ -193,6 +193,12 @@ typedef struct fhh_stats {
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);
+/* Select the k_expand variant (LDS table layout / blocks per lane / workgroup size / work
+ * distribution). All variants are bit-identical; they differ in speed. */
+int fhh_set_variant(fhh_ctx* ctx, int variant);
+/* Describe variant: layout name, workgroup size, persistent grid on the current device.
+ * Returns FHH_E_ARG past the last variant. */
+int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* grid_per_device);
 int fhh_reset_stats(fhh_ctx* ctx);
 /* 1 to time every k_expand launch with HIP events (default 1). */
 int fhh_set_timing(fhh_ctx* ctx, int enabled);

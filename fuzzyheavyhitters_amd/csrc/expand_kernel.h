@@ -132,11 +132,14 @@ __host__ __device__ __forceinline__ void aes0_mmo_tab(uint32_t (&s)[NB][4], cons
 #pragma unroll
         for (int b = 0; b < NB; b++)
 #pragma unroll
-            for (int c = 0; c < 4; c++)
-                y[b][c] = Tab::template term<0>(tbl, b0, b1, x[b][c]) ^
-                          Tab::template term<1>(tbl, b0, b1, x[b][(c + 1) & 3]) ^
-                          Tab::template term<2>(tbl, b0, b1, x[b][(c + 2) & 3]) ^
-                          Tab::template term<3>(tbl, b0, b1, x[b][(c + 3) & 3]) ^ ZERO_RK.w[r][c];
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[b][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[b][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[b][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[b][(c + 3) & 3]);
+                // two v_bitop3_b32 (3-input XOR) instead of four v_xor_b32
+                y[b][c] = Ops::xor3(Ops::xor3(t0, t1, t2), t3, ZERO_RK.w[r][c]);
+            }
 #pragma unroll
         for (int b = 0; b < NB; b++)
 #pragma unroll
@@ -153,16 +156,20 @@ __host__ __device__ __forceinline__ void aes0_mmo_tab(uint32_t (&s)[NB][4], cons
             const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[b][(c + 1) & 3]);
             const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[b][(c + 2) & 3]);
             const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[b][(c + 3) & 3]);
-            o[c] = Ops::perm(a1, a0, sel_lo) ^ Ops::perm(a3, a2, sel_hi) ^ ZERO_RK.w[10][c];
+            o[c] = Ops::xor3(Ops::perm(a1, a0, sel_lo), Ops::perm(a3, a2, sel_hi), ZERO_RK.w[10][c]);
         }
 #pragma unroll
-        for (int c = 0; c < 4; c++) s[b][c] ^= o[c];
+        for (int c = 0; c < 4; c++) s[b][c] ^= o[c];   // MMO feed-forward (prg.rs:227-230)
     }
 }
 
 struct DevOpsX : DevOps {
     static __device__ __forceinline__ uint32_t bfe(uint32_t x, uint32_t off, uint32_t w) {
         return (x >> off) & ((1u << w) - 1u);
+    }
+    // gfx950 v_bitop3_b32, truth table 0x96 = a ^ b ^ c (hipcc does not form it from ^ chains)
+    static __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+        return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
     }
 };
 

@@ -26,7 +26,7 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kDefaultVariant = 0;
+constexpr int kDefaultVariant = 3;   // 4 tables, 128 KiB, 1024 thr, dynamic items (tools/ab_expand.py, r01)
 
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
 
@@ -86,7 +86,6 @@ struct DimTable {
     size_t cap[2] = {0, 0};       // entries
     int cur = 0;                  // buffer that holds the frontier's entries
     std::vector<uint32_t> live;   // frontier entries (indices into buffer `cur`), ordered
-    DevBuf live_dev;
 };
 
 struct Node {
@@ -102,7 +101,9 @@ using Limbs10 = std::array<uint32_t, 10>;
 
 struct fhh_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;       // execution stream (own_stream, or the peer's in pair mode)
+    hipStream_t own_stream = nullptr;
+    fhh_ctx* peer = nullptr;            // pair mode: ctx whose staging/timing this ctx's syncs also retire
     uint32_t L = 0, d = 0, K = 0;
     uint64_t n = 0, npad = 0, nw = 0;
     uint64_t client_base = 0;
@@ -124,7 +125,9 @@ struct fhh_ctx {
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist;   // per depth: (parent, i)
     uint64_t pending_C = 0;
     int child_buf[kMaxDims] = {0};
-    DevBuf parent_pos;            // [F][d] u32 for pending children
+    DevBuf lists;                 // per crawl: live lists of every dim + parent_pos, one upload
+    const uint32_t* live_ptr[kMaxDims] = {nullptr};
+    const uint32_t* parent_pos_ptr = nullptr;   // [F][d] u32 for pending children
 
     // frontier_last (collect.rs:33, 909-914): surviving (parent, i) + values
     std::vector<std::pair<uint32_t, uint32_t>> last_nodes;
@@ -205,8 +208,27 @@ int sync(fhh_ctx* ctx) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     timing_resolve(ctx);
     ctx->stage_used = 0;
+    if (ctx->peer) {
+        timing_resolve(ctx->peer);
+        ctx->peer->stage_used = 0;
+    }
     return FHH_OK;
 }
+
+// Pair mode (in-process two-server harness): c1 runs on c0's stream, so one stream carries
+// both servers' work in order and the level loop needs a single host sync.
+struct PairScope {
+    fhh_ctx *c0, *c1;
+    PairScope(fhh_ctx* a, fhh_ctx* b) : c0(a), c1(b) {
+        c1->stream = c0->stream;
+        c0->peer = c1;
+    }
+    ~PairScope() {
+        (void)hipStreamSynchronize(c0->stream);
+        c1->stream = c1->own_stream;
+        c0->peer = nullptr;
+    }
+};
 
 // pinned host staging that stays valid until the next sync(ctx)
 void* stage_bytes(fhh_ctx* ctx, size_t bytes) {
@@ -379,14 +401,31 @@ int upload_u32(fhh_ctx* ctx, DevBuf& dst, const std::vector<uint32_t>& v) {
     return FHH_OK;
 }
 
-// Prepare expansion jobs for one ctx: dst buffers sized, live lists uploaded.
+// One H2D copy per crawl: [live_0 | ... | live_{d-1} | parent_pos[F][d]] (u32).
+int upload_lists(fhh_ctx* ctx) {
+    std::vector<uint32_t> v;
+    size_t off[kMaxDims + 1];
+    for (uint32_t j = 0; j < ctx->d; j++) {
+        off[j] = v.size();
+        v.insert(v.end(), ctx->tab[j].live.begin(), ctx->tab[j].live.end());
+    }
+    off[ctx->d] = v.size();
+    for (const Node& nd : ctx->frontier)
+        for (uint32_t j = 0; j < ctx->d; j++) v.push_back(nd.pos[j]);
+    int rc = upload_u32(ctx, ctx->lists, v);
+    if (rc) return rc;
+    const uint32_t* base = ctx->lists.as<uint32_t>();
+    for (uint32_t j = 0; j < ctx->d; j++) ctx->live_ptr[j] = base + off[j];
+    ctx->parent_pos_ptr = base + off[ctx->d];
+    return FHH_OK;
+}
+
+// Prepare expansion jobs for one ctx (dst buffers sized; lists already on the device).
 int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         const int src = T.cur, dst = 1 - T.cur;
         int rc = table_ensure(ctx, T, dst, 2 * T.live.size());
-        if (rc) return rc;
-        rc = upload_u32(ctx, T.live_dev, T.live);
         if (rc) return rc;
         ExpandJob& J = jobs[(*njobs)++];
         J.cw_seed = ctx->cw_seed.as<uint4>();
@@ -397,7 +436,7 @@ int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
         J.dst_seed = T.seed[dst].as<uint4>();
         J.dst_t = T.t[dst].as<uint64_t>();
         J.dst_y = T.y[dst].as<uint64_t>();
-        J.live = T.live_dev.as<uint32_t>();
+        J.live = ctx->live_ptr[j];
         J.n_live = (uint32_t)T.live.size();
         J.level = ctx->level;
         J.dim = j;
@@ -438,11 +477,6 @@ uint64_t launch_blocks(const fhh_ctx* ctx) {
 int post_expand(fhh_ctx* ctx, bool last) {
     const uint64_t F = ctx->frontier.size();
     ctx->pending_C = F << ctx->d;
-    std::vector<uint32_t> pp(F * ctx->d);
-    for (uint64_t p = 0; p < F; p++)
-        for (uint32_t j = 0; j < ctx->d; j++) pp[p * ctx->d + j] = ctx->frontier[p].pos[j];
-    int rc = upload_u32(ctx, ctx->parent_pos, pp);
-    if (rc) return rc;
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         ctx->child_buf[j] = 1 - T.cur;
@@ -482,6 +516,8 @@ int check_can_crawl(fhh_ctx* ctx) {
 int crawl_one(fhh_ctx* ctx, bool last) {
     int rc = check_can_crawl(ctx);
     if (rc) return rc;
+    rc = upload_lists(ctx);
+    if (rc) return rc;
     ExpandLaunch La{};
     La.njobs = 0;
     rc = prepare_expand(ctx, La.job, &La.njobs);
@@ -501,14 +537,22 @@ int crawl_pair(fhh_ctx* c0, fhh_ctx* c1, bool last) {
     if (rc) return rc;
     rc = check_can_crawl(c1);
     if (rc) return rc;
-    HIP_TRY(c1, hipStreamSynchronize(c1->stream));
+    if (c1->stream != c0->stream) HIP_TRY(c1, hipStreamSynchronize(c1->stream));
+    // both servers prune with the same keep masks, so their frontiers and live lists are
+    // identical: upload once and let server 1's jobs read server 0's copy
+    if (c0->frontier.size() != c1->frontier.size()) return c0->fail(FHH_E_ARG, "pair: frontiers differ");
+    for (uint32_t j = 0; j < c0->d; j++)
+        if (c0->tab[j].live != c1->tab[j].live) return c0->fail(FHH_E_ARG, "pair: live lists differ");
+    rc = upload_lists(c0);
+    if (rc) return rc;
+    for (uint32_t j = 0; j < c0->d; j++) c1->live_ptr[j] = c0->live_ptr[j];
+    c1->parent_pos_ptr = c0->parent_pos_ptr;
     ExpandLaunch La{};
     La.njobs = 0;
     rc = prepare_expand(c0, La.job, &La.njobs);
     if (rc) return rc;
     rc = prepare_expand(c1, La.job, &La.njobs);
     if (rc) return rc;
-    HIP_TRY(c1, hipStreamSynchronize(c1->stream));   // c1's live lists uploaded
     finalize_launch(La, c0->grid, c0->variant);
     size_t slot = 0;
     const uint64_t blocks = launch_blocks(c0) + launch_blocks(c1);
@@ -530,7 +574,7 @@ ChildArgs child_args(fhh_ctx* c0, fhh_ctx* c1) {
         a.s1.t[j] = o->tab[j].t[o->child_buf[j]].as<uint64_t>();
         a.s1.y[j] = o->tab[j].y[o->child_buf[j]].as<uint64_t>();
     }
-    a.parent_pos = c0->parent_pos.as<uint32_t>();
+    a.parent_pos = c0->parent_pos_ptr;
     a.valid = c0->valid.as<uint64_t>();
     a.C = c0->pending_C;
     a.d = c0->d;
@@ -558,23 +602,24 @@ int prune_impl(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
     const uint32_t d = ctx->d;
     std::vector<Node> nf;
     std::vector<std::pair<uint32_t, uint32_t>> h;
-    std::vector<std::unordered_map<uint32_t, uint32_t>> remap(d);
     std::vector<std::vector<uint32_t>> new_live(d);
+    // child entry e of dim j lies in [0, 2 * |live_j|): flat remap, first reference wins
+    thread_local std::vector<int32_t> remap[kMaxDims];
+    for (uint32_t j = 0; j < d; j++) remap[j].assign(2 * ctx->tab[j].live.size(), -1);
+    nf.reserve(n);
+    h.reserve(n);
     for (uint64_t c = 0; c < n; c++) {
         if (!keep[c]) continue;
         const uint32_t p = (uint32_t)(c >> d), i = (uint32_t)(c & ((1u << d) - 1));
         Node node{};
         for (uint32_t j = 0; j < d; j++) {
             const uint32_t e = 2 * ctx->frontier[p].pos[j] + ((i >> j) & 1);
-            auto it = remap[j].find(e);
-            if (it == remap[j].end()) {
-                const uint32_t k = (uint32_t)new_live[j].size();
-                remap[j].emplace(e, k);
+            int32_t& r = remap[j][e];
+            if (r < 0) {
+                r = (int32_t)new_live[j].size();
                 new_live[j].push_back(e);
-                node.pos[j] = k;
-            } else {
-                node.pos[j] = it->second;
             }
+            node.pos[j] = (uint32_t)r;
         }
         nf.push_back(node);
         h.emplace_back(p, i);
@@ -616,7 +661,7 @@ int check_pair(fhh_ctx* c0, fhh_ctx* c1) {
     for (size_t k = 0; k < c0->frontier.size(); k++)
         for (uint32_t j = 0; j < c0->d; j++)
             if (c0->frontier[k].pos[j] != c1->frontier[k].pos[j]) return c0->fail(FHH_E_ARG, "sim: frontiers differ");
-    HIP_TRY(c1, hipStreamSynchronize(c1->stream));
+    if (c1->stream != c0->stream) HIP_TRY(c1, hipStreamSynchronize(c1->stream));
     return FHH_OK;
 }
 
@@ -717,7 +762,8 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
     ctx->L = data_len;
     ctx->d = n_dims;
     ctx->K = 2 * n_dims;
-    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    ctx->stream = ctx->own_stream;
     if (e != hipSuccess) {
         g_err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
         delete ctx;
@@ -727,7 +773,7 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
     ctx->grid = expand_grid(device, ctx->variant);
     if (ctx->work_counter.ensure(256) != hipSuccess) {
         g_err = "work counter allocation failed";
-        (void)hipStreamDestroy(ctx->stream);
+        (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;
         return FHH_E_NOMEM;
     }
@@ -743,7 +789,7 @@ void fhh_destroy(fhh_ctx* ctx) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
     }
-    (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->own_stream);
     for (auto* b : ctx->stage) delete b;
     delete ctx;
 }
@@ -1170,6 +1216,8 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     if (rc) return rc;
     rc = fhh_tree_init(c1);
     if (rc) return rc;
+    if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");
+    PairScope pair(c0, c1);
     // leader.rs:193-194 and 245-246
     const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
     const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));

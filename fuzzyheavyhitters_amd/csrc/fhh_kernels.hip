@@ -106,7 +106,86 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
     }
 }
 
-template <class Tab, int NB, int THR, int MINW>
+// NB = 4 with the next entry's seeds / t / y prefetched while the current entry's AES runs.
+template <class Tab>
+__device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
+                                               uint32_t b0, uint32_t b1) {
+    const uint32_t w = (uint32_t)(local % J.nw);
+    const uint32_t g = (uint32_t)(local / J.nw);
+    const uint32_t c = w * 64 + lane;
+    const size_t npad = J.npad, nw = J.nw;
+    const size_t krow = (size_t)J.level * J.K + 2 * J.dim;
+    uint4 cw[2];
+    uint64_t cwp[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        cw[s] = J.cw_seed[(krow + s) * npad + c];
+#pragma unroll
+        for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
+    }
+    const uint32_t e_begin = g * J.group;
+    const uint32_t e_end = min(e_begin + J.group, J.n_live);
+    if (e_begin >= e_end) return;
+    uint4 sd[2];
+    uint64_t tw[2], yw[2];
+    {
+        const uint32_t src = J.live[e_begin];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            sd[s] = J.src_seed[((size_t)src * 2 + s) * npad + c];
+            tw[s] = J.src_t[((size_t)src * 2 + s) * nw + w];
+            yw[s] = J.src_y[((size_t)src * 2 + s) * nw + w];
+        }
+    }
+    for (uint32_t e = e_begin; e < e_end; e++) {
+        uint32_t blk[4][4];
+        uint64_t pb[4], py[4];
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const uint32_t sw[4] = {sd[s].x, sd[s].y, sd[s].z, sd[s].w};
+#pragma unroll
+            for (int dir = 0; dir < 2; dir++) {
+                prg_ctr(sw, dir, blk[s * 2 + dir]);
+                uint32_t bit, ybit;
+                prg_ctrl_bits(blk[s * 2 + dir][0], dir, bit, ybit);
+                pb[s * 2 + dir] = __ballot(bit);
+                py[s * 2 + dir] = __ballot(ybit);
+            }
+        }
+        const uint64_t ctw[2] = {tw[0], tw[1]}, cyw[2] = {yw[0], yw[1]};
+        if (e + 1 < e_end) {   // prefetch (wave-uniform branch)
+            const uint32_t src = J.live[e + 1];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                sd[s] = J.src_seed[((size_t)src * 2 + s) * npad + c];
+                tw[s] = J.src_t[((size_t)src * 2 + s) * nw + w];
+                yw[s] = J.src_y[((size_t)src * 2 + s) * nw + w];
+            }
+        }
+        aes0_mmo_tab<DevOpsX, Tab, 4>(blk, tbl, b0, b1);
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const uint32_t tmask = 0u - (uint32_t)((ctw[s] >> lane) & 1);
+#pragma unroll
+            for (int dir = 0; dir < 2; dir++) {
+                const uint32_t* o = blk[s * 2 + dir];
+                uint4 out;
+                out.x = o[0] ^ (cw[s].x & tmask);
+                out.y = o[1] ^ (cw[s].y & tmask);
+                out.z = o[2] ^ (cw[s].z & tmask);
+                out.w = o[3] ^ (cw[s].w & tmask);
+                const size_t de = (size_t)(2 * e + dir) * 2 + s;
+                J.dst_seed[de * npad + c] = out;
+                if (lane == 0) {
+                    J.dst_t[de * nw + w] = pb[s * 2 + dir] ^ (ctw[s] & cwp[s][dir]);
+                    J.dst_y[de * nw + w] = py[s * 2 + dir] ^ (ctw[s] & cwp[s][2 + dir]) ^ cyw[s];
+                }
+            }
+        }
+    }
+}
+
+template <class Tab, int NB, int THR, int MINW, bool PF = false>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
@@ -126,7 +205,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     while (item < a.total_items) {
         uint32_t ji = 0;
         while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
-        expand_item<Tab, NB>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
+        if constexpr (PF) expand_item_pf<Tab>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
+        else expand_item<Tab, NB>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
         if (work_counter) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(work_counter, 1u);
@@ -150,7 +230,9 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     X(8, TabT0R32<DevOpsX>, 2, 384, 1, false)           \
     X(9, TabT0R32<DevOpsX>, 2, 512, 8, false)           \
     X(10, TabT0R64<DevOpsX>, 2, 1024, 8, false)         \
-    X(11, TabT0R64<DevOpsX>, 2, 768, 1, true)
+    X(11, TabT0R64<DevOpsX>, 2, 768, 1, true)          \
+    X(12, Tab4T32<DevOpsX>, 4, 1024, 1, true, true)     \
+    X(13, Tab4T32<DevOpsX>, 4, 1024, 1, false, true)
 
 struct VariantInfo {
     const void* fn;
@@ -161,15 +243,15 @@ struct VariantInfo {
 
 static VariantInfo variant_info(int v) {
     switch (v) {
-#define FHH_CASE(id, TAB, NB, THR, MINW, DYN) \
-    case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW>), THR, DYN, TAB::kName};
+#define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
+    case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), THR, DYN, TAB::kName};
         FHH_EXPAND_VARIANTS(FHH_CASE)
 #undef FHH_CASE
         default: return VariantInfo{nullptr, 0, false, ""};
     }
 }
 
-int expand_variant_count() { return 12; }
+int expand_variant_count() { return 14; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
@@ -187,8 +269,8 @@ hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t*
         ctr = work_counter;
     }
     switch (variant) {
-#define FHH_CASE(id, TAB, NB, THR, MINW, DYN) \
-    case id: hipLaunchKernelGGL((k_expand<TAB, NB, THR, MINW>), dim3(g), dim3(THR), 0, stream, a, ctr); break;
+#define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
+    case id: hipLaunchKernelGGL((k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), dim3(g), dim3(THR), 0, stream, a, ctr); break;
         FHH_EXPAND_VARIANTS(FHH_CASE)
 #undef FHH_CASE
         default: return hipErrorInvalidValue;

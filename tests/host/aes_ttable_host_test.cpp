@@ -28,6 +28,7 @@ struct HostOps {
         return tbl[byte_addr / 4];
     }
     static uint32_t bfe(uint32_t x, uint32_t off, uint32_t w) { return (x >> off) & ((1u << w) - 1u); }
+    static uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
 };
 
 // every LDS layout of expand_kernel.h: same outputs as the byte-oriented reference, every lane,

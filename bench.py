@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords"],
+                    help="zipf = configs[1] (default); coords = configs[3] (d=2 lat/lon, data_len 16)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample-clients", type=int, default=4096)
@@ -101,8 +103,16 @@ def main():
     n_local = args.clients
     n_total = n_local * world
     t_gen = time.perf_counter()
-    wl = workload.zipf_workload(n_local, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
-                                ball_size=args.ball, seed=args.seed, client_offset=rank * n_local)
+    if args.workload == "coords":
+        # configs[3]: src/bin/config.json (data_len 16, n_dims 2, ball 1, threshold 0.075)
+        args.data_len, args.dims = 16, 2
+        if args.threshold == 0.001:
+            args.threshold = 0.075
+        wl = workload.coords_workload(n_local, ball_size=args.ball, zipf_s=args.zipf, seed=args.seed,
+                                      client_offset=rank * n_local)
+    else:
+        wl = workload.zipf_workload(n_local, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
+                                    ball_size=args.ball, seed=args.seed, client_offset=rank * n_local)
     c0 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     c1 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
@@ -171,7 +181,9 @@ def main():
             "dtype": "u32",
             "data": "synthetic (seeded Zipf workload shaped like leader.rs; random-init keys via GPU keygen)",
             "config": {
-                "workload": "configs[1]: Zipf clients, data_len 512 ibDCF tree crawl, two in-process servers",
+                "workload": ("configs[1]: Zipf clients, data_len 512 ibDCF tree crawl, two in-process servers"
+                             if args.workload == "zipf" else
+                             "configs[3]: lat/lon l-inf balls (county-centroid-shaped points), d=2, data_len 16"),
                 "clients_per_gpu": n_local, "clients_total": n_total, "data_len": args.data_len,
                 "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
                 "threshold": args.threshold, "mode": args.mode, "parallelism": f"client-shard x{world}",
@@ -202,7 +214,7 @@ def main():
             out["measured_valu_peak_tops"] = r.value / 1e12
             fhh.lib().fhh_microbench(local_rank, 1, ctypes.byref(r))
             out["measured_lds_peak_gbps"] = r.value / 1e9
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "zipf":
             out["cpu_baseline"] = cpu_baseline(args, n_total)
         else:
             out["cpu_baseline"] = None

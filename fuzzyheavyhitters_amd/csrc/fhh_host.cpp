@@ -771,7 +771,7 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
     }
     ctx->variant = kDefaultVariant;
     ctx->grid = expand_grid(device, ctx->variant);
-    if (ctx->work_counter.ensure(256) != hipSuccess) {
+    if (ctx->work_counter.ensure(256) != hipSuccess || hipMemset(ctx->work_counter.p, 0, 256) != hipSuccess) {
         g_err = "work counter allocation failed";
         (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;

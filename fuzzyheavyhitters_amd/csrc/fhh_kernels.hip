@@ -215,6 +215,15 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             item += nwaves;
         }
     }
+    // dynamic mode: every wave drew exactly one item past the end; the last wave to leave
+    // re-arms the counter for the next launch (no memset between launches)
+    if (work_counter && lane == 0) {
+        const uint32_t done = atomicAdd(work_counter + 1, 1u);
+        if (done + 1 == (uint32_t)nwaves) {
+            atomicExch(work_counter, 0u);
+            atomicExch(work_counter + 1, 0u);
+        }
+    }
 }
 
 // Variant table (fhh_set_variant). Order matters: index = variant id.
@@ -262,12 +271,8 @@ hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t*
     const uint64_t wpb = vi.threads / 64;
     const uint64_t blocks_needed = (a.total_items + wpb - 1) / wpb;
     const int g = (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
-    uint32_t* ctr = nullptr;
-    if (vi.dynamic) {
-        hipError_t e = hipMemsetAsync(work_counter, 0, 4, stream);
-        if (e != hipSuccess) return e;
-        ctr = work_counter;
-    }
+    // dynamic mode: work_counter[0..1] must be zero at launch; the kernel re-arms it on exit
+    uint32_t* ctr = vi.dynamic ? work_counter : nullptr;
     switch (variant) {
 #define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
     case id: hipLaunchKernelGGL((k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), dim3(g), dim3(THR), 0, stream, a, ctr); break;

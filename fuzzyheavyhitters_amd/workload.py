@@ -118,6 +118,55 @@ def zipf_workload(n: int, data_len: int = 512, n_dims: int = 1, num_sites: int =
     return Workload(alpha, left, right, np.ascontiguousarray(roots), sites)
 
 
+def synthetic_centroids(num: int = 3233, seed: int = 0xC0DE) -> np.ndarray:
+    """County-centroid-shaped points (lat, lon) in degrees: mostly the contiguous US, a few in
+    Alaska, Hawaii and the territories — the shape of data/county_centroids.csv (3 233 rows,
+    lat -14.5..69.3, lon -171..145.8), synthesised here (the reference's file is not used)."""
+    rng = np.random.default_rng(seed)
+    n_ak, n_hi, n_terr = 30, 5, 78
+    n_us = num - n_ak - n_hi - n_terr
+    us = np.stack([rng.uniform(25.0, 49.0, n_us), rng.uniform(-124.5, -67.0, n_us)], 1)
+    ak = np.stack([rng.uniform(55.0, 69.3, n_ak), rng.uniform(-171.0, -130.0, n_ak)], 1)
+    hi = np.stack([rng.uniform(19.0, 22.2, n_hi), rng.uniform(-160.0, -155.0, n_hi)], 1)
+    terr = np.stack([rng.uniform(-14.5, 18.5, n_terr),
+                     np.where(rng.random(n_terr) < 0.8, rng.uniform(-67.3, -64.5, n_terr),
+                              rng.uniform(144.6, 145.8, n_terr))], 1)
+    return np.concatenate([us, ak, hi, terr])
+
+
+def geo_to_int(lat: np.ndarray, lon: np.ndarray):
+    """sample_driving_data.rs:11-15: centidegrees, rounded, as i16."""
+    return np.round(lat * 100.0).astype(np.int16), np.round(lon * 100.0).astype(np.int16)
+
+
+def coords_workload(n: int, ball_size: int = 1, num_centroids: int = 3233, zipf_s: float = 1.03,
+                    side_km: float = 10.0, seed: int = 0x5EED, client_offset: int = 0) -> Workload:
+    """Config D: d = 2 (lat, lon), data_len = 16. Points = Zipf-weighted county-like centroids
+    jittered uniformly in a side_km square (`uniform_in_square`, sample_covid_data.rs:45-62),
+    converted to i16 centidegrees; keys per `gen_l_inf_ball_from_coords` (ibDCF.rs:189-205):
+    bounds (c -/+ ball) clamped to +-9000 (lat) / +-18000 (lon), i16 -> 16 bits MSB first
+    (two's complement, sample_driving_data.rs:25-28)."""
+    cents = synthetic_centroids(num_centroids)
+    idx = zipf_indices(np.random.default_rng([seed, 11]), client_offset + n, num_centroids, zipf_s)[client_offset:]
+    jr = np.random.default_rng([seed, 12])
+    u = jr.random((client_offset + n, 2))[client_offset:]
+    lat0, lon0 = cents[idx, 0], cents[idx, 1]
+    a_lat = (side_km / 2.0) / 111.32
+    a_lon = (side_km / 2.0) / (111.32 * np.cos(np.radians(lat0)))
+    lat = np.clip(lat0 + (2 * u[:, 0] - 1) * a_lat, -90.0, 90.0)
+    lon = np.clip(lon0 + (2 * u[:, 1] - 1) * a_lon, -180.0, 180.0)
+    la, lo = geo_to_int(lat, lon)
+    la32, lo32 = la.astype(np.int32), lo.astype(np.int32)
+    b = int(ball_size)
+    left = np.stack([i16_to_bits(np.clip(la32 - b, -9000, 9000)), i16_to_bits(np.clip(lo32 - b, -18000, 18000))], 1)
+    right = np.stack([i16_to_bits(np.clip(la32 + b, -9000, 9000)), i16_to_bits(np.clip(lo32 + b, -18000, 18000))], 1)
+    alpha = np.stack([i16_to_bits(la32), i16_to_bits(lo32)], 1)
+    rrng = np.random.default_rng([seed, 13])
+    roots = rrng.integers(0, 256, size=(client_offset + n, 2, 2, 2, 16), dtype=np.uint8)[client_offset:]
+    return Workload(alpha, np.ascontiguousarray(left), np.ascontiguousarray(right), np.ascontiguousarray(roots),
+                    idx)
+
+
 def plaintext_heavy_hitters(alpha_left: np.ndarray, alpha_right: np.ndarray, threshold_count: int):
     """Brute-force recount (no crypto): heavy prefixes of the full depth whose box is
     contained in at least `threshold_count` clients' [l, r] boxes, crawled level by level

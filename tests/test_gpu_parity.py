@@ -246,3 +246,27 @@ def test_sim_crawl_matches_oracle_crawl(kc, oracle, d, n, L, sites, thr):
     else:
         assert st["aes_blocks"] * 2 <= ores.aes_blocks
         assert st["ref_evals"] * 2 == ores.aes_blocks
+
+
+def test_every_expand_variant_bit_exact(kc, oracle):
+    """All compiled k_expand variants (LDS layout / blocks per lane / workgroup size /
+    static or dynamic items) give the oracle's crawl, twice in a row (the dynamic-item
+    counter re-arms itself between launches)."""
+    import ctypes
+    from fuzzyheavyhitters_amd import lib, sim_crawl, workload
+    wl = workload.zipf_workload(700, 64, 1, num_sites=9, seed=5)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    ores = oracle.crawl(k0, k1, 0.01, mode="count")
+    exp_counts = np.concatenate(ores.counts)
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    v = 0
+    buf = ctypes.create_string_buffer(64)
+    while lib().fhh_variant_info(v, buf, 64, None, None) == 0:
+        c0.set_variant(v)
+        c1.set_variant(v)
+        for _ in range(2):
+            res = sim_crawl(c0, c1, 0.01, mode="count")
+            assert np.array_equal(np.concatenate(res.counts), exp_counts), f"variant {v} ({buf.value})"
+        s0, t0, y0 = c0.export_states()
+        v += 1
+    assert v >= 8

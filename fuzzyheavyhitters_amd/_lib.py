@@ -63,12 +63,14 @@ class FhhSimConfig(ctypes.Structure):
         ("level_kept", u64p),
         ("counts", u64p),
         ("counts_capacity", ctypes.c_uint64),
+        ("host_loop", ctypes.c_uint32),
+        ("init_capacity", ctypes.c_uint32),
     ]
 
 
 def build(verbose: bool = False) -> str:
     """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box)."""
-    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_microbench.hip", "fhh_host.cpp")]
+    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp")]
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            *srcs, "-o", LIB_PATH]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -8,6 +8,7 @@
 // on the host and never moves state (the reference does O(F) Vec::remove of whole nodes,
 // collect.rs:918-929).
 #include "fhh_internal.h"
+#include "field_arith.h"
 #include "../../include/fhh.h"
 
 #include <hip/hip_runtime.h>
@@ -240,86 +241,30 @@ void* stage_bytes(fhh_ctx* ctx, size_t bytes) {
 }
 
 // ---- FE / FE255 host arithmetic --------------------------------------------------------------
-uint64_t fe_canon_from_limbs(uint64_t lo, uint64_t hi) {
-    // value = lo + hi * 2^32 (< 2^96 for any realistic n), reduced mod p_FE
-    unsigned __int128 v = (unsigned __int128)lo + ((unsigned __int128)hi << 32);
-    return (uint64_t)(v % kFeP);
-}
+uint64_t fe_canon_from_limbs(uint64_t lo, uint64_t hi) { return fhh::fe_canon_from_limbs(lo, hi); }
 
 uint64_t fe_canon(uint64_t v) { return v % kFeP; }
 
 // carry-propagate 8 u64 limb sums (limb k weight 2^(32k)) into 10 u32 limbs
 Limbs10 limbs_from_partials(const uint64_t* p8) {
     Limbs10 out{};
-    unsigned __int128 carry = 0;
-    for (int k = 0; k < 10; k++) {
-        unsigned __int128 acc = carry + (k < 8 ? p8[k] : 0);
-        out[k] = (uint32_t)acc;
-        carry = acc >> 32;
-    }
+    fhh::limbs10_from_partials(p8, out.data());
     return out;
 }
 
-// x mod (2^255 - 19) for x given as 10 u32 limbs (< 2^320)
 std::array<uint32_t, 8> fe255_reduce(const Limbs10& x) {
-    // fold: x = hi * 2^255 + lo  ->  lo + 19 * hi, repeated
-    uint64_t w[5] = {0, 0, 0, 0, 0};
-    for (int k = 0; k < 10; k++) w[k / 2] |= (uint64_t)x[k] << (32 * (k % 2));
-    for (int iter = 0; iter < 3; iter++) {
-        uint64_t hi[2] = {(w[3] >> 63) | (w[4] << 1), w[4] >> 63};
-        uint64_t lo[4] = {w[0], w[1], w[2], w[3] & 0x7FFFFFFFFFFFFFFFull};
-        unsigned __int128 acc = (unsigned __int128)lo[0] + (unsigned __int128)hi[0] * 19;
-        w[0] = (uint64_t)acc;
-        acc = (acc >> 64) + lo[1] + (unsigned __int128)hi[1] * 19;
-        w[1] = (uint64_t)acc;
-        acc = (acc >> 64) + lo[2];
-        w[2] = (uint64_t)acc;
-        acc = (acc >> 64) + lo[3];
-        w[3] = (uint64_t)acc;
-        w[4] = (uint64_t)(acc >> 64);
-    }
-    // now w < 2^255 + small; conditional subtract p
-    for (int iter = 0; iter < 2; iter++) {
-        uint64_t t[4];
-        unsigned __int128 acc = (unsigned __int128)w[0] + 19;
-        t[0] = (uint64_t)acc;
-        for (int k = 1; k < 4; k++) {
-            acc = (acc >> 64) + w[k];
-            t[k] = (uint64_t)acc;
-        }
-        if (t[3] >> 63) {   // w >= p
-            w[0] = t[0];
-            w[1] = t[1];
-            w[2] = t[2];
-            w[3] = t[3] & 0x7FFFFFFFFFFFFFFFull;
-        }
-    }
     std::array<uint32_t, 8> out{};
-    for (int k = 0; k < 8; k++) out[k] = (uint32_t)(w[k / 2] >> (32 * (k % 2)));
+    fhh::fe255_reduce(x.data(), out.data());
     return out;
 }
 
-// (a - b) mod p255 on canonical values
 std::array<uint32_t, 8> fe255_sub(const std::array<uint32_t, 8>& a, const std::array<uint32_t, 8>& b) {
-    // a + p - b (> 0 for a, b < p), then reduce
-    static const uint32_t P[8] = {0xFFFFFFED, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF,
-                                  0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0x7FFFFFFF};
-    Limbs10 x{};
-    int64_t carry = 0;
-    for (int k = 0; k < 8; k++) {
-        const int64_t v = (int64_t)a[k] + (int64_t)P[k] - (int64_t)b[k] + carry;
-        x[k] = (uint32_t)((uint64_t)v & 0xFFFFFFFFull);
-        carry = (v - (int64_t)x[k]) / ((int64_t)1 << 32);
-    }
-    x[8] = (uint32_t)carry;
-    return fe255_reduce(x);
+    std::array<uint32_t, 8> out{};
+    fhh::fe255_sub(a.data(), b.data(), out.data());
+    return out;
 }
 
-bool fe255_ge_u32(const std::array<uint32_t, 8>& v, uint32_t t) {
-    for (int k = 7; k >= 1; k--)
-        if (v[k]) return true;
-    return v[0] >= t;
-}
+bool fe255_ge_u32(const std::array<uint32_t, 8>& v, uint32_t t) { return fhh::fe255_ge_u32(v.data(), t); }
 
 // ---- device key / table management -----------------------------------------------------------
 int alloc_keys(fhh_ctx* ctx, uint64_t n) {
@@ -730,6 +675,376 @@ int set_device(fhh_ctx* ctx) {
 }
 
 }  // namespace
+
+// ---- device-resident level loop (fhh_sim_crawl, host_loop = 0) ---------------------------------
+struct LoopBuffers {
+    DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
+    std::vector<DevBuf*> hist_epochs;            // hist rows; a new epoch per F_cap growth
+    std::vector<uint32_t*> hist_ptr;             // per level
+    uint32_t E_cap = 0, F_cap = 0;
+    PinnedBuf ctl_host, rec;                     // ctl readback; per-level partial records
+    std::vector<size_t> rec_off;                 // per level offset (u64) into rec
+    std::vector<uint32_t> rec_stride;            // per level C_cap at that time
+    ~LoopBuffers() {
+        for (auto* b : hist_epochs) delete b;
+    }
+};
+
+uint32_t next_pow2(uint32_t v) {
+    uint32_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+// grow one buffer of a dim table, preserving the first `keep` entries
+int table_grow(fhh_ctx* ctx, DimTable& T, int buf, size_t cap, size_t keep) {
+    if (cap <= T.cap[buf] && T.seed[buf].p) return FHH_OK;
+    DevBuf ns, nt, ny;
+    HIP_TRY(ctx, ns.ensure(cap * 2 * ctx->npad * 16));
+    HIP_TRY(ctx, nt.ensure(cap * 2 * ctx->nw * 8));
+    HIP_TRY(ctx, ny.ensure(cap * 2 * ctx->nw * 8));
+    if (keep) {
+        HIP_TRY(ctx, hipMemcpyAsync(ns.p, T.seed[buf].p, keep * 2 * ctx->npad * 16, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(nt.p, T.t[buf].p, keep * 2 * ctx->nw * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(ny.p, T.y[buf].p, keep * 2 * ctx->nw * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    std::swap(T.seed[buf].p, ns.p);
+    std::swap(T.seed[buf].bytes, ns.bytes);
+    std::swap(T.t[buf].p, nt.p);
+    std::swap(T.t[buf].bytes, nt.bytes);
+    std::swap(T.y[buf].p, ny.p);
+    std::swap(T.y[buf].bytes, ny.bytes);
+    T.cap[buf] = cap;
+    return FHH_OK;
+}
+
+// (re)size the loop buffers; preserve what a resumed prune of `level` still reads
+int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uint32_t levels, uint32_t level,
+                bool preserve, uint32_t keep_nodes, uint32_t keep_children, uint32_t per) {
+    const uint32_t d = c0->d;
+    const size_t C_old = (size_t)B.F_cap << d, C_new = (size_t)F_cap << d;
+    HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+    for (int b = 0; b < 2; b++) {
+        DevBuf nl;
+        HIP_TRY(c0, nl.ensure((size_t)d * E_cap * 4));
+        std::swap(B.live[b].p, nl.p);
+        std::swap(B.live[b].bytes, nl.bytes);
+        DevBuf np;
+        HIP_TRY(c0, np.ensure((size_t)F_cap * d * 4));
+        const int keep_par = level & 1;
+        if (preserve && b == keep_par && keep_nodes)
+            HIP_TRY(c0, hipMemcpy(np.p, B.pos[b].p, (size_t)keep_nodes * d * 4, hipMemcpyDeviceToDevice));
+        std::swap(B.pos[b].p, np.p);
+        std::swap(B.pos[b].bytes, np.bytes);
+    }
+    HIP_TRY(c0, B.mark.ensure((size_t)d * E_cap * 4));
+    {
+        DevBuf npart;
+        HIP_TRY(c0, npart.ensure(C_new * 16 * 8));
+        if (preserve && keep_children)
+            HIP_TRY(c0, hipMemcpy(npart.p, B.partials.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice));
+        std::swap(B.partials.p, npart.p);
+        std::swap(B.partials.bytes, npart.bytes);
+    }
+    (void)C_old;
+    // hist rows for levels >= level live in a new epoch of stride F_cap
+    DevBuf* ep = new DevBuf();
+    if (ep->ensure((size_t)(levels - level) * F_cap * 4) != hipSuccess) {
+        delete ep;
+        return c0->fail(FHH_E_NOMEM, "loop: hist allocation failed");
+    }
+    B.hist_epochs.push_back(ep);
+    B.hist_ptr.resize(levels, nullptr);
+    for (uint32_t lv = level; lv < levels; lv++) B.hist_ptr[lv] = ep->as<uint32_t>() + (size_t)(lv - level) * F_cap;
+    B.E_cap = E_cap;
+    B.F_cap = F_cap;
+    return FHH_OK;
+}
+
+int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, uint32_t levels, uint64_t thr,
+                          uint32_t thr_last) {
+    const uint32_t d = c0->d;
+    const int variant = c0->variant;
+    const uint64_t grid_waves = (uint64_t)c0->grid * (expand_threads(variant) / 64);
+    const uint32_t per_level_per = cfg->mode == 0 ? 1 : 4;   // partial u64 per child (non-last)
+    LoopBuffers B;
+    uint32_t cap0 = cfg->init_capacity ? next_pow2(cfg->init_capacity) : 256;
+    // tables: both buffers of every dim of both servers hold >= E_cap entries
+    fhh_ctx* cs[2] = {c0, c1};
+    for (fhh_ctx* c : cs)
+        for (uint32_t j = 0; j < d; j++)
+            for (int b = 0; b < 2; b++) {
+                int rc = table_grow(c, c->tab[j], b, std::max<size_t>(cap0, c->tab[j].cap[b]), 0);
+                if (rc) return rc;
+            }
+    int rc = fhh_tree_init(c0);   // fills buffer 0 with the roots (after the growth above)
+    if (rc) return rc;
+    rc = fhh_tree_init(c1);
+    if (rc) return rc;
+    PairScope pair(c0, c1);
+    HIP_TRY(c0, B.ctl.ensure(sizeof(LoopCtl)));
+    HIP_TRY(c0, B.sizes.ensure((size_t)levels * (4 + kMaxDims) * 4));
+    HIP_TRY(c0, hipMemsetAsync(B.sizes.p, 0, (size_t)levels * (4 + kMaxDims) * 4, c0->stream));
+    HIP_TRY(c0, B.ctl_host.ensure(sizeof(LoopCtl)));
+    rc = loop_resize(c0, B, cap0, cap0, levels, 0, false, 0, 0, 1);
+    if (rc) return rc;
+    {
+        uint32_t* l0[kMaxDims] = {nullptr, nullptr, nullptr, nullptr};
+        for (uint32_t j = 0; j < d; j++) l0[j] = B.live[0].as<uint32_t>() + (size_t)j * B.E_cap;
+        for (uint32_t j = d; j < kMaxDims; j++) l0[j] = l0[0];
+        HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, (uint32_t)c0->nw, d, 2, grid_waves,
+                                     B.pos[0].as<uint32_t>(), l0, c0->stream));
+    }
+    const bool record = cfg->counts != nullptr;
+    const uint32_t kBatch = 32;
+    bool prune_only = false;           // resume after growth: prune of this level only
+    for (uint32_t lv = 0; lv < levels;) {
+        const bool last = lv + 1 == levels;
+        const int par = lv & 1;
+        const uint32_t pmode = cfg->mode == 0 ? 0 : (last ? 2 : 1);
+        const uint32_t per = pmode == 0 ? 1 : (pmode == 1 ? 4 : 16);
+        const uint64_t C_cap = (uint64_t)B.F_cap << d;
+        if (!prune_only) {
+            // -- k_expand, both servers, sizes from LoopCtl
+            ExpandLaunch La{};
+            La.njobs = 2 * d;
+            La.jobs_per_ctx = d;
+            La.ctl = B.ctl.as<LoopCtl>();
+            for (int s = 0; s < 2; s++)
+                for (uint32_t j = 0; j < d; j++) {
+                    fhh_ctx* c = cs[s];
+                    DimTable& T = c->tab[j];
+                    ExpandJob& J = La.job[s * d + j];
+                    J.cw_seed = c->cw_seed.as<uint4>();
+                    J.cw_bits = c->cw_bits.as<uint64_t>();
+                    J.src_seed = T.seed[par].as<uint4>();
+                    J.src_t = T.t[par].as<uint64_t>();
+                    J.src_y = T.y[par].as<uint64_t>();
+                    J.dst_seed = T.seed[1 - par].as<uint4>();
+                    J.dst_t = T.t[1 - par].as<uint64_t>();
+                    J.dst_y = T.y[1 - par].as<uint64_t>();
+                    J.live = B.live[par].as<uint32_t>() + (size_t)j * B.E_cap;
+                    J.level = lv;
+                    J.dim = j;
+                    J.K = c->K;
+                    J.npad = (uint32_t)c->npad;
+                    J.nw = (uint32_t)c->nw;
+                }
+            size_t slot = 0;
+            if (c0->timing) HIP_TRY(c0, timing_begin(c0, &slot));
+            La.total_items = 1;   // non-zero: the real count comes from LoopCtl
+            HIP_TRY(c0, launch_expand(La, variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
+            if (c0->timing) HIP_TRY(c0, timing_end(c0, slot, 0));
+            c0->stats.expand_launches++;
+            // -- equality count / simulated OT sums per child
+            ChildArgs a{};
+            for (uint32_t j = 0; j < d; j++) {
+                a.s0.t[j] = c0->tab[j].t[1 - par].as<uint64_t>();
+                a.s0.y[j] = c0->tab[j].y[1 - par].as<uint64_t>();
+                a.s1.t[j] = c1->tab[j].t[1 - par].as<uint64_t>();
+                a.s1.y[j] = c1->tab[j].y[1 - par].as<uint64_t>();
+            }
+            a.parent_pos = B.pos[par].as<uint32_t>();
+            a.valid = c0->valid.as<uint64_t>();
+            a.C = C_cap;   // grid hint; the real C comes from LoopCtl
+            a.d = d;
+            a.nw = (uint32_t)c0->nw;
+            a.client_base = c0->client_base;
+            a.prf_seed = cfg->prf_seed;
+            a.level = lv;
+            a.n = (uint32_t)c0->n;
+            a.ctl = B.ctl.as<LoopCtl>();
+            uint64_t* part = B.partials.as<uint64_t>();
+            if (pmode == 0) HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
+            else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream));
+            else HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
+            // -- cross-rank sum (client-sharded multi-GPU)
+            if (cfg->allreduce) {
+                const uint64_t count = C_cap * per;
+                if (!cfg->xchg_dev || cfg->xchg_capacity < count)
+                    return c0->fail(FHH_E_ARG, "sim: all-reduce exchange buffer too small");
+                HIP_TRY(c0, hipMemcpyAsync(cfg->xchg_dev, part, count * 8, hipMemcpyDeviceToDevice, c0->stream));
+                rc = sync(c0);
+                if (rc) return rc;
+                if (cfg->allreduce(cfg->xchg_dev, count, cfg->allreduce_user) != 0)
+                    return c0->fail(FHH_E_CALLBACK, "all-reduce callback failed");
+                HIP_TRY(c0, hipMemcpyAsync(part, cfg->xchg_dev, count * 8, hipMemcpyDeviceToDevice, c0->stream));
+            }
+            if (record) {
+                const size_t off = B.rec_off.empty() ? 0 : B.rec_off.back() + (size_t)B.rec_stride.back();
+                const size_t need = (off + C_cap * per) * 8;
+                if (B.rec.bytes < need) {
+                    PinnedBuf nb;
+                    HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+                    HIP_TRY(c0, nb.ensure(std::max(need * 2, (size_t)1 << 20)));
+                    if (B.rec.p) std::memcpy(nb.p, B.rec.p, B.rec.bytes);
+                    std::swap(B.rec.p, nb.p);
+                    std::swap(B.rec.bytes, nb.bytes);
+                }
+                B.rec_off.resize(lv + 1);
+                B.rec_stride.resize(lv + 1);
+                B.rec_off[lv] = off;
+                B.rec_stride[lv] = (uint32_t)(C_cap * per);   // u64 words recorded for this level
+                // mode 0: counts; FE: the 4 limbs; FE255: the 16 limbs (v0 - v1 derived at the end)
+                const size_t cpy = (size_t)C_cap * per * 8;
+                HIP_TRY(c0, hipMemcpyAsync(B.rec.as<uint64_t>() + off, part, cpy, hipMemcpyDeviceToHost, c0->stream));
+            }
+        }
+        prune_only = false;
+        // -- leader keep decision + prune (or final list at the last level)
+        if (last) HIP_TRY(c0, B.final_vals.ensure((size_t)B.F_cap * 20 * 4));
+        PruneArgs pa{};
+        pa.ctl = B.ctl.as<LoopCtl>();
+        pa.partials = B.partials.as<uint64_t>();
+        pa.mode = pmode;
+        pa.d = d;
+        pa.thr = thr;
+        pa.thr_last = thr_last;
+        pa.last = last ? 1 : 0;
+        pa.pos_in = B.pos[par].as<uint32_t>();
+        pa.pos_out = B.pos[1 - par].as<uint32_t>();
+        for (uint32_t j = 0; j < kMaxDims; j++)
+            pa.live_out[j] = B.live[1 - par].as<uint32_t>() + (size_t)std::min(j, d - 1) * B.E_cap;
+        pa.mark = B.mark.as<uint32_t>();
+        pa.hist_out = B.hist_ptr[lv];
+        pa.sizes_out = B.sizes.as<uint32_t>() + (size_t)lv * (4 + kMaxDims);
+        pa.final_vals = last ? B.final_vals.as<uint32_t>() : nullptr;
+        pa.E_cap = B.E_cap;
+        pa.F_cap = B.F_cap;
+        pa.level = lv;
+        pa.nw = (uint32_t)c0->nw;
+        pa.njobs_per_ctx = d;
+        pa.nctx = 2;
+        pa.grid_waves = grid_waves;
+        HIP_TRY(c0, launch_prune(pa, c0->stream));
+        lv++;
+        if (lv % kBatch == 0 || lv == levels) {
+            HIP_TRY(c0, hipMemcpyAsync(B.ctl_host.p, B.ctl.p, sizeof(LoopCtl), hipMemcpyDeviceToHost, c0->stream));
+            rc = sync(c0);
+            if (rc) return rc;
+            const LoopCtl* h = B.ctl_host.as<LoopCtl>();
+            if (h->abort) {
+                // grow, keep what the prune of abort_level reads, resume there
+                const uint32_t la = h->abort_level;
+                const bool la_last = la + 1 == levels;
+                const uint32_t nE = std::max(B.E_cap, next_pow2(std::max<uint32_t>(h->need_entries, 1)) * 2);
+                const uint32_t nF = std::max(B.F_cap, next_pow2(std::max<uint32_t>(h->need_nodes, 1)) * 2);
+                const uint32_t la_per = cfg->mode == 0 ? 1 : (la_last ? 16 : 4);
+                for (fhh_ctx* c : cs)
+                    for (uint32_t j = 0; j < d; j++) {
+                        // child tables of level la (parity 1 - la&1) hold 2 * n_live(la) entries
+                        rc = table_grow(c, c->tab[j], 1 - (la & 1), nE, 2 * (size_t)h->n_live[j]);
+                        if (rc) return rc;
+                        rc = table_grow(c, c->tab[j], la & 1, nE, 0);
+                        if (rc) return rc;
+                    }
+                rc = loop_resize(c0, B, nE, nF, levels, la, true, h->F, h->C, la_per);
+                if (rc) return rc;
+                const uint32_t zero = 0;
+                HIP_TRY(c0, hipMemcpy(B.ctl.p, &zero, 4, hipMemcpyHostToDevice));   // abort = 0
+                lv = la;
+                prune_only = true;
+                (void)per_level_per;
+            }
+        }
+    }
+    // ---- readback: sizes, hist, final values -> host-side state of both servers ----
+    std::vector<uint32_t> sz((size_t)levels * (4 + kMaxDims));
+    HIP_TRY(c0, hipMemcpy(sz.data(), B.sizes.p, sz.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist(levels);
+    const uint32_t mask = (1u << d) - 1;
+    for (uint32_t lv = 0; lv < levels; lv++) {
+        const uint32_t nf = sz[(size_t)lv * (4 + kMaxDims) + 1];
+        std::vector<uint32_t> hc(nf);
+        if (nf) HIP_TRY(c0, hipMemcpy(hc.data(), B.hist_ptr[lv], (size_t)nf * 4, hipMemcpyDeviceToHost));
+        hist[lv].reserve(nf);
+        for (uint32_t c : hc) hist[lv].emplace_back(c >> d, c & mask);
+    }
+    const uint32_t nfin = sz[(size_t)(levels - 1) * (4 + kMaxDims) + 1];
+    std::vector<uint32_t> fv((size_t)nfin * 20);
+    if (nfin) HIP_TRY(c0, hipMemcpy(fv.data(), B.final_vals.p, fv.size() * 4, hipMemcpyDeviceToHost));
+    // frontier before the last crawl: depth levels-1, states in table buffer (levels-1)&1
+    const int fpar = (levels - 1) & 1;
+    const uint32_t Ffront = levels >= 2 ? sz[(size_t)(levels - 2) * (4 + kMaxDims) + 1] : 1;
+    std::vector<uint32_t> fpos((size_t)Ffront * d);
+    if (Ffront) HIP_TRY(c0, hipMemcpy(fpos.data(), B.pos[fpar].p, fpos.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<std::vector<uint32_t>> flive(d);
+    for (uint32_t j = 0; j < d; j++) {
+        const uint32_t nl = levels >= 2 ? sz[(size_t)(levels - 2) * (4 + kMaxDims) + 4 + j] : 1;
+        flive[j].resize(nl);
+        if (nl)
+            HIP_TRY(c0, hipMemcpy(flive[j].data(), B.live[fpar].as<uint32_t>() + (size_t)j * B.E_cap, (size_t)nl * 4,
+                                  hipMemcpyDeviceToHost));
+    }
+    for (int s = 0; s < 2; s++) {
+        fhh_ctx* c = cs[s];
+        c->hist.assign(hist.begin(), hist.begin() + (levels - 1));
+        c->last_hist = c->hist;
+        c->last_depth = levels;
+        c->last_nodes = hist[levels - 1];
+        c->last_values.assign(nfin, Limbs10{});
+        for (uint32_t k = 0; k < nfin; k++) {
+            if (cfg->mode == 0 && s == 1) continue;   // count mode: values on server 0 (host loop convention)
+            std::memcpy(c->last_values[k].data(), &fv[(size_t)k * 20 + (cfg->mode == 0 ? 0 : 10 * s)], 40);
+        }
+        c->frontier.assign(Ffront, Node{});
+        for (uint32_t k = 0; k < Ffront; k++)
+            for (uint32_t j = 0; j < d; j++) c->frontier[k].pos[j] = fpos[(size_t)k * d + j];
+        for (uint32_t j = 0; j < d; j++) {
+            c->tab[j].live = flive[j];
+            c->tab[j].cur = fpar;
+            c->child_buf[j] = 1 - fpar;
+        }
+        c->level = levels - 1;
+        c->pending_C = 0;
+        c->phase = Phase::kFrontier;   // after tree_prune_last (collect.rs:931-942)
+        for (uint32_t lv = 0; lv < levels; lv++) {
+            const uint32_t* row = &sz[(size_t)lv * (4 + kMaxDims)];
+            uint64_t live_sum = 0;
+            for (uint32_t j = 0; j < d; j++) live_sum += lv == 0 ? 1 : sz[(size_t)(lv - 1) * (4 + kMaxDims) + 4 + j];
+            c->stats.aes_blocks += live_sum * 4 * c->n;
+            c->stats.ref_evals += (uint64_t)row[0] * c->n * 2 * d;
+            c->stats.levels += 1;
+        }
+    }
+    // expand_blocks_timed for c0's timed launches: both servers
+    {
+        uint64_t blocks = 0;
+        for (uint32_t lv = 0; lv < levels; lv++) {
+            uint64_t live_sum = 0;
+            for (uint32_t j = 0; j < d; j++) live_sum += lv == 0 ? 1 : sz[(size_t)(lv - 1) * (4 + kMaxDims) + 4 + j];
+            blocks += live_sum * 4 * c0->n * 2;
+        }
+        if (c0->timing) c0->stats.expand_blocks_timed += blocks;
+    }
+    // optional per-level records
+    uint64_t off = 0;
+    for (uint32_t lv = 0; lv < levels; lv++) {
+        const uint32_t C = sz[(size_t)lv * (4 + kMaxDims)];
+        if (cfg->level_children) cfg->level_children[lv] = C;
+        if (cfg->level_kept) cfg->level_kept[lv] = sz[(size_t)lv * (4 + kMaxDims) + 1];
+        if (record && lv < B.rec_off.size()) {
+            const uint64_t* r = B.rec.as<uint64_t>() + B.rec_off[lv];
+            const bool lvl_last = lv + 1 == levels;
+            for (uint32_t c = 0; c < C && off + c < cfg->counts_capacity; c++) {
+                uint64_t v;
+                if (cfg->mode == 0) {
+                    v = r[c];
+                } else if (!lvl_last) {
+                    v = fe_sub_canon(fe_canon_from_limbs(r[c * 4], r[c * 4 + 1]), fe_canon_from_limbs(r[c * 4 + 2], r[c * 4 + 3]));
+                } else {
+                    const auto dv = fe255_sub(fe255_reduce(limbs_from_partials(r + (size_t)c * 16)),
+                                              fe255_reduce(limbs_from_partials(r + (size_t)c * 16 + 8)));
+                    v = (uint64_t)dv[0] | ((uint64_t)dv[1] << 32);
+                }
+                cfg->counts[off + c] = v;
+            }
+        }
+        off += C;
+    }
+    return FHH_OK;
+}
 
 // ================================================================================================
 // C ABI
@@ -1212,15 +1527,17 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
     if (levels > c0->L) return c0->fail(FHH_E_ARG, "sim_crawl: levels > data_len");
     if (cfg->mode > 1) return c0->fail(FHH_E_ARG, "sim_crawl: bad mode");
+    if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");
+    if (c0->d != c1->d || c0->L != c1->L) return c0->fail(FHH_E_ARG, "sim_crawl: ctx shapes differ");
+    // leader.rs:193-194 and 245-246
+    const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
+    const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));
+    if (!cfg->host_loop) return sim_crawl_device_loop(c0, c1, cfg, levels, thr, thr_last);
     rc = fhh_tree_init(c0);
     if (rc) return rc;
     rc = fhh_tree_init(c1);
     if (rc) return rc;
-    if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");
     PairScope pair(c0, c1);
-    // leader.rs:193-194 and 245-246
-    const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
-    const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));
     uint64_t counts_off = 0;
     std::vector<uint64_t> vals, s0, s1;
     std::vector<uint32_t> l0, l1;

@@ -43,11 +43,30 @@ struct ExpandJob {
     uint64_t item_begin;
 };
 
+// Device-resident level loop (fhh_sim_crawl with the GPU loop): the frontier sizes live in
+// device memory, written by k_prune and read by the next level's kernels, so a whole crawl is
+// enqueued without host round trips. `abort` is sticky: once a capacity check fails every
+// later kernel is a no-op and the host grows the buffers and resumes from abort_level.
+struct LoopCtl {
+    uint32_t abort;
+    uint32_t abort_level;
+    uint32_t need_entries;      // entries a dim table must hold to continue
+    uint32_t need_nodes;        // frontier nodes to continue
+    uint32_t F;                 // frontier nodes
+    uint32_t C;                 // pending children (F << d)
+    uint32_t n_live[kMaxDims];  // live entries per dim (same for both servers)
+    uint32_t group;             // entries per work item for the next k_expand
+    uint32_t pad_;
+    uint64_t item_begin[kMaxJobs];
+    uint64_t total_items;
+};
+
 struct ExpandLaunch {
     ExpandJob job[kMaxJobs];
     uint32_t njobs;
-    uint32_t pad_;
+    uint32_t jobs_per_ctx;      // = d (LoopCtl::n_live index = job % jobs_per_ctx)
     uint64_t total_items;
+    const LoopCtl* ctl;         // non-null: n_live / group / item_begin / total_items from here
 };
 
 // Pending children: child c -> parent p = c >> d, i = c & (2^d - 1); its dim-j entry in
@@ -68,6 +87,30 @@ struct ChildArgs {
     uint64_t prf_seed;
     uint32_t level;
     uint32_t n;                 // real clients on this ctx
+    const LoopCtl* ctl;         // non-null: C from here (0 once aborted)
+};
+
+struct PruneArgs {
+    LoopCtl* ctl;
+    const uint64_t* partials;   // [C][per] u64 (after the cross-rank sum)
+    uint32_t mode;              // 0 counts, 1 FE limbs [C][4], 2 FE255 limbs [C][16] (last level)
+    uint32_t d;
+    uint64_t thr;               // leader.rs:193-194
+    uint32_t thr_last;          // leader.rs:245-246
+    uint32_t last;              // tree_crawl_last: record final values
+    const uint32_t* pos_in;     // [F][d]
+    uint32_t* pos_out;          // [F'][d]
+    uint32_t* live_out[kMaxDims];
+    uint32_t* mark;             // scratch [kMaxDims][E_cap]
+    uint32_t* hist_out;         // [F_cap] kept children of this level (child index c)
+    uint32_t* sizes_out;        // [4 + kMaxDims]: C, F', abort, -, n_live'...
+    uint32_t* final_vals;       // last level: [F_cap][20] u32 (server 0 / server 1 unreduced)
+    uint32_t E_cap, F_cap;
+    uint32_t level;
+    uint32_t nw;
+    uint32_t njobs_per_ctx;     // = d
+    uint32_t nctx;              // 2 (pair)
+    uint64_t grid_waves;        // persistent k_expand waves (for the group size)
 };
 
 struct KeygenArgs {
@@ -102,5 +145,9 @@ hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
                                 hipStream_t stream);
 // occupancy-derived persistent grid for k_expand variant on `device`
 int expand_grid(int device, int variant);
+// device-resident level loop (fhh_loop.hip)
+hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
+                            uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims], hipStream_t stream);
 
 }  // namespace fhh

@@ -196,17 +196,30 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     Tab::bases(lane, b0, b1);
     const uint64_t wpb = THR / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    // sizes: kernel arguments (host-driven crawl) or LoopCtl (device-resident loop)
+    const LoopCtl* ctl = a.ctl;
+    const uint64_t total = ctl ? (ctl->abort ? 0 : ctl->total_items) : a.total_items;
     uint64_t item = work_counter ? 0 : (uint64_t)blockIdx.x * wpb + wave_id_uniform();
     if (work_counter) {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(work_counter, 1u);
         item = __builtin_amdgcn_readfirstlane(v);
     }
-    while (item < a.total_items) {
+    while (item < total) {
         uint32_t ji = 0;
-        while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
-        if constexpr (PF) expand_item_pf<Tab>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
-        else expand_item<Tab, NB>(a.job[ji], item - a.job[ji].item_begin, tbl, lane, b0, b1);
+        if (ctl) {
+            while (ji + 1 < a.njobs && item >= ctl->item_begin[ji + 1]) ji++;
+        } else {
+            while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
+        }
+        ExpandJob J = a.job[ji];
+        if (ctl) {
+            J.n_live = ctl->n_live[ji % a.jobs_per_ctx];
+            J.group = ctl->group;
+            J.item_begin = ctl->item_begin[ji];
+        }
+        if constexpr (PF) expand_item_pf<Tab>(J, item - J.item_begin, tbl, lane, b0, b1);
+        else expand_item<Tab, NB>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
             uint32_t v = 0;
             if (lane == 0) v = atomicAdd(work_counter, 1u);
@@ -270,7 +283,8 @@ hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t*
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;
     const uint64_t blocks_needed = (a.total_items + wpb - 1) / wpb;
-    const int g = (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
+    // device-resident loop: the item count is only known on the device -> full persistent grid
+    const int g = a.ctl ? grid : (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
     // dynamic mode: work_counter[0..1] must be zero at launch; the kernel re-arms it on exit
     uint32_t* ctr = vi.dynamic ? work_counter : nullptr;
     switch (variant) {
@@ -325,6 +339,10 @@ __device__ __forceinline__ void block_sum_u64(uint64_t (&v)[NV], uint64_t* red /
     __syncthreads();
 }
 
+__device__ __forceinline__ uint64_t child_count(const ChildArgs& a) {
+    return a.ctl ? (a.ctl->abort ? 0 : a.ctl->C) : a.C;
+}
+
 __device__ __forceinline__ void child_entries(const ChildArgs& a, uint64_t c, uint32_t (&e)[kMaxDims]) {
     const uint64_t p = c >> a.d;
     const uint32_t i = (uint32_t)(c & ((1u << a.d) - 1));
@@ -353,7 +371,8 @@ __device__ __forceinline__ uint64_t eq_word(const ChildArgs& a, const uint32_t (
 
 __global__ __launch_bounds__(kReduceThreads) void k_eq_count(ChildArgs a, uint64_t* counts) {
     __shared__ uint64_t red[kReduceThreads / 64];
-    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         uint64_t v[1] = {0};
@@ -373,7 +392,8 @@ hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t str
 
 // out [C][2d][nw]: left dims then right dims, E = y ^ t (collect.rs:399-405)
 __global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, uint64_t* out) {
-    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) {
@@ -410,7 +430,8 @@ constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[4 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         const uint64_t bc = mix64(base ^ c);
@@ -462,7 +483,8 @@ __device__ __forceinline__ void fe255_canon(uint64_t (&x)[4]) {
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[16 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    for (uint64_t c = blockIdx.x; c < a.C; c += gridDim.x) {
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         const uint64_t bc = mix64(base ^ c);

@@ -1,0 +1,211 @@
+// Device-resident level loop: the leader's keep decision and the servers' prune
+// (keep_values / keep_values_last, collect.rs:945-989; tree_prune, collect.rs:918-929) run on
+// the GPU so that k_expand -> count/sums -> [all-reduce] -> k_prune repeat without host round
+// trips. Sizes of the next level live in LoopCtl (device memory).
+//
+// k_prune is one 1024-thread workgroup: C (children) and n_live (entries) are at most a few
+// thousand, so the scans fit one workgroup.
+#include "fhh_internal.h"
+#include "field_arith.h"
+
+namespace fhh {
+
+constexpr int kPruneThreads = 1024;
+
+// exclusive scan of one u32 per thread over the workgroup; *total = sum (uniform)
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds /*[16]*/, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+    for (uint32_t i = 0; i < nw; i++) {
+        const uint32_t t = lds[i];
+        if (i < wid) wbase += t;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + x - v;
+}
+
+__device__ __forceinline__ bool keep_of(const PruneArgs& a, uint32_t c) {
+    if (a.mode == 0) return a.partials[c] >= (a.last ? (uint64_t)a.thr_last : a.thr);
+    if (a.mode == 1) {
+        const uint64_t* p = a.partials + (size_t)c * 4;
+        const uint64_t s0 = fe_canon_from_limbs(p[0], p[1]), s1 = fe_canon_from_limbs(p[2], p[3]);
+        return fe_sub_canon(s0, s1) >= a.thr % kFieldFeP;
+    }
+    const uint64_t* p = a.partials + (size_t)c * 16;
+    uint32_t v0[10], v1[10], r0[8], r1[8], d[8];
+    limbs10_from_partials(p, v0);
+    limbs10_from_partials(p + 8, v1);
+    fe255_reduce(v0, r0);
+    fe255_reduce(v1, r1);
+    fe255_sub(r0, r1, d);
+    return fe255_ge_u32(d, a.thr_last);
+}
+
+__global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
+    __shared__ uint32_t lds[16];
+    LoopCtl* ctl = a.ctl;
+    if (ctl->abort) return;
+    const uint32_t C = ctl->C, d = a.d, mask = (1u << d) - 1;
+
+    // 1. keep flags -> ordered list of kept children (tree_prune keeps order, collect.rs:918-929)
+    uint32_t nf = 0;
+    for (uint32_t base = 0; base < C; base += blockDim.x) {
+        const uint32_t c = base + threadIdx.x;
+        const uint32_t flag = (c < C && keep_of(a, c)) ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(flag, lds, &tot);
+        if (flag && nf + ex < a.F_cap) a.hist_out[nf + ex] = c;
+        nf += tot;
+    }
+    if (threadIdx.x == 0) {
+        a.sizes_out[0] = C;
+        a.sizes_out[1] = nf;
+    }
+    __syncthreads();
+
+    if (a.last) {
+        // tree_crawl_last: the kept children are frontier_last; record their values
+        if (nf > a.F_cap) {
+            if (threadIdx.x == 0) {
+                ctl->need_nodes = nf;
+                ctl->abort_level = a.level;
+                ctl->abort = 1;
+                a.sizes_out[2] = 1;
+            }
+            return;
+        }
+        for (uint32_t k = threadIdx.x; k < nf; k += blockDim.x) {
+            const uint32_t c = a.hist_out[k];
+            uint32_t* out = a.final_vals + (size_t)k * 20;
+            if (a.mode == 2) {
+                limbs10_from_partials(a.partials + (size_t)c * 16, out);
+                limbs10_from_partials(a.partials + (size_t)c * 16 + 8, out + 10);
+            } else {
+                const uint64_t v = a.mode == 0 ? a.partials[c]
+                                               : fe_sub_canon(fe_canon_from_limbs(a.partials[c * 4], a.partials[c * 4 + 1]),
+                                                              fe_canon_from_limbs(a.partials[c * 4 + 2],
+                                                                                  a.partials[c * 4 + 3]));
+                for (int q = 0; q < 20; q++) out[q] = 0;
+                out[0] = (uint32_t)v;
+                out[1] = (uint32_t)(v >> 32);
+            }
+        }
+        return;   // frontier unchanged by tree_crawl_last (collect.rs:909-914)
+    }
+
+    // 2. per dim: referenced child entries -> new live list (sorted) and node positions
+    uint32_t n_live_new[kMaxDims] = {0, 0, 0, 0};
+    bool fits = nf <= a.F_cap;
+    for (uint32_t j = 0; j < d && fits; j++) {
+        const uint32_t E = 2 * ctl->n_live[j];
+        uint32_t* mk = a.mark + (size_t)j * a.E_cap;
+        for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) mk[e] = 0;
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nf; k += blockDim.x) {
+            const uint32_t c = a.hist_out[k], p = c >> d, i = c & mask;
+            mk[2 * a.pos_in[(size_t)p * d + j] + ((i >> j) & 1)] = 1;
+        }
+        __syncthreads();
+        uint32_t nl = 0;
+        for (uint32_t base = 0; base < E; base += blockDim.x) {
+            const uint32_t e = base + threadIdx.x;
+            const uint32_t flag = e < E ? mk[e] : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan(flag, lds, &tot);
+            if (flag) {
+                mk[e] = nl + ex + 1;                     // index + 1
+                if (nl + ex < a.E_cap) a.live_out[j][nl + ex] = e;
+            }
+            nl += tot;
+        }
+        n_live_new[j] = nl;
+        if (2 * nl > a.E_cap) fits = false;             // next k_expand writes 2 * nl entries
+        __syncthreads();
+        if (fits)
+            for (uint32_t k = threadIdx.x; k < nf; k += blockDim.x) {
+                const uint32_t c = a.hist_out[k], p = c >> d, i = c & mask;
+                a.pos_out[(size_t)k * d + j] = mk[2 * a.pos_in[(size_t)p * d + j] + ((i >> j) & 1)] - 1;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    if (!fits) {
+        uint32_t need = 0;
+        for (uint32_t j = 0; j < d; j++) need = max(need, 2 * n_live_new[j]);
+        ctl->need_entries = need;
+        ctl->need_nodes = nf;
+        ctl->abort_level = a.level;
+        ctl->abort = 1;
+        a.sizes_out[2] = 1;
+        return;
+    }
+    // 3. next level's sizes and k_expand work decomposition (as finalize_launch on the host)
+    uint64_t entry_words = 0;
+    for (uint32_t j = 0; j < d; j++) {
+        ctl->n_live[j] = n_live_new[j];
+        a.sizes_out[4 + j] = n_live_new[j];
+        entry_words += (uint64_t)n_live_new[j] * a.nw * a.nctx;
+    }
+    uint64_t g = entry_words / (2 * a.grid_waves);
+    g = g < 1 ? 1 : (g > 8 ? 8 : g);
+    uint64_t begin = 0;
+    for (uint32_t k = 0; k < a.nctx * a.njobs_per_ctx; k++) {
+        ctl->item_begin[k] = begin;
+        begin += (uint64_t)a.nw * ((n_live_new[k % a.njobs_per_ctx] + g - 1) / g);
+    }
+    ctl->group = (uint32_t)g;
+    ctl->total_items = begin;
+    ctl->F = nf;
+    ctl->C = nf << d;
+}
+
+hipError_t launch_prune(const PruneArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_prune, dim3(1), dim3(kPruneThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+__global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
+                            uint64_t grid_waves, uint32_t* pos0, uint32_t* l0, uint32_t* l1, uint32_t* l2,
+                            uint32_t* l3) {
+    if (threadIdx.x != 0) return;
+    uint32_t* lv[kMaxDims] = {l0, l1, l2, l3};
+    ctl->abort = 0;
+    ctl->abort_level = 0;
+    ctl->need_entries = 0;
+    ctl->need_nodes = 0;
+    ctl->F = 1;
+    ctl->C = 1u << d;
+    for (uint32_t j = 0; j < kMaxDims; j++) ctl->n_live[j] = j < d ? 1 : 0;
+    for (uint32_t j = 0; j < d; j++) {
+        pos0[j] = 0;
+        lv[j][0] = 0;
+    }
+    uint64_t g = ((uint64_t)nw * nctx * d) / (2 * grid_waves);
+    g = g < 1 ? 1 : (g > 8 ? 8 : g);
+    uint64_t begin = 0;
+    for (uint32_t k = 0; k < nctx * njobs_per_ctx; k++) {
+        ctl->item_begin[k] = begin;
+        begin += (uint64_t)nw * ((1 + g - 1) / g);
+    }
+    ctl->group = (uint32_t)g;
+    ctl->total_items = begin;
+}
+
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
+                            uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims], hipStream_t stream) {
+    hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, stream, ctl, d, nw, njobs_per_ctx, nctx, grid_waves, pos0,
+                       live0[0], live0[1], live0[2], live0[3]);
+    return hipGetLastError();
+}
+
+}  // namespace fhh

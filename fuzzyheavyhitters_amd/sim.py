@@ -56,7 +56,8 @@ class _TorchAllReduce:
 
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
-              distributed: bool = False, xchg_capacity: int = 1 << 16) -> SimResult:
+              distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
+              init_capacity: int = 0) -> SimResult:
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -65,6 +66,8 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.mode = {"count": 0, "fe": 1}[mode]
     cfg.levels = L
     cfg.prf_seed = prf_seed
+    cfg.host_loop = 1 if host_loop else 0
+    cfg.init_capacity = init_capacity
     ar = None
     if distributed:
         ar = _TorchAllReduce(xchg_capacity, c0.device)

@@ -123,7 +123,7 @@ def synthetic_centroids(num: int = 3233, seed: int = 0xC0DE) -> np.ndarray:
     Alaska, Hawaii and the territories — the shape of data/county_centroids.csv (3 233 rows,
     lat -14.5..69.3, lon -171..145.8), synthesised here (the reference's file is not used)."""
     rng = np.random.default_rng(seed)
-    n_ak, n_hi, n_terr = 30, 5, 78
+    n_ak, n_hi, n_terr = (num * 30) // 3233, (num * 5) // 3233, (num * 78) // 3233
     n_us = num - n_ak - n_hi - n_terr
     us = np.stack([rng.uniform(25.0, 49.0, n_us), rng.uniform(-124.5, -67.0, n_us)], 1)
     ak = np.stack([rng.uniform(55.0, 69.3, n_ak), rng.uniform(-171.0, -130.0, n_ak)], 1)

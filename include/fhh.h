@@ -173,6 +173,13 @@ typedef struct fhh_sim_config {
     uint64_t* level_kept;      /* [levels] */
     uint64_t* counts;          /* concatenated per-level child counts/values (mode 0) */
     uint64_t counts_capacity;
+    /* 0 (default): device-resident level loop — keep decision and prune run on the GPU and
+     * the whole crawl is enqueued without per-level host round trips; 1: host-driven loop
+     * (the same sequence the drop-in entry points perform). Identical results. */
+    uint32_t host_loop;
+    /* device loop: initial frontier / per-dim entry capacity (0 = 256); buffers grow on
+     * demand (the loop pauses, grows, and resumes at the level that overflowed). */
+    uint32_t init_capacity;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x

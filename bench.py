@@ -121,9 +121,20 @@ def main():
     log(f"[rank {rank}] workload+keygen {time.perf_counter() - t_gen:.2f}s "
         f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
 
+    comm, collective = None, "none"
+    if world > 1:
+        # native RCCL all-reduce on the engine stream (no host sync per level); the torch
+        # host-callback path stays available if the communicator cannot be created
+        try:
+            comm = fhh.RcclComm(local_rank)
+            collective = "rccl-native (ncclAllReduce on the engine stream)"
+        except Exception as e:  # pragma: no cover - reported in the JSON line
+            log(f"[rank {rank}] native RCCL comm unavailable ({e}); using torch.distributed callback")
+            collective = "torch.distributed all_reduce (host callback)"
+
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, distributed=world > 1)
+                             record=False, distributed=world > 1 and comm is None, comm=comm)
 
     def barrier():
         if dist is not None:
@@ -187,6 +198,7 @@ def main():
                 "clients_per_gpu": n_local, "clients_total": n_total, "data_len": args.data_len,
                 "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
                 "threshold": args.threshold, "mode": args.mode, "parallelism": f"client-shard x{world}",
+                "collective": collective,
             },
             "full_crawl_wall_s": elapsed / args.steps,
             "ref_equiv_evals_per_s": ref_evals / elapsed,
@@ -219,6 +231,8 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

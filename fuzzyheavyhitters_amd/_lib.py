@@ -33,6 +33,8 @@ EXPORTS = [
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
     "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench",
     "fhh_set_variant", "fhh_variant_info",
+    "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
+    "fhh_comm_last_error",
 ]
 
 
@@ -65,14 +67,16 @@ class FhhSimConfig(ctypes.Structure):
         ("counts_capacity", ctypes.c_uint64),
         ("host_loop", ctypes.c_uint32),
         ("init_capacity", ctypes.c_uint32),
+        ("comm", ctypes.c_void_p),
     ]
 
 
 def build(verbose: bool = False) -> str:
     """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box)."""
-    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp")]
+    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp",
+                                                 "fhh_comm.cpp")]
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           *srcs, "-o", LIB_PATH]
+           *srcs, "-ldl", "-o", LIB_PATH]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
@@ -130,6 +134,12 @@ def lib():
         "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
         "fhh_set_variant": (i, [vp, i]),
         "fhh_variant_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i), P(i)]),
+        "fhh_rccl_load": (i, [ctypes.c_char_p]),
+        "fhh_comm_unique_id": (i, [u8p]),
+        "fhh_comm_create": (i, [P(vp), i, i, u8p, i]),
+        "fhh_comm_destroy": (None, [vp]),
+        "fhh_comm_allreduce_u64": (i, [vp, vp, vp, u64, vp]),
+        "fhh_comm_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

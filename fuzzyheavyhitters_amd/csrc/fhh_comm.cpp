@@ -1,0 +1,165 @@
+// Native RCCL communicator for client-sharded multi-GPU crawls (include/fhh.h).
+//
+// The reference moves per-child sums as an RPC of Vec<FE> from each server to the leader
+// once per level (collect.rs:487-501, leader.rs:182-197). Sharding clients over G GPUs turns
+// the per-server sum into a sum over ranks as well: one ncclAllReduce(sum, u64) of the
+// per-child 32-bit-limb partials (≤ C x 16 u64, a few tens of KB — latency bound over xGMI),
+// enqueued on the engine's stream between the child kernel and k_prune.
+//
+// RCCL is dlopen'ed instead of linked: a PyTorch process already carries its own librccl,
+// and reusing that instance (RTLD_NOLOAD first) avoids two RCCL runtimes in one process.
+#include "fhh_internal.h"
+#include "../../include/fhh.h"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+
+struct fhh_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+};
+
+namespace {
+
+thread_local std::string g_comm_err;
+
+struct Rccl {
+    void* handle = nullptr;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl g_rccl;
+std::mutex g_rccl_mu;
+
+int fail(int code, const std::string& msg) {
+    g_comm_err = msg;
+    return code;
+}
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    std::string m = std::string(what) + ": ";
+    m += g_rccl.error_string ? g_rccl.error_string(r) : "rccl error";
+    return fail(FHH_E_COMM, m);
+}
+
+int load_locked(const char* path) {
+    if (g_rccl.handle) return FHH_OK;
+    void* h = nullptr;
+    if (path && *path) {
+        h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+    } else {
+        for (const char* name : {"librccl.so", "librccl.so.1"}) {
+            h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);   // already in the process (e.g. torch's)
+            if (h) break;
+        }
+        if (!h)
+            for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+                h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+                if (h) break;
+            }
+    }
+    if (!h) return fail(FHH_E_COMM, std::string("dlopen librccl failed: ") + (dlerror() ? dlerror() : "?"));
+    Rccl r;
+    r.handle = h;
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string)
+        return fail(FHH_E_COMM, "librccl lacks an expected symbol");
+    g_rccl = r;
+    return FHH_OK;
+}
+
+int ensure_loaded() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    return load_locked(nullptr);
+}
+
+}  // namespace
+
+namespace fhh {
+
+int comm_allreduce(fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t count, hipStream_t stream,
+                   std::string* err) {
+    const ncclResult_t r = g_rccl.all_reduce(send, recv, count, ncclUint64, ncclSum, c->comm, stream);
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclAllReduce: ") + g_rccl.error_string(r);
+        return FHH_E_COMM;
+    }
+    return FHH_OK;
+}
+
+}  // namespace fhh
+
+extern "C" {
+
+int fhh_rccl_load(const char* path) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    return load_locked(path);
+}
+
+int fhh_comm_unique_id(uint8_t id[128]) {
+    if (!id) return fail(FHH_E_ARG, "null id");
+    int rc = ensure_loaded();
+    if (rc) return rc;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId u;
+    const ncclResult_t r = g_rccl.get_unique_id(&u);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+    std::memcpy(id, &u, 128);
+    return FHH_OK;
+}
+
+int fhh_comm_create(fhh_comm** out, int nranks, int rank, const uint8_t id[128], int device) {
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(FHH_E_ARG, "bad comm arguments");
+    *out = nullptr;
+    int rc = ensure_loaded();
+    if (rc) return rc;
+    if (hipSetDevice(device) != hipSuccess) return fail(FHH_E_HIP, "hipSetDevice failed");
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    auto* c = new fhh_comm();
+    const ncclResult_t r = g_rccl.comm_init_rank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return nccl_fail(r, "ncclCommInitRank");
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    *out = c;
+    return FHH_OK;
+}
+
+void fhh_comm_destroy(fhh_comm* comm) {
+    if (!comm) return;
+    if (comm->comm && g_rccl.comm_destroy) {
+        (void)hipSetDevice(comm->device);
+        (void)g_rccl.comm_destroy(comm->comm);
+    }
+    delete comm;
+}
+
+int fhh_comm_allreduce_u64(fhh_comm* comm, const uint64_t* send_dev, uint64_t* recv_dev, uint64_t count,
+                           void* stream) {
+    if (!comm || !send_dev || !recv_dev) return fail(FHH_E_ARG, "null comm or buffer");
+    if (hipSetDevice(comm->device) != hipSuccess) return fail(FHH_E_HIP, "hipSetDevice failed");
+    std::string err;
+    const int rc = fhh::comm_allreduce(comm, send_dev, recv_dev, count, static_cast<hipStream_t>(stream), &err);
+    if (rc) return fail(rc, err);
+    return FHH_OK;
+}
+
+const char* fhh_comm_last_error(void) { return g_comm_err.c_str(); }
+
+}  // extern "C"

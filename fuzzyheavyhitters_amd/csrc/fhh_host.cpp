@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -110,6 +111,7 @@ struct fhh_ctx {
     uint64_t client_base = 0;
     int variant = 0;              // k_expand variant (fhh_set_variant)
     int grid = 0;
+    uint32_t loop_cap_hint = 0;   // device loop: capacity the previous crawl grew to
     DevBuf work_counter;          // dynamic item distribution
 
     // host-staged keys (add_key); uploaded at tree_init
@@ -613,7 +615,11 @@ int check_pair(fhh_ctx* c0, fhh_ctx* c1) {
 // partials on device -> (optional all-reduce) -> host
 int fetch_partials(fhh_ctx* ctx, const fhh_sim_config* cfg, uint64_t* dev, uint64_t count, uint64_t* host) {
     if (count == 0) return FHH_OK;
-    if (cfg && cfg->allreduce) {
+    if (cfg && cfg->comm) {
+        std::string err;
+        if (comm_allreduce(cfg->comm, dev, dev, count, ctx->stream, &err)) return ctx->fail(FHH_E_COMM, err);
+        HIP_TRY(ctx, hipMemcpyAsync(host, dev, count * 8, hipMemcpyDeviceToHost, ctx->stream));
+    } else if (cfg && cfg->allreduce) {
         if (!cfg->xchg_dev || cfg->xchg_capacity < count)
             return ctx->fail(FHH_E_ARG, "sim: all-reduce exchange buffer too small");
         HIP_TRY(ctx, hipMemcpyAsync(cfg->xchg_dev, dev, count * 8, hipMemcpyDeviceToDevice, ctx->stream));
@@ -679,6 +685,11 @@ int set_device(fhh_ctx* ctx) {
 // ---- device-resident level loop (fhh_sim_crawl, host_loop = 0) ---------------------------------
 struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
+    // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
+    // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
+    DevBuf reduced;
+    bool distributed = false;
+    uint64_t* red() const { return distributed ? reduced.as<uint64_t>() : partials.as<uint64_t>(); }
     std::vector<DevBuf*> hist_epochs;            // hist rows; a new epoch per F_cap growth
     std::vector<uint32_t*> hist_ptr;             // per level
     uint32_t E_cap = 0, F_cap = 0;
@@ -740,12 +751,23 @@ int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uin
     }
     HIP_TRY(c0, B.mark.ensure((size_t)d * E_cap * 4));
     {
-        DevBuf npart;
+        // a resumed prune reads the (reduced) partials of `level`
+        DevBuf npart, nred;
         HIP_TRY(c0, npart.ensure(C_new * 16 * 8));
-        if (preserve && keep_children)
+        if (B.distributed) HIP_TRY(c0, nred.ensure(C_new * 16 * 8));
+        // ... and, multi-rank, the local partials too: the all-reduces of the no-op levels
+        // after an abort re-reduce them, which must reproduce the same sums
+        if (preserve && keep_children) {
             HIP_TRY(c0, hipMemcpy(npart.p, B.partials.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice));
+            if (B.distributed)
+                HIP_TRY(c0, hipMemcpy(nred.p, B.reduced.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice));
+        }
         std::swap(B.partials.p, npart.p);
         std::swap(B.partials.bytes, npart.bytes);
+        if (B.distributed) {
+            std::swap(B.reduced.p, nred.p);
+            std::swap(B.reduced.bytes, nred.bytes);
+        }
     }
     (void)C_old;
     // hist rows for levels >= level live in a new epoch of stride F_cap
@@ -769,7 +791,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     const uint64_t grid_waves = (uint64_t)c0->grid * (expand_threads(variant) / 64);
     const uint32_t per_level_per = cfg->mode == 0 ? 1 : 4;   // partial u64 per child (non-last)
     LoopBuffers B;
-    uint32_t cap0 = cfg->init_capacity ? next_pow2(cfg->init_capacity) : 256;
+    B.distributed = cfg->comm || cfg->allreduce;
+    uint32_t cap0 = std::max(cfg->init_capacity ? next_pow2(cfg->init_capacity) : 256u, c0->loop_cap_hint);
     // tables: both buffers of every dim of both servers hold >= E_cap entries
     fhh_ctx* cs[2] = {c0, c1};
     for (fhh_ctx* c : cs)
@@ -860,7 +883,12 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream));
             else HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
             // -- cross-rank sum (client-sharded multi-GPU)
-            if (cfg->allreduce) {
+            // (the count is the capacity bound: entries past C are never read)
+            if (cfg->comm) {
+                std::string err;
+                if (comm_allreduce(cfg->comm, part, B.red(), C_cap * per, c0->stream, &err))
+                    return c0->fail(FHH_E_COMM, err);
+            } else if (cfg->allreduce) {
                 const uint64_t count = C_cap * per;
                 if (!cfg->xchg_dev || cfg->xchg_capacity < count)
                     return c0->fail(FHH_E_ARG, "sim: all-reduce exchange buffer too small");
@@ -869,7 +897,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 if (rc) return rc;
                 if (cfg->allreduce(cfg->xchg_dev, count, cfg->allreduce_user) != 0)
                     return c0->fail(FHH_E_CALLBACK, "all-reduce callback failed");
-                HIP_TRY(c0, hipMemcpyAsync(part, cfg->xchg_dev, count * 8, hipMemcpyDeviceToDevice, c0->stream));
+                HIP_TRY(c0, hipMemcpyAsync(B.red(), cfg->xchg_dev, count * 8, hipMemcpyDeviceToDevice, c0->stream));
             }
             if (record) {
                 const size_t off = B.rec_off.empty() ? 0 : B.rec_off.back() + (size_t)B.rec_stride.back();
@@ -888,7 +916,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 B.rec_stride[lv] = (uint32_t)(C_cap * per);   // u64 words recorded for this level
                 // mode 0: counts; FE: the 4 limbs; FE255: the 16 limbs (v0 - v1 derived at the end)
                 const size_t cpy = (size_t)C_cap * per * 8;
-                HIP_TRY(c0, hipMemcpyAsync(B.rec.as<uint64_t>() + off, part, cpy, hipMemcpyDeviceToHost, c0->stream));
+                HIP_TRY(c0, hipMemcpyAsync(B.rec.as<uint64_t>() + off, B.red(), cpy, hipMemcpyDeviceToHost, c0->stream));
             }
         }
         prune_only = false;
@@ -896,7 +924,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         if (last) HIP_TRY(c0, B.final_vals.ensure((size_t)B.F_cap * 20 * 4));
         PruneArgs pa{};
         pa.ctl = B.ctl.as<LoopCtl>();
-        pa.partials = B.partials.as<uint64_t>();
+        pa.partials = B.red();
         pa.mode = pmode;
         pa.d = d;
         pa.thr = thr;
@@ -931,6 +959,10 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 const uint32_t nE = std::max(B.E_cap, next_pow2(std::max<uint32_t>(h->need_entries, 1)) * 2);
                 const uint32_t nF = std::max(B.F_cap, next_pow2(std::max<uint32_t>(h->need_nodes, 1)) * 2);
                 const uint32_t la_per = cfg->mode == 0 ? 1 : (la_last ? 16 : 4);
+                if (std::getenv("FHH_DEBUG_LOOP"))
+                    std::fprintf(stderr, "[fhh loop] abort at level %u (batch end %u): need_entries %u need_nodes %u "
+                                 "F %u C %u -> E_cap %u F_cap %u\n", la, lv, h->need_entries, h->need_nodes, h->F,
+                                 h->C, nE, nF);
                 for (fhh_ctx* c : cs)
                     for (uint32_t j = 0; j < d; j++) {
                         // child tables of level la (parity 1 - la&1) hold 2 * n_live(la) entries
@@ -949,6 +981,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             }
         }
     }
+    c0->loop_cap_hint = std::max(B.E_cap, B.F_cap);   // the next crawl starts at this size
     // ---- readback: sizes, hist, final values -> host-side state of both servers ----
     std::vector<uint32_t> sz((size_t)levels * (4 + kMaxDims));
     HIP_TRY(c0, hipMemcpy(sz.data(), B.sizes.p, sz.size() * 4, hipMemcpyDeviceToHost));

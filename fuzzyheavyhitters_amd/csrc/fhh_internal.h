@@ -15,6 +15,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
+struct fhh_comm;   // include/fhh.h (fhh_comm.cpp)
+
 namespace fhh {
 
 constexpr int kMaxDims = 4;
@@ -145,6 +149,9 @@ hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
                                 hipStream_t stream);
 // occupancy-derived persistent grid for k_expand variant on `device`
 int expand_grid(int device, int variant);
+// RCCL all-reduce (sum, u64) on `stream` (fhh_comm.cpp); asynchronous
+int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t count, hipStream_t stream,
+                   std::string* err);
 // device-resident level loop (fhh_loop.hip)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
 hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,

@@ -106,6 +106,8 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
     // 2. per dim: referenced child entries -> new live list (sorted) and node positions
     uint32_t n_live_new[kMaxDims] = {0, 0, 0, 0};
     bool fits = nf <= a.F_cap;
+    if (!fits)   // entries are not counted then; n_live' <= nf bounds them (one abort, not two)
+        for (uint32_t j = 0; j < d; j++) n_live_new[j] = nf;
     for (uint32_t j = 0; j < d && fits; j++) {
         const uint32_t E = 2 * ctl->n_live[j];
         uint32_t* mk = a.mark + (size_t)j * a.E_cap;

@@ -4,8 +4,9 @@ replaced by either plaintext equality of the two share strings (mode "count") or
 OT share values (mode "fe": r0 from a fixed PRF, r1 = r0 + 1, v0 = r1, v1 = eq ? r0 : r1).
 
 Clients may be sharded across GPUs (one process per GPU): each rank holds both servers'
-keys for its client range, and the per-child partial sums are all-reduced over RCCL with
-torch.distributed before the leader's keep decision.
+keys for its client range, and the per-child partial sums are all-reduced over RCCL (native
+communicator on the engine stream, comm.py; or torch.distributed in a host callback) before
+the leader's keep decision.
 """
 from __future__ import annotations
 
@@ -57,7 +58,11 @@ class _TorchAllReduce:
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
-              init_capacity: int = 0) -> SimResult:
+              init_capacity: int = 0, comm=None) -> SimResult:
+    """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
+    sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
+    the engine stream) or, with `distributed=True`, through torch.distributed in a host
+    callback (synchronises once per level; the gloo rehearsal path uses this)."""
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -69,7 +74,10 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.host_loop = 1 if host_loop else 0
     cfg.init_capacity = init_capacity
     ar = None
-    if distributed:
+    if comm is not None:
+        cfg.comm = comm.handle
+        cfg.allreduce = ALLREDUCE_FN()
+    elif distributed:
         ar = _TorchAllReduce(xchg_capacity, c0.device)
         cfg.allreduce = ar.cb
         cfg.xchg_dev = ctypes.cast(ctypes.c_void_p(ar.buf.data_ptr()), u64p)

@@ -46,6 +46,7 @@ extern "C" {
 #define FHH_E_HIP (-3)      /* HIP runtime error                                           */
 #define FHH_E_NOMEM (-4)    /* device allocation failed                                    */
 #define FHH_E_CALLBACK (-5) /* all-reduce callback failed                                  */
+#define FHH_E_COMM (-6)     /* RCCL not loadable / collective failed                        */
 
 #define FHH_MAX_DIMS 4
 
@@ -158,6 +159,26 @@ int fhh_sim_ot_sums(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t prf_seed, void* sums0
  * across ranks and return 0 once the result is visible to the device. */
 typedef int (*fhh_allreduce_fn)(uint64_t* buf_dev, uint64_t count, void* user);
 
+/* ---- native RCCL communicator (client-sharded multi-GPU) ----------------------
+ * The per-level exchange of the reference is an RPC of Vec<FE> per server to the leader
+ * (collect.rs:487-501 -> leader.rs:182-197); with clients sharded over GPUs it becomes one
+ * ncclAllReduce(sum, u64) of the per-child partial sums, enqueued on the engine's stream so a
+ * crawl needs no host round trip per level. RCCL is dlopen'ed (the copy the process already
+ * loaded — e.g. torch's — is preferred so one RCCL instance serves the process). */
+typedef struct fhh_comm fhh_comm;
+/* Load RCCL: `path` NULL -> an already loaded librccl, else the default search path. */
+int fhh_rccl_load(const char* path);
+/* Rank 0 creates the id (128 bytes) and distributes it out of band (e.g. torch.distributed). */
+int fhh_comm_unique_id(uint8_t id[128]);
+int fhh_comm_create(fhh_comm** out, int nranks, int rank, const uint8_t id[128], int device);
+void fhh_comm_destroy(fhh_comm* comm);
+/* Sum count u64 from send_dev into recv_dev (may alias) across ranks, on `stream`
+ * (hipStream_t; NULL = the null stream). Asynchronous. */
+int fhh_comm_allreduce_u64(fhh_comm* comm, const uint64_t* send_dev, uint64_t* recv_dev, uint64_t count,
+                           void* stream);
+/* Last error of the calling thread's fhh_rccl_* / fhh_comm_* call. */
+const char* fhh_comm_last_error(void);
+
 typedef struct fhh_sim_config {
     double threshold;          /* fraction, leader.rs:193-194 / 245-246             */
     uint64_t nclients_total;   /* nreqs (all ranks)                                   */
@@ -180,6 +201,9 @@ typedef struct fhh_sim_config {
     /* device loop: initial frontier / per-dim entry capacity (0 = 256); buffers grow on
      * demand (the loop pauses, grows, and resumes at the level that overflowed). */
     uint32_t init_capacity;
+    /* native RCCL communicator (takes precedence over `allreduce`): the per-level sum is
+     * ncclAllReduce on ctx0's stream, no host synchronisation per level. NULL on one GPU. */
+    fhh_comm* comm;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x

@@ -129,7 +129,7 @@ def test_sharded_crawl_equals_single_process(oracle, mode):
     assert sorted(final) == sorted(tuple(tuple(int(b) for b in pj) for pj in p) for p in ref.final_paths)
 
 
-def _gpu_worker(rank, world, port, wl_args, thr, mode, q):
+def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0):
     import sys
     sys.path.insert(0, ROOT)
     import torch
@@ -149,7 +149,8 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q):
         fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
         c0.set_client_base(rank * n_local)
         c1.set_client_base(rank * n_local)
-        res = fhh.sim_crawl(c0, c1, thr, nclients_total=wl_args["n"], mode=mode, prf_seed=7, distributed=True)
+        res = fhh.sim_crawl(c0, c1, thr, nclients_total=wl_args["n"], mode=mode, prf_seed=7, distributed=True,
+                            host_loop=host_loop, init_capacity=init_capacity)
         if rank == 0:
             q.put((res.level_children.tolist(), [c.tolist() for c in res.counts],
                    sorted(tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final)))
@@ -159,14 +160,19 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["count", "fe"])
-def test_gpu_two_ranks_allreduce_hook(oracle, mode):
+@pytest.mark.parametrize("loop", ["device_grow", "host"])
+def test_gpu_two_ranks_allreduce_hook(oracle, mode, loop):
+    """Two ranks share one GPU over the host all-reduce hook. device_grow starts the device
+    loop at capacity 2 so it aborts and resumes several times: the cross-rank sum of an
+    aborted level must not be applied twice (out-of-place reduction)."""
     from fuzzyheavyhitters_amd import workload
     wl_args = {"n": 256, "L": 48, "d": 1, "sites": 6, "seed": 77}
     thr = 0.02
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, wl_args, thr, mode, q)) for r in range(2)]
+    kw = {"host_loop": loop == "host", "init_capacity": 2 if loop == "device_grow" else 0}
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, wl_args, thr, mode, q), kwargs=kw) for r in range(2)]
     for p in procs:
         p.start()
     children, counts, final = _collect(procs, q, 300)

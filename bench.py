@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--cpu-sample-clients", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
+    ap.add_argument("--variant", type=int, default=-1, help="k_expand variant (-1 = library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +117,9 @@ def main():
     c0 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     c1 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    if args.variant >= 0:
+        c0.set_variant(args.variant)
+        c1.set_variant(args.variant)
     c0.set_client_base(rank * n_local)
     c1.set_client_base(rank * n_local)
     log(f"[rank {rank}] workload+keygen {time.perf_counter() - t_gen:.2f}s "

@@ -71,17 +71,35 @@ class FhhSimConfig(ctypes.Structure):
     ]
 
 
+SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp",
+           "fhh_comm.cpp")
+
+
 def build(verbose: bool = False) -> str:
-    """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box)."""
-    srcs = [os.path.join(_CSRC, f) for f in ("fhh_kernels.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp",
-                                                 "fhh_comm.cpp")]
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           *srcs, "-ldl", "-o", LIB_PATH]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box): one object per
+    source, compiled in parallel, then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(_HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+
+    def compile_one(f):
+        obj = os.path.join(objdir, f + ".o")
+        r = subprocess.run(["hipcc", *flags, "-c", os.path.join(_CSRC, f), "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {f}:\n" + r.stdout + r.stderr)
+        return obj, r.stdout + r.stderr
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
+        res = list(ex.map(compile_one, SOURCES))
+    r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *[o for o, _ in res], "-ldl", "-o",
+                        LIB_PATH], capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + r.stdout + r.stderr)
-    if verbose and (r.stdout or r.stderr):
-        print(r.stdout + r.stderr)
+        raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
+    if verbose:
+        for _, msg in res:
+            if msg:
+                print(msg)
     return LIB_PATH
 
 

@@ -118,6 +118,8 @@ struct fhh_ctx {
     std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;
     uint64_t h_n = 0;
     bool dev_keys = false;        // keys resident on the device (uploaded or generated)
+    bool keys_bs = false;         // cw_seed / root_seed rows in the bitsliced layout
+    bool tab_bs = false;          // prefix tables (since the last tree_init) in the bitsliced layout
 
     DevBuf cw_seed, cw_bits, root_seed, key_idx, valid;
     DimTable tab[kMaxDims];
@@ -309,6 +311,7 @@ int upload_staged_keys(fhh_ctx* ctx) {
     rc = sync(ctx);
     if (rc) return rc;
     ctx->dev_keys = true;
+    ctx->keys_bs = false;
     ctx->h_key_idx.clear();
     ctx->h_root.clear();
     ctx->h_cws.clear();
@@ -367,8 +370,50 @@ int upload_lists(fhh_ctx* ctx) {
     return FHH_OK;
 }
 
+// Convert the device keys' 16-byte seed rows (CW seeds [L][K], root seeds [K]) to the layout
+// the selected k_expand variant reads (bitsliced for kBsVariant, client-major otherwise).
+int ensure_key_layout(fhh_ctx* ctx) {
+    const bool want = variant_is_bs(ctx->variant);
+    if (ctx->keys_bs == want) return FHH_OK;
+    DevBuf* bufs[2] = {&ctx->cw_seed, &ctx->root_seed};
+    const uint64_t rows[2] = {(uint64_t)ctx->L * ctx->K, (uint64_t)ctx->K};
+    for (int b = 0; b < 2; b++) {
+        DevBuf tmp;
+        HIP_TRY(ctx, tmp.ensure(rows[b] * ctx->npad * 16));
+        HIP_TRY(ctx, launch_bitslice(bufs[b]->as<uint4>(), tmp.as<uint4>(), rows[b], (uint32_t)ctx->npad, want ? 1 : 0,
+                                     ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        std::swap(bufs[b]->p, tmp.p);
+        std::swap(bufs[b]->bytes, tmp.bytes);
+    }
+    ctx->keys_bs = want;
+    return FHH_OK;
+}
+
+// bitsliced rows [rows][32][ng] uint4 -> client-major [rows][npad] uint4 (host; export paths)
+void host_unbitslice(std::vector<uint8_t>& buf, size_t rows, size_t npad) {
+    const size_t ng = npad / 32;
+    std::vector<uint8_t> out(buf.size());
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(buf.data());
+    uint32_t* o = reinterpret_cast<uint32_t*>(out.data());
+    for (size_t r = 0; r < rows; r++)
+        for (size_t g = 0; g < ng; g++) {
+            uint32_t w[128];
+            for (int i = 0; i < 128; i++) w[i] = in[((r * 32 + i / 4) * ng + g) * 4 + i % 4];
+            for (int j = 0; j < 32; j++)
+                for (int k = 0; k < 4; k++) {
+                    uint32_t v = 0;
+                    for (int b = 0; b < 32; b++) v |= ((w[32 * k + b] >> j) & 1u) << b;
+                    o[(r * npad + 32 * g + j) * 4 + k] = v;
+                }
+        }
+    buf.swap(out);
+}
+
 // Prepare expansion jobs for one ctx (dst buffers sized; lists already on the device).
 int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
+    if (ctx->tab_bs != variant_is_bs(ctx->variant))
+        return ctx->fail(FHH_E_STATE, "k_expand variant changed seed layout mid-crawl; call tree_init");
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         const int src = T.cur, dst = 1 - T.cur;
@@ -399,17 +444,17 @@ int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
 
 void finalize_launch(ExpandLaunch& L, int grid, int variant) {
     uint64_t entry_words = 0;
-    for (uint32_t k = 0; k < L.njobs; k++) entry_words += (uint64_t)L.job[k].n_live * L.job[k].nw;
+    for (uint32_t k = 0; k < L.njobs; k++) entry_words += (uint64_t)L.job[k].n_live * expand_unit(variant, L.job[k].nw);
     const uint64_t waves = (uint64_t)grid * (expand_threads(variant) / 64);
     uint64_t g = entry_words / (2 * waves);
     if (g < 1) g = 1;
-    if (g > 8) g = 8;
+    if (g > expand_max_group(variant)) g = expand_max_group(variant);
     uint64_t begin = 0;
     for (uint32_t k = 0; k < L.njobs; k++) {
         ExpandJob& J = L.job[k];
         J.group = (uint32_t)g;
         J.item_begin = begin;
-        begin += (uint64_t)J.nw * ((J.n_live + g - 1) / g);
+        begin += (uint64_t)expand_unit(variant, J.nw) * ((J.n_live + g - 1) / g);
     }
     L.total_items = begin;
 }
@@ -816,8 +861,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         uint32_t* l0[kMaxDims] = {nullptr, nullptr, nullptr, nullptr};
         for (uint32_t j = 0; j < d; j++) l0[j] = B.live[0].as<uint32_t>() + (size_t)j * B.E_cap;
         for (uint32_t j = d; j < kMaxDims; j++) l0[j] = l0[0];
-        HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, (uint32_t)c0->nw, d, 2, grid_waves,
-                                     B.pos[0].as<uint32_t>(), l0, c0->stream));
+        HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, expand_unit(variant, c0->nw), expand_max_group(variant),
+                                     d, 2, grid_waves, B.pos[0].as<uint32_t>(), l0, c0->stream));
     }
     const bool record = cfg->counts != nullptr;
     const uint32_t kBatch = 32;
@@ -945,6 +990,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.njobs_per_ctx = d;
         pa.nctx = 2;
         pa.grid_waves = grid_waves;
+        pa.unit = expand_unit(variant, c0->nw);
+        pa.max_group = expand_max_group(variant);
         HIP_TRY(c0, launch_prune(pa, c0->stream));
         lv++;
         if (lv % kBatch == 0 || lv == levels) {
@@ -1153,6 +1200,7 @@ int fhh_reset(fhh_ctx* ctx) {
     ctx->h_cwb.clear();
     ctx->h_n = 0;
     ctx->dev_keys = false;
+    ctx->keys_bs = false;
     ctx->n = ctx->npad = ctx->nw = 0;
     ctx->phase = Phase::kNoInit;
     ctx->frontier.clear();
@@ -1243,6 +1291,7 @@ int fhh_gen_keys_pair(fhh_ctx* c0, fhh_ctx* c1, uint64_t n, const uint8_t* left_
     if (rc) return rc;
     c0->stats.keygen_ms += ms;
     c0->dev_keys = c1->dev_keys = true;
+    c0->keys_bs = c1->keys_bs = false;
     return FHH_OK;
 }
 
@@ -1272,6 +1321,10 @@ int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t*
     HIP_TRY(ctx, hipMemcpy(roots.data(), ctx->root_seed.p, roots.size(), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(cwb.data(), ctx->cw_bits.p, cwb.size() * 8, hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(kidx.data(), ctx->key_idx.p, kidx.size() * 8, hipMemcpyDeviceToHost));
+    if (ctx->keys_bs) {
+        host_unbitslice(cws, L * K, npad);
+        host_unbitslice(roots, K, npad);
+    }
     for (size_t c = 0; c < n; c++)
         for (size_t kk = 0; kk < K; kk++) {
             const size_t w = c / 64, bit = c % 64;
@@ -1297,6 +1350,9 @@ int fhh_tree_init(fhh_ctx* ctx) {
     rc = upload_staged_keys(ctx);
     if (rc) return rc;
     if (!ctx->dev_keys || ctx->n == 0) return ctx->fail(FHH_E_STATE, "tree_init with no keys (collect.rs:83)");
+    rc = ensure_key_layout(ctx);
+    if (rc) return rc;
+    ctx->tab_bs = ctx->keys_bs;
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         T.cur = 0;
@@ -1463,6 +1519,7 @@ int fhh_export_states(fhh_ctx* ctx, uint64_t* n_nodes, uint8_t* seeds, uint8_t* 
         HIP_TRY(ctx, hipMemcpy(hs.data(), T.seed[buf].p, hs.size(), hipMemcpyDeviceToHost));
         HIP_TRY(ctx, hipMemcpy(ht.data(), T.t[buf].p, ht.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(ctx, hipMemcpy(hy.data(), T.y[buf].p, hy.size() * 8, hipMemcpyDeviceToHost));
+        if (ctx->tab_bs) host_unbitslice(hs, T.cap[buf] * 2, npad);
         for (uint64_t node = 0; node < F; node++) {
             uint32_t e;
             if (pending) {

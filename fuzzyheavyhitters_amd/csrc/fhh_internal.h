@@ -115,6 +115,8 @@ struct PruneArgs {
     uint32_t njobs_per_ctx;     // = d
     uint32_t nctx;              // 2 (pair)
     uint64_t grid_waves;        // persistent k_expand waves (for the group size)
+    uint32_t unit;              // k_expand items per entry group (nw; bitsliced: 4 * ceil(nw / 32))
+    uint32_t max_group;         // entries per item cap (8; bitsliced: 1)
 };
 
 struct KeygenArgs {
@@ -152,9 +154,27 @@ int expand_grid(int device, int variant);
 // RCCL all-reduce (sum, u64) on `stream` (fhh_comm.cpp); asynchronous
 int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t count, hipStream_t stream,
                    std::string* err);
-// device-resident level loop (fhh_loop.hip)
+// device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
+// entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
-hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
-                            uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims], hipStream_t stream);
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
+                            uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
+                            hipStream_t stream);
+
+// ---- bitsliced k_expand (fhh_expand_bs.hip) -------------------------------------------------
+// Variant kBsVariant selects it; seeds (CW, root, prefix tables) are then stored per key row as
+// [32 quads][npad / 32] uint4 bitsliced words (see fhh_expand_bs.hip). Work item = one
+// (entry, side, dir) x 2048 clients: 4 * ceil(nw / 32) items per entry, one entry per item.
+constexpr int kBsVariant = 14;
+hipError_t launch_expand_bs(const ExpandLaunch& a, int grid, uint32_t* work_counter, hipStream_t stream);
+const void* expand_bs_fn();
+int expand_bs_threads();
+// to_bs = 1: client-major [rows][npad] uint4 -> bitsliced; 0: inverse (out-of-place)
+hipError_t launch_bitslice(const uint4* in, uint4* out, uint64_t rows, uint32_t npad, int to_bs, hipStream_t stream);
+inline bool variant_is_bs(int variant) { return variant == kBsVariant; }
+inline uint32_t expand_unit(int variant, uint64_t nw) {
+    return variant_is_bs(variant) ? (uint32_t)(4 * ((nw + 31) / 32)) : (uint32_t)nw;
+}
+inline uint32_t expand_max_group(int variant) { return variant_is_bs(variant) ? 1u : 8u; }
 
 }  // namespace fhh

@@ -264,6 +264,7 @@ struct VariantInfo {
 };
 
 static VariantInfo variant_info(int v) {
+    if (v == kBsVariant) return VariantInfo{expand_bs_fn(), expand_bs_threads(), true, "bitsliced/v_bitop3/no-LDS"};
     switch (v) {
 #define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
     case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), THR, DYN, TAB::kName};
@@ -273,12 +274,13 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return 14; }
+int expand_variant_count() { return kBsVariant + 1; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
 hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream) {
     if (a.total_items == 0) return hipSuccess;
+    if (variant == kBsVariant) return launch_expand_bs(a, grid, work_counter, stream);
     const VariantInfo vi = variant_info(variant);
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;

@@ -156,14 +156,14 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
     for (uint32_t j = 0; j < d; j++) {
         ctl->n_live[j] = n_live_new[j];
         a.sizes_out[4 + j] = n_live_new[j];
-        entry_words += (uint64_t)n_live_new[j] * a.nw * a.nctx;
+        entry_words += (uint64_t)n_live_new[j] * a.unit * a.nctx;
     }
     uint64_t g = entry_words / (2 * a.grid_waves);
-    g = g < 1 ? 1 : (g > 8 ? 8 : g);
+    g = g < 1 ? 1 : (g > a.max_group ? a.max_group : g);
     uint64_t begin = 0;
     for (uint32_t k = 0; k < a.nctx * a.njobs_per_ctx; k++) {
         ctl->item_begin[k] = begin;
-        begin += (uint64_t)a.nw * ((n_live_new[k % a.njobs_per_ctx] + g - 1) / g);
+        begin += (uint64_t)a.unit * ((n_live_new[k % a.njobs_per_ctx] + g - 1) / g);
     }
     ctl->group = (uint32_t)g;
     ctl->total_items = begin;
@@ -176,7 +176,8 @@ hipError_t launch_prune(const PruneArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-__global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
+__global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
+                            uint32_t nctx,
                             uint64_t grid_waves, uint32_t* pos0, uint32_t* l0, uint32_t* l1, uint32_t* l2,
                             uint32_t* l3) {
     if (threadIdx.x != 0) return;
@@ -192,20 +193,22 @@ __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njob
         pos0[j] = 0;
         lv[j][0] = 0;
     }
-    uint64_t g = ((uint64_t)nw * nctx * d) / (2 * grid_waves);
-    g = g < 1 ? 1 : (g > 8 ? 8 : g);
+    uint64_t g = ((uint64_t)unit * nctx * d) / (2 * grid_waves);
+    g = g < 1 ? 1 : (g > max_group ? max_group : g);
     uint64_t begin = 0;
     for (uint32_t k = 0; k < nctx * njobs_per_ctx; k++) {
         ctl->item_begin[k] = begin;
-        begin += (uint64_t)nw * ((1 + g - 1) / g);
+        begin += (uint64_t)unit * ((1 + g - 1) / g);
     }
     ctl->group = (uint32_t)g;
     ctl->total_items = begin;
 }
 
-hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t nw, uint32_t njobs_per_ctx, uint32_t nctx,
-                            uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims], hipStream_t stream) {
-    hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, stream, ctl, d, nw, njobs_per_ctx, nctx, grid_waves, pos0,
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
+                            uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
+                            hipStream_t stream) {
+    hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, stream, ctl, d, unit, max_group, njobs_per_ctx, nctx,
+                       grid_waves, pos0,
                        live0[0], live0[1], live0[2], live0[3]);
     return hipGetLastError();
 }

@@ -41,11 +41,15 @@ def test_device_loop_equals_host_loop(path, cap):
     assert [r.path for r in r1] == [r.path for r in dev.final]
 
 
-def test_device_loop_large_with_growth(oracle):
+@pytest.mark.parametrize("variant", [None, 14], ids=["default", "bitsliced"])
+def test_device_loop_large_with_growth(oracle, variant):
     """data_len 512, frontier well past the initial capacity: several grow-and-resume cycles."""
     from fuzzyheavyhitters_amd import sim_crawl, workload
     wl = workload.zipf_workload(4000, 512, 1, num_sites=60, seed=99)
     c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    if variant is not None:
+        c0.set_variant(variant)
+        c1.set_variant(variant)
     host = sim_crawl(c0, c1, 0.002, mode="count", host_loop=True)
     st_host = c0.stats()
     c0.reset_stats()

@@ -66,8 +66,12 @@ def test_keygen_ragged_and_tiny(kc, oracle):
         assert np.array_equal(cs, k1.cw_seed) and np.array_equal(cb, k1.cw_bits)
 
 
+BS_VARIANT = 14   # bitsliced k_expand (csrc/fhh_expand_bs.hip): seeds stored bitsliced
+
+
+@pytest.mark.parametrize("variant", [None, BS_VARIANT], ids=["default", "bitsliced"])
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
-def test_level_states_bit_exact(kc, oracle, path):
+def test_level_states_bit_exact(kc, oracle, path, variant):
     """Every level: EvalState seeds/t/y of all children, share planes and equality counts
     equal the oracle's (reference child order), pruning with the oracle's keep masks."""
     g = load(path)
@@ -75,8 +79,15 @@ def test_level_states_bit_exact(kc, oracle, path):
     k0, k1 = oracle.gen_keys(g["left"], g["right"], g["root_seeds"])
     for build in ("gen", "add"):
         c0, c1 = make_pair(kc, g["left"], g["right"], g["root_seeds"]) if build == "gen" else add_pair(kc, k0, k1)
+        if variant is not None:
+            c0.set_variant(variant)
+            c1.set_variant(variant)
         c0.tree_init()
         c1.tree_init()
+        if variant is not None:   # keys now live in the variant's layout; the export undoes it
+            _, rs, cs, cb = c1.export_keys()
+            assert np.array_equal(rs, k1.root_seed) and np.array_equal(cs, k1.cw_seed)
+            assert np.array_equal(cb, k1.cw_bits)
         s0, s1 = oracle.tree_init(k0), oracle.tree_init(k1)
         seeds, t, y = c0.export_states()
         assert np.array_equal(seeds, s0.seed) and np.array_equal(t, s0.t) and np.array_equal(y, s0.y)

@@ -164,16 +164,23 @@ hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t ma
 // ---- bitsliced k_expand (fhh_expand_bs.hip) -------------------------------------------------
 // Variant kBsVariant selects it; seeds (CW, root, prefix tables) are then stored per key row as
 // [32 quads][npad / 32] uint4 bitsliced words (see fhh_expand_bs.hip). Work item = one
-// (entry, side, dir) x 2048 clients: 4 * ceil(nw / 32) items per entry, one entry per item.
-constexpr int kBsVariant = 14;
-hipError_t launch_expand_bs(const ExpandLaunch& a, int grid, uint32_t* work_counter, hipStream_t stream);
-const void* expand_bs_fn();
-int expand_bs_threads();
+// (entry, side, dir) x 2048 clients (pair mode: (entry, side) x 2048 clients, both dirs), one
+// entry per item.
+constexpr int kBsVariant = 14;   // first bitsliced variant; expand_bs_count() of them
+hipError_t launch_expand_bs(const ExpandLaunch& a, int which, int grid, uint32_t* work_counter, hipStream_t stream);
+const void* expand_bs_fn(int which);
+int expand_bs_count();
+int expand_bs_threads(int which);
+size_t expand_bs_dyn_lds(int which);   // dynamic LDS bytes a variant launches with
+// pair mode (which >= 2): one 2-wave workgroup per (entry, side, chunk), both dirs
+inline bool bs_pair_mode(int which) { return which != 0 && which != 1 && which != 5; }
 // to_bs = 1: client-major [rows][npad] uint4 -> bitsliced; 0: inverse (out-of-place)
 hipError_t launch_bitslice(const uint4* in, uint4* out, uint64_t rows, uint32_t npad, int to_bs, hipStream_t stream);
-inline bool variant_is_bs(int variant) { return variant == kBsVariant; }
+inline bool variant_is_bs(int variant) { return variant >= kBsVariant; }
 inline uint32_t expand_unit(int variant, uint64_t nw) {
-    return variant_is_bs(variant) ? (uint32_t)(4 * ((nw + 31) / 32)) : (uint32_t)nw;
+    if (!variant_is_bs(variant)) return (uint32_t)nw;
+    const uint32_t per_chunk = bs_pair_mode(variant - kBsVariant) ? 2 : 4;   // (side[, dir]) per chunk
+    return (uint32_t)(per_chunk * ((nw + 31) / 32));
 }
 inline uint32_t expand_max_group(int variant) { return variant_is_bs(variant) ? 1u : 8u; }
 

@@ -264,7 +264,18 @@ struct VariantInfo {
 };
 
 static VariantInfo variant_info(int v) {
-    if (v == kBsVariant) return VariantInfo{expand_bs_fn(), expand_bs_threads(), true, "bitsliced/v_bitop3/no-LDS"};
+    if (v >= kBsVariant) {
+        static const char* names[] = {"bitsliced/2 waves/fence2", "bitsliced/3 waves/fence1",
+                                      "bitsliced pair+LDS/2 waves", "bitsliced pair+LDS/3 waves",
+                                      "bitsliced pair+LDS/rolled", "bitsliced/2 waves/rolled",
+                                      "bitsliced pair+LDS/rolled/PROFILE", "bitsliced pair2/rolled",
+                                      "bitsliced pair2/rolled/PROFILE", "bitsliced pair2/unrolled",
+                                      "bitsliced pair2/rolled/carry4 (slow-path test)",
+                                      "bitsliced pair2/rolled/3 waves", "bitsliced pair2/unrolled/3 waves"};
+        const int w = v - kBsVariant;
+        if (w >= expand_bs_count()) return VariantInfo{nullptr, 0, false, ""};
+        return VariantInfo{expand_bs_fn(w), expand_bs_threads(w), true, names[w]};
+    }
     switch (v) {
 #define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
     case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), THR, DYN, TAB::kName};
@@ -274,13 +285,13 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + 1; }
+int expand_variant_count() { return kBsVariant + expand_bs_count(); }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
 hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream) {
     if (a.total_items == 0) return hipSuccess;
-    if (variant == kBsVariant) return launch_expand_bs(a, grid, work_counter, stream);
+    if (variant >= kBsVariant) return launch_expand_bs(a, variant - kBsVariant, grid, work_counter, stream);
     const VariantInfo vi = variant_info(variant);
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;
@@ -304,7 +315,8 @@ int expand_grid(int device, int variant) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const VariantInfo vi = variant_info(variant);
     int per_cu = 0;
-    if (!vi.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vi.fn, vi.threads, 0) != hipSuccess ||
+    const size_t dyn = variant >= kBsVariant ? expand_bs_dyn_lds(variant - kBsVariant) : 0;
+    if (!vi.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vi.fn, vi.threads, dyn) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
     return cus * per_cu;

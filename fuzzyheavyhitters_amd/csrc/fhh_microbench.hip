@@ -26,6 +26,25 @@ __global__ __launch_bounds__(256) void k_valu_peak(uint32_t* out, uint32_t iters
     if (acc == 0x12345678u) out[0] = acc;   // keep live
 }
 
+// v_bitop3_b32 with three distinct VGPR sources (the bitsliced AES's only op)
+__global__ __launch_bounds__(256) void k_bitop3_peak(uint32_t* out, uint32_t iters, uint32_t seed) {
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = seed * (threadIdx.x + 1) + k * 0x9e3779b9u + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                x[k] = __builtin_amdgcn_bitop3_b32(x[k], x[(k + 1 + r) & 15], x[(k + 6 + r) & 15], 0x6A);
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc ^= x[k];
+    if (acc == 0x12345678u) out[0] = acc;   // keep live
+}
+
 __global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters) {
     __shared__ uint32_t tbl[256 * 64];
     for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) tbl[i] = (uint32_t)i * 2654435761u;
@@ -63,11 +82,17 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
     double ops = 0;
     float ms = 0.f;
     for (int rep = 0; rep < 2; rep++) {   // first pass warms clocks
-        if (which == 0) {
-            const int blocks = cus * 8;   // 8 waves/SIMD
+        if (which == 0 || which >= 2) {
+            // 0: v_xor_b32, 8 waves/SIMD; 2: v_bitop3_b32, 8 waves/SIMD;
+            // 3: v_bitop3_b32, 2 waves/SIMD; 4: v_xor_b32, 2 waves/SIMD
+            const int wps = (which == 3 || which == 4) ? 2 : 8;
+            const int blocks = cus * wps;   // 256-thread blocks = 4 waves = one per SIMD
             const uint32_t iters = 4096;
             (void)hipEventRecord(a, 0);
-            hipLaunchKernelGGL(fhh::k_valu_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            if (which == 0 || which == 4)
+                hipLaunchKernelGGL(fhh::k_valu_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else
+                hipLaunchKernelGGL(fhh::k_bitop3_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             (void)hipEventRecord(b, 0);
             ops = (double)blocks * threads * iters * 8 * 16;
         } else {

@@ -235,7 +235,8 @@ int fhh_reset_stats(fhh_ctx* ctx);
 int fhh_set_timing(fhh_ctx* ctx, int enabled);
 
 /* Peak-rate microbenchmarks pinning the roofline denominators on the running device:
- * which = 0 -> v_xor_b32 lane-ops/s; which = 1 -> ds_read_b32 bytes/s (k_expand pattern). */
+ * which = 0 -> v_xor_b32 lane-ops/s; which = 1 -> ds_read_b32 bytes/s (k_expand pattern);
+ * 2 -> v_bitop3_b32 lane-ops/s; 3 -> v_bitop3_b32 at 2 waves/SIMD; 4 -> v_xor_b32 at 2 waves/SIMD. */
 int fhh_microbench(int device, int which, double* rate);
 
 /* Device properties the library targets (gfx950). */

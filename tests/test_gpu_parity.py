@@ -69,7 +69,8 @@ def test_keygen_ragged_and_tiny(kc, oracle):
 BS_VARIANT = 14   # bitsliced k_expand (csrc/fhh_expand_bs.hip): seeds stored bitsliced
 
 
-@pytest.mark.parametrize("variant", [None, BS_VARIANT], ids=["default", "bitsliced"])
+@pytest.mark.parametrize("variant", [None, BS_VARIANT, BS_VARIANT + 2, BS_VARIANT + 7, BS_VARIANT + 10],
+                         ids=["default", "bitsliced", "bitsliced-pair", "bitsliced-pair2", "pair2-carry4"])
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_level_states_bit_exact(kc, oracle, path, variant):
     """Every level: EvalState seeds/t/y of all children, share planes and equality counts

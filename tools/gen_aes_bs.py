@@ -372,10 +372,60 @@ def mixcol_net():
     return net
 
 
+def peak_live(prog, inputs, outputs):
+    """max simultaneously live values (inputs until their last use, outputs to the end)"""
+    uses = {}
+    for _, leaves, _ in prog:
+        for l in set(leaves):
+            uses[l] = uses.get(l, 0) + 1
+    live = set(inputs)
+    peak = len(live)
+    outs = set(outputs)
+    for n, leaves, _ in prog:
+        for l in set(leaves):
+            uses[l] -= 1
+            if uses[l] == 0 and l not in outs:
+                live.discard(l)
+        live.add(n)
+        peak = max(peak, len(live))
+    return peak
+
+
+def schedule(prog, inputs, outputs, trials, rng):
+    """reorder a LUT program (topologically) to minimise peak register pressure: randomised
+    greedy list scheduling that prefers ops freeing the most operands"""
+    best, best_peak = list(prog), peak_live(prog, inputs, outputs)
+    byname = {n: (n, leaves, tt) for n, leaves, tt in prog}
+    outs = set(outputs)
+    for _ in range(trials):
+        uses = {}
+        for _, leaves, _ in prog:
+            for l in set(leaves):
+                uses[l] = uses.get(l, 0) + 1
+        avail = set(inputs)
+        pending = {n for n, _, _ in prog}
+        order = []
+        while pending:
+            ready = [n for n in pending if all(l in avail for l in byname[n][1])]
+            def score(n):
+                freed = sum(1 for l in set(byname[n][1]) if uses[l] == 1 and l not in outs)
+                return freed - 1 + rng.random() * 0.9
+            n = max(ready, key=score)
+            pending.discard(n)
+            for l in set(byname[n][1]):
+                uses[l] -= 1
+            avail.add(n)
+            order.append(byname[n])
+        pk = peak_live(order, inputs, outputs)
+        if pk < best_peak:
+            best, best_peak = order, pk
+    return best, best_peak
+
+
 class Program:
     """LUT program with named inputs/outputs; outputs may be complemented at emission."""
 
-    def __init__(self, net, trials=1):
+    def __init__(self, net, trials=1, sched_trials=0):
         self.net = net
         self.prog = lut_map(net)
         rng = random.Random(12345)
@@ -385,6 +435,9 @@ class Program:
                 self.prog = p
         self.inputs = list(net.pis)
         self.outputs = list(net.pos)
+        self.peak = peak_live(self.prog, self.inputs, self.outputs)
+        if sched_trials:
+            self.prog, self.peak = schedule(self.prog, self.inputs, self.outputs, sched_trials, rng)
 
     def __len__(self):
         return len(self.prog)
@@ -457,11 +510,12 @@ def emit_prog(em, P, inmap, comp):
     return out
 
 
-def gen_aes(em, SB, MC):
-    """state operands st[i] (bit i) -> AES_0 rounds 1..10 (round 0 key is zero)."""
+def gen_aes(em, SB, MC, rounds=range(1, 11), keyed=True):
+    """state operands st[i] (bit i) -> AES_0 rounds `rounds` (round 0 key is zero); keyed=False
+    leaves AddRoundKey out (the rolled form applies it at run time)."""
     st = [f"s[{i}]" for i in range(128)]
-    for r in range(1, 11):
-        rk_bits = [(RK[r][i >> 3] >> (i & 7)) & 1 for i in range(128)]
+    for r in rounds:
+        rk_bits = [(RK[r][i >> 3] >> (i & 7)) & 1 if keyed else 0 for i in range(128)]
         sub = [None] * 128
         for byte in range(16):
             inmap = {f"x{i}": st[8 * byte + (7 - i)] for i in range(8)}
@@ -490,6 +544,20 @@ def gen_aes(em, SB, MC):
                     new[8 * (4 * c + row) + k] = o[names[8 * row + k]]
         st = new
     return st
+
+
+def run_words(em, final, words):
+    """run the emitted op list on 128 bitsliced words; returns the 128 output words"""
+    M = 0xFFFFFFFF
+    env = {f"s[{i}]": w for i, w in enumerate(words)}
+    for d, a, b, c, imm in em.ops:
+        A, B, C = env[a], env[b], env[c]
+        r = 0
+        for m in range(8):
+            if (imm >> m) & 1:
+                r |= (A if m & 4 else ~A & M) & (B if m & 2 else ~B & M) & (C if m & 1 else ~C & M)
+        env[d] = r
+    return [env[f] for f in final]
 
 
 def simulate(em, final, blocks):
@@ -525,11 +593,11 @@ def main():
                            {f"x{i}": (x >> (7 - i)) & 1 for i in range(8)})[f"s{i}"] << (7 - i) for i in range(8))
            != SBOX[x]]
     assert not bad, f"S-box circuit wrong on {len(bad)} inputs"
-    SB = Program(sb, trials=300)
+    SB = Program(sb, trials=300, sched_trials=400)
     for x in range(256):
         e = run_prog(SB.prog, {f"x{i}": (x >> (7 - i)) & 1 for i in range(8)})
         assert sum(e[f"s{i}"] << (7 - i) for i in range(8)) == SBOX[x]
-    MC = Program(mixcol_net(), trials=50)
+    MC = Program(mixcol_net(), trials=50, sched_trials=400)
     em = Emitter()
     final = gen_aes(em, SB, MC)
     rnd = random.Random(1)
@@ -538,13 +606,32 @@ def main():
     for blk, g in zip(blocks, got):
         assert g == aes_ref(blk), "bitsliced program disagrees with AES reference"
     assert bytes(got[0]).hex() == "66e94bd4ef8a2c3b884cfa59ca342b2e"
+    # rolled form: 9 x (keyless round, then AddRoundKey at run time) + keyed last round
+    em_r, em_l = Emitter(), Emitter()
+    fin_r = gen_aes(em_r, SB, MC, rounds=[1], keyed=False)
+    fin_l = gen_aes(em_l, SB, MC, rounds=[10], keyed=True)
+    words = [0] * 128
+    for i in range(128):
+        for j, blk in enumerate(blocks):
+            words[i] |= ((blk[i >> 3] >> (i & 7)) & 1) << j
+    for r in range(1, 10):
+        words = run_words(em_r, fin_r, words)
+        words = [w ^ (0xFFFFFFFF if (RK[r][i >> 3] >> (i & 7)) & 1 else 0) for i, w in enumerate(words)]
+    words = run_words(em_l, fin_l, words)
+    for j, blk in enumerate(blocks):
+        out = [0] * 16
+        for i in range(128):
+            out[i >> 3] |= ((words[i] >> j) & 1) << (i & 7)
+        assert out == aes_ref(blk), "rolled bitsliced program disagrees with AES reference"
     nops = len(em.ops)
-    print(f"S-box {len(SB)} LUTs, MixColumns {len(MC)} LUTs/column, total {nops} v_bitop3 per 32 blocks "
+    print(f"S-box {len(SB)} LUTs (peak live {SB.peak}), MixColumns {len(MC)} LUTs/column (peak live {MC.peak}), total {nops} v_bitop3 per 32 blocks "
           f"= {nops / 32:.1f} per block", file=sys.stderr)
     if check_only:
         return
     body = "\n".join(em.lines)
     outs = ", ".join(final)
+    body_r, outs_r = "\n".join(em_r.lines), ", ".join(fin_r)
+    body_l, outs_l = "\n".join(em_l.lines), ", ".join(fin_l)
     hdr = f"""// GENERATED by tools/gen_aes_bs.py — do not edit.
 // Bitsliced AES-128 with the all-zero key (src/prg.rs:185-234 FixedKeyPrgStream's cipher):
 // s[i] holds bit i of 32 blocks (bit i = bit (i & 7) of byte (i >> 3)); on return s holds
@@ -564,6 +651,24 @@ template <class Ops>
 __host__ __device__ __forceinline__ void aes0_bs(uint32_t (&s)[128]) {{
 {body}
     const uint32_t out_[128] = {{{outs}}};
+#pragma unroll
+    for (int i = 0; i < 128; i++) s[i] = out_[i];
+}}
+
+// Rolled form (code ~1/8 the size): rounds 1..9 = aes0_bs_round + AddRoundKey applied by the
+// caller at run time; then aes0_bs_last (round 10, its key folded). {len(em_r.ops)} + {len(em_l.ops)} ops.
+template <class Ops>
+__host__ __device__ __forceinline__ void aes0_bs_round(uint32_t (&s)[128]) {{
+{body_r}
+    const uint32_t out_[128] = {{{outs_r}}};
+#pragma unroll
+    for (int i = 0; i < 128; i++) s[i] = out_[i];
+}}
+
+template <class Ops>
+__host__ __device__ __forceinline__ void aes0_bs_last(uint32_t (&s)[128]) {{
+{body_l}
+    const uint32_t out_[128] = {{{outs_l}}};
 #pragma unroll
     for (int i = 0; i < 128; i++) s[i] = out_[i];
 }}

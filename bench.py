@@ -61,6 +61,59 @@ def cpu_baseline(args, n_total):
     }
 
 
+def sketch_bench(args, world, rank, local_rank, dist):
+    """configs[4]: one step = one level of sketch verification (main.rs:14-70) for
+    --sketch-keys keys per GPU x --sketch-nodes frontier nodes, both servers in-process:
+    sketch_at (AES-128-CTR PrgStream + 3 FE inner products per key), MulState cor/out shares,
+    verify. Inputs resident in HBM. Keys shard by GPU (weak scaling, no collective: each key's
+    check is independent; the leader gathers accept bits only)."""
+    import numpy as np
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload(args.sketch_keys, args.sketch_nodes, seed=args.seed + rank, bad_fraction=0.01)
+    kc = fhh.KeyCollection(8, 1, device=local_rank)
+    b = S.DeviceSketchBatch(wl, device=local_rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        S.sim_sketch_verify(kc, b)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        S.sim_sketch_verify(kc, b)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = b.ok.cpu().numpy().astype(bool)
+    assert np.array_equal(ok, wl.honest), "sketch verification disagrees with the workload's ground truth"
+    keys = args.sketch_keys * world * args.steps
+    elems = keys * args.sketch_nodes * 2   # both servers
+    blocks = keys * 2 * ((args.sketch_nodes + 4) // 2)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "sketch key x node evaluations/sec (configs[4] sketch + Beaver verification)",
+            "value": elems / elapsed, "unit": "key-node evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64 (GF(2^62-2^30-1))",
+            "data": "synthetic one-hot frontier vectors, MAC keys and Beaver triples (sketch.rs:84-150 shape)",
+            "config": {"workload": "configs[4]: sketch_at + MulState verify, both servers in-process",
+                       "keys_per_gpu": args.sketch_keys, "nodes": args.sketch_nodes, "parallelism": f"key-shard x{world}"},
+            "keys_verified_per_s": keys / elapsed, "aes_blocks_per_s": blocks / elapsed,
+            "accepted": int(ok.sum()), "rejected": int((~ok).sum()),
+        }), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -74,8 +127,11 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
-    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords"],
-                    help="zipf = configs[1] (default); coords = configs[3] (d=2 lat/lon, data_len 16)")
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch"],
+                    help="zipf = configs[1] (default); coords = configs[3] (d=2 lat/lon, data_len 16); "
+                         "sketch = configs[4] (sketch + Beaver verification batch)")
+    ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
+    ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-sample-clients", type=int, default=4096)
@@ -100,6 +156,9 @@ def main():
 
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
+
+    if args.workload == "sketch":
+        return sketch_bench(args, world, rank, local_rank, dist)
 
     n_local = args.clients
     n_total = n_local * world

@@ -35,6 +35,8 @@ EXPORTS = [
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
     "fhh_comm_last_error",
+    "fhh_sketch_at_fe", "fhh_mul_cor_share_fe", "fhh_mul_cor_fe", "fhh_mul_out_share_fe", "fhh_mul_verify_fe",
+    "fhh_sim_sketch_verify_fe",
 ]
 
 
@@ -71,8 +73,25 @@ class FhhSimConfig(ctypes.Structure):
     ]
 
 
-SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_loop.hip", "fhh_microbench.hip", "fhh_host.cpp",
-           "fhh_comm.cpp")
+SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_loop.hip", "fhh_microbench.hip",
+           "fhh_host.cpp", "fhh_comm.cpp")
+
+
+class FhhSketchBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_keys", ctypes.c_uint64),
+        ("n_nodes", ctypes.c_uint32),
+        ("force_sequential", ctypes.c_uint32),
+        ("seeds_dev", ctypes.c_void_p),
+        ("x_dev", ctypes.c_void_p * 2),
+        ("kx_dev", ctypes.c_void_p * 2),
+        ("mac_dev", ctypes.c_void_p * 2),
+        ("mac2_dev", ctypes.c_void_p * 2),
+        ("triples_dev", ctypes.c_void_p * 2),
+        ("sketch_dev", ctypes.c_void_p * 2),
+        ("ok_dev", ctypes.c_void_p),
+        ("out_shares_dev", ctypes.c_void_p),
+    ]
 
 
 def build(verbose: bool = False) -> str:
@@ -114,6 +133,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise FhhError(f"{LIB_PATH} not built: run __graft_entry__.build() (the HIP extension is required; "
                        "there is no CPU fallback)")
+    # One HIP runtime per process: when PyTorch is present, load it first so libfhh.so's
+    # libamdhip64.so.7 dependency binds to the copy torch ships (torch cannot initialise the
+    # GPU after a second runtime has claimed the soname; the other order is the one that works).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     i = ctypes.c_int
     u32 = ctypes.c_uint32
@@ -158,6 +184,12 @@ def lib():
         "fhh_comm_destroy": (None, [vp]),
         "fhh_comm_allreduce_u64": (i, [vp, vp, vp, u64, vp]),
         "fhh_comm_last_error": (ctypes.c_char_p, []),
+        "fhh_sketch_at_fe": (i, [vp, u64, u32, u8p, u64p, u64p, u64p]),
+        "fhh_mul_cor_share_fe": (i, [vp, u64, u64p, u64p, u64p, u64p, u64p]),
+        "fhh_mul_cor_fe": (i, [u64, u64p, u64p, u64p]),
+        "fhh_mul_out_share_fe": (i, [vp, i, u64, u64p, u64p, u64p, u64p, u64p, u64p]),
+        "fhh_mul_verify_fe": (i, [u64, u64p, u64p, u8p]),
+        "fhh_sim_sketch_verify_fe": (i, [vp, P(FhhSketchBatch)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -1756,3 +1756,150 @@ int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus) {
 }
 
 }  // extern "C"
+
+// ---- sketch + Beaver verification (row a9) ------------------------------------------------
+namespace {
+uint64_t fe_canon_u64(uint64_t v) {   // any FE val -> value() (fastfield.rs:86-107,147-152)
+    const uint64_t mask = (1ull << 62) - 1;
+    uint64_t r = (v & mask) + (v >> 62) + ((v >> 62) << 30);
+    while (r >= kFeP) r -= kFeP;
+    return r;
+}
+}  // namespace
+
+int fhh_sketch_at_fe(fhh_ctx* ctx, uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint64_t* x,
+                     const uint64_t* kx, uint64_t* sketch6) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (n_keys == 0) return FHH_OK;
+    if (!seeds || !sketch6 || (n_nodes && (!x || !kx))) return ctx->fail(FHH_E_ARG, "sketch_at_fe: NULL buffer");
+    const size_t vb = (size_t)n_keys * n_nodes * 8;
+    DevBuf ds, dx, dkx, dout;
+    HIP_TRY(ctx, ds.ensure(n_keys * 16));
+    HIP_TRY(ctx, dx.ensure(vb));
+    HIP_TRY(ctx, dkx.ensure(vb));
+    HIP_TRY(ctx, dout.ensure(n_keys * 48));
+    HIP_TRY(ctx, hipMemcpyAsync(ds.p, seeds, n_keys * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (vb) {
+        HIP_TRY(ctx, hipMemcpyAsync(dx.p, x, vb, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(dkx.p, kx, vb, hipMemcpyHostToDevice, ctx->stream));
+    }
+    SketchArgs a{};
+    a.seeds = ds.as<uint8_t>();
+    a.x = dx.as<uint64_t>();
+    a.kx = dkx.as<uint64_t>();
+    a.out = dout.as<uint64_t>();
+    a.n_keys = n_keys;
+    a.n_nodes = n_nodes;
+    HIP_TRY(ctx, launch_sketch_fe(a, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(sketch6, dout.p, n_keys * 48, hipMemcpyDeviceToHost, ctx->stream));
+    return sync(ctx);
+}
+
+static int mul_fe_host(fhh_ctx* ctx, uint32_t mode, int server_idx, uint64_t n, const uint64_t* sketch6,
+                       const uint64_t* mac, const uint64_t* mac2, const uint64_t* triples9, const uint64_t* cor6,
+                       uint64_t* out) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return FHH_OK;
+    if (!sketch6 || !mac || !mac2 || !triples9 || !out || (mode == 1 && !cor6))
+        return ctx->fail(FHH_E_ARG, "mul_fe: NULL buffer");
+    DevBuf dsk, dm, dm2, dt, dc, dout;
+    const size_t out_words = mode == 0 ? 6 : 1;
+    HIP_TRY(ctx, dsk.ensure(n * 48));
+    HIP_TRY(ctx, dm.ensure(n * 8));
+    HIP_TRY(ctx, dm2.ensure(n * 8));
+    HIP_TRY(ctx, dt.ensure(n * 72));
+    HIP_TRY(ctx, dc.ensure(n * 48));
+    HIP_TRY(ctx, dout.ensure(n * 8 * out_words));
+    HIP_TRY(ctx, hipMemcpyAsync(dsk.p, sketch6, n * 48, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dm.p, mac, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dm2.p, mac2, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dt.p, triples9, n * 72, hipMemcpyHostToDevice, ctx->stream));
+    if (mode == 1) HIP_TRY(ctx, hipMemcpyAsync(dc.p, cor6, n * 48, hipMemcpyHostToDevice, ctx->stream));
+    MulArgs a{};
+    a.sketch = dsk.as<uint64_t>();
+    a.mac = dm.as<uint64_t>();
+    a.mac2 = dm2.as<uint64_t>();
+    a.triples = dt.as<uint64_t>();
+    a.cor = dc.as<uint64_t>();
+    a.out = dout.as<uint64_t>();
+    a.n = n;
+    a.mode = mode;
+    a.server_idx = server_idx ? 1 : 0;
+    HIP_TRY(ctx, launch_mul_fe(a, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(out, dout.p, n * 8 * out_words, hipMemcpyDeviceToHost, ctx->stream));
+    return sync(ctx);
+}
+
+int fhh_mul_cor_share_fe(fhh_ctx* ctx, uint64_t n, const uint64_t* sketch6, const uint64_t* mac_key,
+                         const uint64_t* mac_key2, const uint64_t* triples9, uint64_t* cor_share6) {
+    return mul_fe_host(ctx, 0, 0, n, sketch6, mac_key, mac_key2, triples9, nullptr, cor_share6);
+}
+
+int fhh_mul_out_share_fe(fhh_ctx* ctx, int server_idx, uint64_t n, const uint64_t* sketch6, const uint64_t* mac_key,
+                         const uint64_t* mac_key2, const uint64_t* triples9, const uint64_t* cor6, uint64_t* out) {
+    return mul_fe_host(ctx, 1, server_idx, n, sketch6, mac_key, mac_key2, triples9, cor6, out);
+}
+
+int fhh_mul_cor_fe(uint64_t n, const uint64_t* share0, const uint64_t* share1, uint64_t* cor6) {
+    if (n && (!share0 || !share1 || !cor6)) {
+        g_err = "mul_cor_fe: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < 6 * n; i++) {
+        const uint64_t s = fe_canon_u64(share0[i]) + fe_canon_u64(share1[i]);
+        cor6[i] = s >= kFeP ? s - kFeP : s;
+    }
+    return FHH_OK;
+}
+
+int fhh_mul_verify_fe(uint64_t n, const uint64_t* out0, const uint64_t* out1, uint8_t* ok) {
+    if (n && (!out0 || !out1 || !ok)) {
+        g_err = "mul_verify_fe: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t s = fe_canon_u64(out0[i]) + fe_canon_u64(out1[i]);
+        ok[i] = (s >= kFeP ? s - kFeP : s) == 0;
+    }
+    return FHH_OK;
+}
+
+int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!b) return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: NULL batch");
+    if (b->n_keys == 0) return FHH_OK;
+    if (!b->seeds_dev || !b->ok_dev) return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: NULL buffer");
+    for (int s = 0; s < 2; s++)
+        if (!b->mac_dev[s] || !b->mac2_dev[s] || !b->triples_dev[s] || !b->sketch_dev[s] ||
+            (b->n_nodes && (!b->x_dev[s] || !b->kx_dev[s])))
+            return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: NULL buffer");
+    for (int s = 0; s < 2; s++) {
+        SketchArgs a{};
+        a.seeds = b->seeds_dev;
+        a.x = b->x_dev[s];
+        a.kx = b->kx_dev[s];
+        a.out = b->sketch_dev[s];
+        a.n_keys = b->n_keys;
+        a.n_nodes = b->n_nodes;
+        a.force_sequential = b->force_sequential;
+        HIP_TRY(ctx, launch_sketch_fe(a, ctx->stream));
+    }
+    VerifyArgs v{};
+    for (int s = 0; s < 2; s++) {
+        v.sketch[s] = b->sketch_dev[s];
+        v.mac[s] = b->mac_dev[s];
+        v.mac2[s] = b->mac2_dev[s];
+        v.triples[s] = b->triples_dev[s];
+    }
+    v.ok = b->ok_dev;
+    v.out_shares = b->out_shares_dev;
+    v.n = b->n_keys;
+    HIP_TRY(ctx, launch_verify_fe(v, ctx->stream));
+    return sync(ctx);
+}

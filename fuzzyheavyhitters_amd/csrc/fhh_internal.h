@@ -161,6 +161,40 @@ hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t ma
                             uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
                             hipStream_t stream);
 
+// ---- sketch + Beaver verification (fhh_sketch.hip), FE values as u64 (any representation) ----
+struct SketchArgs {
+    const uint8_t* seeds;   // [n_keys][16] PrgStream seeds (sketch_at's rand_stream)
+    const uint64_t* x;      // [n_keys][n_nodes]
+    const uint64_t* kx;     // [n_keys][n_nodes]
+    uint64_t* out;          // [n_keys][6] canonical {r_x, r2_x, r_kx, rand1, rand2, rand3}
+    uint64_t n_keys;
+    uint32_t n_nodes;
+    uint32_t force_sequential;   // 1: every key takes the sequential-stream path (tests)
+};
+struct MulArgs {
+    const uint64_t* sketch;   // [n][6]
+    const uint64_t* mac;      // [n]
+    const uint64_t* mac2;     // [n]
+    const uint64_t* triples;  // [n][3][a, b, c]
+    const uint64_t* cor;      // [n][6] (mode 1)
+    uint64_t* out;            // mode 0: [n][6] cor share; mode 1: [n] out share
+    uint64_t n;
+    uint32_t mode;
+    uint32_t server_idx;
+};
+struct VerifyArgs {
+    const uint64_t* sketch[2];
+    const uint64_t* mac[2];
+    const uint64_t* mac2[2];
+    const uint64_t* triples[2];
+    uint8_t* ok;              // [n]
+    uint64_t* out_shares;     // [2][n] or null
+    uint64_t n;
+};
+hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream);
+hipError_t launch_mul_fe(const MulArgs& a, hipStream_t stream);
+hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream);
+
 // ---- bitsliced k_expand (fhh_expand_bs.hip) -------------------------------------------------
 // Variant kBsVariant selects it; seeds (CW, root, prefix tables) are then stored per key row as
 // [32 quads][npad / 32] uint4 bitsliced words (see fhh_expand_bs.hip). Work item = one

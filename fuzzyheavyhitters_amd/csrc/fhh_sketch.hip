@@ -1,0 +1,384 @@
+// Sketch + Beaver-triple verification: SketchDPFKey::sketch_at
+// (src/sketch.rs:157-200) and MulState (src/mpc.rs:83-220), both fully commented out in the
+// reference; restated from the commented text for T = FE (GF(2^62 - 2^30 - 1)).
+//
+//   k_sketch_fe   one wave per key: the key's PrgStream (AES-128-CTR, key = the key's sketch
+//                 seed, IV 0, prg.rs:82-90) is random-access, so lane l produces keystream
+//                 blocks l, l+64, ... (two u64 draws each: rand1..3, then r_j for node j),
+//                 reads its nodes' (x, kx) coalesced, accumulates <r,x>, <r^2,x>, <r,kx> mod p
+//                 and the wave reduces. FE::from_rng redraws on a draw >= p (P ~ 2^-32): a
+//                 wave that sees one falls back to the sequential stream for that key.
+//   k_mul_fe      MulState::cor_share / out_share per key (one lane per key).
+//   k_verify_fe   MulState::cor + out shares of both servers + verify, fused (in-process).
+#include "fhh_internal.h"
+#include "expand_kernel.h"
+#include "aes_tables.h"
+#include "field_arith.h"
+
+namespace fhh {
+
+constexpr uint64_t kFeP_ = kFieldFeP;
+
+__constant__ WordTable c_T0_sk = T0;
+
+// ---- FE, canonical representatives in [0, p) ---------------------------------------------
+__device__ __forceinline__ uint64_t fe_addc(uint64_t a, uint64_t b) {
+    const uint64_t s = a + b;
+    return s >= kFeP_ ? s - kFeP_ : s;
+}
+__device__ __forceinline__ uint64_t fe_negc(uint64_t a) { return a ? kFeP_ - a : 0; }
+__device__ __forceinline__ uint64_t fe_subc(uint64_t a, uint64_t b) { return fe_addc(a, fe_negc(b)); }
+// a * b mod p, a, b < 2^63: 2^62 = 2^30 + 1 (mod p) folds the product twice (fastfield.rs:299-328)
+__device__ __forceinline__ uint64_t fe_mulc(uint64_t a, uint64_t b) {
+    const unsigned __int128 v = (unsigned __int128)a * b;
+    const uint64_t mask = (1ull << 62) - 1;
+    const unsigned __int128 h = v >> 62;
+    const unsigned __int128 t = (v & mask) + h + (h << 30);
+    const uint64_t h2 = (uint64_t)(t >> 62);
+    uint64_t r = ((uint64_t)t & mask) + h2 + (h2 << 30);
+    if (r >= kFeP_) r -= kFeP_;
+    if (r >= kFeP_) r -= kFeP_;
+    return r;
+}
+__device__ __forceinline__ uint64_t fe_canon_dev(uint64_t v) {   // any u64 val -> value()
+    const uint64_t mask = (1ull << 62) - 1;
+    uint64_t r = (v & mask) + (v >> 62) + ((v >> 62) << 30);
+    if (r >= kFeP_) r -= kFeP_;
+    if (r >= kFeP_) r -= kFeP_;
+    return r;
+}
+
+// ---- AES-128 with a per-key schedule (the PrgStream cipher) -------------------------------
+// Key schedule on little-endian column words (FIPS-197 5.2): RotWord = rotr 8, rcon in byte 0.
+// SubWord reads S[x] = byte 1 of T0[x] from the LDS table (TabT0R32: entry x, replica lane % 32
+// at word 32 x + lane % 32) — 4 independent ds_read_b32 per round instead of dependent scalar
+// loads from constant memory.
+__device__ __forceinline__ uint32_t sub_word(uint32_t w, const uint32_t* tbl, uint32_t rep) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) o |= ((tbl[(((w >> (8 * k)) & 0xFF) << 5) + rep] >> 8) & 0xFF) << (8 * k);
+    return o;
+}
+
+__device__ __forceinline__ void key_schedule(const uint32_t key[4], uint32_t (&rk)[11][4], const uint32_t* tbl,
+                                             uint32_t rep) {
+    uint32_t w[44];
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = key[i];
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int i = 4; i < 44; i++) {
+        uint32_t t = w[i - 1];
+        if (i % 4 == 0) {
+            t = sub_word((t >> 8) | (t << 24), tbl, rep) ^ rcon;
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+        }
+        w[i] = w[i - 4] ^ t;
+    }
+#pragma unroll
+    for (int r = 0; r < 11; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) rk[r][c] = w[4 * r + c];
+}
+
+// T-table rounds (layout TabT0R32: 32 KiB, 32 replicas) with runtime round keys
+template <class Tab, int NB>
+__device__ __forceinline__ void aes_rk(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                       const uint32_t (&rk)[11][4]) {
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[q][c] = s[q][c] ^ rk[0][c];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                y[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, rk[r][c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = y[q][c];
+    }
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi), rk[10][c]);
+        }
+}
+
+using SkTab = TabT0R32<DevOpsX>;
+constexpr int kSketchThreads = 256;
+
+// keystream block b (< 2^32): AES_seed(BE128(b)) -> two LE u64 draws (positions 2b, 2b+1)
+__device__ __forceinline__ void ks_block(uint64_t b, const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                         const uint32_t (&rk)[11][4], uint64_t& d0, uint64_t& d1) {
+    uint32_t s[1][4] = {{0u, 0u, __builtin_bswap32((uint32_t)(b >> 32)), __builtin_bswap32((uint32_t)b)}};
+    aes_rk<SkTab, 1>(s, tbl, b0, b1, rk);
+    d0 = (uint64_t)s[0][0] | ((uint64_t)s[0][1] << 32);
+    d1 = (uint64_t)s[0][2] | ((uint64_t)s[0][3] << 32);
+}
+
+// draw `pos` of the key's stream (value v = low 62 bits): rand1..3 or node j = pos - 3
+__device__ __forceinline__ void sketch_draw(uint64_t pos, uint64_t v, uint64_t xv, uint64_t kxv, uint64_t F,
+                                            int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1, uint64_t& rx,
+                                            uint64_t& r2x, uint64_t& rkx) {
+    if (pos < 3) {
+        // lane 0 holds rand1, rand2 (block 0); lane 1 holds rand3 (block 1, draw 0)
+        rej |= v >= kFeP_;
+        if (h == 0) rnd0 = v;
+        else rnd1 = v;
+    } else if (pos < F + 3) {
+        rej |= v >= kFeP_;
+        const uint64_t r2 = fe_mulc(v, v);
+        xv = fe_canon_dev(xv);
+        rx = fe_addc(rx, fe_mulc(xv, v));
+        r2x = fe_addc(r2x, fe_mulc(xv, r2));
+        rkx = fe_addc(rkx, fe_mulc(fe_canon_dev(kxv), v));
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_fe_sum(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fe_addc(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
+    __shared__ uint32_t tbl[SkTab::kWords];
+    for (int i = threadIdx.x; i < SkTab::kWords; i += kSketchThreads) tbl[i] = SkTab::word(c_T0_sk.v, i);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t b0, b1;
+    SkTab::bases(lane, b0, b1);
+    const uint64_t mask = (1ull << 62) - 1;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kSketchThreads / 64);
+    const uint64_t F = a.n_nodes;
+    const uint64_t nb = (F + 3 + 1) / 2;   // draws 0..F+2
+    for (uint64_t key = (uint64_t)blockIdx.x * (kSketchThreads / 64) + (threadIdx.x >> 6); key < a.n_keys;
+         key += nwaves) {
+        const uint64_t k = __builtin_amdgcn_readfirstlane((uint32_t)key) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(key >> 32)) << 32);
+        uint32_t seed[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            seed[c] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(a.seeds)[4 * k + c]);
+        uint32_t rk[11][4];
+        key_schedule(seed, rk, tbl, lane & 31);
+        const uint64_t* x = a.x + k * F;
+        const uint64_t* kx = a.kx + k * F;
+        uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
+        bool rej = false;
+        if (!a.force_sequential) {
+            // two keystream blocks per lane per pass (AES in lockstep for ILP); the pass's four
+            // (x, kx) pairs are loaded before the AES so their latency hides behind it
+            for (uint64_t bb = lane; bb < nb; bb += 128) {
+                uint64_t xv[4] = {0, 0, 0, 0}, kxv[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint64_t pos = 2 * (bb + 64 * q) + h;
+                        if (pos >= 3 && pos < F + 3) {
+                            xv[2 * q + h] = x[pos - 3];
+                            kxv[2 * q + h] = kx[pos - 3];
+                        }
+                    }
+                uint32_t st[2][4];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const uint64_t b = bb + 64 * q;
+                    st[q][0] = 0u;
+                    st[q][1] = 0u;
+                    st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
+                    st[q][3] = __builtin_bswap32((uint32_t)b);
+                }
+                aes_rk<SkTab, 2>(st, tbl, b0, b1, rk);
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const uint64_t b = bb + 64 * q;
+                    if (b >= nb) break;
+                    const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
+                                            (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+                        sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1, rx,
+                                    r2x, rkx);
+                }
+            }
+        }
+        const bool any_rej = a.force_sequential || __ballot(rej) != 0;
+        if (!any_rej) {
+            rx = wave_fe_sum(rx);
+            r2x = wave_fe_sum(r2x);
+            rkx = wave_fe_sum(rkx);
+            const uint64_t rand1 = __shfl(rnd0, 0, 64);
+            const uint64_t rand2 = __shfl(rnd1, 0, 64);
+            const uint64_t rand3 = __shfl(rnd0, 1, 64);
+            if (lane == 0) {
+                uint64_t* o = a.out + 6 * k;
+                o[0] = rx;
+                o[1] = r2x;
+                o[2] = rkx;
+                o[3] = rand1;
+                o[4] = rand2;
+                o[5] = rand3;
+            }
+        } else if (lane == 0) {
+            // sequential PrgStream with FE::from_rng redraws (field.rs:252-264) for this key
+            uint64_t pos = 0, cur_b = ~0ull, d[2] = {0, 0};
+            auto draw = [&]() -> uint64_t {
+                for (;;) {
+                    const uint64_t b = pos >> 1;
+                    if (b != cur_b) {
+                        ks_block(b, tbl, b0, b1, rk, d[0], d[1]);
+                        cur_b = b;
+                    }
+                    const uint64_t v = d[pos & 1] & mask;
+                    pos++;
+                    if (v < kFeP_) return v;
+                }
+            };
+            const uint64_t rand1 = draw(), rand2 = draw(), rand3 = draw();
+            uint64_t sx = 0, s2x = 0, skx = 0;
+            for (uint64_t j = 0; j < F; j++) {
+                const uint64_t r = draw();
+                const uint64_t r2 = fe_mulc(r, r);
+                const uint64_t xv = fe_canon_dev(x[j]), kxv = fe_canon_dev(kx[j]);
+                sx = fe_addc(sx, fe_mulc(xv, r));
+                s2x = fe_addc(s2x, fe_mulc(xv, r2));
+                skx = fe_addc(skx, fe_mulc(kxv, r));
+            }
+            uint64_t* o = a.out + 6 * k;
+            o[0] = sx;
+            o[1] = s2x;
+            o[2] = skx;
+            o[3] = rand1;
+            o[4] = rand2;
+            o[5] = rand3;
+        }
+    }
+}
+
+hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
+    if (a.n_keys == 0) return hipSuccess;
+    int cus = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t waves_needed = a.n_keys;
+    uint64_t blocks = (waves_needed + 3) / 4;
+    const uint64_t cap = (uint64_t)cus * 16;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_sketch_fe, dim3((unsigned)blocks), dim3(kSketchThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+// ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------
+// MulState::new: xs = [r_x, k, r_x], ys = [r_x, k, k], zs = [-r2_x, -k2, -r_kx],
+// rs = [rand1, rand2, rand3] (sketch6 = {r_x, r2_x, r_kx, rand1, rand2, rand3}).
+struct MulView {
+    uint64_t xs[3], ys[3], zs[3], rs[3];
+};
+
+__device__ __forceinline__ MulView mul_view(const uint64_t* sk, uint64_t mac, uint64_t mac2) {
+    MulView m;
+    const uint64_t rx = fe_canon_dev(sk[0]), r2x = fe_canon_dev(sk[1]), rkx = fe_canon_dev(sk[2]);
+    mac = fe_canon_dev(mac);
+    mac2 = fe_canon_dev(mac2);
+    m.xs[0] = rx;  m.ys[0] = rx;  m.zs[0] = fe_negc(r2x);
+    m.xs[1] = mac; m.ys[1] = mac; m.zs[1] = fe_negc(mac2);
+    m.xs[2] = rx;  m.ys[2] = mac; m.zs[2] = fe_negc(rkx);
+    for (int i = 0; i < 3; i++) m.rs[i] = fe_canon_dev(sk[3 + i]);
+    return m;
+}
+
+// out_share term sum: sum_i r_i * ([server 1] d*e + d*b + e*a + c + z)
+__device__ __forceinline__ uint64_t out_share_fe(const MulView& m, int server_idx, const uint64_t* tr,
+                                                 const uint64_t* cor) {
+    uint64_t out = 0;
+    for (int i = 0; i < 3; i++) {
+        const uint64_t d = fe_canon_dev(cor[i]), e = fe_canon_dev(cor[3 + i]);
+        const uint64_t ta = fe_canon_dev(tr[3 * i]), tb = fe_canon_dev(tr[3 * i + 1]), tc = fe_canon_dev(tr[3 * i + 2]);
+        uint64_t term = server_idx ? fe_mulc(d, e) : 0;
+        term = fe_addc(term, fe_mulc(d, tb));
+        term = fe_addc(term, fe_mulc(e, ta));
+        term = fe_addc(term, tc);
+        term = fe_addc(term, m.zs[i]);
+        out = fe_addc(out, fe_mulc(term, m.rs[i]));
+    }
+    return out;
+}
+
+// mode 0: cor_share (mpc.rs:142-158) -> out [n][6] {d0,d1,d2,e0,e1,e2}
+// mode 1: out_share (mpc.rs:182-212) -> out [n]
+__global__ __launch_bounds__(256) void k_mul_fe(MulArgs a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const MulView m = mul_view(a.sketch + 6 * i, a.mac[i], a.mac2[i]);
+        const uint64_t* tr = a.triples + 9 * i;
+        if (a.mode == 0) {
+            for (int t = 0; t < 3; t++) {
+                a.out[6 * i + t] = fe_subc(m.xs[t], fe_canon_dev(tr[3 * t]));
+                a.out[6 * i + 3 + t] = fe_subc(m.ys[t], fe_canon_dev(tr[3 * t + 1]));
+            }
+        } else {
+            a.out[i] = out_share_fe(m, a.server_idx, tr, a.cor + 6 * i);
+        }
+    }
+}
+
+// both servers in one process: cor shares, cor = share0 + share1, out shares, verify
+__global__ __launch_bounds__(256) void k_verify_fe(VerifyArgs a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        MulView m[2];
+        uint64_t cor[6] = {0, 0, 0, 0, 0, 0};
+        for (int s = 0; s < 2; s++) {
+            m[s] = mul_view(a.sketch[s] + 6 * i, a.mac[s][i], a.mac2[s][i]);
+            const uint64_t* tr = a.triples[s] + 9 * i;
+            for (int t = 0; t < 3; t++) {
+                cor[t] = fe_addc(cor[t], fe_subc(m[s].xs[t], fe_canon_dev(tr[3 * t])));
+                cor[3 + t] = fe_addc(cor[3 + t], fe_subc(m[s].ys[t], fe_canon_dev(tr[3 * t + 1])));
+            }
+        }
+        const uint64_t o0 = out_share_fe(m[0], 0, a.triples[0] + 9 * i, cor);
+        const uint64_t o1 = out_share_fe(m[1], 1, a.triples[1] + 9 * i, cor);
+        if (a.out_shares) {
+            a.out_shares[i] = o0;
+            a.out_shares[a.n + i] = o1;
+        }
+        a.ok[i] = fe_addc(o0, o1) == 0 ? 1 : 0;   // MulState::verify (mpc.rs:214-220)
+    }
+}
+
+static unsigned grid_for(uint64_t n) {
+    const uint64_t b = (n + 255) / 256;
+    return (unsigned)(b < 65535 ? (b ? b : 1) : 65535);
+}
+
+hipError_t launch_mul_fe(const MulArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mul_fe, dim3(grid_for(a.n)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify_fe, dim3(grid_for(a.n)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace fhh

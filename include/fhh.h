@@ -211,6 +211,49 @@ typedef struct fhh_sim_config {
  * prune_last. Heavy hitters are then read with fhh_final_shares(ctx0, ...). */
 int fhh_sim_crawl(fhh_ctx* ctx0, fhh_ctx* ctx1, const fhh_sim_config* cfg);
 
+/* ---- sketch + Beaver-triple verification ------------------------------
+ * SketchDPFKey::sketch_at (src/sketch.rs:157-200) and MulState (src/mpc.rs:83-220), for
+ * T = FE. Both files are fully commented out in the reference (parity unpinned beyond the
+ * protocol's identities). FE values may be passed in any u64 representation; every output is
+ * canonical. One key = one client's vector over the frontier: x[key][node], kx[key][node]
+ * (the (x, k.x) pairs `vector_in` of sketch_at), with the key's rand_stream given as the
+ * PrgStream seed (AES-128-CTR, key = seed, IV 0: PrgSeed::to_rng, prg.rs:82-90).
+ * sketch6 per key = {r_x, r2_x, r_kx, rand1, rand2, rand3} (SketchOutput, sketch.rs:27-42).
+ * triples9 per key = the level's 3 TripleShares {a, b, c} (mpc.rs:18-45). */
+
+/* sketch_at for n_keys keys (host buffers: seeds [n][16], x / kx [n][n_nodes], out [n][6]). */
+int fhh_sketch_at_fe(fhh_ctx* ctx, uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint64_t* x,
+                     const uint64_t* kx, uint64_t* sketch6);
+/* MulState::new + cor_share (mpc.rs:83-158): cor_share6 [n][6] = {d0, d1, d2, e0, e1, e2}. */
+int fhh_mul_cor_share_fe(fhh_ctx* ctx, uint64_t n, const uint64_t* sketch6, const uint64_t* mac_key,
+                         const uint64_t* mac_key2, const uint64_t* triples9, uint64_t* cor_share6);
+/* MulState::cor (mpc.rs:160-180): cor6 = share0 + share1 (host arithmetic). */
+int fhh_mul_cor_fe(uint64_t n, const uint64_t* share0, const uint64_t* share1, uint64_t* cor6);
+/* MulState::out_share (mpc.rs:182-212); server_idx 1 adds d*e. out [n]. */
+int fhh_mul_out_share_fe(fhh_ctx* ctx, int server_idx, uint64_t n, const uint64_t* sketch6, const uint64_t* mac_key,
+                         const uint64_t* mac_key2, const uint64_t* triples9, const uint64_t* cor6, uint64_t* out);
+/* MulState::verify (mpc.rs:214-220): ok[i] = out0[i] + out1[i] == 0 (host arithmetic). */
+int fhh_mul_verify_fe(uint64_t n, const uint64_t* out0, const uint64_t* out1, uint8_t* ok);
+
+/* In-process leader + both servers, device-resident batch (main.rs:14-70 verify_sketches):
+ * both servers' sketch_at, cor shares, cor, out shares, verify. All pointers are device
+ * pointers on ctx's GPU; synchronous. */
+typedef struct fhh_sketch_batch {
+    uint64_t n_keys;
+    uint32_t n_nodes;
+    uint32_t force_sequential;        /* 1: sequential-stream path for every key (tests)   */
+    const uint8_t* seeds_dev;         /* [n][16], the same stream seeds on both servers    */
+    const uint64_t* x_dev[2];         /* per server [n][n_nodes]                           */
+    const uint64_t* kx_dev[2];
+    const uint64_t* mac_dev[2];       /* [n] shares of the MAC key k                       */
+    const uint64_t* mac2_dev[2];      /* [n] shares of k^2                                 */
+    const uint64_t* triples_dev[2];   /* [n][9]                                            */
+    uint64_t* sketch_dev[2];          /* out [n][6]                                        */
+    uint8_t* ok_dev;                  /* out [n]                                           */
+    uint64_t* out_shares_dev;         /* out [2][n] or NULL                                */
+} fhh_sketch_batch;
+int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* batch);
+
 /* ---- statistics ------------------------------------------------------------------------ */
 
 typedef struct fhh_stats {

@@ -470,3 +470,165 @@ static inline uint64_t mix64(uint64_t z) {
 uint64_t orc_sim_prf(uint64_t seed, uint64_t level, uint64_t child, uint64_t client, uint32_t word) {
     return mix64(mix64(mix64(mix64(seed ^ level) ^ child) ^ client) ^ word);
 }
+
+/* ------------------------------------------------------------------ */
+/* Sketch + Beaver-triple verification (row a9; DEAD in the reference: */
+/* src/sketch.rs and src/mpc.rs are fully commented out, so this      */
+/* restates the commented text — parity unpinned beyond the protocol's */
+/* own identities, see tests/test_sketch.py).                          */
+/* ------------------------------------------------------------------ */
+
+/* PrgSeed::to_rng (prg.rs:82-90): AES-128-CTR, key = seed, IV = 0. Crate `aes-ctr 0.4`
+ * (Cargo.lock) counts the whole 128-bit block big-endian from the IV, so keystream block b is
+ * AES_seed(BE128(b)). PrgStream::next_u64 = next_u64_via_fill (prg.rs:166-168, rand_core):
+ * the next 8 keystream bytes, little-endian. Draw number `pos` = bytes [8 pos, 8 pos + 8). */
+uint64_t orc_prg_stream_u64(const uint8_t seed[16], uint64_t pos) {
+    oracle_init();
+    uint8_t rk[176], ctr[16] = {0}, ks[16];
+    key_expand(seed, rk);
+    const uint64_t b = pos >> 1;
+    for (int i = 0; i < 8; i++) ctr[15 - i] = (uint8_t)(b >> (8 * i));
+    aes128_encrypt_rk(rk, ctr, ks);
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)ks[8 * (pos & 1) + i] << (8 * i);
+    return v;
+}
+
+/* FE::from_rng (field.rs:252-264 + fastfield.rs:125-139): redraw until the low 62 bits are
+ * below p. Returns the FE val; *pos advances past the draws used. */
+static uint64_t fe_from_stream(const uint8_t rk[176], uint64_t* pos, uint8_t ks[16], uint64_t* ks_block) {
+    for (;;) {
+        const uint64_t b = *pos >> 1;
+        if (*ks_block != b) {
+            uint8_t ctr[16] = {0};
+            for (int i = 0; i < 8; i++) ctr[15 - i] = (uint8_t)(b >> (8 * i));
+            aes128_encrypt_rk(rk, ctr, ks);
+            *ks_block = b;
+        }
+        uint64_t v = 0;
+        for (int i = 0; i < 8; i++) v |= (uint64_t)ks[8 * (*pos & 1) + i] << (8 * i);
+        (*pos)++;
+        v &= FE_MASK;
+        if (v < FE_P) return v;
+    }
+}
+
+/* SketchDPFKey::sketch_at (sketch.rs:157-200) for T = FE, one key:
+ *   rand1..3 = from_rng, then per (x, kx): r = from_rng; r2 = r*r;
+ *   r_x += x*r; r2_x += x*r2; r_kx += kx*r   (mul_lazy = mul, add_lazy = add for FE).
+ * out6 = canonical {r_x, r2_x, r_kx, rand1, rand2, rand3}; x / kx as FE vals. */
+void orc_sketch_fe(const uint8_t seed[16], uint32_t n_nodes, const uint64_t* x, const uint64_t* kx, uint64_t* out6) {
+    oracle_init();
+    uint8_t rk[176], ks[16];
+    key_expand(seed, rk);
+    uint64_t pos = 0, blk = ~(uint64_t)0;
+    const uint64_t rand1 = fe_from_stream(rk, &pos, ks, &blk);
+    const uint64_t rand2 = fe_from_stream(rk, &pos, ks, &blk);
+    const uint64_t rand3 = fe_from_stream(rk, &pos, ks, &blk);
+    uint64_t r_x = 0, r2_x = 0, r_kx = 0;
+    for (uint32_t j = 0; j < n_nodes; j++) {
+        const uint64_t r = fe_from_stream(rk, &pos, ks, &blk);
+        const uint64_t r2 = orc_fe_mul(r, r);
+        r_x = orc_fe_add(r_x, orc_fe_mul(x[j], r));
+        r2_x = orc_fe_add(r2_x, orc_fe_mul(x[j], r2));
+        r_kx = orc_fe_add(r_kx, orc_fe_mul(kx[j], r));
+    }
+    out6[0] = orc_fe_value(r_x);
+    out6[1] = orc_fe_value(r2_x);
+    out6[2] = orc_fe_value(r_kx);
+    out6[3] = orc_fe_value(rand1);
+    out6[4] = orc_fe_value(rand2);
+    out6[5] = orc_fe_value(rand3);
+}
+
+void orc_sketch_fe_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint64_t* x,
+                         const uint64_t* kx, uint64_t* out6, int nthreads) {
+    oracle_init();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < (int64_t)n_keys; i++)
+        orc_sketch_fe(seeds + 16 * i, n_nodes, x + (uint64_t)i * n_nodes, kx + (uint64_t)i * n_nodes, out6 + 6 * i);
+}
+
+/* MulState::new (mpc.rs:83-140) for T = FE: xs = [r_x, k, r_x], ys = [r_x, k, k],
+ * zs = [-r2_x, -k2, -r_kx], rs = [rand1, rand2, rand3]. */
+static void mul_state(const uint64_t* sk6, uint64_t mac, uint64_t mac2, uint64_t xs[3], uint64_t ys[3],
+                      uint64_t zs[3], uint64_t rs[3]) {
+    xs[0] = sk6[0]; ys[0] = sk6[0]; zs[0] = orc_fe_neg(sk6[1]);
+    xs[1] = mac;    ys[1] = mac;    zs[1] = orc_fe_neg(mac2);
+    xs[2] = sk6[0]; ys[2] = mac;    zs[2] = orc_fe_neg(sk6[2]);
+    rs[0] = sk6[3]; rs[1] = sk6[4]; rs[2] = sk6[5];
+}
+
+/* MulState::cor_share (mpc.rs:142-158): d_i = x_i - a_i, e_i = y_i - b_i.
+ * triples9 = {a0,b0,c0, a1,b1,c1, a2,b2,c2}; out6 = canonical {d0,d1,d2,e0,e1,e2}. */
+void orc_mul_cor_share_fe(const uint64_t* sk6, uint64_t mac, uint64_t mac2, const uint64_t* triples9,
+                          uint64_t* out6) {
+    uint64_t xs[3], ys[3], zs[3], rs[3];
+    mul_state(sk6, mac, mac2, xs, ys, zs, rs);
+    for (int i = 0; i < 3; i++) {
+        out6[i] = orc_fe_value(orc_fe_sub(xs[i], triples9[3 * i]));
+        out6[3 + i] = orc_fe_value(orc_fe_sub(ys[i], triples9[3 * i + 1]));
+    }
+}
+
+/* MulState::cor (mpc.rs:160-180): d = d0 + d1, e = e0 + e1. */
+void orc_mul_cor_fe(const uint64_t* s0, const uint64_t* s1, uint64_t* cor6) {
+    for (int k = 0; k < 6; k++) cor6[k] = orc_fe_value(orc_fe_add(orc_fe_add(0, s0[k]), s1[k]));
+}
+
+/* MulState::out_share (mpc.rs:182-212): sum_i r_i * ([server 1] d*e + d*b + e*a + c + z). */
+uint64_t orc_mul_out_share_fe(int server_idx, const uint64_t* sk6, uint64_t mac, uint64_t mac2,
+                              const uint64_t* triples9, const uint64_t* cor6) {
+    uint64_t xs[3], ys[3], zs[3], rs[3];
+    mul_state(sk6, mac, mac2, xs, ys, zs, rs);
+    uint64_t out = 0;
+    for (int i = 0; i < 3; i++) {
+        const uint64_t d = cor6[i], e = cor6[3 + i];
+        const uint64_t a = triples9[3 * i], b = triples9[3 * i + 1], c = triples9[3 * i + 2];
+        uint64_t term = 0;
+        if (server_idx) term = orc_fe_add(term, orc_fe_mul(d, e));
+        term = orc_fe_add(term, orc_fe_mul(d, b));
+        term = orc_fe_add(term, orc_fe_mul(e, a));
+        term = orc_fe_add(term, c);
+        term = orc_fe_add(term, zs[i]);
+        term = orc_fe_mul(term, rs[i]);
+        out = orc_fe_add(out, term);
+    }
+    return orc_fe_value(out);
+}
+
+/* MulState::verify (mpc.rs:214-220): out0 + out1 == 0. */
+int orc_mul_verify_fe(uint64_t out0, uint64_t out1) { return orc_fe_value(orc_fe_add(out0, out1)) == 0; }
+
+/* The whole per-level check of main.rs:14-70 (verify_sketches) for a batch of keys, both
+ * servers in one process: sketch, cor shares, cor, out shares, verify -> ok[n]. */
+void orc_sketch_verify_fe_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint64_t* x0,
+                                const uint64_t* kx0, const uint64_t* x1, const uint64_t* kx1,
+                                const uint64_t* mac /*[2][n]*/, const uint64_t* mac2 /*[2][n]*/,
+                                const uint64_t* triples /*[2][n][9]*/, uint8_t* ok, uint64_t* out_shares /*[2][n]*/,
+                                int nthreads) {
+    oracle_init();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < (int64_t)n_keys; i++) {
+        uint64_t sk[2][6], cs[2][6], cor[6], o[2];
+        const uint64_t* xs[2] = {x0, x1};
+        const uint64_t* kxs[2] = {kx0, kx1};
+        for (int s = 0; s < 2; s++)
+            orc_sketch_fe(seeds + 16 * i, n_nodes, xs[s] + (uint64_t)i * n_nodes, kxs[s] + (uint64_t)i * n_nodes,
+                          sk[s]);
+        for (int s = 0; s < 2; s++)
+            orc_mul_cor_share_fe(sk[s], mac[s * n_keys + i], mac2[s * n_keys + i], triples + (s * n_keys + i) * 9,
+                                 cs[s]);
+        orc_mul_cor_fe(cs[0], cs[1], cor);
+        for (int s = 0; s < 2; s++)
+            o[s] = orc_mul_out_share_fe(s, sk[s], mac[s * n_keys + i], mac2[s * n_keys + i],
+                                        triples + (s * n_keys + i) * 9, cor);
+        ok[i] = (uint8_t)orc_mul_verify_fe(o[0], o[1]);
+        if (out_shares) {
+            out_shares[i] = o[0];
+            out_shares[n_keys + i] = o[1];
+        }
+    }
+}

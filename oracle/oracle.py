@@ -52,6 +52,11 @@ def lib():
         L.orc_fe_fold_sum.restype = ctypes.c_uint64
         L.orc_sim_prf.restype = ctypes.c_uint64
         L.orc_sim_prf.argtypes = [ctypes.c_uint64] * 4 + [ctypes.c_uint32]
+        L.orc_prg_stream_u64.restype = ctypes.c_uint64
+        L.orc_prg_stream_u64.argtypes = [u8p, ctypes.c_uint64]
+        L.orc_mul_out_share_fe.restype = ctypes.c_uint64
+        L.orc_mul_out_share_fe.argtypes = [ctypes.c_int, u64p, ctypes.c_uint64, ctypes.c_uint64, u64p, u64p]
+        L.orc_mul_verify_fe.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         _LIB = L
     return _LIB
 
@@ -478,3 +483,61 @@ def l_inf_ball_bounds(alpha, size: int):
 def i16_to_bitvec(v: int):                     # sample_driving_data.rs:25-28
     u = v & 0xFFFF
     return [bool((u >> (15 - i)) & 1) for i in range(16)]
+
+
+# ---- sketch + Beaver verification (row a9; sketch.rs / mpc.rs, dead in the reference) -------
+def prg_stream_u64(seed: bytes, pos: int) -> int:
+    """PrgStream::next_u64 draw `pos` of PrgSeed::to_rng (prg.rs:82-90,161-182)."""
+    s = np.frombuffer(bytes(seed), np.uint8).copy()
+    return int(lib().orc_prg_stream_u64(_p(s), ctypes.c_uint64(pos)))
+
+
+def sketch_fe(seeds: np.ndarray, x: np.ndarray, kx: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """sketch_at (sketch.rs:157-200), T = FE, for [n] keys -> [n][6] canonical."""
+    seeds = np.ascontiguousarray(seeds, np.uint8)
+    x = np.ascontiguousarray(x, np.uint64)
+    kx = np.ascontiguousarray(kx, np.uint64)
+    n, F = x.shape
+    out = np.zeros((n, 6), np.uint64)
+    lib().orc_sketch_fe_batch(ctypes.c_uint64(n), ctypes.c_uint32(F), _p(seeds), _p(x, u64p), _p(kx, u64p),
+                              _p(out, u64p), ctypes.c_int(nthreads))
+    return out
+
+
+def mul_cor_share_fe(sketch6, mac, mac2, triples9) -> np.ndarray:
+    """MulState::new + cor_share (mpc.rs:83-158) per key."""
+    n = sketch6.shape[0]
+    out = np.zeros((n, 6), np.uint64)
+    for i in range(n):
+        sk = np.ascontiguousarray(sketch6[i], np.uint64)
+        tr = np.ascontiguousarray(triples9[i], np.uint64)
+        o = np.zeros(6, np.uint64)
+        lib().orc_mul_cor_share_fe(_p(sk, u64p), ctypes.c_uint64(int(mac[i])), ctypes.c_uint64(int(mac2[i])),
+                                   _p(tr, u64p), _p(o, u64p))
+        out[i] = o
+    return out
+
+
+def mul_out_share_fe(server_idx: int, sketch6, mac, mac2, triples9, cor6) -> np.ndarray:
+    """MulState::out_share (mpc.rs:182-212) per key."""
+    n = sketch6.shape[0]
+    out = np.zeros(n, np.uint64)
+    for i in range(n):
+        sk = np.ascontiguousarray(sketch6[i], np.uint64)
+        tr = np.ascontiguousarray(triples9[i], np.uint64)
+        c = np.ascontiguousarray(cor6[i], np.uint64)
+        out[i] = lib().orc_mul_out_share_fe(int(server_idx), _p(sk, u64p), int(mac[i]), int(mac2[i]), _p(tr, u64p),
+                                            _p(c, u64p))
+    return out
+
+
+def sketch_verify_fe(seeds, x0, kx0, x1, kx1, mac, mac2, triples, nthreads: int = 0):
+    """main.rs:14-70 verify_sketches for one level, both servers: (ok [n], out shares [2][n]).
+    mac / mac2 [2][n], triples [2][n][9]."""
+    n, F = x0.shape
+    ok = np.zeros(n, np.uint8)
+    outs = np.zeros((2, n), np.uint64)
+    a = [np.ascontiguousarray(v, np.uint64) for v in (x0, kx0, x1, kx1, mac, mac2, triples)]
+    lib().orc_sketch_verify_fe_batch(ctypes.c_uint64(n), ctypes.c_uint32(F), _p(np.ascontiguousarray(seeds, np.uint8)),
+                                     *[_p(v, u64p) for v in a], _p(ok), _p(outs, u64p), ctypes.c_int(nthreads))
+    return ok.astype(bool), outs

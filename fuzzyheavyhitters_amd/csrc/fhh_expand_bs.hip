@@ -534,6 +534,7 @@ __device__ __forceinline__ void bs_pair2_body(const ExpandLaunch& a, uint32_t* w
     if (threadIdx.x == 0) item_slot = atomicAdd(work_counter, 1u);
     __syncthreads();
     uint64_t item = __builtin_amdgcn_readfirstlane(item_slot);
+    __syncthreads();
     prof_mark<PROF>(tl, acc, 0);
     while (item < total) {
         uint32_t nxt = 0;
@@ -554,6 +555,7 @@ __device__ __forceinline__ void bs_pair2_body(const ExpandLaunch& a, uint32_t* w
         if (threadIdx.x == 0) item_slot = nxt;
         __syncthreads();   // both waves are done with yl; the next item is published
         item = __builtin_amdgcn_readfirstlane(item_slot);
+        __syncthreads();   // the slot may alias y storage: both waves read it before y is rewritten
         prof_mark<PROF>(tl, acc, 5);   // 5: end barrier
     }
     if constexpr (PROF) {
@@ -572,21 +574,22 @@ __device__ __forceinline__ void bs_pair2_body(const ExpandLaunch& a, uint32_t* w
 
 template <int WAVES, int FENCE, bool ROLLED, bool PROF = false, int CWORDS = 24>
 __global__ __launch_bounds__(128, 2) void k_expand_bs_pair2(ExpandLaunch a, uint32_t* work_counter) {
+    // exactly 32 KiB of LDS (the item slot lives in the last y word, see bs_pair2_body), so a
+    // pair fits beside a 128 KiB T-table workgroup on one CU (hybrid runs)
     __shared__ SeedQuads yl;
-    __shared__ uint32_t item_slot;
-    bs_pair2_body<FENCE, ROLLED, PROF, CWORDS>(a, work_counter, yl, item_slot);
+    bs_pair2_body<FENCE, ROLLED, PROF, CWORDS>(a, work_counter, yl, reinterpret_cast<uint32_t*>(&yl[31][63])[3]);
 }
 
 // 3 waves/SIMD: the LDS (32 KiB per pair) admits 5 pairs = 2.5 waves/SIMD, which the
 // compiler's occupancy model floors to 2 — the LDS is dynamic so the 168-VGPR budget holds
-constexpr size_t kPair2DynLds = sizeof(SeedQuads) + 16;
+constexpr size_t kPair2DynLds = sizeof(SeedQuads);
 template <int FENCE, bool ROLLED, int CWORDS>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_expand_bs_pair2_w3(
     ExpandLaunch a, uint32_t* work_counter) {
     // dynamic LDS (kPair2DynLds bytes at launch): invisible to the compiler's occupancy model
     extern __shared__ uint8_t dyn_lds[];
     SeedQuads& yl = *reinterpret_cast<SeedQuads*>(dyn_lds);
-    uint32_t& item_slot = *reinterpret_cast<uint32_t*>(dyn_lds + sizeof(SeedQuads));
+    uint32_t& item_slot = reinterpret_cast<uint32_t*>(&yl[31][63])[3];
     bs_pair2_body<FENCE, ROLLED, false, CWORDS>(a, work_counter, yl, item_slot);
 }
 
@@ -703,7 +706,7 @@ const void* expand_bs_fn(int which) {
     }
 }
 
-int expand_bs_count() { return 13; }
+int expand_bs_count() { return kBsCount; }
 size_t expand_bs_dyn_lds(int which) { return (which == 11 || which == 12) ? kPair2DynLds : 0; }
 
 }  // namespace fhh

@@ -200,7 +200,8 @@ hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream);
 // [32 quads][npad / 32] uint4 bitsliced words (see fhh_expand_bs.hip). Work item = one
 // (entry, side, dir) x 2048 clients (pair mode: (entry, side) x 2048 clients, both dirs), one
 // entry per item.
-constexpr int kBsVariant = 14;   // first bitsliced variant; expand_bs_count() of them
+constexpr int kBsVariant = 14;   // first bitsliced variant
+constexpr int kBsCount = 13;     // bitsliced variants 14..26; T-table variants 0..13 and 27..
 hipError_t launch_expand_bs(const ExpandLaunch& a, int which, int grid, uint32_t* work_counter, hipStream_t stream);
 const void* expand_bs_fn(int which);
 int expand_bs_count();
@@ -210,7 +211,7 @@ size_t expand_bs_dyn_lds(int which);   // dynamic LDS bytes a variant launches w
 inline bool bs_pair_mode(int which) { return which != 0 && which != 1 && which != 5; }
 // to_bs = 1: client-major [rows][npad] uint4 -> bitsliced; 0: inverse (out-of-place)
 hipError_t launch_bitslice(const uint4* in, uint4* out, uint64_t rows, uint32_t npad, int to_bs, hipStream_t stream);
-inline bool variant_is_bs(int variant) { return variant >= kBsVariant; }
+inline bool variant_is_bs(int variant) { return variant >= kBsVariant && variant < kBsVariant + kBsCount; }
 inline uint32_t expand_unit(int variant, uint64_t nw) {
     if (!variant_is_bs(variant)) return (uint32_t)nw;
     const uint32_t per_chunk = bs_pair_mode(variant - kBsVariant) ? 2 : 4;   // (side[, dir]) per chunk

@@ -254,7 +254,9 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     X(10, TabT0R64<DevOpsX>, 2, 1024, 8, false)         \
     X(11, TabT0R64<DevOpsX>, 2, 768, 1, true)          \
     X(12, Tab4T32<DevOpsX>, 4, 1024, 1, true, true)     \
-    X(13, Tab4T32<DevOpsX>, 4, 1024, 1, false, true)
+    X(13, Tab4T32<DevOpsX>, 4, 1024, 1, false, true)   \
+    X(27, Tab4T32<DevOpsX>, 4, 512, 1, true)            \
+    X(28, Tab4T32<DevOpsX>, 4, 512, 1, true, true)
 
 struct VariantInfo {
     const void* fn;
@@ -264,7 +266,7 @@ struct VariantInfo {
 };
 
 static VariantInfo variant_info(int v) {
-    if (v >= kBsVariant) {
+    if (variant_is_bs(v)) {
         static const char* names[] = {"bitsliced/2 waves/fence2", "bitsliced/3 waves/fence1",
                                       "bitsliced pair+LDS/2 waves", "bitsliced pair+LDS/3 waves",
                                       "bitsliced pair+LDS/rolled", "bitsliced/2 waves/rolled",
@@ -285,13 +287,13 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + expand_bs_count(); }
+int expand_variant_count() { return kBsVariant + kBsCount + 2; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
 hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream) {
     if (a.total_items == 0) return hipSuccess;
-    if (variant >= kBsVariant) return launch_expand_bs(a, variant - kBsVariant, grid, work_counter, stream);
+    if (variant_is_bs(variant)) return launch_expand_bs(a, variant - kBsVariant, grid, work_counter, stream);
     const VariantInfo vi = variant_info(variant);
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;
@@ -315,7 +317,7 @@ int expand_grid(int device, int variant) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const VariantInfo vi = variant_info(variant);
     int per_cu = 0;
-    const size_t dyn = variant >= kBsVariant ? expand_bs_dyn_lds(variant - kBsVariant) : 0;
+    const size_t dyn = variant_is_bs(variant) ? expand_bs_dyn_lds(variant - kBsVariant) : 0;
     if (!vi.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vi.fn, vi.threads, dyn) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;

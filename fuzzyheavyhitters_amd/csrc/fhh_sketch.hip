@@ -159,41 +159,53 @@ __device__ __forceinline__ uint64_t wave_fe_sum(uint64_t v) {
     return v;
 }
 
+// segment (LPK lanes = one key) reductions
+template <int LPK>
+__device__ __forceinline__ uint64_t seg_fe_sum(uint64_t v) {
+#pragma unroll
+    for (int off = LPK / 2; off > 0; off >>= 1) v = fe_addc(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// KPW keys per wave, LPK = 64 / KPW lanes per key: lane l of a key's segment produces keystream
+// blocks l, l + LPK, ... two per pass in lockstep, with the pass's (x, kx) loads issued first.
+// The key schedule is per lane (each segment has its own key).
+template <int KPW>
 __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
+    constexpr int LPK = 64 / KPW;
     __shared__ uint32_t tbl[SkTab::kWords];
     for (int i = threadIdx.x; i < SkTab::kWords; i += kSketchThreads) tbl[i] = SkTab::word(c_T0_sk.v, i);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t seg = lane / LPK, sl = lane % LPK;
     uint32_t b0, b1;
     SkTab::bases(lane, b0, b1);
     const uint64_t mask = (1ull << 62) - 1;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kSketchThreads / 64);
     const uint64_t F = a.n_nodes;
     const uint64_t nb = (F + 3 + 1) / 2;   // draws 0..F+2
-    for (uint64_t key = (uint64_t)blockIdx.x * (kSketchThreads / 64) + (threadIdx.x >> 6); key < a.n_keys;
-         key += nwaves) {
-        const uint64_t k = __builtin_amdgcn_readfirstlane((uint32_t)key) |
-                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(key >> 32)) << 32);
+    const uint64_t wave = (uint64_t)blockIdx.x * (kSketchThreads / 64) + (threadIdx.x >> 6);
+    for (uint64_t kbase = wave * KPW; kbase < a.n_keys; kbase += nwaves * KPW) {
+        const uint64_t k = kbase + seg;
+        const bool kact = k < a.n_keys;
+        const uint64_t kk = kact ? k : kbase;
         uint32_t seed[4];
 #pragma unroll
-        for (int c = 0; c < 4; c++)
-            seed[c] = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t*>(a.seeds)[4 * k + c]);
+        for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
         uint32_t rk[11][4];
         key_schedule(seed, rk, tbl, lane & 31);
-        const uint64_t* x = a.x + k * F;
-        const uint64_t* kx = a.kx + k * F;
+        const uint64_t* x = a.x + kk * F;
+        const uint64_t* kx = a.kx + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
         bool rej = false;
         if (!a.force_sequential) {
-            // two keystream blocks per lane per pass (AES in lockstep for ILP); the pass's four
-            // (x, kx) pairs are loaded before the AES so their latency hides behind it
-            for (uint64_t bb = lane; bb < nb; bb += 128) {
+            for (uint64_t bb = sl; bb < nb; bb += 2 * LPK) {
                 uint64_t xv[4] = {0, 0, 0, 0}, kxv[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int q = 0; q < 2; q++)
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        const uint64_t pos = 2 * (bb + 64 * q) + h;
+                        const uint64_t pos = 2 * (bb + LPK * q) + h;
                         if (pos >= 3 && pos < F + 3) {
                             xv[2 * q + h] = x[pos - 3];
                             kxv[2 * q + h] = kx[pos - 3];
@@ -202,7 +214,7 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
                 uint32_t st[2][4];
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
-                    const uint64_t b = bb + 64 * q;
+                    const uint64_t b = bb + LPK * q;
                     st[q][0] = 0u;
                     st[q][1] = 0u;
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
@@ -211,7 +223,7 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
                 aes_rk<SkTab, 2>(st, tbl, b0, b1, rk);
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
-                    const uint64_t b = bb + 64 * q;
+                    const uint64_t b = bb + LPK * q;
                     if (b >= nb) break;
                     const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
                                             (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
@@ -222,24 +234,25 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
                 }
             }
         }
-        const bool any_rej = a.force_sequential || __ballot(rej) != 0;
-        if (!any_rej) {
-            rx = wave_fe_sum(rx);
-            r2x = wave_fe_sum(r2x);
-            rkx = wave_fe_sum(rkx);
-            const uint64_t rand1 = __shfl(rnd0, 0, 64);
-            const uint64_t rand2 = __shfl(rnd1, 0, 64);
-            const uint64_t rand3 = __shfl(rnd0, 1, 64);
-            if (lane == 0) {
-                uint64_t* o = a.out + 6 * k;
-                o[0] = rx;
-                o[1] = r2x;
-                o[2] = rkx;
-                o[3] = rand1;
-                o[4] = rand2;
-                o[5] = rand3;
-            }
-        } else if (lane == 0) {
+        // per-key rejection flag over the key's segment
+        const uint64_t rej_mask = __ballot(rej);
+        const uint64_t seg_bits = (LPK == 64 ? ~0ull : ((1ull << LPK) - 1)) << (seg * LPK);
+        const bool key_rej = a.force_sequential || (rej_mask & seg_bits) != 0;
+        rx = seg_fe_sum<LPK>(rx);
+        r2x = seg_fe_sum<LPK>(r2x);
+        rkx = seg_fe_sum<LPK>(rkx);
+        const uint64_t rand1 = __shfl(rnd0, seg * LPK, 64);
+        const uint64_t rand2 = __shfl(rnd1, seg * LPK, 64);
+        const uint64_t rand3 = __shfl(rnd0, seg * LPK + 1, 64);
+        if (kact && !key_rej && sl == 0) {
+            uint64_t* o = a.out + 6 * k;
+            o[0] = rx;
+            o[1] = r2x;
+            o[2] = rkx;
+            o[3] = rand1;
+            o[4] = rand2;
+            o[5] = rand3;
+        } else if (kact && key_rej && sl == 0) {
             // sequential PrgStream with FE::from_rng redraws (field.rs:252-264) for this key
             uint64_t pos = 0, cur_b = ~0ull, d[2] = {0, 0};
             auto draw = [&]() -> uint64_t {
@@ -254,7 +267,7 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
                     if (v < kFeP_) return v;
                 }
             };
-            const uint64_t rand1 = draw(), rand2 = draw(), rand3 = draw();
+            const uint64_t q1 = draw(), q2 = draw(), q3 = draw();
             uint64_t sx = 0, s2x = 0, skx = 0;
             for (uint64_t j = 0; j < F; j++) {
                 const uint64_t r = draw();
@@ -268,23 +281,28 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
             o[0] = sx;
             o[1] = s2x;
             o[2] = skx;
-            o[3] = rand1;
-            o[4] = rand2;
-            o[5] = rand3;
+            o[3] = q1;
+            o[4] = q2;
+            o[5] = q3;
         }
     }
 }
 
+constexpr int kSketchKeysPerWave = 4;
+
 hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     if (a.n_keys == 0) return hipSuccess;
-    int cus = 256, dev = 0;
+    int cus = 256, dev = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t waves_needed = a.n_keys;
+    const void* fn = reinterpret_cast<const void*>(&k_sketch_fe<kSketchKeysPerWave>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSketchThreads, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint64_t waves_needed = (a.n_keys + kSketchKeysPerWave - 1) / kSketchKeysPerWave;
     uint64_t blocks = (waves_needed + 3) / 4;
-    const uint64_t cap = (uint64_t)cus * 16;
+    const uint64_t cap = (uint64_t)cus * per_cu;   // one resident wave set; keys are strided over it
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(k_sketch_fe, dim3((unsigned)blocks), dim3(kSketchThreads), 0, stream, a);
+    hipLaunchKernelGGL(k_sketch_fe<kSketchKeysPerWave>, dim3((unsigned)blocks), dim3(kSketchThreads), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -26,7 +26,7 @@ FHH_MAX_DIMS = 4
 # every symbol include/fhh.h declares
 EXPORTS = [
     "fhh_create", "fhh_destroy", "fhh_last_error", "fhh_reset", "fhh_set_client_base",
-    "fhh_add_keys", "fhh_gen_keys_pair", "fhh_num_clients", "fhh_export_keys",
+    "fhh_add_keys", "fhh_add_keys_bincode", "fhh_gen_keys_pair", "fhh_num_clients", "fhh_export_keys",
     "fhh_tree_init", "fhh_tree_crawl", "fhh_tree_crawl_last", "fhh_node_sums_fe",
     "fhh_node_sums_fe255", "fhh_tree_prune", "fhh_tree_prune_last", "fhh_frontier_size",
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
@@ -153,6 +153,7 @@ def lib():
         "fhh_set_client_base": (i, [vp, u64]),
         "fhh_add_keys": (i, [vp, u64, u8p, u8p, u8p, u8p]),
         "fhh_gen_keys_pair": (i, [vp, vp, u64, u8p, u8p, u8p]),
+        "fhh_add_keys_bincode": (i, [vp, u8p, u64]),
         "fhh_num_clients": (i, [vp, u64p]),
         "fhh_export_keys": (i, [vp, u8p, u8p, u8p, u8p]),
         "fhh_tree_init": (i, [vp]),

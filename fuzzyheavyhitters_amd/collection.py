@@ -62,6 +62,13 @@ class KeyCollection:
         a = [np.ascontiguousarray(x, np.uint8) for x in (key_idx, root_seed, cw_seed, cw_bits)]
         self._chk(lib().fhh_add_keys(self._h, n, *[ptr(x) for x in a]))
 
+    def add_keys_bincode(self, request: bytes):
+        """The `add_keys` RPC payload (rpc.rs:12-15: `Vec<Vec<(ibDCFKey, ibDCFKey)>>` in bincode
+        legacy encoding), decoded on the GPU straight into the device layout."""
+        buf = np.frombuffer(bytes(request), np.uint8) if not isinstance(request, np.ndarray) else \
+            np.ascontiguousarray(request, np.uint8)
+        self._chk(lib().fhh_add_keys_bincode(self._h, ptr(buf), buf.size))
+
     def num_clients(self) -> int:
         n = ctypes.c_uint64()
         self._chk(lib().fhh_num_clients(self._h, ctypes.byref(n)))

@@ -1343,6 +1343,44 @@ int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t*
     return FHH_OK;
 }
 
+int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!req || len < 8) return ctx->fail(FHH_E_ARG, "add_keys_bincode: buffer shorter than the u64 length");
+    if (ctx->dev_keys || ctx->h_n) return ctx->fail(FHH_E_STATE, "add_keys_bincode: ctx already holds keys");
+    uint64_t n = 0;
+    for (int i = 0; i < 8; i++) n |= (uint64_t)req[i] << (8 * i);
+    const uint64_t KB = 25 + 20ull * ctx->L, R = 8 + (uint64_t)ctx->K * KB;
+    if (n == 0) return ctx->fail(FHH_E_ARG, "add_keys_bincode: no clients");
+    if (n > (len - 8) / R || 8 + n * R != len)
+        return ctx->fail(FHH_E_ARG, "add_keys_bincode: length does not match n clients x n_dims x data_len");
+    rc = alloc_keys(ctx, n);
+    if (rc) return rc;
+    DevBuf buf, err;
+    HIP_TRY(ctx, buf.ensure(len));
+    HIP_TRY(ctx, err.ensure(4));
+    HIP_TRY(ctx, hipMemsetAsync(err.p, 0, 4, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(buf.p, req, len, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_keys_from_bincode(buf.as<uint8_t>(), n, ctx->d, ctx->L, (uint32_t)ctx->npad, (uint32_t)ctx->nw,
+                                          ctx->cw_seed.as<uint4>(), ctx->cw_bits.as<uint64_t>(),
+                                          ctx->root_seed.as<uint4>(), ctx->key_idx.as<uint64_t>(), err.as<uint32_t>(),
+                                          ctx->stream));
+    uint32_t herr = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    if (herr) {
+        ctx->n = 0;
+        return ctx->fail(FHH_E_ARG, std::string("add_keys_bincode: malformed request (") +
+                                        ((herr & 1) ? "bool byte > 1 " : "") + ((herr & 2) ? "cor_words length " : "") +
+                                        ((herr & 4) ? "dims per client" : "") + ")");
+    }
+    ctx->dev_keys = true;
+    ctx->keys_bs = false;
+    return FHH_OK;
+}
+
 int fhh_tree_init(fhh_ctx* ctx) {
     CTX_CHECK(ctx);
     int rc = set_device(ctx);

@@ -149,6 +149,9 @@ hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
                                 const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
                                 uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
                                 hipStream_t stream);
+hipError_t launch_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L, uint32_t npad, uint32_t nw,
+                                    uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
+                                    uint32_t* err, hipStream_t stream);
 // occupancy-derived persistent grid for k_expand variant on `device`
 int expand_grid(int device, int variant);
 // RCCL all-reduce (sum, u64) on `stream` (fhh_comm.cpp); asynchronous

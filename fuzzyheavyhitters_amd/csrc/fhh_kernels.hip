@@ -783,6 +783,93 @@ __global__ void k_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
     }
 }
 
+// AddKeysRequest.keys (rpc.rs:12-15) in bincode 1.x legacy encoding (as `bincode::serialize`,
+// leader.rs:101): u64 n, then per client u64 d and d x (ibDCFKey left, ibDCFKey right); an
+// ibDCFKey (ibDCF.rs:16-21) = key_idx bool (1 B), root_seed (16 B), u64 L, L x CorWord
+// (ibDCF.rs:9-14: seed 16 B, bits.0, bits.1, y_bits.0, y_bits.1 as 1-byte bools). Records
+// are fixed-size, so every (level, key, 64-client word) item is decoded in place into the
+// SoA device layout; malformed bools / lengths set bits of *err (bool > 1: 1, L: 2, d: 4).
+__device__ __forceinline__ uint64_t load_u64_le(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+
+__device__ __forceinline__ uint4 load_seed(const uint8_t* p) {
+    uint32_t x[4];
+    for (int k = 0; k < 4; k++)
+        x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+               ((uint32_t)p[4 * k + 3] << 24);
+    return make_uint4(x[0], x[1], x[2], x[3]);
+}
+
+__global__ void k_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L, uint32_t npad,
+                                    uint32_t nw, uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root,
+                                    uint64_t* d_key_idx, uint32_t* err) {
+    const uint32_t K = 2 * d;
+    const uint64_t KB = 25 + 20ull * L;      // one serialized ibDCFKey
+    const uint64_t R = 8 + (uint64_t)K * KB;  // one client: u64 d + d (left, right) pairs
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    const uint64_t items = (uint64_t)(L + 1) * K * nw;   // level L = roots / key_idx
+    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items; item += nwaves) {
+        const uint32_t w = (uint32_t)(item % nw);
+        const uint32_t kk = (uint32_t)((item / nw) % K);
+        const uint32_t l = (uint32_t)(item / ((uint64_t)nw * K));
+        const uint64_t c = (uint64_t)w * 64 + lane;
+        const bool valid = c < n;
+        const uint8_t* rec = buf + 8 + c * R;
+        const uint8_t* key = rec + 8 + (uint64_t)kk * KB;
+        uint32_t bad = 0;
+        if (l < L) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            uint32_t nib = 0;
+            if (valid) {
+                const uint8_t* cw = key + 25 + 20ull * l;
+                v = load_seed(cw);
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t x = cw[16 + b];
+                    bad |= x > 1 ? 1u : 0u;
+                    nib |= (x & 1u) << b;
+                }
+            }
+            const size_t row = (size_t)l * K + kk;
+            d_cw_seed[row * npad + c] = v;
+            uint64_t q[4];
+            for (int b = 0; b < 4; b++) q[b] = __ballot((nib >> b) & 1);
+            if (lane == 0)
+                for (int b = 0; b < 4; b++) d_cw_bits[(row * 4 + b) * nw + w] = q[b];
+        } else {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            uint32_t ki = 0;
+            if (valid) {
+                ki = key[0];
+                bad |= ki > 1 ? 1u : 0u;
+                v = load_seed(key + 1);
+                bad |= load_u64_le(key + 17) != L ? 2u : 0u;
+                if (kk == 0) bad |= load_u64_le(rec) != d ? 4u : 0u;
+            }
+            d_root[(size_t)kk * npad + c] = v;
+            const uint64_t q = __ballot(ki & 1u);
+            if (lane == 0) d_key_idx[(size_t)kk * nw + w] = q;
+        }
+        if (bad) atomicOr(err, bad);
+    }
+}
+
+hipError_t launch_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L, uint32_t npad, uint32_t nw,
+                                    uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
+                                    uint32_t* err, hipStream_t stream) {
+    const uint64_t items = (uint64_t)(L + 1) * 2 * d * nw;
+    uint64_t blocks = (items + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_keys_from_bincode, dim3((unsigned)blocks), dim3(256), 0, stream, buf, n, d, L, npad, nw,
+                       d_cw_seed, d_cw_bits, d_root, d_key_idx, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
                                 const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
                                 uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,

@@ -197,3 +197,25 @@ def plaintext_heavy_hitters(alpha_left: np.ndarray, alpha_right: np.ndarray, thr
                 kept.append(ch)
         frontier = kept
     return sorted(frontier)
+
+
+def add_keys_request_bincode(key_idx: np.ndarray, root_seed: np.ndarray, cw_seed: np.ndarray,
+                             cw_bits: np.ndarray) -> np.ndarray:
+    """Serialize keys (add_keys layout: [n][d][2], [n][d][2][16], [n][d][2][L][16],
+    [n][d][2][L] nibbles) as `AddKeysRequest.keys` (rpc.rs:12-15) in bincode 1.x legacy
+    encoding: u64 n; per client u64 d, then d (left, right) ibDCFKeys = key_idx bool,
+    root_seed[16], u64 L, L x (seed[16], bits.0, bits.1, y_bits.0, y_bits.1)."""
+    n, d, _, L = cw_bits.shape
+    KB = 25 + 20 * L
+    rec = np.zeros((n, 8 + 2 * d * KB), np.uint8)
+    rec[:, 0:8] = np.frombuffer(np.uint64(d).tobytes(), np.uint8)
+    keys = rec[:, 8:].reshape(n, 2 * d, KB)
+    keys[:, :, 0] = key_idx.reshape(n, 2 * d)
+    keys[:, :, 1:17] = root_seed.reshape(n, 2 * d, 16)
+    keys[:, :, 17:25] = np.frombuffer(np.uint64(L).tobytes(), np.uint8)
+    cw = keys[:, :, 25:].reshape(n, 2 * d, L, 20)
+    cw[:, :, :, 0:16] = cw_seed.reshape(n, 2 * d, L, 16)
+    nib = cw_bits.reshape(n, 2 * d, L)
+    for b in range(4):
+        cw[:, :, :, 16 + b] = (nib >> b) & 1
+    return np.concatenate([np.frombuffer(np.uint64(n).tobytes(), np.uint8), rec.reshape(-1)])

@@ -77,6 +77,15 @@ int fhh_set_client_base(fhh_ctx* ctx, uint64_t client_base);
 int fhh_add_keys(fhh_ctx* ctx, uint64_t n, const uint8_t* key_idx, const uint8_t* root_seed,
                  const uint8_t* cw_seed, const uint8_t* cw_bits);
 
+/* The `add_keys` RPC payload as it arrives at the server (rpc.rs:12-15, server.rs:71-77):
+ * `AddKeysRequest.keys: Vec<Vec<(ibDCFKey, ibDCFKey)>>` in bincode 1.x legacy encoding
+ * (`bincode::serialize`, as leader.rs:101 sizes a key: 1 + 16 + 8 + 20 L bytes), decoded on
+ * the GPU straight into the device layout (no host AoS->SoA pass). Every
+ * client must carry n_dims (left, right) pairs of data_len-level keys; bools must be 0/1.
+ * The ctx must hold no keys yet. FHH_E_ARG on any malformed field (the reference's RPC
+ * decode fails the request). */
+int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len);
+
 /* Leader-side batched `gen_l_inf_ball` keygen on the GPU (ibDCF.rs:84-119,138-188),
  * writing server 0's keys into ctx0 and server 1's into ctx1 (both must be empty and on the
  * same device). Replaces the leader's per-client `add_fuzzy_keys` loop (leader.rs:130-163).

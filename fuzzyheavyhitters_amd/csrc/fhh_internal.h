@@ -220,6 +220,12 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
     const uint32_t per_chunk = bs_pair_mode(variant - kBsVariant) ? 2 : 4;   // (side[, dir]) per chunk
     return (uint32_t)(per_chunk * ((nw + 31) / 32));
 }
-inline uint32_t expand_max_group(int variant) { return variant_is_bs(variant) ? 1u : 8u; }
+// entries per work item (CW reuse and counter traffic vs. end-of-level tail): variant 29 is
+// variant 3 drawing the next item one entry ahead; 30 / 31 are variant 3 with up to 16 / 32
+// entries per item; 32 / 33 store child seeds nontemporally with up to 8 / 16 entries per item
+inline uint32_t expand_max_group(int variant) {
+    if (variant_is_bs(variant)) return 1u;
+    return (variant == 30 || variant == 33) ? 16u : variant == 31 ? 32u : 8u;
+}
 
 }  // namespace fhh

@@ -33,9 +33,18 @@ __device__ __forceinline__ void fill_table(uint32_t* tbl) {
 // CorWords of (level, dim, side, client) are loaded once per work item and reused for
 // `group` entries. Work items are dealt grid-stride (static) or from an atomic counter.
 // --------------------------------------------------------------------------------------
-template <class Tab, int NB>
+// ahead != nullptr: draw the next work item from the counter right after the first entry's
+// seeds have been consumed, so the (contended) atomic completes under that entry's AES instead
+// of stalling the next item's start (vmcnt retires in issue order, so it must not precede the
+// loads this item waits on)
+typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+
+// NT: child seeds are written with the nontemporal hint — they are read again only at the next
+// level, and 1.3 GB per launch left dirty in L2 costs a writeback at every kernel boundary
+template <class Tab, int NB, bool NT = false>
 __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
-                                            uint32_t b0, uint32_t b1) {
+                                            uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
+                                            uint32_t* next = nullptr) {
     const uint32_t w = (uint32_t)(local % J.nw);
     const uint32_t g = (uint32_t)(local / J.nw);
     const uint32_t c = w * 64 + lane;
@@ -77,6 +86,7 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
                     py[q * 2 + dir] = __ballot(ybit);
                 }
             }
+            if (ahead && e == e_begin && s0 == 0 && lane == 0) *next = atomicAdd(ahead, 1u);
 
             aes0_mmo_tab<DevOpsX, Tab, NB>(blk, tbl, b0, b1);
 
@@ -93,7 +103,12 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
                     out.z = o[2] ^ (cw[s].z & tmask);
                     out.w = o[3] ^ (cw[s].w & tmask);
                     const size_t de = (size_t)(2 * e + dir) * 2 + s;
-                    J.dst_seed[de * npad + c] = out;
+                    if constexpr (NT) {
+                        v4u32_t o4 = {out.x, out.y, out.z, out.w};
+                        __builtin_nontemporal_store(o4, reinterpret_cast<v4u32_t*>(J.dst_seed + de * npad + c));
+                    } else {
+                        J.dst_seed[de * npad + c] = out;
+                    }
                     if (lane == 0) {
                         // new_bit = tau.bits[dir] ^ (t & cw.bits[dir]);
                         // new_y = tau.y_bits[dir] ^ (t & cw.y_bits[dir]) ^ y   (ibDCF.rs:211-219)
@@ -185,8 +200,11 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
     }
 }
 
-template <class Tab, int NB, int THR, int MINW, bool PF = false>
+// FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores
+template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
+    constexpr bool AHEAD = (FLAGS & 1) != 0;
+    constexpr bool NT = (FLAGS & 2) != 0;
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
@@ -218,11 +236,13 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             J.group = ctl->group;
             J.item_begin = ctl->item_begin[ji];
         }
+        uint32_t nxt = 0;
         if constexpr (PF) expand_item_pf<Tab>(J, item - J.item_begin, tbl, lane, b0, b1);
-        else expand_item<Tab, NB>(J, item - J.item_begin, tbl, lane, b0, b1);
+        else if constexpr (AHEAD) expand_item<Tab, NB, NT>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
+        else expand_item<Tab, NB, NT>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
-            uint32_t v = 0;
-            if (lane == 0) v = atomicAdd(work_counter, 1u);
+            uint32_t v = nxt;
+            if (!AHEAD && lane == 0) v = atomicAdd(work_counter, 1u);
             item = __builtin_amdgcn_readfirstlane(v);
         } else {
             item += nwaves;
@@ -256,7 +276,12 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     X(12, Tab4T32<DevOpsX>, 4, 1024, 1, true, true)     \
     X(13, Tab4T32<DevOpsX>, 4, 1024, 1, false, true)   \
     X(27, Tab4T32<DevOpsX>, 4, 512, 1, true)            \
-    X(28, Tab4T32<DevOpsX>, 4, 512, 1, true, true)
+    X(28, Tab4T32<DevOpsX>, 4, 512, 1, true, true)      \
+    X(29, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 1)    \
+    X(30, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
+    X(31, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
+    X(32, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
+    X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)
 
 struct VariantInfo {
     const void* fn;
@@ -287,7 +312,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 2; }
+int expand_variant_count() { return kBsVariant + kBsCount + 7; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

@@ -114,6 +114,93 @@ def sketch_bench(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def gc_bench(args, world, rank, local_rank, dist):
+    """Row f1: one step = the garbled-circuit equality tests of one crawl level at configs[1]
+    scale (--gc-groups children x --clients clients per GPU, 2d-bit share strings):
+    k_gc_garble (server 0: labels, 2 half-gate ciphertexts per AND) then k_gc_eval (server 1),
+    transcript through HBM, inputs resident. Tests shard by client across GPUs (weak scaling, no
+    collective)."""
+    import numpy as np
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    G, N, bits = args.gc_groups, args.clients, 2 * args.dims
+    rng = np.random.default_rng(args.seed + rank)
+    nw = (N + 63) // 64
+    gb = rng.integers(0, 1 << 63, (G, bits, nw), dtype=np.uint64)
+    ev = gb.copy()
+    # about one client in eight differs (unequal strings) in each child
+    ev[:, 0, :] ^= rng.integers(0, 1 << 63, (G, nw), dtype=np.uint64) & rng.integers(0, 1 << 63, (G, nw), dtype=np.uint64) \
+        & rng.integers(0, 1 << 63, (G, nw), dtype=np.uint64)
+    kc = fhh.KeyCollection(8, 1, device=local_rank)
+    key, delta = rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    b = gc.DeviceGcBatch(gb, ev, N, 1, key, delta, device=local_rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        gc.equality_device(kc, b)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        gc.equality_device(kc, b)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # ground truth: eq = all planes equal at the client's bit
+    out = b.out.cpu().numpy().reshape(G, N)
+    diff = np.zeros((G, nw), np.uint64)
+    for j in range(bits):
+        diff |= gb[:, j] ^ ev[:, j]
+    eq = ((np.unpackbits(diff.view(np.uint8).reshape(G, nw, 8), axis=2, bitorder="little").reshape(G, nw * 64)[:, :N])
+          == 0)
+    assert np.array_equal((out ^ 1).astype(bool), eq), "GC outputs disagree with plaintext equality"
+    tests = G * N * world * args.steps
+    ands = tests * (bits - 1)
+    aes_per_test = (2 * bits + 1) + 12 * (bits - 1)   # labels + 8 (garble) + 4 (eval) per AND
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import oracle as O
+        O.build()
+        m = min(G * N, 1 << 18)
+        g_s = rng.integers(0, 2, (m, bits), dtype=np.uint8)
+        t1 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t1 < args.cpu_baseline_seconds / 3 or reps == 0:
+            tb, gl, el, dc = O.gc_garble_eq(g_s, g_s, 1, key, delta)
+            O.gc_eval_eq(tb, gl, el, dc)
+            reps += 1
+        cpu_t = time.perf_counter() - t1
+        cpu = {"value": m * reps / cpu_t, "unit": "equality tests/s", "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
+               "kind": "port", "sample": f"{m} tests x {reps} reps, oracle garble+eval (byte AES, OpenMP)"}
+    if rank == 0:
+        lds_bytes = tests * aes_per_test * LDS_BYTES_PER_BLOCK
+        print(json.dumps({
+            "metric": "garbled-circuit equality tests/sec (garble + evaluate, one crawl level)",
+            "value": tests / elapsed, "unit": "equality tests/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (AES-128 blocks)",
+            "data": "synthetic share planes (1 in 8 clients unequal per child), random garbler key and Delta",
+            "config": {"workload": "row f1: GC equality tests of one configs[1] level", "groups": G,
+                       "clients_per_gpu": N, "bits": bits, "parallelism": f"client-shard x{world}"},
+            "and_gates_per_s": ands / elapsed, "aes_blocks_per_s": tests * aes_per_test / elapsed,
+            "roofline": {"bound": "lds", "achieved": lds_bytes / elapsed / 1e9, "peak": LDS_PEAK_GBPS, "unit": "GB/s",
+                         "frac": lds_bytes / elapsed / 1e9 / LDS_PEAK_GBPS, "traffic": None,
+                         "kernel": "k_gc_garble + k_gc_eval (whole step)",
+                         "algorithmic": f"640 B of ds_read_b32 per AES block, {aes_per_test} blocks per test"},
+            "cpu_baseline": cpu,
+        }), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,9 +214,12 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
-    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch"],
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc"],
                     help="zipf = configs[1] (default); coords = configs[3] (d=2 lat/lon, data_len 16); "
-                         "sketch = configs[4] (sketch + Beaver verification batch)")
+                         "sketch = configs[4] (sketch + Beaver verification batch); "
+                         "gc = row f1 (garbled-circuit equality tests of one level)")
+    ap.add_argument("--gc-groups", type=int, default=256, help="--workload gc: children per level")
+    ap.add_argument("--gc", action="store_true", help="crawl with the GPU garbled-circuit equality test (mode fe)")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -138,6 +228,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
     ap.add_argument("--variant", type=int, default=-1, help="k_expand variant (-1 = library default)")
+    ap.add_argument("--timing-every", type=int, default=1,
+                    help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +251,10 @@ def main():
 
     if args.workload == "sketch":
         return sketch_bench(args, world, rank, local_rank, dist)
+    if args.workload == "gc":
+        return gc_bench(args, world, rank, local_rank, dist)
+    if args.gc and args.mode != "fe":
+        args.mode = "fe"   # the GC equality test feeds the OT share conversion (collect.rs:419-482)
 
     n_local = args.clients
     n_total = n_local * world
@@ -181,6 +277,7 @@ def main():
         c1.set_variant(args.variant)
     c0.set_client_base(rank * n_local)
     c1.set_client_base(rank * n_local)
+    c0.set_timing(args.timing_every)
     log(f"[rank {rank}] workload+keygen {time.perf_counter() - t_gen:.2f}s "
         f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
 
@@ -197,7 +294,7 @@ def main():
 
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, distributed=world > 1 and comm is None, comm=comm)
+                             record=False, distributed=world > 1 and comm is None, comm=comm, gc=args.gc)
 
     def barrier():
         if dist is not None:
@@ -226,7 +323,7 @@ def main():
         blocks, ref_evals = int(b[0].item()), int(b[1].item())
 
     if rank == 0:
-        launches = max(1, s0["expand_launches"])
+        launches = max(1, s0["expand_launches_timed"])
         avg_launch_s = s0["expand_ms"] / launches / 1e3
         blocks_per_launch = s0["expand_blocks_timed"] / launches
         lds_gbps = blocks_per_launch * LDS_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0

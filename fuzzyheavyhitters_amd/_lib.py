@@ -32,11 +32,13 @@ EXPORTS = [
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
     "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench",
+    "fhh_debug_launch_gaps",
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
     "fhh_comm_last_error",
     "fhh_sketch_at_fe", "fhh_mul_cor_share_fe", "fhh_mul_cor_fe", "fhh_mul_out_share_fe", "fhh_mul_verify_fe",
     "fhh_sim_sketch_verify_fe",
+    "fhh_gc_equality_device", "fhh_gc_equality_host",
 ]
 
 
@@ -49,6 +51,7 @@ class FhhStats(ctypes.Structure):
         ("expand_blocks_timed", ctypes.c_uint64),
         ("levels", ctypes.c_uint64),
         ("keygen_ms", ctypes.c_double),
+        ("expand_launches_timed", ctypes.c_uint64),
     ]
 
 
@@ -70,11 +73,12 @@ class FhhSimConfig(ctypes.Structure):
         ("host_loop", ctypes.c_uint32),
         ("init_capacity", ctypes.c_uint32),
         ("comm", ctypes.c_void_p),
+        ("gc", ctypes.c_uint32),
     ]
 
 
-SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_loop.hip", "fhh_microbench.hip",
-           "fhh_host.cpp", "fhh_comm.cpp")
+SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_loop.hip",
+           "fhh_microbench.hip", "fhh_host.cpp", "fhh_comm.cpp")
 
 
 class FhhSketchBatch(ctypes.Structure):
@@ -91,6 +95,27 @@ class FhhSketchBatch(ctypes.Structure):
         ("sketch_dev", ctypes.c_void_p * 2),
         ("ok_dev", ctypes.c_void_p),
         ("out_shares_dev", ctypes.c_void_p),
+    ]
+
+
+class FhhGcBatch(ctypes.Structure):
+    _fields_ = [
+        ("groups", ctypes.c_uint64),
+        ("clients", ctypes.c_uint32),
+        ("words", ctypes.c_uint32),
+        ("bits", ctypes.c_uint32),
+        ("mask", ctypes.c_uint32),
+        ("label_key", ctypes.c_uint8 * 16),
+        ("delta", ctypes.c_uint8 * 16),
+        ("label_nonce", ctypes.c_uint64),
+        ("gate_base", ctypes.c_uint64),
+        ("gb_planes_dev", ctypes.c_void_p),
+        ("ev_planes_dev", ctypes.c_void_p),
+        ("tables_dev", ctypes.c_void_p),
+        ("gb_labels_dev", ctypes.c_void_p),
+        ("ev_labels_dev", ctypes.c_void_p),
+        ("decode_dev", ctypes.c_void_p),
+        ("out_dev", ctypes.c_void_p),
     ]
 
 
@@ -177,6 +202,7 @@ def lib():
         "fhh_set_timing": (i, [vp, i]),
         "fhh_device_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i)]),
         "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
+        "fhh_debug_launch_gaps": (i, [i, i, i, P(ctypes.c_double)]),
         "fhh_set_variant": (i, [vp, i]),
         "fhh_variant_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i), P(i)]),
         "fhh_rccl_load": (i, [ctypes.c_char_p]),
@@ -191,6 +217,8 @@ def lib():
         "fhh_mul_out_share_fe": (i, [vp, i, u64, u64p, u64p, u64p, u64p, u64p, u64p]),
         "fhh_mul_verify_fe": (i, [u64, u64p, u64p, u8p]),
         "fhh_sim_sketch_verify_fe": (i, [vp, P(FhhSketchBatch)]),
+        "fhh_gc_equality_device": (i, [vp, P(FhhGcBatch)]),
+        "fhh_gc_equality_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u64, u8p, u8p, u8p, u8p, u8p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

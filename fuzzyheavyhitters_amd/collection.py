@@ -153,8 +153,8 @@ class KeyCollection:
         if F:
             self._chk(lib().fhh_final_shares(self._h, ctypes.byref(nf), ctypes.byref(lv), ptr(paths),
                                              ptr(vals, u32p)))
-        return [Result([[bool(b) for b in paths[k, j, :L]] for j in range(self.n_dims)], limbs10_to_int(vals[k]))
-                for k in range(F)]
+        bits = paths[:, :, :L].astype(bool).tolist()
+        return [Result(bits[k], limbs10_to_int(vals[k])) for k in range(F)]
 
     def export_states(self):
         """EvalStates of the frontier (or pending children) as [node][n][d][2] seed/t/y."""
@@ -171,6 +171,10 @@ class KeyCollection:
         s = FhhStats()
         self._chk(lib().fhh_get_stats(self._h, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in FhhStats._fields_}
+
+    def set_timing(self, every: int):
+        """0: no k_expand events; 1: time every launch; K > 1: every K-th level-loop launch."""
+        self._chk(lib().fhh_set_timing(self._h, every))
 
     def set_variant(self, variant: int):
         """Select the k_expand variant (bit-identical outputs, different speed)."""

@@ -1,0 +1,49 @@
+// AES-128 T-table rounds with runtime round keys (any table layout of expand_kernel.h), shared
+// by the sketch PrgStream (fhh_sketch.hip) and the garbled-circuit kernels (fhh_gc.hip).
+#pragma once
+#include "expand_kernel.h"
+
+namespace fhh {
+
+// s <- AES_rk(s) for NB independent blocks (little-endian column words)
+template <class Tab, int NB>
+__device__ __forceinline__ void aes_rk(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                       const uint32_t (&rk)[11][4]) {
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[q][c] = s[q][c] ^ rk[0][c];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                y[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, rk[r][c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = y[q][c];
+    }
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi), rk[10][c]);
+        }
+}
+
+}  // namespace fhh

@@ -1,0 +1,255 @@
+// Garbled-circuit equality test on the GPU: the circuit of
+// `multiple_gb_equality_test` / `multiple_ev_equality_test` (src/equalitytest.rs:25-219) —
+// per test, z_j = NOT(x_j XOR y_j) over the 2d share bits (`bin_eq_bundles`, :128-147),
+// eq = AND of the z_j folded left to right (`and_many`), out = eq XOR mask
+// (`multi_bin_eq_bundles_shared`, :165-189) — garbled with free-XOR + half-gates (Zahur, Rosulek,
+// Evans 2015) and the TCCR hash H(x, i) = pi(pi(x) ^ i) ^ pi(x) (Guo, Katz, Wang, Yu 2020), as
+// the swanky `fancy-garbling` garbler the reference links (@553ede0, not vendored: its fixed AES
+// key and wire format cannot be restated, so pi here is AES-128 with the all-zero key, the same
+// fixed-key permutation as the ibDCF PRG).
+//
+//   k_gc_garble  one lane per test: the garbler's zero labels from AES-128-CTR under its key,
+//                2 ciphertexts per AND gate (4 TCCR = 8 AES), its active input labels, the
+//                evaluator's active labels (ideal OT: the labels an OT extension would deliver)
+//                and the output decoding bit
+//   k_gc_eval    one lane per test: 2 TCCR (4 AES) per AND gate, output bit = colour ^ decode
+//
+// Both use the 4-table / 32-replica LDS T-table (conflict-free, as k_expand) and SoA outputs, so
+// a wave's 64 lanes read and write 64 consecutive 16-B blocks.
+#include "fhh_internal.h"
+#include "aes_keyed.h"
+
+namespace fhh {
+
+__constant__ WordTable c_T0_gc = T0;
+using GcTab = Tab4T32<DevOpsX>;
+constexpr int kGcThreads = 1024;
+constexpr size_t kGcLds = (size_t)GcTab::kWords * 4;
+
+__device__ __forceinline__ void gc_fill(uint32_t* tbl) {
+    for (int i = threadIdx.x; i < GcTab::kWords; i += blockDim.x) tbl[i] = GcTab::word(c_T0_gc.v, i);
+    __syncthreads();
+}
+
+__device__ __forceinline__ void zero_rk(uint32_t (&rk)[11][4]) {
+#pragma unroll
+    for (int r = 0; r < 11; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) rk[r][c] = ZERO_RK.w[r][c];
+}
+
+// TCCR on NB blocks: x <- pi(pi(x) ^ tweak) ^ pi(x), tweak in the low 64 bits
+template <int NB>
+__device__ __forceinline__ void tccr(uint32_t (&x)[NB][4], const uint64_t (&tw)[NB], const uint32_t* tbl,
+                                     uint32_t b0, uint32_t b1, const uint32_t (&zrk)[11][4]) {
+    uint32_t p[NB][4], q[NB][4];
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) p[k][c] = x[k][c];
+    aes_rk<GcTab, NB>(p, tbl, b0, b1, zrk);
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        q[k][0] = p[k][0] ^ (uint32_t)tw[k];
+        q[k][1] = p[k][1] ^ (uint32_t)(tw[k] >> 32);
+        q[k][2] = p[k][2];
+        q[k][3] = p[k][3];
+    }
+    aes_rk<GcTab, NB>(q, tbl, b0, b1, zrk);
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[k][c] = q[k][c] ^ p[k][c];
+}
+
+__device__ __forceinline__ uint32_t plane_bit(const uint64_t* planes, uint64_t g, uint32_t bits, uint32_t j,
+                                              uint32_t nw, uint32_t i) {
+    return (uint32_t)(planes[((size_t)g * bits + j) * nw + (i >> 6)] >> (i & 63)) & 1u;
+}
+
+// tests to run: G * N, or, inside the level loop, the children the previous prune left
+__device__ __forceinline__ uint64_t gc_active(const GcArgs& a) {
+    if (!a.ctl) return a.G * a.N;
+    if (a.ctl->abort) return 0;
+    const uint64_t C = a.ctl->C;
+    return (C < a.G ? C : a.G) * a.N;
+}
+
+__device__ __forceinline__ void st_blk(uint4* base, uint64_t row, uint64_t n, uint64_t t, const uint32_t (&v)[4]) {
+    base[row * n + t] = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void ld_blk(const uint4* base, uint64_t row, uint64_t n, uint64_t t, uint32_t (&v)[4]) {
+    const uint4 q = base[row * n + t];
+    v[0] = q.x;
+    v[1] = q.y;
+    v[2] = q.z;
+    v[3] = q.w;
+}
+
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
+    extern __shared__ uint32_t tbl_gc[];
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(threadIdx.x & 63, b0, b1);
+    uint32_t zrk[11][4];
+    zero_rk(zrk);
+    const uint64_t n = a.G * a.N;
+    const uint32_t D[4] = {a.delta[0], a.delta[1], a.delta[2], a.delta[3]};
+    uint32_t lrk[11][4];   // uniform: the label key schedule stays in SGPRs
+#pragma unroll
+    for (int r = 0; r < 11; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) lrk[r][c] = a.rk_label[r][c];
+    constexpr int W = 2 * B + 1;
+    const uint64_t n_act = gc_active(a);
+    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
+        const uint64_t g = t / a.N;
+        const uint32_t i = (uint32_t)(t - g * a.N);
+        // zero labels, generated per wire pair as the gates consume them (registers do not
+        // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B
+        const uint64_t ctr0 = a.label_nonce + t * W;
+        uint32_t acc[4];
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            uint32_t s[2][4] = {{(uint32_t)(ctr0 + k), (uint32_t)((ctr0 + k) >> 32), 0u, 0u},
+                                {(uint32_t)(ctr0 + B + 1 + k), (uint32_t)((ctr0 + B + 1 + k) >> 32), 0u, 0u}};
+            aes_rk<GcTab, 2>(s, tbl_gc, b0, b1, lrk);
+            // active labels: the garbler's bit (sent in the clear), the evaluator's (via OT)
+            const uint32_t gb = plane_bit(a.gb_planes, g, B, k, a.nw, i);
+            const uint32_t eb = plane_bit(a.ev_planes, g, B, k, a.nw, i);
+            uint32_t x[4], y[4], bz[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                x[c] = s[0][c] ^ (gb ? D[c] : 0u);
+                y[c] = s[1][c] ^ (eb ? D[c] : 0u);
+                bz[c] = s[0][c] ^ s[1][c] ^ D[c];   // z_k = NOT(x_k ^ y_k): free XOR, NOT = ^Delta
+            }
+            st_blk(a.gb_labels, k, n, t, x);
+            st_blk(a.ev_labels, k, n, t, y);
+            if (k == 0) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) acc[c] = bz[c];
+                continue;
+            }
+            // half-gates AND(acc, z_k), gate index gate_base + t (B - 1) + k - 1
+            uint32_t h[4][4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                h[0][c] = acc[c];
+                h[1][c] = acc[c] ^ D[c];
+                h[2][c] = bz[c];
+                h[3][c] = bz[c] ^ D[c];
+            }
+            const uint32_t pa = acc[0] & 1u, pb = bz[0] & 1u;
+            const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
+            const uint64_t tw[4] = {j, j, j + 1, j + 1};
+            tccr<4>(h, tw, tbl_gc, b0, b1, zrk);
+            uint32_t TG[4], TE[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                TG[c] = h[0][c] ^ h[1][c] ^ (pb ? D[c] : 0u);
+                TE[c] = h[2][c] ^ h[3][c] ^ acc[c];
+                const uint32_t wg = h[0][c] ^ (pa ? TG[c] : 0u);
+                const uint32_t we = h[2][c] ^ (pb ? (TE[c] ^ acc[c]) : 0u);
+                acc[c] = wg ^ we;
+            }
+            st_blk(a.tables, 2 * (k - 1), n, t, TG);
+            st_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
+        }
+        // mask wire; out = eq ^ mask has zero label acc ^ M0, decoding bit = its colour
+        uint32_t m[1][4] = {{(uint32_t)(ctr0 + B), (uint32_t)((ctr0 + B) >> 32), 0u, 0u}};
+        aes_rk<GcTab, 1>(m, tbl_gc, b0, b1, lrk);
+        a.decode[t] = (uint8_t)((acc[0] ^ m[0][0]) & 1u);
+#pragma unroll
+        for (int c = 0; c < 4; c++) m[0][c] ^= a.mask ? D[c] : 0u;
+        st_blk(a.gb_labels, B, n, t, m[0]);
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
+    extern __shared__ uint32_t tbl_gc[];
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(threadIdx.x & 63, b0, b1);
+    uint32_t zrk[11][4];
+    zero_rk(zrk);
+    const uint64_t n = a.G * a.N;
+    const uint64_t n_act = gc_active(a);
+    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
+        uint32_t acc[4], x[4], y[4];
+        ld_blk(a.gb_labels, 0, n, t, x);
+        ld_blk(a.ev_labels, 0, n, t, y);
+#pragma unroll
+        for (int c = 0; c < 4; c++) acc[c] = x[c] ^ y[c];   // NOT is free for the evaluator
+#pragma unroll
+        for (int k = 1; k < B; k++) {
+            uint32_t h[2][4], TG[4], TE[4];
+            ld_blk(a.gb_labels, k, n, t, x);
+            ld_blk(a.ev_labels, k, n, t, y);
+            ld_blk(a.tables, 2 * (k - 1), n, t, TG);
+            ld_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                h[0][c] = acc[c];
+                h[1][c] = x[c] ^ y[c];
+            }
+            const uint32_t sa = acc[0] & 1u, sb = h[1][0] & 1u;
+            const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
+            const uint64_t tw[2] = {j, j + 1};
+            tccr<2>(h, tw, tbl_gc, b0, b1, zrk);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t wg = h[0][c] ^ (sa ? TG[c] : 0u);
+                const uint32_t we = h[1][c] ^ (sb ? (TE[c] ^ acc[c]) : 0u);
+                acc[c] = wg ^ we;
+            }
+        }
+        ld_blk(a.gb_labels, B, n, t, x);   // mask wire
+        a.out[t] = (uint8_t)(((acc[0] ^ x[0]) & 1u) ^ a.decode[t]);
+    }
+}
+
+template <int B>
+static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
+    const void* fn = garble ? (const void*)k_gc_garble<B> : (const void*)k_gc_eval<B>;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[garble]) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGcLds);
+        if (e != hipSuccess) return e;
+        attr_set[garble] = true;
+    }
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const uint64_t n = a.G * a.N;
+    const uint64_t need = (n + kGcThreads - 1) / kGcThreads;
+    const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
+    if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), kGcLds, stream, a);
+    else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), kGcLds, stream, a);
+    return hipGetLastError();
+}
+
+static hipError_t gc_dispatch(const GcArgs& a, bool garble, hipStream_t stream) {
+    if (a.G * a.N == 0) return hipSuccess;
+    switch (a.bits) {
+        case 1: return gc_launch<1>(a, garble, stream);
+        case 2: return gc_launch<2>(a, garble, stream);
+        case 3: return gc_launch<3>(a, garble, stream);
+        case 4: return gc_launch<4>(a, garble, stream);
+        case 5: return gc_launch<5>(a, garble, stream);
+        case 6: return gc_launch<6>(a, garble, stream);
+        case 7: return gc_launch<7>(a, garble, stream);
+        case 8: return gc_launch<8>(a, garble, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, true, stream); }
+hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, false, stream); }
+
+}  // namespace fhh

@@ -9,12 +9,14 @@
 // collect.rs:918-929).
 #include "fhh_internal.h"
 #include "field_arith.h"
+#include "aes_tables.h"
 #include "../../include/fhh.h"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -146,6 +148,7 @@ struct fhh_ctx {
 
     fhh_stats stats{};
     bool timing = true;
+    uint32_t timing_every = 1;   // device level loop: time every K-th k_expand launch
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     std::vector<std::pair<size_t, uint64_t>> ev_pending;   // (pool index, blocks)
     size_t ev_next = 0;
@@ -203,6 +206,7 @@ void timing_resolve(fhh_ctx* ctx) {
         if (hipEventElapsedTime(&ms, ctx->ev_pool[pr.first].first, ctx->ev_pool[pr.first].second) == hipSuccess) {
             ctx->stats.expand_ms += ms;
             ctx->stats.expand_blocks_timed += pr.second;
+            ctx->stats.expand_launches_timed++;
         }
     }
     ctx->ev_pending.clear();
@@ -727,9 +731,108 @@ int set_device(fhh_ctx* ctx) {
 
 }  // namespace
 
+// ---- garbled-circuit equality test helpers (row f1) ------------------------------------------
+namespace {
+// FIPS-197 key expansion on little-endian column words (RotWord = rotr 8, rcon in byte 0), the
+// convention of the device T-table rounds (aes_keyed.h)
+void host_key_schedule(const uint8_t key[16], uint32_t (&rk)[11][4]) {
+    uint32_t w[44];
+    for (int i = 0; i < 4; i++)
+        w[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+               ((uint32_t)key[4 * i + 3] << 24);
+    uint32_t rcon = 1;
+    for (int i = 4; i < 44; i++) {
+        uint32_t t = w[i - 1];
+        if (i % 4 == 0) {
+            t = (t >> 8) | (t << 24);
+            t = (uint32_t)SBOX.v[t & 0xFF] | ((uint32_t)SBOX.v[(t >> 8) & 0xFF] << 8) |
+                ((uint32_t)SBOX.v[(t >> 16) & 0xFF] << 16) | ((uint32_t)SBOX.v[t >> 24] << 24);
+            t ^= rcon;
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+        }
+        w[i] = w[i - 4] ^ t;
+    }
+    for (int r = 0; r < 11; r++)
+        for (int c = 0; c < 4; c++) rk[r][c] = w[4 * r + c];
+}
+
+void words_from_bytes(const uint8_t b[16], uint32_t (&w)[4]) {
+    for (int c = 0; c < 4; c++)
+        w[c] = (uint32_t)b[4 * c] | ((uint32_t)b[4 * c + 1] << 8) | ((uint32_t)b[4 * c + 2] << 16) |
+               ((uint32_t)b[4 * c + 3] << 24);
+}
+
+uint64_t host_mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// the level loop's per-level garbler secrets (a fresh key, Delta and mask per tree_crawl call)
+void gc_level_material(uint64_t prf_seed, uint32_t level, uint8_t key[16], uint8_t delta[16], uint32_t* mask) {
+    uint64_t z = host_mix64(prf_seed ^ 0x67635f6c6576656cull ^ ((uint64_t)level << 20));
+    for (int h = 0; h < 2; h++) {
+        z = host_mix64(z);
+        std::memcpy(key + 8 * h, &z, 8);
+    }
+    for (int h = 0; h < 2; h++) {
+        z = host_mix64(z);
+        std::memcpy(delta + 8 * h, &z, 8);
+    }
+    *mask = (uint32_t)(host_mix64(z) & 1);
+}
+
+// validated GcArgs from a batch (device pointers)
+int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
+    if (!b) return ctx->fail(FHH_E_ARG, "gc: NULL batch");
+    if (b->bits < 1 || b->bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
+    if ((uint64_t)b->words * 64 < b->clients) return ctx->fail(FHH_E_ARG, "gc: words < ceil(clients / 64)");
+    const uint64_t n = b->groups * b->clients;
+    if (n && (!b->gb_planes_dev || !b->ev_planes_dev || !b->gb_labels_dev || !b->ev_labels_dev || !b->decode_dev ||
+              !b->out_dev || (b->bits > 1 && !b->tables_dev)))
+        return ctx->fail(FHH_E_ARG, "gc: NULL device buffer");
+    a = GcArgs{};
+    a.gb_planes = b->gb_planes_dev;
+    a.ev_planes = b->ev_planes_dev;
+    a.G = b->groups;
+    a.N = b->clients;
+    a.nw = b->words;
+    a.bits = b->bits;
+    a.mask = b->mask & 1u;
+    host_key_schedule(b->label_key, a.rk_label);
+    words_from_bytes(b->delta, a.delta);
+    a.delta[0] |= 1u;   // colour bit of Delta = 1 (point-and-permute)
+    a.label_nonce = b->label_nonce;
+    a.gate_base = b->gate_base;
+    a.tables = reinterpret_cast<uint4*>(b->tables_dev);
+    a.gb_labels = reinterpret_cast<uint4*>(b->gb_labels_dev);
+    a.ev_labels = reinterpret_cast<uint4*>(b->ev_labels_dev);
+    a.decode = b->decode_dev;
+    a.out = b->out_dev;
+    a.ctl = nullptr;
+    return FHH_OK;
+}
+}  // namespace
+
 // ---- device-resident level loop (fhh_sim_crawl, host_loop = 0) ---------------------------------
+// FHH_DEBUG_PHASES=1 prints host wall-clock per crawl phase to stderr (setup / loop / readback)
+struct PhaseClock {
+    bool on = std::getenv("FHH_DEBUG_PHASES") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[fhh phase] %-10s %9.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
+    DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
+    DevBuf gc_planes[2], gc_tables, gc_gbl, gc_evl, gc_decode, gc_out;   // cfg->gc (row f1)
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
@@ -835,6 +938,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     const int variant = c0->variant;
     const uint64_t grid_waves = (uint64_t)c0->grid * (expand_threads(variant) / 64);
     const uint32_t per_level_per = cfg->mode == 0 ? 1 : 4;   // partial u64 per child (non-last)
+    PhaseClock pc;
     LoopBuffers B;
     B.distributed = cfg->comm || cfg->allreduce;
     uint32_t cap0 = std::max(cfg->init_capacity ? next_pow2(cfg->init_capacity) : 256u, c0->loop_cap_hint);
@@ -864,6 +968,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, expand_unit(variant, c0->nw), expand_max_group(variant),
                                      d, 2, grid_waves, B.pos[0].as<uint32_t>(), l0, c0->stream));
     }
+    pc.mark("setup");
     const bool record = cfg->counts != nullptr;
     const uint32_t kBatch = 32;
     bool prune_only = false;           // resume after growth: prune of this level only
@@ -900,10 +1005,11 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     J.nw = (uint32_t)c->nw;
                 }
             size_t slot = 0;
-            if (c0->timing) HIP_TRY(c0, timing_begin(c0, &slot));
+            const bool timed = c0->timing && lv % c0->timing_every == 0;
+            if (timed) HIP_TRY(c0, timing_begin(c0, &slot));
             La.total_items = 1;   // non-zero: the real count comes from LoopCtl
             HIP_TRY(c0, launch_expand(La, variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
-            if (c0->timing) HIP_TRY(c0, timing_end(c0, slot, 0));
+            if (timed) HIP_TRY(c0, timing_end(c0, slot, 0));
             c0->stats.expand_launches++;
             // -- equality count / simulated OT sums per child
             ChildArgs a{};
@@ -924,6 +1030,45 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             a.n = (uint32_t)c0->n;
             a.ctl = B.ctl.as<LoopCtl>();
             uint64_t* part = B.partials.as<uint64_t>();
+            if (cfg->gc && pmode != 0) {
+                // garbled-circuit equality (tree_crawl with gc_sender, collect.rs:419-482):
+                // both servers' share planes, server 0 garbles, server 1 evaluates
+                const uint32_t bits = 2 * d;
+                const uint64_t tests = C_cap * c0->n;
+                const size_t plane_bytes = (size_t)C_cap * bits * c0->nw * 8;
+                for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
+                HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
+                HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
+                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * tests * 16));
+                HIP_TRY(c0, B.gc_decode.ensure(tests));
+                HIP_TRY(c0, B.gc_out.ensure(tests));
+                ChildArgs pa = a;
+                HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[0].as<uint64_t>(), c0->stream));
+                pa.s0 = a.s1;
+                HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[1].as<uint64_t>(), c0->stream));
+                fhh_gc_batch gb{};
+                gb.groups = C_cap;
+                gb.clients = (uint32_t)c0->n;
+                gb.words = (uint32_t)c0->nw;
+                gb.bits = bits;
+                gc_level_material(cfg->prf_seed, lv, gb.label_key, gb.delta, &gb.mask);
+                gb.gb_planes_dev = B.gc_planes[0].as<uint64_t>();
+                gb.ev_planes_dev = B.gc_planes[1].as<uint64_t>();
+                gb.tables_dev = B.gc_tables.as<uint8_t>();
+                gb.gb_labels_dev = B.gc_gbl.as<uint8_t>();
+                gb.ev_labels_dev = B.gc_evl.as<uint8_t>();
+                gb.decode_dev = B.gc_decode.as<uint8_t>();
+                gb.out_dev = B.gc_out.as<uint8_t>();
+                GcArgs g{};
+                rc = gc_args(c0, &gb, g);
+                if (rc) return rc;
+                g.ctl = B.ctl.as<LoopCtl>();
+                HIP_TRY(c0, launch_gc_garble(g, c0->stream));
+                HIP_TRY(c0, launch_gc_eval(g, c0->stream));
+                a.gc_out = g.out;
+                a.gc_N = g.N;
+                a.gc_mask = g.mask;
+            }
             if (pmode == 0) HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
             else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream));
             else HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
@@ -1029,17 +1174,31 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         }
     }
     c0->loop_cap_hint = std::max(B.E_cap, B.F_cap);   // the next crawl starts at this size
+    pc.mark("loop");
     // ---- readback: sizes, hist, final values -> host-side state of both servers ----
+    // every level's hist row is packed on the device (k_gather_hist) and copied in one transfer
+    const uint64_t hist_cap = (uint64_t)levels * B.F_cap;
+    HIP_TRY(c0, B.hist_rows.ensure((size_t)levels * sizeof(uint32_t*)));
+    HIP_TRY(c0, B.hist_packed.ensure(hist_cap * 4));
+    HIP_TRY(c0, hipMemcpyAsync(B.hist_rows.p, B.hist_ptr.data(), (size_t)levels * sizeof(uint32_t*),
+                               hipMemcpyHostToDevice, c0->stream));
+    HIP_TRY(c0, launch_gather_hist(B.sizes.as<uint32_t>(), 4 + kMaxDims, B.hist_rows.as<const uint32_t*>(), levels,
+                                   B.hist_packed.as<uint32_t>(), hist_cap, c0->stream));
     std::vector<uint32_t> sz((size_t)levels * (4 + kMaxDims));
     HIP_TRY(c0, hipMemcpy(sz.data(), B.sizes.p, sz.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t hist_total = 0;
+    for (uint32_t lv = 0; lv < levels; lv++) hist_total += sz[(size_t)lv * (4 + kMaxDims) + 1];
+    if (hist_total > hist_cap) return c0->fail(FHH_E_STATE, "loop: kept-children lists exceed their capacity");
+    std::vector<uint32_t> packed(hist_total);
+    if (hist_total)
+        HIP_TRY(c0, hipMemcpy(packed.data(), B.hist_packed.p, hist_total * 4, hipMemcpyDeviceToHost));
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist(levels);
     const uint32_t mask = (1u << d) - 1;
-    for (uint32_t lv = 0; lv < levels; lv++) {
+    for (uint32_t lv = 0, off = 0; lv < levels; lv++) {
         const uint32_t nf = sz[(size_t)lv * (4 + kMaxDims) + 1];
-        std::vector<uint32_t> hc(nf);
-        if (nf) HIP_TRY(c0, hipMemcpy(hc.data(), B.hist_ptr[lv], (size_t)nf * 4, hipMemcpyDeviceToHost));
         hist[lv].reserve(nf);
-        for (uint32_t c : hc) hist[lv].emplace_back(c >> d, c & mask);
+        for (uint32_t k = 0; k < nf; k++) hist[lv].emplace_back(packed[off + k] >> d, packed[off + k] & mask);
+        off += nf;
     }
     const uint32_t nfin = sz[(size_t)(levels - 1) * (4 + kMaxDims) + 1];
     std::vector<uint32_t> fv((size_t)nfin * 20);
@@ -1094,7 +1253,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         for (uint32_t lv = 0; lv < levels; lv++) {
             uint64_t live_sum = 0;
             for (uint32_t j = 0; j < d; j++) live_sum += lv == 0 ? 1 : sz[(size_t)(lv - 1) * (4 + kMaxDims) + 4 + j];
-            blocks += live_sum * 4 * c0->n * 2;
+            if (lv % c0->timing_every == 0) blocks += live_sum * 4 * c0->n * 2;
         }
         if (c0->timing) c0->stats.expand_blocks_timed += blocks;
     }
@@ -1123,6 +1282,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         }
         off += C;
     }
+    pc.mark("readback");
     return FHH_OK;
 }
 
@@ -1655,12 +1815,20 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
     if (levels > c0->L) return c0->fail(FHH_E_ARG, "sim_crawl: levels > data_len");
     if (cfg->mode > 1) return c0->fail(FHH_E_ARG, "sim_crawl: bad mode");
+    if (cfg->gc && (cfg->mode != 1 || cfg->host_loop))
+        return c0->fail(FHH_E_ARG, "sim_crawl: gc needs mode 1 (OT share values) and the device loop");
+    if (cfg->gc && 2 * c0->d > (uint32_t)kGcMaxBits) return c0->fail(FHH_E_ARG, "sim_crawl: gc supports d <= 4");
     if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");
     if (c0->d != c1->d || c0->L != c1->L) return c0->fail(FHH_E_ARG, "sim_crawl: ctx shapes differ");
     // leader.rs:193-194 and 245-246
     const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
     const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));
-    if (!cfg->host_loop) return sim_crawl_device_loop(c0, c1, cfg, levels, thr, thr_last);
+    if (!cfg->host_loop) {
+        PhaseClock total;
+        rc = sim_crawl_device_loop(c0, c1, cfg, levels, thr, thr_last);   // incl. buffer teardown
+        total.mark("total");
+        return rc;
+    }
     rc = fhh_tree_init(c0);
     if (rc) return rc;
     rc = fhh_tree_init(c1);
@@ -1775,7 +1943,9 @@ int fhh_reset_stats(fhh_ctx* ctx) {
 
 int fhh_set_timing(fhh_ctx* ctx, int enabled) {
     CTX_CHECK(ctx);
+    if (enabled < 0) return ctx->fail(FHH_E_ARG, "set_timing: enabled must be >= 0");
     ctx->timing = enabled != 0;
+    ctx->timing_every = enabled > 1 ? (uint32_t)enabled : 1;
     return FHH_OK;
 }
 
@@ -1940,4 +2110,85 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
     v.n = b->n_keys;
     HIP_TRY(ctx, launch_verify_fe(v, ctx->stream));
     return sync(ctx);
+}
+
+// ---- garbled-circuit equality test (row f1) ------------------------------------------------
+int fhh_gc_equality_device(fhh_ctx* ctx, const fhh_gc_batch* b) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    GcArgs a;
+    rc = gc_args(ctx, b, a);
+    if (rc) return rc;
+    HIP_TRY(ctx, launch_gc_garble(a, ctx->stream));
+    HIP_TRY(ctx, launch_gc_eval(a, ctx->stream));
+    return sync(ctx);
+}
+
+int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                         uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
+                         uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
+                         uint8_t* decode, uint8_t* out) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
+    if (n == 0) return FHH_OK;
+    if (!gb_bits || !ev_bits || !label_key || !delta || !out) return ctx->fail(FHH_E_ARG, "gc: NULL argument");
+    if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc: n must fit 32 bits");
+    const uint64_t nw = (n + 63) / 64;
+    std::vector<uint64_t> planes[2];
+    const uint8_t* src[2] = {gb_bits, ev_bits};
+    for (int s = 0; s < 2; s++) {
+        planes[s].assign((size_t)bits * nw, 0);
+        for (uint64_t t = 0; t < n; t++)
+            for (uint32_t j = 0; j < bits; j++)
+                if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
+    }
+    DevBuf dp[2], dt, dg, de, dd, dout;
+    for (int s = 0; s < 2; s++) {
+        HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
+        HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, dt.ensure((size_t)std::max(bits - 1, 1u) * 2 * n * 16));
+    HIP_TRY(ctx, dg.ensure((size_t)(bits + 1) * n * 16));
+    HIP_TRY(ctx, de.ensure((size_t)bits * n * 16));
+    HIP_TRY(ctx, dd.ensure(n));
+    HIP_TRY(ctx, dout.ensure(n));
+    fhh_gc_batch b{};
+    b.groups = 1;
+    b.clients = (uint32_t)n;
+    b.words = (uint32_t)nw;
+    b.bits = bits;
+    b.mask = mask;
+    std::memcpy(b.label_key, label_key, 16);
+    std::memcpy(b.delta, delta, 16);
+    b.label_nonce = label_nonce;
+    b.gate_base = gate_base;
+    b.gb_planes_dev = dp[0].as<uint64_t>();
+    b.ev_planes_dev = dp[1].as<uint64_t>();
+    b.tables_dev = dt.as<uint8_t>();
+    b.gb_labels_dev = dg.as<uint8_t>();
+    b.ev_labels_dev = de.as<uint8_t>();
+    b.decode_dev = dd.as<uint8_t>();
+    b.out_dev = dout.as<uint8_t>();
+    rc = fhh_gc_equality_device(ctx, &b);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    if (decode) HIP_TRY(ctx, hipMemcpy(decode, dd.p, n, hipMemcpyDeviceToHost));
+    // SoA [row][t][16] -> AoS [t][row][16]
+    auto soa_to_aos = [&](const DevBuf& d, uint32_t rows, uint8_t* dst) -> int {
+        if (!dst || rows == 0) return FHH_OK;
+        std::vector<uint8_t> h((size_t)rows * n * 16);
+        HIP_TRY(ctx, hipMemcpy(h.data(), d.p, h.size(), hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < rows; r++)
+            for (uint64_t t = 0; t < n; t++)
+                std::memcpy(dst + (t * rows + r) * 16, h.data() + ((size_t)r * n + t) * 16, 16);
+        return FHH_OK;
+    };
+    rc = soa_to_aos(dt, 2 * (bits - 1), tables);
+    if (rc) return rc;
+    rc = soa_to_aos(dg, bits + 1, gb_labels);
+    if (rc) return rc;
+    return soa_to_aos(de, bits, ev_labels);
 }

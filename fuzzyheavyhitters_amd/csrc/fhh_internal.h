@@ -92,6 +92,34 @@ struct ChildArgs {
     uint32_t level;
     uint32_t n;                 // real clients on this ctx
     const LoopCtl* ctl;         // non-null: C from here (0 once aborted)
+    // GC mode (row f1): the equality bit of (child c, client i) is the evaluator's garbled-
+    // circuit output gc_out[c * gc_N + i] XOR the garbler's mask (ideal OT, collect.rs:437-471)
+    const uint8_t* gc_out;
+    uint32_t gc_N;
+    uint32_t gc_mask;
+};
+
+// Garbled-circuit equality tests (row f1, equalitytest.rs:25-219): tests t = g * N + i for
+// groups g < G (children) and i < N (clients); a test compares the garbler's `bits`-bit string
+// with the evaluator's. Inputs are bit planes [G][bits][nw] (as k_share_planes writes them);
+// outputs are SoA over t (16-B blocks; one lane per test, coalesced).
+constexpr int kGcMaxBits = 8;
+struct GcArgs {
+    const uint64_t* gb_planes;   // garbler's share bits
+    const uint64_t* ev_planes;   // evaluator's share bits (ideal OT: only their labels leave)
+    uint64_t G;
+    uint32_t N, nw, bits, mask;
+    uint32_t rk_label[11][4];    // garbler's label PRG key schedule (AES-128-CTR)
+    uint32_t delta[4];           // free-XOR offset, lsb 1
+    uint64_t label_nonce;        // label of (t, w) = AES_k(label_nonce + t * (2 bits + 1) + w)
+    uint64_t gate_base;          // half-gate tweaks 2 (gate_base + t (bits - 1) + k) (+1)
+    uint4* tables;               // [(bits-1)][2][n]  (T_G, T_E)
+    uint4* gb_labels;            // [bits + 1][n]     garbler's active input labels (+ mask)
+    uint4* ev_labels;            // [bits][n]         evaluator's active labels (ideal OT out)
+    uint8_t* decode;             // [n]               output decoding bit
+    uint8_t* out;                // [n]               evaluator's output bit = eq ^ mask
+    const LoopCtl* ctl;          // non-null (level loop): groups = min(G, ctl->C), 0 once aborted;
+                                 // G * N stays the SoA stride
 };
 
 struct PruneArgs {
@@ -160,6 +188,10 @@ int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t
 // device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
 // entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
+hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
+hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
+hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,
+                              uint32_t* out, uint64_t cap, hipStream_t stream);
 hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
                             uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
                             hipStream_t stream);

@@ -410,14 +410,23 @@ __device__ __forceinline__ uint64_t eq_word(const ChildArgs& a, const uint32_t (
     return m;
 }
 
-__global__ __launch_bounds__(kReduceThreads) void k_eq_count(ChildArgs a, uint64_t* counts) {
-    __shared__ uint64_t red[kReduceThreads / 64];
+// 1024 threads per child and two words per thread per pass, both words' loads issued before
+// either popcount: at configs[1] (nw = 1563) one pass covers a child, so the kernel is one
+// round of load latency instead of six dependent ones (r01: 10 us per level at 256 threads)
+constexpr int kEqThreads = 1024;
+__global__ __launch_bounds__(kEqThreads) void k_eq_count(ChildArgs a, uint64_t* counts) {
+    __shared__ uint64_t red[kEqThreads / 64];
     const uint64_t C_ = child_count(a);
     for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         uint64_t v[1] = {0};
-        for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) v[0] += __popcll(eq_word(a, e, w));
+        for (uint32_t w = threadIdx.x; w < a.nw; w += 2 * kEqThreads) {
+            const uint32_t w1 = w + kEqThreads;
+            const uint64_t m0 = eq_word(a, e, w);
+            const uint64_t m1 = w1 < a.nw ? eq_word(a, e, w1) : 0;
+            v[0] += __popcll(m0) + __popcll(m1);
+        }
         block_sum_u64<1>(v, red);
         if (threadIdx.x == 0) counts[c] = v[0];
     }
@@ -427,7 +436,7 @@ static int child_grid(uint64_t C) { return (int)(C < 65535 ? (C ? C : 1) : 65535
 
 hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_eq_count, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, counts);
+    hipLaunchKernelGGL(k_eq_count, dim3(child_grid(a.C)), dim3(kEqThreads), 0, stream, a, counts);
     return hipGetLastError();
 }
 
@@ -468,6 +477,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;
 
+// the equality bit the OT conversion consumes: plaintext (t, y) comparison, or in GC mode the
+// evaluator's garbled-circuit output XOR the garbler's mask (the OT receiver's choice bit and
+// the sender's message order, collect.rs:437-471: the received value is r0 iff eq)
+__device__ __forceinline__ bool sim_eq_bit(const ChildArgs& a, const uint32_t (&e)[kMaxDims], uint64_t c, uint32_t i) {
+    if (a.gc_out) return ((a.gc_out[c * a.gc_N + i] ^ a.gc_mask) & 1u) != 0;
+    return (eq_word(a, e, i >> 6) >> (i & 63)) & 1;
+}
+
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[4 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
@@ -478,8 +495,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         const uint64_t bc = mix64(base ^ c);
         uint64_t v[4] = {0, 0, 0, 0};
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const uint64_t eqw = eq_word(a, e, i >> 6);
-            const bool eq = (eqw >> (i & 63)) & 1;
+            const bool eq = sim_eq_bit(a, e, c, i);
             uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
             if (r0 >= kFeP) r0 -= kFeP;
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
@@ -533,8 +549,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = 0;
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const uint64_t eqw = eq_word(a, e, i >> 6);
-            const bool eq = (eqw >> (i & 63)) & 1;
+            const bool eq = sim_eq_bit(a, e, c, i);
             const uint64_t bi = mix64(bc ^ (a.client_base + i));
             uint64_t r0[4];
 #pragma unroll

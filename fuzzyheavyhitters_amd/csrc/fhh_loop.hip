@@ -176,6 +176,32 @@ hipError_t launch_prune(const PruneArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// End-of-crawl readback: pack every level's kept-children list (hist rows live at per-level
+// pointers, possibly in several capacity epochs) into one array, so the host copies it with
+// one D2H transfer instead of one synchronous copy per level. Block lv computes its offset as
+// the sum of the kept counts of the levels before it (sizes[k * stride + 1]).
+__global__ __launch_bounds__(256) void k_gather_hist(const uint32_t* sizes, uint32_t stride,
+                                                     const uint32_t* const* rows, uint32_t* out, uint64_t cap) {
+    __shared__ uint64_t red[4];
+    const uint32_t lv = blockIdx.x;
+    uint64_t v = 0;
+    for (uint32_t k = threadIdx.x; k < lv; k += blockDim.x) v += sizes[(size_t)k * stride + 1];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint64_t base = red[0] + red[1] + red[2] + red[3];
+    const uint32_t nf = sizes[(size_t)lv * stride + 1];
+    const uint32_t* src = rows[lv];
+    for (uint32_t i = threadIdx.x; i < nf && base + i < cap; i += blockDim.x) out[base + i] = src[i];
+}
+
+hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,
+                              uint32_t* out, uint64_t cap, hipStream_t stream) {
+    if (levels == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_hist, dim3(levels), dim3(256), 0, stream, sizes, stride, rows, out, cap);
+    return hipGetLastError();
+}
+
 __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
                             uint32_t nctx,
                             uint64_t grid_waves, uint32_t* pos0, uint32_t* l0, uint32_t* l1, uint32_t* l2,

@@ -66,7 +66,100 @@ __global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters)
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// launch-gap probe: a kernel that only touches its dynamic LDS (so the LDS allocation is
+// real) and, from one lane, one word of global memory
+__global__ void k_gap_probe(uint32_t* out, uint32_t tag) {
+    extern __shared__ uint32_t lds_dyn[];
+    lds_dyn[threadIdx.x] = tag;
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[1] = lds_dyn[(threadIdx.x + 1) % blockDim.x];
+}
+
+// writes `words_per_thread` u32 per thread (coalesced), normal or nontemporal stores
+template <bool NT>
+__global__ void k_gap_writer(uint32_t* dst, uint32_t words_per_thread) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t k = 0; k < words_per_thread; k++, i += stride) {
+        if (NT) __builtin_nontemporal_store((uint32_t)k, dst + i);
+        else dst[i] = (uint32_t)k;
+    }
+}
+
 }  // namespace fhh
+
+// Device time per kernel of a back-to-back chain on one stream (HIP events around `reps`
+// launches). which: 0 = 256 x 1024 threads, no LDS; 1 = 256 x 1024, 128 KiB LDS (k_expand's
+// footprint); 2 = alternate 256 x 1024 / 128 KiB with 1 x 1024 / 4 KiB (expand -> prune);
+// 3 = 1 x 1024 threads, 4 KiB (prune alone); 4 / 5 = alternate a 256 x 1024 kernel writing
+// 64 MiB (normal / nontemporal stores) with 1 x 1024 (does dirty L2 cost the next launch?).
+extern "C" int fhh_debug_launch_gaps(int device, int which, int reps, double* us_per_kernel) {
+    if (!us_per_kernel || reps < 1 || which < 0 || which > 7) return FHH_E_ARG;
+    const bool graph = which >= 6;   // 6 / 7: as 2 / 4, captured once into a hipGraph and replayed
+    if (graph) which = which == 6 ? 2 : 4;
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    uint32_t* out = nullptr;
+    if (hipMalloc(&out, 64u << 20) != hipSuccess) return FHH_E_NOMEM;
+    hipStream_t st;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipFree(out);
+        return FHH_E_HIP;
+    }
+    (void)hipFuncSetAttribute((const void*)fhh::k_gap_probe, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    float ms = 0.f;
+    hipGraphExec_t gexec = nullptr;
+    for (int pass = 0; pass < 2; pass++) {
+        if (graph && gexec) {
+            (void)hipEventRecord(a, st);
+            (void)hipGraphLaunch(gexec, st);
+            (void)hipEventRecord(b, st);
+            if (hipEventSynchronize(b) != hipSuccess) break;
+            (void)hipEventElapsedTime(&ms, a, b);
+            continue;
+        }
+        hipGraph_t g = nullptr;
+        if (graph) {
+            if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) break;
+        } else {
+            (void)hipEventRecord(a, st);
+        }
+        for (int r = 0; r < reps; r++) {
+            if (which >= 4 && (r & 1) == 0) {
+                if (which == 4) hipLaunchKernelGGL(fhh::k_gap_writer<false>, dim3(256), dim3(1024), 0, st, out, 64u);
+                else hipLaunchKernelGGL(fhh::k_gap_writer<true>, dim3(256), dim3(1024), 0, st, out, 64u);
+                continue;
+            }
+            const bool big = which == 1 || (which == 2 && (r & 1) == 0);
+            const bool one = which >= 3 || (which == 2 && (r & 1) == 1);
+            hipLaunchKernelGGL(fhh::k_gap_probe, dim3(one ? 1 : 256), dim3(1024), big ? 131072 : 4096, st, out,
+                               (uint32_t)r);
+        }
+        if (graph) {
+            if (hipStreamEndCapture(st, &g) != hipSuccess) break;
+            const hipError_t ge = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ge != hipSuccess) break;
+            (void)hipGraphLaunch(gexec, st);   // warm-up replay; pass 1 times the next one
+            (void)hipStreamSynchronize(st);
+            continue;
+        }
+        (void)hipEventRecord(b, st);
+        if (hipEventSynchronize(b) != hipSuccess) break;
+        (void)hipEventElapsedTime(&ms, a, b);
+    }
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    const hipError_t e = hipGetLastError();
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipStreamDestroy(st);
+    (void)hipFree(out);
+    if (e != hipSuccess) return FHH_E_HIP;
+    *us_per_kernel = ms * 1e3 / reps;
+    return FHH_OK;
+}
 
 extern "C" int fhh_microbench(int device, int which, double* rate) {
     if (!rate) return FHH_E_ARG;

@@ -58,11 +58,13 @@ class _TorchAllReduce:
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
-              init_capacity: int = 0, comm=None) -> SimResult:
+              init_capacity: int = 0, comm=None, gc: bool = False) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
-    callback (synchronises once per level; the gloo rehearsal path uses this)."""
+    callback (synchronises once per level; the gloo rehearsal path uses this). `gc=True` (mode
+    "fe", device loop) takes each (child, client) equality bit from the GPU garbled-circuit
+    equality test (server 0 garbles, server 1 evaluates; OT ideal) instead of comparing shares."""
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -73,6 +75,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.prf_seed = prf_seed
     cfg.host_loop = 1 if host_loop else 0
     cfg.init_capacity = init_capacity
+    cfg.gc = 1 if gc else 0
     ar = None
     if comm is not None:
         cfg.comm = comm.handle

@@ -213,6 +213,12 @@ typedef struct fhh_sim_config {
     /* native RCCL communicator (takes precedence over `allreduce`): the per-level sum is
      * ncclAllReduce on ctx0's stream, no host synchronisation per level. NULL on one GPU. */
     fhh_comm* comm;
+    /* mode 1, device loop: 1 = the per-(child, client) equality bit comes from the garbled-
+     * circuit equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
+     * evaluates; OT of the evaluator's labels and of the FE shares is ideal), as
+     * tree_crawl does with gc_sender (collect.rs:419-482). Same sums as 0; fresh garbler key,
+     * Delta and mask per level, derived from prf_seed. */
+    uint32_t gc;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x
@@ -263,6 +269,49 @@ typedef struct fhh_sketch_batch {
 } fhh_sketch_batch;
 int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* batch);
 
+/* ---- garbled-circuit equality test -------------------------------------
+ * multiple_gb_equality_test / multiple_ev_equality_test (equalitytest.rs:25-219): per test,
+ * eq = AND_j NOT(x_j XOR y_j) over `bits` share bits, revealed to the evaluator as eq XOR mask.
+ * Free-XOR + half-gates, hash TCCR(x, i) = pi(pi(x) ^ i) ^ pi(x) with pi = AES-128 under the
+ * all-zero key (swanky's fixed key and wire format are not restatable: DESIGN.md §5.3). Labels
+ * are 16-B blocks, colour = bit 0 of byte 0; the garbler's zero label of wire w of test t is
+ * AES_label_key(LE128(label_nonce + t (2 bits + 1) + w)) (w < bits: its string, w = bits: the
+ * mask, w > bits: the evaluator's string); AND gate k of test t has tweaks 2 g, 2 g + 1 with
+ * g = gate_base + t (bits - 1) + k. Tests t = g N + i (g < groups, i < clients); inputs are bit
+ * planes [groups][bits][words] (bit i % 64 of word i / 64, as fhh_tree_crawl's share planes);
+ * outputs are SoA over t: tables [(bits-1) * 2][t] (T_G, T_E), gb_labels [bits + 1][t] (the
+ * garbler's active labels, mask last), ev_labels [bits][t] (the evaluator's active labels — the
+ * output of an ideal OT; a deployment runs OT extension instead), decode [t], out [t]. The
+ * reference draws one mask per call (`rng.clone().gen_bool()`, equalitytest.rs:38-43, the clone
+ * never advances), so `mask` is one bit for the whole batch. */
+typedef struct fhh_gc_batch {
+    uint64_t groups;
+    uint32_t clients;              /* tests per group                                      */
+    uint32_t words;                /* plane words per (group, bit), >= ceil(clients / 64)  */
+    uint32_t bits;                 /* string length (2d), 1..8                             */
+    uint32_t mask;                 /* garbler's mask bit                                   */
+    uint8_t label_key[16];         /* garbler's label PRG key                              */
+    uint8_t delta[16];             /* free-XOR offset (bit 0 is forced to 1)               */
+    uint64_t label_nonce;
+    uint64_t gate_base;
+    const uint64_t* gb_planes_dev; /* garbler's bits   [groups][bits][words]               */
+    const uint64_t* ev_planes_dev; /* evaluator's bits [groups][bits][words]               */
+    uint8_t* tables_dev;           /* [(bits - 1) * 2][groups * clients][16]               */
+    uint8_t* gb_labels_dev;        /* [bits + 1][groups * clients][16]                     */
+    uint8_t* ev_labels_dev;        /* [bits][groups * clients][16]                         */
+    uint8_t* decode_dev;           /* [groups * clients]                                   */
+    uint8_t* out_dev;              /* [groups * clients] evaluator's eq XOR mask           */
+} fhh_gc_batch;
+/* Garbler then evaluator on ctx's stream (device buffers); returns after both finish. */
+int fhh_gc_equality_device(fhh_ctx* ctx, const fhh_gc_batch* batch);
+/* The same on host buffers, one group: gb_bits / ev_bits [n][bits] (0/1 bytes); outputs AoS
+ * (tables [n][bits-1][2][16], gb_labels [n][bits+1][16], ev_labels [n][bits][16], decode [n],
+ * out [n]); any output but `out` may be NULL. */
+int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                         uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
+                         uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
+                         uint8_t* decode, uint8_t* out);
+
 /* ---- statistics ------------------------------------------------------------------------ */
 
 typedef struct fhh_stats {
@@ -273,6 +322,7 @@ typedef struct fhh_stats {
     uint64_t expand_blocks_timed; /* AES blocks covered by expand_ms                     */
     uint64_t levels;            /* crawled levels                                        */
     double keygen_ms;
+    uint64_t expand_launches_timed; /* k_expand launches covered by expand_ms             */
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);
@@ -283,13 +333,20 @@ int fhh_set_variant(fhh_ctx* ctx, int variant);
  * Returns FHH_E_ARG past the last variant. */
 int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* grid_per_device);
 int fhh_reset_stats(fhh_ctx* ctx);
-/* 1 to time every k_expand launch with HIP events (default 1). */
+/* 1 to time every k_expand launch with HIP events (default 1); K > 1 times every K-th launch
+ * of the device level loop (a pair of event records costs the stream a few microseconds). */
 int fhh_set_timing(fhh_ctx* ctx, int enabled);
 
 /* Peak-rate microbenchmarks pinning the roofline denominators on the running device:
  * which = 0 -> v_xor_b32 lane-ops/s; which = 1 -> ds_read_b32 bytes/s (k_expand pattern);
  * 2 -> v_bitop3_b32 lane-ops/s; 3 -> v_bitop3_b32 at 2 waves/SIMD; 4 -> v_xor_b32 at 2 waves/SIMD. */
 int fhh_microbench(int device, int which, double* rate);
+/* Device time per kernel of `reps` back-to-back launches of an empty kernel on one stream
+ * (launch-overhead probe for the level loop): which = 0 -> 256 x 1024 threads, 4 KiB LDS;
+ * 1 -> 256 x 1024, 128 KiB LDS (k_expand's footprint); 2 -> alternating 256 x 1024 / 128 KiB and
+ * 1 x 1024 (expand -> prune); 3 -> 1 x 1024; 4 / 5 -> alternating a 64 MiB writer (normal /
+ * nontemporal stores) with 1 x 1024; 6 / 7 -> as 2 / 4 captured in a hipGraph and replayed. */
+int fhh_debug_launch_gaps(int device, int which, int reps, double* us_per_kernel);
 
 /* Device properties the library targets (gfx950). */
 int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus);

@@ -632,3 +632,124 @@ void orc_sketch_verify_fe_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t
         }
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* Row f1: garbled-circuit equality test (equalitytest.rs:25-219).    */
+/* Third-party algorithm: swanky `fancy-garbling` @553ede0 (not       */
+/* vendored). Restated from the published schemes it implements:     */
+/* free-XOR + half-gates (Zahur, Rosulek, Evans, EUROCRYPT 2015) with */
+/* the TCCR hash H(x, i) = pi(pi(x) ^ i) ^ pi(x) (Guo, Katz, Wang, Yu,*/
+/* S&P 2020), pi = AES-128 under the all-zero key (swanky's fixed key */
+/* is not restatable). Circuit: bin_eq_bundles (:128-147) = and_many  */
+/* of NOT(x_j ^ y_j), folded left; XOR the garbler's mask (:165-189). */
+/* Parity: functional (eq_gc, :222-266) — wire format unpinned.       */
+/* ------------------------------------------------------------------ */
+static void gc_tccr(const uint8_t x[16], uint64_t tweak, uint8_t out[16]) {
+    uint8_t px[16], q[16], y[16];
+    orc_aes128_zero_encrypt(x, px);
+    memcpy(q, px, 16);
+    for (int k = 0; k < 8; k++) q[k] ^= (uint8_t)(tweak >> (8 * k));
+    orc_aes128_zero_encrypt(q, y);
+    for (int k = 0; k < 16; k++) out[k] = y[k] ^ px[k];
+}
+
+static void gc_xor(uint8_t* d, const uint8_t* a, const uint8_t* b) {
+    for (int k = 0; k < 16; k++) d[k] = a[k] ^ b[k];
+}
+
+/* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits. The evaluator's
+ * active labels (what OT delivers, gb_set_fancy_inputs :67-82) are output too. Layouts:
+ * tables [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last), ev_labels [n][bits][16]. */
+void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits, uint32_t mask,
+                      const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
+                      uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels, uint8_t* decode) {
+    oracle_init();
+    uint8_t rk[176], D[16];
+    key_expand(key, rk);
+    memcpy(D, delta_in, 16);
+    D[0] |= 1;
+    const uint64_t W = 2 * (uint64_t)bits + 1;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t L[17][16], acc[16];
+        for (uint64_t w = 0; w < W; w++) {           /* zero labels: AES_key(LE128(nonce + t W + w)) */
+            uint8_t ctr[16] = {0};
+            const uint64_t c = label_nonce + (uint64_t)t * W + w;
+            for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
+            aes128_encrypt_rk(rk, ctr, L[w]);
+        }
+        for (uint32_t j = 0; j < bits; j++) {        /* active input labels */
+            uint8_t* g = gb_labels + ((uint64_t)t * (bits + 1) + j) * 16;
+            uint8_t* e = ev_labels + ((uint64_t)t * bits + j) * 16;
+            memcpy(g, L[j], 16);
+            memcpy(e, L[bits + 1 + j], 16);
+            if (gb_bits[(uint64_t)t * bits + j] & 1) gc_xor(g, g, D);
+            if (ev_bits[(uint64_t)t * bits + j] & 1) gc_xor(e, e, D);
+        }
+        uint8_t* m = gb_labels + ((uint64_t)t * (bits + 1) + bits) * 16;
+        memcpy(m, L[bits], 16);
+        if (mask & 1) gc_xor(m, m, D);
+        /* z_0 = NOT(x_0 ^ y_0): zero label X0 ^ Y0 ^ D */
+        gc_xor(acc, L[0], L[bits + 1]);
+        gc_xor(acc, acc, D);
+        for (uint32_t k = 1; k < bits; k++) {         /* and_many: acc = AND(acc, z_k) */
+            uint8_t bz[16], a1[16], b1[16], hA0[16], hA1[16], hB0[16], hB1[16], TG[16], TE[16], WG[16], WE[16];
+            gc_xor(bz, L[k], L[bits + 1 + k]);
+            gc_xor(bz, bz, D);
+            gc_xor(a1, acc, D);
+            gc_xor(b1, bz, D);
+            const int pa = acc[0] & 1, pb = bz[0] & 1;
+            const uint64_t j = 2 * (gate_base + (uint64_t)t * (bits - 1) + (k - 1));
+            gc_tccr(acc, j, hA0);
+            gc_tccr(a1, j, hA1);
+            gc_tccr(bz, j + 1, hB0);
+            gc_tccr(b1, j + 1, hB1);
+            gc_xor(TG, hA0, hA1);                     /* T_G = H(A0) ^ H(A1) ^ pb D */
+            if (pb) gc_xor(TG, TG, D);
+            memcpy(WG, hA0, 16);                      /* W_G0 = H(A0) ^ pa T_G */
+            if (pa) gc_xor(WG, WG, TG);
+            gc_xor(TE, hB0, hB1);                     /* T_E = H(B0) ^ H(B1) ^ A0 */
+            gc_xor(TE, TE, acc);
+            memcpy(WE, hB0, 16);                      /* W_E0 = H(B0) ^ pb (T_E ^ A0) */
+            if (pb) {
+                uint8_t te_a[16];
+                gc_xor(te_a, TE, acc);
+                gc_xor(WE, WE, te_a);
+            }
+            uint8_t* tb = tables + ((uint64_t)t * (bits - 1) + (k - 1)) * 32;
+            memcpy(tb, TG, 16);
+            memcpy(tb + 16, TE, 16);
+            gc_xor(acc, WG, WE);
+        }
+        decode[t] = (uint8_t)((acc[0] ^ L[bits][0]) & 1);   /* colour of out's zero label */
+    }
+}
+
+/* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */
+void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* gb_labels,
+                    const uint8_t* ev_labels, const uint8_t* decode, uint64_t gate_base, uint8_t* out) {
+    oracle_init();
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t acc[16];
+        gc_xor(acc, gb_labels + (uint64_t)t * (bits + 1) * 16, ev_labels + (uint64_t)t * bits * 16);
+        for (uint32_t k = 1; k < bits; k++) {
+            uint8_t b[16], hA[16], hB[16];
+            gc_xor(b, gb_labels + ((uint64_t)t * (bits + 1) + k) * 16, ev_labels + ((uint64_t)t * bits + k) * 16);
+            const int sa = acc[0] & 1, sb = b[0] & 1;
+            const uint64_t j = 2 * (gate_base + (uint64_t)t * (bits - 1) + (k - 1));
+            const uint8_t* tb = tables + ((uint64_t)t * (bits - 1) + (k - 1)) * 32;
+            gc_tccr(acc, j, hA);
+            gc_tccr(b, j + 1, hB);
+            if (sa) gc_xor(hA, hA, tb);                /* W_G = H(A) ^ sa T_G */
+            if (sb) {                                  /* W_E = H(B) ^ sb (T_E ^ A) */
+                uint8_t te_a[16];
+                gc_xor(te_a, tb + 16, acc);
+                gc_xor(hB, hB, te_a);
+            }
+            gc_xor(acc, hA, hB);
+        }
+        const uint8_t* m = gb_labels + ((uint64_t)t * (bits + 1) + bits) * 16;
+        out[t] = (uint8_t)(((acc[0] ^ m[0]) & 1) ^ decode[t]);
+    }
+}

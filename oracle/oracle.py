@@ -541,3 +541,38 @@ def sketch_verify_fe(seeds, x0, kx0, x1, kx1, mac, mac2, triples, nthreads: int 
     lib().orc_sketch_verify_fe_batch(ctypes.c_uint64(n), ctypes.c_uint32(F), _p(np.ascontiguousarray(seeds, np.uint8)),
                                      *[_p(v, u64p) for v in a], _p(ok), _p(outs, u64p), ctypes.c_int(nthreads))
     return ok.astype(bool), outs
+
+
+# --------------------------------------------------------------------------------------
+# Row f1: garbled-circuit equality test (equalitytest.rs:25-219), see fhh_oracle.c
+# --------------------------------------------------------------------------------------
+def gc_garble_eq(gb_bits: np.ndarray, ev_bits: np.ndarray, mask: int, key: bytes, delta: bytes,
+                 label_nonce: int = 0, gate_base: int = 0):
+    """Garbler for n tests of `bits` bits (gb_bits / ev_bits [n][bits] 0/1). Returns
+    (tables [n][bits-1][2][16], gb_labels [n][bits+1][16], ev_labels [n][bits][16], decode [n])."""
+    g = np.ascontiguousarray(gb_bits, np.uint8)
+    e = np.ascontiguousarray(ev_bits, np.uint8)
+    n, bits = g.shape
+    tables = np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8)
+    gbl = np.zeros((n, bits + 1, 16), np.uint8)
+    evl = np.zeros((n, bits, 16), np.uint8)
+    dec = np.zeros(n, np.uint8)
+    k = np.frombuffer(key, np.uint8).copy()
+    d = np.frombuffer(delta, np.uint8).copy()
+    lib().orc_gc_garble_eq(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(e), ctypes.c_uint32(mask & 1), _p(k),
+                           _p(d), ctypes.c_uint64(label_nonce), ctypes.c_uint64(gate_base), _p(tables), _p(gbl),
+                           _p(evl), _p(dec))
+    return tables, gbl, evl, dec
+
+
+def gc_eval_eq(tables, gb_labels, ev_labels, decode, gate_base: int = 0) -> np.ndarray:
+    """Evaluator: out [n] = eq ^ mask."""
+    t = np.ascontiguousarray(tables, np.uint8)
+    g = np.ascontiguousarray(gb_labels, np.uint8)
+    e = np.ascontiguousarray(ev_labels, np.uint8)
+    d = np.ascontiguousarray(decode, np.uint8)
+    n, bits = e.shape[0], e.shape[1]
+    out = np.zeros(n, np.uint8)
+    lib().orc_gc_eval_eq(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(t), _p(g), _p(e), _p(d),
+                         ctypes.c_uint64(gate_base), _p(out))
+    return out

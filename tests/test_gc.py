@@ -1,0 +1,173 @@
+"""Row f1: the garbled-circuit equality test (equalitytest.rs:25-219).
+
+swanky (`fancy-garbling` @553ede0) is not vendored, so the wire format is parity-unpinned; the
+oracle restates the published half-gates + TCCR scheme (fhh_oracle.c) and is pinned by the
+reference's own functional test `eq_gc` (equalitytest.rs:222-266: masks[i] ^ results[i] ==
+(gb_value[i] == ev_value[i])) and by garbling's defining properties; the HIP path is then
+checked bit-exact against the oracle (tables, labels, decoding bits, outputs) and, inside the
+level loop, against the plaintext-equality crawl."""
+import numpy as np
+import pytest
+
+# equalitytest.rs:224-225
+GB_VALUE = [[0, 1, 1, 0], [0, 0, 0, 0], [1, 1, 1, 0]]
+EV_VALUE = [[0, 1, 1, 0], [0, 0, 0, 0], [1, 1, 1, 0]]
+KEY = bytes(range(16))
+DELTA = bytes(range(100, 116))
+
+
+def _cases(rng, n, bits, p_equal=0.5):
+    g = rng.integers(0, 2, (n, bits), dtype=np.uint8)
+    e = g.copy()
+    flip = rng.random(n) >= p_equal
+    if bits:
+        e[flip, rng.integers(0, bits, int(flip.sum()))] ^= 1
+    return g, e
+
+
+def test_oracle_eq_gc_reference_vectors(oracle):
+    g = np.array(GB_VALUE, np.uint8)
+    e = np.array(EV_VALUE, np.uint8)
+    expected = (g == e).all(axis=1)
+    for mask in (0, 1):
+        tables, gbl, evl, dec = oracle.gc_garble_eq(g, e, mask, KEY, DELTA)
+        results = oracle.gc_eval_eq(tables, gbl, evl, dec)
+        masks = np.full(len(results), mask, np.uint8)
+        assert np.array_equal((masks ^ results).astype(bool), expected)
+    # and with the evaluator's strings changed, the unequal tests come out unequal
+    e2 = e.copy()
+    e2[0, 3] ^= 1
+    e2[2, 0] ^= 1
+    t, gl, el, d = oracle.gc_garble_eq(g, e2, 1, KEY, DELTA)
+    assert np.array_equal((oracle.gc_eval_eq(t, gl, el, d) ^ 1).astype(bool), [False, True, False])
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3, 4, 6, 8])
+def test_oracle_functional_random(oracle, bits):
+    rng = np.random.default_rng(bits)
+    g, e = _cases(rng, 700, bits)
+    for mask in (0, 1):
+        t, gl, el, d = oracle.gc_garble_eq(g, e, mask, KEY, DELTA, label_nonce=5, gate_base=9)
+        out = oracle.gc_eval_eq(t, gl, el, d, gate_base=9)
+        assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))
+
+
+def test_oracle_garbling_is_input_independent(oracle):
+    """The garbled tables and decoding bits depend on the key / Delta / tweaks only, never on
+    the inputs (what lets the garbler send them before OT), and the active labels differ from
+    the zero labels by exactly Delta (with its colour bit forced to 1) on the set bits."""
+    rng = np.random.default_rng(3)
+    g, e = _cases(rng, 200, 4)
+    t0, gl0, el0, d0 = oracle.gc_garble_eq(np.zeros_like(g), np.zeros_like(e), 0, KEY, DELTA)
+    t1, gl1, el1, d1 = oracle.gc_garble_eq(g, e, 1, KEY, DELTA)
+    assert np.array_equal(t0, t1) and np.array_equal(d0, d1)
+    D = np.frombuffer(DELTA, np.uint8).copy()
+    D[0] |= 1
+    assert np.array_equal(gl0[:, :4] ^ gl1[:, :4], g[:, :, None] * D)
+    assert np.array_equal(el0 ^ el1, e[:, :, None] * D)
+    assert np.array_equal(gl0[:, 4] ^ gl1[:, 4], np.broadcast_to(D, (200, 16)))   # mask wire, mask = 1
+    # a wrong evaluator label (the other wire value) flips the result of a single-gate test
+    tests = np.array([[0, 0], [1, 1]], np.uint8)
+    t, gl, el, d = oracle.gc_garble_eq(tests, tests, 0, KEY, DELTA)
+    assert oracle.gc_eval_eq(t, gl, el, d).tolist() == [1, 1]
+    el_bad = el.copy()
+    el_bad[:, 1] ^= D
+    assert oracle.gc_eval_eq(t, gl, el_bad, d).tolist() == [0, 0]
+
+
+# ---- HIP path -------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bits", [(1, 1), (3, 4), (63, 2), (64, 2), (65, 3), (1000, 2), (4097, 8), (20000, 4)])
+def test_gpu_gc_bit_exact(oracle, n, bits):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    rng = np.random.default_rng(n * 10 + bits)
+    g, e = _cases(rng, n, bits)
+    kc = fhh.KeyCollection(8, 1)
+    for mask in (0, 1):
+        out, tr = gc.equality_test(kc, g, e, mask, KEY, DELTA, label_nonce=123, gate_base=77, transcript=True)
+        t, gl, el, d = oracle.gc_garble_eq(g, e, mask, KEY, DELTA, label_nonce=123, gate_base=77)
+        assert np.array_equal(tr.tables, t)
+        assert np.array_equal(tr.gb_labels, gl)
+        assert np.array_equal(tr.ev_labels, el)
+        assert np.array_equal(tr.decode, d)
+        assert np.array_equal(out, oracle.gc_eval_eq(t, gl, el, d, gate_base=77))
+        assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))
+
+
+@pytest.mark.gpu
+def test_gpu_eq_gc_reference_vectors():
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    kc = fhh.KeyCollection(8, 1)
+    expected = [a == b for a, b in zip(GB_VALUE, EV_VALUE)]
+    for seed in range(4):
+        masks, results = gc.multiple_equality_test(kc, GB_VALUE, EV_VALUE, seed=seed)
+        assert len(set(masks)) == 1   # one mask per call (equalitytest.rs:38-43)
+        assert [m ^ r for m, r in zip(masks, results)] == expected
+
+
+@pytest.mark.gpu
+def test_gpu_gc_device_groups(oracle):
+    """Device-resident batch, G groups x N clients (N not a multiple of 64), planes input."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    rng = np.random.default_rng(11)
+    G, N, bits = 5, 1000, 2
+    g = rng.integers(0, 2, (G, N, bits), dtype=np.uint8)
+    e = g.copy()
+    flip = rng.random((G, N)) < 0.3
+    e[flip, 0] ^= 1
+    kc = fhh.KeyCollection(8, 1)
+    b = gc.DeviceGcBatch(gc.planes_from_bits(g), gc.planes_from_bits(e), N, 1, KEY, DELTA, label_nonce=3,
+                         gate_base=4)
+    gc.equality_device(kc, b)
+    out = b.out.cpu().numpy()
+    t, gl, el, d = oracle.gc_garble_eq(g.reshape(G * N, bits), e.reshape(G * N, bits), 1, KEY, DELTA,
+                                       label_nonce=3, gate_base=4)
+    assert np.array_equal(out, oracle.gc_eval_eq(t, gl, el, d, gate_base=4))
+    assert np.array_equal(out ^ 1, (g == e).all(axis=2).reshape(-1).astype(np.uint8))
+    # SoA tables on the device == the oracle's AoS ones
+    assert np.array_equal(b.tables.cpu().numpy().reshape(bits - 1, 2, G * N, 16).transpose(2, 0, 1, 3), t)
+
+
+def _pair(left, right, roots):
+    import fuzzyheavyhitters_amd as fhh
+    n, d, L = left.shape
+    c0, c1 = fhh.KeyCollection(L, d), fhh.KeyCollection(L, d)
+    fhh.gen_keys_pair(c0, c1, left, right, roots)
+    return c0, c1
+
+
+def _sig(res):
+    return (res.level_children.tolist(), res.level_kept.tolist(), [c.tolist() for c in res.counts],
+            [(r.path, r.value) for r in res.final])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
+def test_gpu_crawl_with_gc_equals_plain(kind):
+    """tree_crawl with the GC equality test (collect.rs:419-482) gives the same FE sums, keep
+    decisions and heavy hitters as the plaintext-equality harness, level by level."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    if kind == "zipf_d1":
+        wl = workload.zipf_workload(3000, 64, 1, num_sites=40, seed=5)
+        thr = 0.01
+    else:
+        wl = workload.coords_workload(1500, ball_size=3, num_centroids=40, side_km=4.0)
+        thr = 0.01
+    c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    plain = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9)
+    with_gc = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9, gc=True, init_capacity=2)
+    assert _sig(with_gc) == _sig(plain)
+    assert len(with_gc.final) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_crawl_gc_rejects_count_mode():
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(200, 40, 1, num_sites=10, seed=1)
+    c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    with pytest.raises(fhh.FhhError):
+        sim_crawl(c0, c1, 0.01, mode="count", gc=True)

@@ -1184,14 +1184,18 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                                hipMemcpyHostToDevice, c0->stream));
     HIP_TRY(c0, launch_gather_hist(B.sizes.as<uint32_t>(), 4 + kMaxDims, B.hist_rows.as<const uint32_t*>(), levels,
                                    B.hist_packed.as<uint32_t>(), hist_cap, c0->stream));
+    // (the engine stream is non-blocking: plain hipMemcpy would not wait for k_gather_hist)
     std::vector<uint32_t> sz((size_t)levels * (4 + kMaxDims));
-    HIP_TRY(c0, hipMemcpy(sz.data(), B.sizes.p, sz.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c0, hipMemcpyAsync(sz.data(), B.sizes.p, sz.size() * 4, hipMemcpyDeviceToHost, c0->stream));
+    HIP_TRY(c0, hipStreamSynchronize(c0->stream));
     uint64_t hist_total = 0;
     for (uint32_t lv = 0; lv < levels; lv++) hist_total += sz[(size_t)lv * (4 + kMaxDims) + 1];
     if (hist_total > hist_cap) return c0->fail(FHH_E_STATE, "loop: kept-children lists exceed their capacity");
     std::vector<uint32_t> packed(hist_total);
-    if (hist_total)
-        HIP_TRY(c0, hipMemcpy(packed.data(), B.hist_packed.p, hist_total * 4, hipMemcpyDeviceToHost));
+    if (hist_total) {
+        HIP_TRY(c0, hipMemcpyAsync(packed.data(), B.hist_packed.p, hist_total * 4, hipMemcpyDeviceToHost, c0->stream));
+        HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+    }
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist(levels);
     const uint32_t mask = (1u << d) - 1;
     for (uint32_t lv = 0, off = 0; lv < levels; lv++) {

@@ -38,7 +38,7 @@ EXPORTS = [
     "fhh_comm_last_error",
     "fhh_sketch_at_fe", "fhh_mul_cor_share_fe", "fhh_mul_cor_fe", "fhh_mul_out_share_fe", "fhh_mul_verify_fe",
     "fhh_sim_sketch_verify_fe",
-    "fhh_gc_equality_device", "fhh_gc_equality_host",
+    "fhh_gc_equality_device", "fhh_gc_equality_host", "fhh_ot_extend_device", "fhh_ot_extend_host",
 ]
 
 
@@ -77,7 +77,7 @@ class FhhSimConfig(ctypes.Structure):
     ]
 
 
-SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_loop.hip",
+SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_ot.hip", "fhh_loop.hip",
            "fhh_microbench.hip", "fhh_host.cpp", "fhh_comm.cpp")
 
 
@@ -116,6 +116,20 @@ class FhhGcBatch(ctypes.Structure):
         ("ev_labels_dev", ctypes.c_void_p),
         ("decode_dev", ctypes.c_void_p),
         ("out_dev", ctypes.c_void_p),
+    ]
+
+
+class FhhOtBatch(ctypes.Structure):
+    _fields_ = [
+        ("m", ctypes.c_uint64),
+        ("choices_dev", ctypes.c_void_p),
+        ("x0_dev", ctypes.c_void_p),
+        ("x1_dev", ctypes.c_void_p),
+        ("delta", ctypes.c_uint8 * 16),
+        ("out_dev", ctypes.c_void_p),
+        ("base_seeds", ctypes.c_uint8 * (128 * 2 * 16)),
+        ("base_choice", ctypes.c_uint8 * 16),
+        ("tweak_base", ctypes.c_uint64),
     ]
 
 
@@ -218,6 +232,8 @@ def lib():
         "fhh_mul_verify_fe": (i, [u64, u64p, u64p, u8p]),
         "fhh_sim_sketch_verify_fe": (i, [vp, P(FhhSketchBatch)]),
         "fhh_gc_equality_device": (i, [vp, P(FhhGcBatch)]),
+        "fhh_ot_extend_device": (i, [vp, P(FhhOtBatch)]),
+        "fhh_ot_extend_host": (i, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
         "fhh_gc_equality_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u64, u8p, u8p, u8p, u8p, u8p]),
     }
     for name, (res, args) in sig.items():

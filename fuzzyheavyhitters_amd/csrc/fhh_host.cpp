@@ -143,6 +143,8 @@ struct fhh_ctx {
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> last_hist;
 
     DevBuf scratch, scratch2;
+    DevBuf ot_buf[8], ot_rk;                     // OT extension scratch (T U Q Tt Qt Y0 Y1 choices)
+    std::vector<uint32_t> ot_rk_host;            // key schedules staged for ot_rk
     std::vector<PinnedBuf*> stage;   // pinned staging for async H2D, recycled at every sync
     size_t stage_used = 0;
 
@@ -811,6 +813,86 @@ int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
     a.decode = b->decode_dev;
     a.out = b->out_dev;
     a.ctl = nullptr;
+    return FHH_OK;
+}
+}  // namespace
+
+// ---- OT extension runner (row f1's OT) --------------------------------------------------------
+namespace {
+uint64_t ot_padded(uint64_t m) { return (m + 8191) / 8192 * 8192; }
+
+// padded choice-bit buffer of the ctx's OT scratch (mp / 32 words, zero past m)
+hipError_t ot_choices_buffer(fhh_ctx* ctx, uint64_t m, uint32_t** out) {
+    const uint64_t mp = ot_padded(m);
+    hipError_t e = ctx->ot_buf[7].ensure(mp / 8);
+    if (e != hipSuccess) return e;
+    *out = ctx->ot_buf[7].as<uint32_t>();
+    return hipSuccess;
+}
+
+struct OtOut {            // optional transcript (device pointers into the scratch)
+    const uint4* U = nullptr;
+    const uint4* Y0 = nullptr;
+    const uint4* Y1 = nullptr;
+    uint64_t nblk = 0;
+};
+
+// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer. Base OTs ideal:
+// the sender gets the key schedules of seeds[i][s_i].
+int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
+           const uint8_t delta[16], uint4* out, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16],
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr) {
+    if (m == 0) return FHH_OK;
+    const uint64_t mp = ot_padded(m);
+    const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
+    for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
+    for (int k = 3; k < 5; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(mp * 16));
+    for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
+    ctx->ot_rk_host.assign((size_t)3 * 128 * 44, 0);
+    for (int i = 0; i < 128; i++) {
+        const int si = (s[i / 8] >> (i % 8)) & 1;
+        uint32_t rk[11][4];
+        for (int b = 0; b < 3; b++) {
+            const uint8_t* key = seeds + (size_t)(i * 2 + (b < 2 ? b : si)) * 16;
+            host_key_schedule(key, rk);
+            std::memcpy(ctx->ot_rk_host.data() + ((size_t)b * 128 + i) * 44, rk, 44 * 4);
+        }
+    }
+    HIP_TRY(ctx, ctx->ot_rk.ensure(ctx->ot_rk_host.size() * 4));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->ot_rk.p, ctx->ot_rk_host.data(), ctx->ot_rk_host.size() * 4,
+                                hipMemcpyHostToDevice, ctx->stream));
+    OtArgs a{};
+    a.m = m;
+    a.mp = mp;
+    a.rk = ctx->ot_rk.as<uint32_t>();
+    words_from_bytes(s, a.s);
+    a.choices = choices;
+    a.T = ctx->ot_buf[0].as<uint4>();
+    a.U = ctx->ot_buf[1].as<uint4>();
+    a.Q = ctx->ot_buf[2].as<uint4>();
+    a.Tt = ctx->ot_buf[3].as<uint4>();
+    a.Qt = ctx->ot_buf[4].as<uint4>();
+    a.x0 = x0;
+    a.x1 = x1;
+    if (delta) words_from_bytes(delta, a.delta);
+    a.Y0 = ctx->ot_buf[5].as<uint4>();
+    a.Y1 = ctx->ot_buf[6].as<uint4>();
+    a.out = out;
+    a.tweak_base = tweak_base;
+    a.ctl = ctl;
+    a.per_group = per_group;
+    HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
+    HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
+    HIP_TRY(ctx, launch_ot_transpose(a.Q, a.Qt, a, ctx->stream));
+    HIP_TRY(ctx, launch_ot_send_hash(a, ctx->stream));       // sender -> receiver: Y0, Y1
+    HIP_TRY(ctx, launch_ot_transpose(a.T, a.Tt, a, ctx->stream));
+    HIP_TRY(ctx, launch_ot_recv_hash(a, ctx->stream));
+    if (tr) {
+        tr->U = a.U;
+        tr->Y0 = a.Y0;
+        tr->Y1 = a.Y1;
+        tr->nblk = mp / 128;
+    }
     return FHH_OK;
 }
 }  // namespace
@@ -2195,4 +2277,71 @@ int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t*
     rc = soa_to_aos(dg, bits + 1, gb_labels);
     if (rc) return rc;
     return soa_to_aos(de, bits, ev_labels);
+}
+
+// ---- OT extension (row f1's OT) ---------------------------------------------------------------
+int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!b) return ctx->fail(FHH_E_ARG, "ot_extend: NULL batch");
+    if (b->m == 0) return FHH_OK;
+    if (!b->choices_dev || !b->x0_dev || !b->out_dev) return ctx->fail(FHH_E_ARG, "ot_extend: NULL device buffer");
+    uint32_t* ch = nullptr;
+    HIP_TRY(ctx, ot_choices_buffer(ctx, b->m, &ch));
+    const uint64_t mp = ot_padded(b->m), words = (b->m + 31) / 32;
+    HIP_TRY(ctx, hipMemsetAsync(ch, 0, mp / 8, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ch, b->choices_dev, words * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    if (b->m % 32) {   // clear the bits past m in the last word
+        std::vector<uint32_t> last(1);
+        HIP_TRY(ctx, hipMemcpyAsync(last.data(), ch + words - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        last[0] &= (1u << (b->m % 32)) - 1;
+        HIP_TRY(ctx, hipMemcpy(ch + words - 1, last.data(), 4, hipMemcpyHostToDevice));
+    }
+    rc = ot_run(ctx, b->m, ch, reinterpret_cast<const uint4*>(b->x0_dev), reinterpret_cast<const uint4*>(b->x1_dev),
+                b->x1_dev ? nullptr : b->delta, reinterpret_cast<uint4*>(b->out_dev), &b->base_seeds[0][0][0],
+                b->base_choice, b->tweak_base, nullptr, 0, nullptr);
+    if (rc) return rc;
+    return sync(ctx);
+}
+
+int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1,
+                       const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                       uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (m == 0) return FHH_OK;
+    if (!choices || !x0 || !out || !base_seeds || !base_choice || (!x1 && !delta))
+        return ctx->fail(FHH_E_ARG, "ot_extend: NULL argument");
+    const uint64_t mp = ot_padded(m);
+    std::vector<uint32_t> bits(mp / 32, 0);
+    for (uint64_t j = 0; j < m; j++)
+        if (choices[j] & 1) bits[j / 32] |= 1u << (j % 32);
+    uint32_t* ch = nullptr;
+    HIP_TRY(ctx, ot_choices_buffer(ctx, m, &ch));
+    HIP_TRY(ctx, hipMemcpyAsync(ch, bits.data(), mp / 8, hipMemcpyHostToDevice, ctx->stream));
+    DevBuf d0, d1, dout;
+    HIP_TRY(ctx, d0.ensure(m * 16));
+    HIP_TRY(ctx, dout.ensure(m * 16));
+    HIP_TRY(ctx, hipMemcpyAsync(d0.p, x0, m * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (x1) {
+        HIP_TRY(ctx, d1.ensure(m * 16));
+        HIP_TRY(ctx, hipMemcpyAsync(d1.p, x1, m * 16, hipMemcpyHostToDevice, ctx->stream));
+    }
+    OtOut tr;
+    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : delta, dout.as<uint4>(),
+                base_seeds, base_choice, tweak_base, nullptr, 0, &tr);
+    if (rc) return rc;
+    rc = sync(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, m * 16, hipMemcpyDeviceToHost));
+    if (y0_out) HIP_TRY(ctx, hipMemcpy(y0_out, tr.Y0, m * 16, hipMemcpyDeviceToHost));
+    if (y1_out) HIP_TRY(ctx, hipMemcpy(y1_out, tr.Y1, m * 16, hipMemcpyDeviceToHost));
+    if (u_out) {   // rows [128][ceil(m / 128)] of the padded [128][mp / 128] matrix
+        const uint64_t nb = (m + 127) / 128;
+        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
+    }
+    return FHH_OK;
 }

@@ -188,6 +188,30 @@ int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t
 // device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
 // entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
+// IKNP / ALSZ OT extension (row f1's OT): m OTs of 16-B messages; base OTs ideal (the sender's
+// key schedules are those of k_i^{s_i}). Bit matrices are [128 rows][mp / 128] uint4 blocks,
+// transposed to [mp] uint4 per-OT rows. With ctl set (level loop) only the first
+// per_group * min(groups, ctl->C) OTs run.
+struct OtArgs {
+    uint64_t m;                  // OTs (capacity)
+    uint64_t mp;                 // m padded to a multiple of 8192 (whole waves per row)
+    const uint32_t* rk;          // [3][128][44]: receiver k_i^0, k_i^1, sender k_i^{s_i}
+    uint32_t s[4];               // sender's base choice bits
+    const uint32_t* choices;     // [mp / 32] receiver's choice bits (0 past m)
+    uint4 *T, *U, *Q;            // [128][mp / 128]
+    uint4 *Tt, *Qt;              // [mp]
+    const uint4 *x0, *x1;        // [m]; x1 == nullptr: x1 = x0 ^ delta (correlated OT)
+    uint32_t delta[4];
+    uint4 *Y0, *Y1, *out;        // [m]
+    uint64_t tweak_base;
+    const LoopCtl* ctl;
+    uint64_t per_group;
+};
+hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,

@@ -1,0 +1,237 @@
+// OT extension on the GPU (the OT half): IKNP in the ALSZ form, the protocol
+// of `ocelot::ot::{AlszSender, AlszReceiver}` that the reference runs for the evaluator's input
+// labels (equalitytest.rs:67-82) and for the FE share conversion (collect.rs:437-471). ocelot is
+// not vendored; the published scheme is restated (oracle/fhh_oracle.c orc_ot_extend):
+//
+//   receiver (choice bits r):  t_i = G(k_i^0),  u_i = t_i ^ G(k_i^1) ^ r        i < 128
+//   sender   (base choice s):  q_i = G(k_i^{s_i}) ^ s_i u_i  =>  q_j = t_j ^ r_j s (columns)
+//   sender:    y_j^b = x_j^b ^ H(j, q_j ^ b s)        receiver:  x_j^{r_j} = y_j^{r_j} ^ H(j, t_j)
+//
+// G = AES-128-CTR under the row key (block c -> OTs 128 c .. 128 c + 127), H(j, x) = TCCR(x,
+// tweak_base + j) with pi = AES-128 under the zero key (as fhh_gc.hip). The 128 base OTs are
+// ideal (the host hands the sender k_i^{s_i}).
+//
+//   k_ot_recv_expand / k_ot_send_expand  one lane per (row, 128-OT block): 2 / 1 AES
+//   k_ot_transpose                        one lane per 32 OTs: 4 in-register 32x32 transposes
+//   k_ot_send_hash / k_ot_recv_hash       one lane per OT: 2 / 1 TCCR (4 / 2 AES)
+#include "fhh_internal.h"
+#include "aes_keyed.h"
+#include "bitslice.h"
+
+namespace fhh {
+
+__constant__ WordTable c_T0_ot = T0;
+using OtTab = Tab4T32<DevOpsX>;
+constexpr int kOtThreads = 1024;
+constexpr size_t kOtLds = (size_t)OtTab::kWords * 4;
+
+__device__ __forceinline__ void ot_fill(uint32_t* tbl) {
+    for (int i = threadIdx.x; i < OtTab::kWords; i += blockDim.x) tbl[i] = OtTab::word(c_T0_ot.v, i);
+    __syncthreads();
+}
+
+// OTs to run: m, or inside the level loop per_group * min(groups, ctl->C)
+__device__ __forceinline__ uint64_t ot_active(const OtArgs& a) {
+    if (!a.ctl) return a.m;
+    if (a.ctl->abort) return 0;
+    const uint64_t v = a.per_group * a.ctl->C;
+    return v < a.m ? v : a.m;
+}
+
+__device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4]) {
+#pragma unroll
+    for (int r = 0; r < 11; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) rk[r][c] = base[4 * r + c];
+}
+
+__device__ __forceinline__ void ot_zero_rk(uint32_t (&rk)[11][4]) {
+#pragma unroll
+    for (int r = 0; r < 11; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) rk[r][c] = ZERO_RK.w[r][c];
+}
+
+template <int NB>
+__device__ __forceinline__ void ot_tccr(uint32_t (&x)[NB][4], uint64_t tw, const uint32_t* tbl, uint32_t b0,
+                                        uint32_t b1, const uint32_t (&zrk)[11][4]) {
+    uint32_t p[NB][4], q[NB][4];
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) p[k][c] = x[k][c];
+    aes_rk<OtTab, NB>(p, tbl, b0, b1, zrk);
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        q[k][0] = p[k][0] ^ (uint32_t)tw;
+        q[k][1] = p[k][1] ^ (uint32_t)(tw >> 32);
+        q[k][2] = p[k][2];
+        q[k][3] = p[k][3];
+    }
+    aes_rk<OtTab, NB>(q, tbl, b0, b1, zrk);
+#pragma unroll
+    for (int k = 0; k < NB; k++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[k][c] = q[k][c] ^ p[k][c];
+}
+
+// one lane per (row i, block c); nblk = mp / 128 is a multiple of 64, so a wave's lanes share
+// the row and its key schedules are uniform (scalar loads)
+template <bool RECV>
+__global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
+    extern __shared__ uint32_t tbl_ot[];
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(threadIdx.x & 63, b0, b1);
+    const uint64_t nblk = a.mp / 128;
+    const uint64_t nblk_act = (ot_active(a) + 127) / 128;
+    const uint64_t total = 128 * nblk;
+    for (uint64_t base = (uint64_t)blockIdx.x * kOtThreads; base < total; base += (uint64_t)gridDim.x * kOtThreads) {
+        const uint64_t idx = base + threadIdx.x;
+        const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(idx / nblk));
+        const uint64_t c = idx - (uint64_t)i * nblk;
+        if (c >= nblk_act) continue;
+        uint32_t s[RECV ? 2 : 1][4];
+#pragma unroll
+        for (int k = 0; k < (RECV ? 2 : 1); k++) {
+            s[k][0] = (uint32_t)c;
+            s[k][1] = (uint32_t)(c >> 32);
+            s[k][2] = 0u;
+            s[k][3] = 0u;
+        }
+        if (RECV) {
+            uint32_t rk0[11][4], rk1[11][4];
+            ld_rk(a.rk + (size_t)i * 44, rk0);
+            ld_rk(a.rk + (size_t)(128 + i) * 44, rk1);
+            uint32_t g0[1][4] = {{s[0][0], s[0][1], s[0][2], s[0][3]}};
+            uint32_t g1[1][4] = {{s[0][0], s[0][1], s[0][2], s[0][3]}};
+            aes_rk<OtTab, 1>(g0, tbl_ot, b0, b1, rk0);
+            aes_rk<OtTab, 1>(g1, tbl_ot, b0, b1, rk1);
+            const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
+            a.T[(uint64_t)i * nblk + c] = make_uint4(g0[0][0], g0[0][1], g0[0][2], g0[0][3]);
+            a.U[(uint64_t)i * nblk + c] = make_uint4(g0[0][0] ^ g1[0][0] ^ r.x, g0[0][1] ^ g1[0][1] ^ r.y,
+                                                     g0[0][2] ^ g1[0][2] ^ r.z, g0[0][3] ^ g1[0][3] ^ r.w);
+        } else {
+            uint32_t rks[11][4];
+            ld_rk(a.rk + (size_t)(256 + i) * 44, rks);
+            aes_rk<OtTab, 1>(reinterpret_cast<uint32_t(&)[1][4]>(s), tbl_ot, b0, b1, rks);
+            const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (si) u = a.U[(uint64_t)i * nblk + c];
+            a.Q[(uint64_t)i * nblk + c] = make_uint4(s[0][0] ^ u.x, s[0][1] ^ u.y, s[0][2] ^ u.z, s[0][3] ^ u.w);
+        }
+    }
+}
+
+// rows [128][mp / 32] u32 -> cols [mp][4] u32: lane w owns OTs 32 w .. 32 w + 31
+__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint32_t* cols, OtArgs a) {
+    const uint64_t W = a.mp / 32;
+    const uint64_t W_act = (ot_active(a) + 31) / 32;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < W_act; w += (uint64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            uint32_t x[32];
+#pragma unroll
+            for (int r = 0; r < 32; r++) x[r] = rows[(uint64_t)(32 * g + r) * W + w];
+            transpose32(x);   // x[k] bit r = row 32 g + r of OT 32 w + k
+#pragma unroll
+            for (int k = 0; k < 32; k++) cols[(32 * w + k) * 4 + g] = x[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
+    extern __shared__ uint32_t tbl_ot[];
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(threadIdx.x & 63, b0, b1);
+    uint32_t zrk[11][4];
+    ot_zero_rk(zrk);
+    const uint64_t m = ot_active(a);
+    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
+        const uint4 q = a.Qt[j];
+        uint32_t h[2][4] = {{q.x, q.y, q.z, q.w}, {q.x ^ a.s[0], q.y ^ a.s[1], q.z ^ a.s[2], q.w ^ a.s[3]}};
+        ot_tccr<2>(h, a.tweak_base + j, tbl_ot, b0, b1, zrk);
+        const uint4 x0 = a.x0[j];
+        const uint4 x1 = a.x1 ? a.x1[j]
+                              : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+        a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
+        a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
+    }
+}
+
+__global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
+    extern __shared__ uint32_t tbl_ot[];
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(threadIdx.x & 63, b0, b1);
+    uint32_t zrk[11][4];
+    ot_zero_rk(zrk);
+    const uint64_t m = ot_active(a);
+    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
+        const uint4 t = a.Tt[j];
+        uint32_t h[1][4] = {{t.x, t.y, t.z, t.w}};
+        ot_tccr<1>(h, a.tweak_base + j, tbl_ot, b0, b1, zrk);
+        const uint32_t r = (a.choices[j >> 5] >> (j & 31)) & 1u;
+        const uint4 y = r ? a.Y1[j] : a.Y0[j];
+        a.out[j] = make_uint4(y.x ^ h[0][0], y.y ^ h[0][1], y.z ^ h[0][2], y.w ^ h[0][3]);
+    }
+}
+
+static hipError_t ot_set_lds(const void* fn, int* done) {
+    if (*done) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOtLds);
+    if (e == hipSuccess) *done = 1;
+    return e;
+}
+
+static int ot_grid(uint64_t items, int threads) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t need = (items + threads - 1) / threads;
+    const uint64_t cap = (uint64_t)cus * (threads >= 1024 ? 4 : 16);
+    return (int)(need < cap ? (need ? need : 1) : cap);
+}
+
+hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
+    static int done = 0;
+    hipError_t e = ot_set_lds((const void*)k_ot_expand<true>, &done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128), kOtThreads)), dim3(kOtThreads), kOtLds,
+                       stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
+    static int done = 0;
+    hipError_t e = ot_set_lds((const void*)k_ot_expand<false>, &done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128), kOtThreads)), dim3(kOtThreads), kOtLds,
+                       stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_ot_transpose, dim3(ot_grid(a.mp / 32, 256)), dim3(256), 0, stream,
+                       reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(cols), a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream) {
+    static int done = 0;
+    hipError_t e = ot_set_lds((const void*)k_ot_send_hash, &done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_ot_send_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), kOtLds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream) {
+    static int done = 0;
+    hipError_t e = ot_set_lds((const void*)k_ot_recv_hash, &done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_ot_recv_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), kOtLds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace fhh

@@ -1,0 +1,37 @@
+"""OT extension on the GPU (the OT of SURVEY §8 row f1): IKNP in the ALSZ form, mirroring
+`ocelot::ot::{AlszSender, AlszReceiver}` as the reference uses them (equalitytest.rs:67-82,
+collect.rs:437-471), backed by fhh_ot.hip. Both parties run in one process; the 128 base OTs
+are ideal. See include/fhh.h (fhh_ot_batch) for the exact construction."""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import check, lib, ptr
+
+
+def ot_extend(kc, choices, x0, x1=None, delta=None, base_seeds=None, base_choice=None, tweak_base: int = 0,
+              transcript: bool = False, seed: int = 0):
+    """m OTs: returns the receiver's messages out [m][16] with out[j] = (x1 if choices[j] else x0)[j]
+    (x1 None: correlated OT, x1 = x0 ^ delta). With transcript, also (U [128][ceil(m/128)][16],
+    Y0, Y1 [m][16]) — the two protocol messages."""
+    ch = np.ascontiguousarray(np.asarray(choices).astype(np.uint8) & 1)
+    m = ch.size
+    a0 = np.ascontiguousarray(x0, np.uint8).reshape(m, 16)
+    a1 = None if x1 is None else np.ascontiguousarray(x1, np.uint8).reshape(m, 16)
+    if a1 is None and delta is None:
+        raise ValueError("ot_extend: x1 or delta required")
+    rng = np.random.default_rng(seed)
+    seeds = (rng.integers(0, 256, (128, 2, 16), dtype=np.uint8) if base_seeds is None
+             else np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16))
+    s = (rng.integers(0, 256, 16, dtype=np.uint8) if base_choice is None
+         else np.frombuffer(bytes(base_choice), np.uint8).copy())
+    d = np.frombuffer(bytes(delta), np.uint8).copy() if delta is not None else np.zeros(16, np.uint8)
+    out = np.zeros((m, 16), np.uint8)
+    nb = (m + 127) // 128
+    u = np.zeros((128, nb, 16), np.uint8) if transcript else None
+    y0 = np.zeros((m, 16), np.uint8) if transcript else None
+    y1 = np.zeros((m, 16), np.uint8) if transcript else None
+    check(lib().fhh_ot_extend_host(kc.handle, m, ptr(ch), ptr(a0), ptr(a1) if a1 is not None else None, ptr(d),
+                                   ptr(seeds), ptr(s), tweak_base, ptr(out), ptr(u) if transcript else None,
+                                   ptr(y0) if transcript else None, ptr(y1) if transcript else None), kc.handle)
+    return (out, u, y0, y1) if transcript else out

@@ -312,6 +312,32 @@ int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t*
                          uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
                          uint8_t* decode, uint8_t* out);
 
+/* ---- OT extension (the OT of row f1) -------------------------------------------------------
+ * IKNP OT extension in the ALSZ form, the protocol of ocelot's AlszSender / AlszReceiver that
+ * the reference runs for the evaluator's input labels (equalitytest.rs:67-82) and the FE share
+ * conversion (collect.rs:437-471): m 1-out-of-2 OTs of 16-B messages; the receiver gets
+ * x_j^{choice_j}. kappa = 128 base OTs are ideal (the receiver's seed pairs base_seeds[i][0..1],
+ * the sender's choice bits base_choice; the sender is handed base_seeds[i][s_i]). G = AES-128-CTR
+ * under each seed (block c = LE128(c) gives OTs 128 c .. 128 c + 127, bit b of byte b / 8),
+ * H(j, x) = TCCR(x, tweak_base + j) as in the GC. x1 == NULL: correlated OT, x1 = x0 ^ delta. */
+typedef struct fhh_ot_batch {
+    uint64_t m;
+    const uint32_t* choices_dev;    /* receiver's choice bits, bit j % 32 of word j / 32       */
+    const uint8_t* x0_dev;          /* sender's messages [m][16] for choice 0                  */
+    const uint8_t* x1_dev;          /* [m][16] for choice 1, or NULL (x0 ^ delta)              */
+    uint8_t delta[16];
+    uint8_t* out_dev;               /* receiver's messages [m][16]                             */
+    uint8_t base_seeds[128][2][16];
+    uint8_t base_choice[16];
+    uint64_t tweak_base;
+} fhh_ot_batch;
+int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* batch);
+/* Host buffers: choices [m] 0/1 bytes; optional transcript u_out [128][ceil(m/128)][16] (the
+ * receiver's message to the sender), y0_out / y1_out [m][16] (the sender's reply). */
+int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1,
+                       const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                       uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out);
+
 /* ---- statistics ------------------------------------------------------------------------ */
 
 typedef struct fhh_stats {

@@ -753,3 +753,87 @@ void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint
         out[t] = (uint8_t)(((acc[0] ^ m[0]) & 1) ^ decode[t]);
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* Row f1's OT: IKNP OT extension in the ALSZ form (u_i = G(k_i^0) ^  */
+/* G(k_i^1) ^ r), as `ocelot::ot::Alsz{Sender,Receiver}` (@553ede0,   */
+/* not vendored) used at equalitytest.rs:67-82 (evaluator labels) and */
+/* collect.rs:437-471 (FE shares). Published scheme restated: kappa = */
+/* 128 base OTs (ideal here: the sender is handed k_i^{s_i}), G =     */
+/* AES-128-CTR under k (block c = LE128(c) gives OT bits 128c..+127),  */
+/* H(j, x) = TCCR(x, tweak_base + j) as the GC hash. Parity:          */
+/* functional (out_j = x_j^{r_j}); wire format unpinned.              */
+/* ------------------------------------------------------------------ */
+static void ot_prg_block(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
+    uint8_t ctr[16] = {0};
+    for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
+    aes128_encrypt_rk(rk, ctr, out);
+}
+
+/* choices: m bits (bit j of byte j/8); x1 NULL -> x1 = x0 ^ delta. Optional transcript:
+ * u_out [128][nblk][16] (nblk = ceil(m / 128)), y0_out / y1_out [m][16]. */
+void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1, const uint8_t delta[16],
+                   const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t tweak_base, uint8_t* out,
+                   uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out) {
+    oracle_init();
+    const uint64_t nblk = (m + 127) / 128;
+    uint8_t* T = (uint8_t*)calloc(128 * nblk * 16, 1);
+    uint8_t* Q = (uint8_t*)calloc(128 * nblk * 16, 1);
+    uint8_t* U = (uint8_t*)calloc(128 * nblk * 16, 1);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < 128; i++) {
+        uint8_t rk0[176], rk1[176], rks[176];
+        key_expand(seeds + (i * 2 + 0) * 16, rk0);
+        key_expand(seeds + (i * 2 + 1) * 16, rk1);
+        const int si = (s[i / 8] >> (i % 8)) & 1;
+        key_expand(seeds + (i * 2 + si) * 16, rks);   /* ideal base OT: the sender holds k_i^{s_i} */
+        for (uint64_t c = 0; c < nblk; c++) {
+            uint8_t g0[16], g1[16], gs[16];
+            ot_prg_block(rk0, c, g0);
+            ot_prg_block(rk1, c, g1);
+            uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
+            uint8_t* u = U + ((uint64_t)i * nblk + c) * 16;
+            for (int k = 0; k < 16; k++) {
+                uint8_t r = 0;
+                for (int b = 0; b < 8; b++) {
+                    const uint64_t j = c * 128 + (uint64_t)k * 8 + b;
+                    if (j < m && ((choices[j / 8] >> (j % 8)) & 1)) r |= (uint8_t)(1u << b);
+                }
+                t[k] = g0[k];
+                u[k] = g0[k] ^ g1[k] ^ r;                 /* receiver -> sender */
+            }
+            ot_prg_block(rks, c, gs);                     /* sender: q_i = G(k_i^{s_i}) ^ s_i u_i */
+            uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
+            for (int k = 0; k < 16; k++) q[k] = gs[k] ^ (si ? u[k] : 0);
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < (int64_t)m; j++) {
+        uint8_t qj[16] = {0}, tj[16] = {0}, qs[16], h0[16], h1[16], ht[16], y0[16], y1[16];
+        const uint64_t c = (uint64_t)j / 128, bit = (uint64_t)j % 128;
+        for (int i = 0; i < 128; i++) {                   /* column j of Q and T */
+            const uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
+            const uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
+            if ((q[bit / 8] >> (bit % 8)) & 1) qj[i / 8] |= (uint8_t)(1u << (i % 8));
+            if ((t[bit / 8] >> (bit % 8)) & 1) tj[i / 8] |= (uint8_t)(1u << (i % 8));
+        }
+        for (int k = 0; k < 16; k++) qs[k] = qj[k] ^ s[k];
+        gc_tccr(qj, tweak_base + (uint64_t)j, h0);
+        gc_tccr(qs, tweak_base + (uint64_t)j, h1);
+        for (int k = 0; k < 16; k++) {
+            const uint8_t a = x0[j * 16 + k];
+            const uint8_t b = x1 ? x1[j * 16 + k] : (uint8_t)(a ^ delta[k]);
+            y0[k] = a ^ h0[k];                            /* sender -> receiver */
+            y1[k] = b ^ h1[k];
+        }
+        if (y0_out) memcpy(y0_out + j * 16, y0, 16);
+        if (y1_out) memcpy(y1_out + j * 16, y1, 16);
+        const int rj = (choices[j / 8] >> (j % 8)) & 1;
+        gc_tccr(tj, tweak_base + (uint64_t)j, ht);
+        for (int k = 0; k < 16; k++) out[j * 16 + k] = (rj ? y1[k] : y0[k]) ^ ht[k];
+    }
+    if (u_out) memcpy(u_out, U, 128 * nblk * 16);
+    free(T);
+    free(Q);
+    free(U);
+}

@@ -576,3 +576,27 @@ def gc_eval_eq(tables, gb_labels, ev_labels, decode, gate_base: int = 0) -> np.n
     lib().orc_gc_eval_eq(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(t), _p(g), _p(e), _p(d),
                          ctypes.c_uint64(gate_base), _p(out))
     return out
+
+
+def ot_extend(choices: np.ndarray, x0: np.ndarray, x1, delta: bytes, seeds: np.ndarray, s: bytes,
+              tweak_base: int = 0, transcript: bool = False):
+    """IKNP/ALSZ OT extension (see fhh_oracle.c): choices [m] 0/1, x0 / x1 [m][16] (x1 None:
+    x1 = x0 ^ delta), seeds [128][2][16], s 16 bytes. Returns out [m][16] (and U [128][nblk][16],
+    Y0, Y1 [m][16] if transcript)."""
+    ch = np.packbits(np.asarray(choices, np.uint8) & 1, bitorder="little")
+    m = len(choices)
+    a0 = np.ascontiguousarray(x0, np.uint8)
+    a1 = None if x1 is None else np.ascontiguousarray(x1, np.uint8)
+    sd = np.ascontiguousarray(seeds, np.uint8)
+    dl = np.frombuffer(delta if delta is not None else bytes(16), np.uint8).copy()
+    sv = np.frombuffer(s, np.uint8).copy()
+    out = np.zeros((m, 16), np.uint8)
+    nblk = (m + 127) // 128
+    u = np.zeros((128, nblk, 16), np.uint8) if transcript else None
+    y0 = np.zeros((m, 16), np.uint8) if transcript else None
+    y1 = np.zeros((m, 16), np.uint8) if transcript else None
+    lib().orc_ot_extend(ctypes.c_uint64(m), _p(np.ascontiguousarray(ch)), _p(a0), None if a1 is None else _p(a1),
+                        _p(dl), _p(sd), _p(sv), ctypes.c_uint64(tweak_base), _p(out),
+                        None if u is None else _p(u), None if y0 is None else _p(y0),
+                        None if y1 is None else _p(y1))
+    return (out, u, y0, y1) if transcript else out

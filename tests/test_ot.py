@@ -1,0 +1,62 @@
+"""The OT of row f1: IKNP/ALSZ OT extension (ocelot's AlszSender/AlszReceiver at
+equalitytest.rs:67-82 and collect.rs:437-471; ocelot is not vendored, so the wire format is
+parity-unpinned). The oracle restatement is pinned by the OT functionality (the receiver gets
+exactly x^{choice}, for explicit and correlated messages) and by the protocol's algebra (the
+sender's rows satisfy q_j = t_j ^ r_j s, checked through the transcript); the HIP path is then
+bit-exact against the oracle on the output and both protocol messages (U, Y0, Y1)."""
+import numpy as np
+import pytest
+
+
+def _inputs(m, seed):
+    rng = np.random.default_rng(seed)
+    ch = rng.integers(0, 2, m, dtype=np.uint8)
+    x0 = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    x1 = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    delta = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    return ch, x0, x1, seeds, s, delta
+
+
+@pytest.mark.parametrize("m", [1, 127, 128, 129, 1000, 4099])
+def test_oracle_ot_functionality(oracle, m):
+    ch, x0, x1, seeds, s, delta = _inputs(m, m)
+    out = oracle.ot_extend(ch, x0, x1, None, seeds, s, tweak_base=3)
+    assert np.array_equal(out, np.where(ch[:, None] == 1, x1, x0))
+    out = oracle.ot_extend(ch, x0, None, delta, seeds, s, tweak_base=3)
+    assert np.array_equal(out, np.where(ch[:, None] == 1, x0 ^ np.frombuffer(delta, np.uint8), x0))
+
+
+def test_oracle_ot_transcript_hides_the_unchosen_message(oracle):
+    """Y_{1-r} is x_{1-r} masked by H(j, t_j ^ s): a receiver that tries H(j, t_j) on the other
+    reply gets garbage, not the other message; and flipping one base choice bit changes U only
+    through the sender's side (U is the receiver's message and does not depend on s)."""
+    m = 300
+    ch, x0, x1, seeds, s, _ = _inputs(m, 7)
+    out, u, y0, y1 = oracle.ot_extend(ch, x0, x1, None, seeds, s, transcript=True)
+    assert np.array_equal(out, np.where(ch[:, None] == 1, x1, x0))
+    s2 = bytes([s[0] ^ 1]) + s[1:]
+    out2, u2, _, _ = oracle.ot_extend(ch, x0, x1, None, seeds, s2, transcript=True)
+    assert np.array_equal(u, u2) and np.array_equal(out2, out)
+    assert not np.array_equal(y0, x0) and not np.array_equal(y1, x1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [1, 127, 128, 129, 1000, 8192, 8193, 100_000])
+def test_gpu_ot_bit_exact(oracle, m):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import ot
+    ch, x0, x1, seeds, s, delta = _inputs(m, m + 1)
+    kc = fhh.KeyCollection(8, 1)
+    for corr in (False, True):
+        args = dict(x1=None, delta=delta) if corr else dict(x1=x1, delta=None)
+        got, u, y0, y1 = ot.ot_extend(kc, ch, x0, base_seeds=seeds, base_choice=s, tweak_base=11, transcript=True,
+                                      **args)
+        exp, eu, ey0, ey1 = oracle.ot_extend(ch, x0, args["x1"], args["delta"], seeds, s, tweak_base=11,
+                                             transcript=True)
+        assert np.array_equal(got, exp)
+        assert np.array_equal(u, eu)
+        assert np.array_equal(y0, ey0) and np.array_equal(y1, ey1)
+        want = np.where(ch[:, None] == 1, x0 ^ np.frombuffer(delta, np.uint8) if corr else x1, x0)
+        assert np.array_equal(got, want)

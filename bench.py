@@ -219,7 +219,9 @@ def main():
                          "sketch = configs[4] (sketch + Beaver verification batch); "
                          "gc = row f1 (garbled-circuit equality tests of one level)")
     ap.add_argument("--gc-groups", type=int, default=256, help="--workload gc: children per level")
-    ap.add_argument("--gc", action="store_true", help="crawl with the GPU garbled-circuit equality test (mode fe)")
+    ap.add_argument("--gc", default="none", choices=["none", "ot", "ideal"],
+                    help="crawl with the GPU garbled-circuit equality test (mode fe): ot = labels and FE shares "
+                         "by GPU OT extension, ideal = ideal OT")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -253,7 +255,7 @@ def main():
         return sketch_bench(args, world, rank, local_rank, dist)
     if args.workload == "gc":
         return gc_bench(args, world, rank, local_rank, dist)
-    if args.gc and args.mode != "fe":
+    if args.gc != "none" and args.mode != "fe":
         args.mode = "fe"   # the GC equality test feeds the OT share conversion (collect.rs:419-482)
 
     n_local = args.clients
@@ -294,7 +296,7 @@ def main():
 
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, distributed=world > 1 and comm is None, comm=comm, gc=args.gc)
+                             record=False, distributed=world > 1 and comm is None, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc])
 
     def barrier():
         if dist is not None:

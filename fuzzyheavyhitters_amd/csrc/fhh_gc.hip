@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
             aes_rk<GcTab, 2>(s, tbl_gc, b0, b1, lrk);
             // active labels: the garbler's bit (sent in the clear), the evaluator's (via OT)
             const uint32_t gb = plane_bit(a.gb_planes, g, B, k, a.nw, i);
-            const uint32_t eb = plane_bit(a.ev_planes, g, B, k, a.nw, i);
+            const uint32_t eb = a.ev_ot ? 0u : plane_bit(a.ev_planes, g, B, k, a.nw, i);
             uint32_t x[4], y[4], bz[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -127,7 +127,8 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
                 bz[c] = s[0][c] ^ s[1][c] ^ D[c];   // z_k = NOT(x_k ^ y_k): free XOR, NOT = ^Delta
             }
             st_blk(a.gb_labels, k, n, t, x);
-            st_blk(a.ev_labels, k, n, t, y);
+            if (a.ev_ot) st_blk(a.ev_labels, t, B, k, y);   // OT sender input x0 = zero label
+            else st_blk(a.ev_labels, k, n, t, y);
             if (k == 0) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) acc[c] = bz[c];
@@ -181,14 +182,16 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
     for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
         uint32_t acc[4], x[4], y[4];
         ld_blk(a.gb_labels, 0, n, t, x);
-        ld_blk(a.ev_labels, 0, n, t, y);
+        if (a.ev_ot) ld_blk(a.ev_labels, t, B, 0, y);
+        else ld_blk(a.ev_labels, 0, n, t, y);
 #pragma unroll
         for (int c = 0; c < 4; c++) acc[c] = x[c] ^ y[c];   // NOT is free for the evaluator
 #pragma unroll
         for (int k = 1; k < B; k++) {
             uint32_t h[2][4], TG[4], TE[4];
             ld_blk(a.gb_labels, k, n, t, x);
-            ld_blk(a.ev_labels, k, n, t, y);
+            if (a.ev_ot) ld_blk(a.ev_labels, t, B, k, y);
+            else ld_blk(a.ev_labels, k, n, t, y);
             ld_blk(a.tables, 2 * (k - 1), n, t, TG);
             ld_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
 #pragma unroll
@@ -250,6 +253,54 @@ static hipError_t gc_dispatch(const GcArgs& a, bool garble, hipStream_t stream) 
 }
 
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, true, stream); }
+
+// evaluator's label-OT choice bits: OT index o = t * bits + j (test-major, so the active tests'
+// OTs are a prefix), bit = plane[g][j][i] with t = g * N + i; zero past G * N * bits
+__global__ void k_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
+                                         uint32_t* choices, uint64_t words) {
+    const uint64_t m = G * N * bits;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < words; q += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t w = 0;
+        for (uint32_t b = 0; b < 32; b++) {
+            const uint64_t o = q * 32 + b;
+            if (o >= m) break;
+            const uint64_t t = o / bits;
+            const uint32_t j = (uint32_t)(o - t * bits);
+            const uint64_t g = t / N;
+            const uint32_t i = (uint32_t)(t - g * N);
+            w |= plane_bit(planes, g, bits, j, nw, i) << b;
+        }
+        choices[q] = w;
+    }
+}
+
+hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
+                                         uint32_t* choices, uint64_t words, hipStream_t stream) {
+    const uint64_t blocks = (words + 255) / 256;
+    hipLaunchKernelGGL(k_ot_choices_from_planes, dim3((unsigned)(blocks < 65535 ? (blocks ? blocks : 1) : 65535)),
+                       dim3(256), 0, stream, planes, G, N, nw, bits, choices, words);
+    return hipGetLastError();
+}
+
+// bytes (bit 0) -> bit words, zero past n
+__global__ void k_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words) {
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < words; q += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t w = 0;
+        for (uint32_t b = 0; b < 32; b++) {
+            const uint64_t o = q * 32 + b;
+            if (o >= n) break;
+            w |= (uint32_t)(in[o] & 1u) << b;
+        }
+        out[q] = w;
+    }
+}
+
+hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words, hipStream_t stream) {
+    const uint64_t blocks = (words + 255) / 256;
+    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)(blocks < 65535 ? (blocks ? blocks : 1) : 65535)), dim3(256), 0,
+                       stream, in, n, out, words);
+    return hipGetLastError();
+}
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, false, stream); }
 
 }  // namespace fhh

@@ -821,6 +821,17 @@ int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
 namespace {
 uint64_t ot_padded(uint64_t m) { return (m + 8191) / 8192 * 8192; }
 
+// the sender's base-OT choice bits of a level-loop OT (ideal base OTs; k_ot_level_keys derives
+// the seeds from the same material on the device)
+void ot_level_choice(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s[4]) {
+    const uint64_t z0 = host_mix64(prf ^ 0x6f745f63686f6963ull ^ ((uint64_t)level << 24) ^ ((uint64_t)salt << 20));
+    const uint64_t z1 = host_mix64(z0);
+    s[0] = (uint32_t)z0;
+    s[1] = (uint32_t)(z0 >> 32);
+    s[2] = (uint32_t)z1;
+    s[3] = (uint32_t)(z1 >> 32);
+}
+
 // padded choice-bit buffer of the ctx's OT scratch (mp / 32 words, zero past m)
 hipError_t ot_choices_buffer(fhh_ctx* ctx, uint64_t m, uint32_t** out) {
     const uint64_t mp = ot_padded(m);
@@ -837,10 +848,30 @@ struct OtOut {            // optional transcript (device pointers into the scrat
     uint64_t nblk = 0;
 };
 
-// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer. Base OTs ideal:
-// the sender gets the key schedules of seeds[i][s_i].
+// the 3 x 128 base-OT key schedules from host seeds (receiver k_i^0, k_i^1; sender k_i^{s_i}),
+// uploaded and synchronised (the staging vector is reused by the next call)
+int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev) {
+    ctx->ot_rk_host.assign((size_t)3 * 128 * 44, 0);
+    for (int i = 0; i < 128; i++) {
+        const int si = (s[i / 8] >> (i % 8)) & 1;
+        uint32_t rk[11][4];
+        for (int b = 0; b < 3; b++) {
+            host_key_schedule(seeds + (size_t)(i * 2 + (b < 2 ? b : si)) * 16, rk);
+            std::memcpy(ctx->ot_rk_host.data() + ((size_t)b * 128 + i) * 44, rk, 44 * 4);
+        }
+    }
+    HIP_TRY(ctx, ctx->ot_rk.ensure(ctx->ot_rk_host.size() * 4));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->ot_rk.p, ctx->ot_rk_host.data(), ctx->ot_rk_host.size() * 4,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *rk_dev = ctx->ot_rk.as<uint32_t>();
+    return FHH_OK;
+}
+
+// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer; rk_dev: the base-OT
+// key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
 int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
-           const uint8_t delta[16], uint4* out, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16],
+           const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
            uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr) {
     if (m == 0) return FHH_OK;
     const uint64_t mp = ot_padded(m);
@@ -848,24 +879,11 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
     for (int k = 3; k < 5; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(mp * 16));
     for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
-    ctx->ot_rk_host.assign((size_t)3 * 128 * 44, 0);
-    for (int i = 0; i < 128; i++) {
-        const int si = (s[i / 8] >> (i % 8)) & 1;
-        uint32_t rk[11][4];
-        for (int b = 0; b < 3; b++) {
-            const uint8_t* key = seeds + (size_t)(i * 2 + (b < 2 ? b : si)) * 16;
-            host_key_schedule(key, rk);
-            std::memcpy(ctx->ot_rk_host.data() + ((size_t)b * 128 + i) * 44, rk, 44 * 4);
-        }
-    }
-    HIP_TRY(ctx, ctx->ot_rk.ensure(ctx->ot_rk_host.size() * 4));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->ot_rk.p, ctx->ot_rk_host.data(), ctx->ot_rk_host.size() * 4,
-                                hipMemcpyHostToDevice, ctx->stream));
     OtArgs a{};
     a.m = m;
     a.mp = mp;
-    a.rk = ctx->ot_rk.as<uint32_t>();
-    words_from_bytes(s, a.s);
+    a.rk = rk_dev;
+    for (int c = 0; c < 4; c++) a.s[c] = s_words[c];
     a.choices = choices;
     a.T = ctx->ot_buf[0].as<uint4>();
     a.U = ctx->ot_buf[1].as<uint4>();
@@ -874,7 +892,8 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     a.Qt = ctx->ot_buf[4].as<uint4>();
     a.x0 = x0;
     a.x1 = x1;
-    if (delta) words_from_bytes(delta, a.delta);
+    if (delta_words)
+        for (int c = 0; c < 4; c++) a.delta[c] = delta_words[c];
     a.Y0 = ctx->ot_buf[5].as<uint4>();
     a.Y1 = ctx->ot_buf[6].as<uint4>();
     a.out = out;
@@ -915,6 +934,7 @@ struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
     DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
     DevBuf gc_planes[2], gc_tables, gc_gbl, gc_evl, gc_decode, gc_out;   // cfg->gc (row f1)
+    DevBuf gc_evact, gc_msg[2], gc_recv;                                  // cfg->gc = 2: OT buffers
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
@@ -1145,11 +1165,53 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 rc = gc_args(c0, &gb, g);
                 if (rc) return rc;
                 g.ctl = B.ctl.as<LoopCtl>();
+                const bool real_ot = cfg->gc >= 2;
+                g.ev_ot = real_ot ? 1u : 0u;
                 HIP_TRY(c0, launch_gc_garble(g, c0->stream));
+                HIP_TRY(c0, c0->ot_rk.ensure((size_t)3 * 128 * 44 * 4));
+                if (real_ot) {
+                    // the evaluator's input labels by OT extension (gb_set_fancy_inputs /
+                    // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1 receives the
+                    // labels of its share bits, server 0 sends (zero label, zero label ^ Delta)
+                    const uint64_t m1 = tests * bits;
+                    uint32_t* ch = nullptr;
+                    HIP_TRY(c0, ot_choices_buffer(c0, m1, &ch));
+                    HIP_TRY(c0, launch_ot_choices_from_planes(B.gc_planes[1].as<uint64_t>(), C_cap, (uint32_t)c0->n,
+                                                              (uint32_t)c0->nw, bits, ch, ot_padded(m1) / 32,
+                                                              c0->stream));
+                    uint32_t sw[4];
+                    ot_level_choice(cfg->prf_seed, lv, 0, sw);
+                    HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 0, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
+                    rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(),
+                                c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * bits, nullptr);
+                    if (rc) return rc;
+                    g.ev_labels = B.gc_evact.as<uint4>();
+                }
                 HIP_TRY(c0, launch_gc_eval(g, c0->stream));
                 a.gc_out = g.out;
                 a.gc_N = g.N;
                 a.gc_mask = g.mask;
+                if (real_ot && pmode == 1) {
+                    // the FE share conversion by OT extension (collect.rs:437-471): server 0 sends
+                    // (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
+                    HIP_TRY(c0, B.gc_msg[0].ensure(tests * 16));
+                    HIP_TRY(c0, B.gc_msg[1].ensure(tests * 16));
+                    HIP_TRY(c0, B.gc_recv.ensure(tests * 16));
+                    HIP_TRY(c0, launch_ot_fe_messages(a, g.mask, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(),
+                                                      c0->stream));
+                    uint32_t* ch = nullptr;
+                    HIP_TRY(c0, ot_choices_buffer(c0, tests, &ch));
+                    HIP_TRY(c0, launch_pack_bits(g.out, tests, ch, ot_padded(tests) / 32, c0->stream));
+                    uint32_t sw[4];
+                    ot_level_choice(cfg->prf_seed, lv, 1, sw);
+                    HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    rc = ot_run(c0, tests, ch, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
+                                B.gc_recv.as<uint4>(), c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(),
+                                (uint64_t)c0->n, nullptr);
+                    if (rc) return rc;
+                    a.ot_recv = B.gc_recv.as<uint4>();
+                }
             }
             if (pmode == 0) HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
             else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream));
@@ -1901,6 +1963,7 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
     if (levels > c0->L) return c0->fail(FHH_E_ARG, "sim_crawl: levels > data_len");
     if (cfg->mode > 1) return c0->fail(FHH_E_ARG, "sim_crawl: bad mode");
+    if (cfg->gc > 2) return c0->fail(FHH_E_ARG, "sim_crawl: gc must be 0, 1 (ideal OT) or 2 (OT extension)");
     if (cfg->gc && (cfg->mode != 1 || cfg->host_loop))
         return c0->fail(FHH_E_ARG, "sim_crawl: gc needs mode 1 (OT share values) and the device loop");
     if (cfg->gc && 2 * c0->d > (uint32_t)kGcMaxBits) return c0->fail(FHH_E_ARG, "sim_crawl: gc supports d <= 4");
@@ -2299,9 +2362,15 @@ int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
         last[0] &= (1u << (b->m % 32)) - 1;
         HIP_TRY(ctx, hipMemcpy(ch + words - 1, last.data(), 4, hipMemcpyHostToDevice));
     }
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, &b->base_seeds[0][0][0], b->base_choice, &rk);
+    if (rc) return rc;
+    uint32_t sw[4], dw[4];
+    words_from_bytes(b->base_choice, sw);
+    words_from_bytes(b->delta, dw);
     rc = ot_run(ctx, b->m, ch, reinterpret_cast<const uint4*>(b->x0_dev), reinterpret_cast<const uint4*>(b->x1_dev),
-                b->x1_dev ? nullptr : b->delta, reinterpret_cast<uint4*>(b->out_dev), &b->base_seeds[0][0][0],
-                b->base_choice, b->tweak_base, nullptr, 0, nullptr);
+                b->x1_dev ? nullptr : dw, reinterpret_cast<uint4*>(b->out_dev), rk, sw, b->tweak_base, nullptr, 0,
+                nullptr);
     if (rc) return rc;
     return sync(ctx);
 }
@@ -2331,8 +2400,14 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
         HIP_TRY(ctx, hipMemcpyAsync(d1.p, x1, m * 16, hipMemcpyHostToDevice, ctx->stream));
     }
     OtOut tr;
-    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : delta, dout.as<uint4>(),
-                base_seeds, base_choice, tweak_base, nullptr, 0, &tr);
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
+    if (rc) return rc;
+    uint32_t sw[4], dw[4] = {0, 0, 0, 0};
+    words_from_bytes(base_choice, sw);
+    if (!x1) words_from_bytes(delta, dw);
+    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : dw, dout.as<uint4>(), rk, sw,
+                tweak_base, nullptr, 0, &tr);
     if (rc) return rc;
     rc = sync(ctx);
     if (rc) return rc;

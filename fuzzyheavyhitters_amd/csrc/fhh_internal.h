@@ -97,6 +97,8 @@ struct ChildArgs {
     const uint8_t* gc_out;
     uint32_t gc_N;
     uint32_t gc_mask;
+    // OT mode: the receiver's FE share of (c, i) is the OT output ot_recv[c * gc_N + i] (low 8 B)
+    const uint4* ot_recv;
 };
 
 // Garbled-circuit equality tests (row f1, equalitytest.rs:25-219): tests t = g * N + i for
@@ -120,6 +122,8 @@ struct GcArgs {
     uint8_t* out;                // [n]               evaluator's output bit = eq ^ mask
     const LoopCtl* ctl;          // non-null (level loop): groups = min(G, ctl->C), 0 once aborted;
                                  // G * N stays the SoA stride
+    uint32_t ev_ot;              // 1: ev_labels holds the evaluator's ZERO labels (OT sender input)
+                                 // test-major [n][bits]; k_gc_eval then reads its OT'd labels there
 };
 
 struct PruneArgs {
@@ -212,6 +216,14 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, const uint32_t s[4], uint32_t* rk,
+                                hipStream_t stream);
+// GC + OT glue (level loop): evaluator's choice bits (OT index t * bits + j) from its share planes;
+// garbler's OT messages for the FE share conversion; 0/1 bytes -> padded bit words
+hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
+                                         uint32_t* choices, uint64_t words, hipStream_t stream);
+hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words, hipStream_t stream);
+hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,

@@ -495,11 +495,16 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         const uint64_t bc = mix64(base ^ c);
         uint64_t v[4] = {0, 0, 0, 0};
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const bool eq = sim_eq_bit(a, e, c, i);
             uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
             if (r0 >= kFeP) r0 -= kFeP;
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
-            const uint64_t v1 = eq ? r0 : r1;                    // receiver gets pair[o] (A.5)
+            uint64_t v1;                                         // receiver gets pair[o] (A.5)
+            if (a.ot_recv) {                                     // ... through the OT extension
+                const uint4 b = a.ot_recv[c * a.gc_N + i];
+                v1 = (uint64_t)b.x | ((uint64_t)b.y << 32);      // FE::try_from(Block), fastfield.rs:414-421
+            } else {
+                v1 = sim_eq_bit(a, e, c, i) ? r0 : r1;
+            }
             v[0] += r1 & 0xFFFFFFFFull;
             v[1] += r1 >> 32;
             v[2] += v1 & 0xFFFFFFFFull;
@@ -509,6 +514,31 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         if (threadIdx.x == 0)
             for (int k = 0; k < 4; k++) partials[c * 4 + k] = v[k];
     }
+}
+
+// the garbler's OT messages of the FE share conversion (collect.rs:437-452): r0 from the same
+// PRF as k_sim_ot_fe, r1 = r0 + 1; (r0, r1) if the mask bit is set, else (r1, r0); blocks carry
+// the value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430)
+__global__ __launch_bounds__(kReduceThreads) void k_ot_fe_messages(ChildArgs a, uint32_t mask, uint4* x0, uint4* x1) {
+    const uint64_t base = mix64(a.prf_seed ^ a.level);
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+        const uint64_t bc = mix64(base ^ c);
+        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
+            uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
+            if (r0 >= kFeP) r0 -= kFeP;
+            const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;
+            const uint64_t m0 = mask ? r0 : r1, m1 = mask ? r1 : r0;
+            x0[c * a.gc_N + i] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
+            x1[c * a.gc_N + i] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
+        }
+    }
+}
+
+hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ot_fe_messages, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, mask, x0, x1);
+    return hipGetLastError();
 }
 
 hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {

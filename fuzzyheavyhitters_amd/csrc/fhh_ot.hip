@@ -178,6 +178,55 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
     }
 }
 
+// Level-loop base OTs (ideal): the 128 seed pairs derived from (prf_seed, level, salt) on the
+// device, so an enqueued level needs no host data; key schedules [3][128][44] (k_i^0, k_i^1,
+// k_i^{s_i}). One thread per key.
+__constant__ ByteTable c_sbox_ot = SBOX;
+
+__device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t ot_seed_word(uint64_t prf, uint32_t level, uint32_t salt, uint32_t i, uint32_t b,
+                                                 int h) {
+    const uint64_t z = ot_mix64(prf ^ 0x6f745f62617365ull ^ ((uint64_t)level << 24) ^ ((uint64_t)salt << 20) ^
+                                ((uint64_t)i << 2) ^ b);
+    return h ? ot_mix64(z) : z;
+}
+
+__global__ void k_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s0, uint32_t s1, uint32_t s2,
+                                uint32_t s3, uint32_t* rk) {
+    const uint32_t k = threadIdx.x;
+    if (k >= 384) return;
+    const uint32_t which = k / 128, i = k % 128;
+    const uint32_t sw[4] = {s0, s1, s2, s3};
+    const uint32_t b = which < 2 ? which : (sw[i >> 5] >> (i & 31)) & 1u;
+    const uint64_t lo = ot_seed_word(prf, level, salt, i, b, 0), hi = ot_seed_word(prf, level, salt, i, b, 1);
+    uint32_t w[44] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    uint32_t rcon = 1;
+    for (int j = 4; j < 44; j++) {
+        uint32_t t = w[j - 1];
+        if (j % 4 == 0) {
+            t = (t >> 8) | (t << 24);
+            t = (uint32_t)c_sbox_ot.v[t & 0xFF] | ((uint32_t)c_sbox_ot.v[(t >> 8) & 0xFF] << 8) |
+                ((uint32_t)c_sbox_ot.v[(t >> 16) & 0xFF] << 16) | ((uint32_t)c_sbox_ot.v[t >> 24] << 24);
+            t ^= rcon;
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+        }
+        w[j] = w[j - 4] ^ t;
+    }
+    for (int j = 0; j < 44; j++) rk[((size_t)which * 128 + i) * 44 + j] = w[j];
+}
+
+hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, const uint32_t s[4], uint32_t* rk,
+                                hipStream_t stream) {
+    hipLaunchKernelGGL(k_ot_level_keys, dim3(1), dim3(384), 0, stream, prf, level, salt, s[0], s[1], s[2], s[3], rk);
+    return hipGetLastError();
+}
+
 static hipError_t ot_set_lds(const void* fn, int* done) {
     if (*done) return hipSuccess;
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOtLds);

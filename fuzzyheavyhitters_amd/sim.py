@@ -58,13 +58,15 @@ class _TorchAllReduce:
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
-              init_capacity: int = 0, comm=None, gc: bool = False) -> SimResult:
+              init_capacity: int = 0, comm=None, gc=False) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
-    callback (synchronises once per level; the gloo rehearsal path uses this). `gc=True` (mode
-    "fe", device loop) takes each (child, client) equality bit from the GPU garbled-circuit
-    equality test (server 0 garbles, server 1 evaluates; OT ideal) instead of comparing shares."""
+    callback (synchronises once per level; the gloo rehearsal path uses this). `gc` (mode "fe",
+    device loop) takes each (child, client) equality bit from the GPU garbled-circuit equality
+    test (server 0 garbles, server 1 evaluates) instead of comparing shares: `True` / "ot" with
+    the evaluator's labels and the FE shares moved by the GPU OT extension (base OTs ideal),
+    "ideal" with both OTs ideal."""
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -75,7 +77,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.prf_seed = prf_seed
     cfg.host_loop = 1 if host_loop else 0
     cfg.init_capacity = init_capacity
-    cfg.gc = 1 if gc else 0
+    cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2}[gc]
     ar = None
     if comm is not None:
         cfg.comm = comm.handle

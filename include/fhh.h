@@ -213,11 +213,12 @@ typedef struct fhh_sim_config {
     /* native RCCL communicator (takes precedence over `allreduce`): the per-level sum is
      * ncclAllReduce on ctx0's stream, no host synchronisation per level. NULL on one GPU. */
     fhh_comm* comm;
-    /* mode 1, device loop: 1 = the per-(child, client) equality bit comes from the garbled-
-     * circuit equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
-     * evaluates; OT of the evaluator's labels and of the FE shares is ideal), as
-     * tree_crawl does with gc_sender (collect.rs:419-482). Same sums as 0; fresh garbler key,
-     * Delta and mask per level, derived from prf_seed. */
+    /* mode 1, device loop: the per-(child, client) equality bit comes from the garbled-circuit
+     * equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
+     * evaluates), as tree_crawl does with gc_sender (collect.rs:419-482). 1 = the OTs (the
+     * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU OT
+     * extension (fhh_ot_*; base OTs ideal; the last level's FieldElm conversion stays ideal).
+     * Same sums as 0; fresh garbler key, Delta, mask and base OTs per level, from prf_seed. */
     uint32_t gc;
 } fhh_sim_config;
 

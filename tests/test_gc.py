@@ -145,8 +145,9 @@ def _sig(res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot"])
 @pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
-def test_gpu_crawl_with_gc_equals_plain(kind):
+def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
     """tree_crawl with the GC equality test (collect.rs:419-482) gives the same FE sums, keep
     decisions and heavy hitters as the plaintext-equality harness, level by level."""
     from fuzzyheavyhitters_amd import sim_crawl, workload
@@ -158,7 +159,7 @@ def test_gpu_crawl_with_gc_equals_plain(kind):
         thr = 0.01
     c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
     plain = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9)
-    with_gc = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9, gc=True, init_capacity=2)
+    with_gc = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9, gc=gc_mode, init_capacity=2)
     assert _sig(with_gc) == _sig(plain)
     assert len(with_gc.final) > 0
 

@@ -255,49 +255,49 @@ static hipError_t gc_dispatch(const GcArgs& a, bool garble, hipStream_t stream) 
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, true, stream); }
 
 // evaluator's label-OT choice bits: OT index o = t * bits + j (test-major, so the active tests'
-// OTs are a prefix), bit = plane[g][j][i] with t = g * N + i; zero past G * N * bits
+// OTs are a prefix), bit = plane[g][j][i] with t = g * N + i; zero past G * N * bits. One lane per
+// OT (32-bit index math: the host keeps G * N * bits < 2^32), a wave ballot forms two words.
 __global__ void k_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
                                          uint32_t* choices, uint64_t words) {
-    const uint64_t m = G * N * bits;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < words; q += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t w = 0;
-        for (uint32_t b = 0; b < 32; b++) {
-            const uint64_t o = q * 32 + b;
-            if (o >= m) break;
-            const uint64_t t = o / bits;
-            const uint32_t j = (uint32_t)(o - t * bits);
-            const uint64_t g = t / N;
-            const uint32_t i = (uint32_t)(t - g * N);
-            w |= plane_bit(planes, g, bits, j, nw, i) << b;
+    const uint32_t m = (uint32_t)(G * N * bits);
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; o0 < words * 32;
+         o0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t o = (uint32_t)o0 + lane;
+        uint32_t bit = 0;
+        if (o0 + lane < m) {
+            const uint32_t t = o / bits, j = o - t * bits;
+            const uint32_t g = t / N;
+            bit = plane_bit(planes, g, bits, j, nw, t - g * N);
         }
-        choices[q] = w;
+        const uint64_t v = __ballot(bit);
+        if (lane < 2 && o0 / 32 + lane < words) choices[o0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
     }
 }
 
 hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
                                          uint32_t* choices, uint64_t words, hipStream_t stream) {
-    const uint64_t blocks = (words + 255) / 256;
-    hipLaunchKernelGGL(k_ot_choices_from_planes, dim3((unsigned)(blocks < 65535 ? (blocks ? blocks : 1) : 65535)),
+    if (G * N * bits >= (1ull << 32)) return hipErrorInvalidValue;
+    const uint64_t blocks = (words * 32 + 255) / 256;
+    hipLaunchKernelGGL(k_ot_choices_from_planes, dim3((unsigned)(blocks < 16384 ? (blocks ? blocks : 1) : 16384)),
                        dim3(256), 0, stream, planes, G, N, nw, bits, choices, words);
     return hipGetLastError();
 }
 
-// bytes (bit 0) -> bit words, zero past n
+// bytes (bit 0) -> bit words, zero past n: one lane per byte, a wave ballot per two words
 __global__ void k_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words) {
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < words; q += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t w = 0;
-        for (uint32_t b = 0; b < 32; b++) {
-            const uint64_t o = q * 32 + b;
-            if (o >= n) break;
-            w |= (uint32_t)(in[o] & 1u) << b;
-        }
-        out[q] = w;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; o0 < words * 32;
+         o0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = o0 + lane;
+        const uint64_t v = __ballot(o < n ? (in[o] & 1u) : 0u);
+        if (lane < 2 && o0 / 32 + lane < words) out[o0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
     }
 }
 
 hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words, hipStream_t stream) {
-    const uint64_t blocks = (words + 255) / 256;
-    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)(blocks < 65535 ? (blocks ? blocks : 1) : 65535)), dim3(256), 0,
+    const uint64_t blocks = (words * 32 + 255) / 256;
+    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)(blocks < 16384 ? (blocks ? blocks : 1) : 16384)), dim3(256), 0,
                        stream, in, n, out, words);
     return hipGetLastError();
 }

@@ -123,20 +123,21 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     }
 }
 
-// rows [128][mp / 32] u32 -> cols [mp][4] u32: lane w owns OTs 32 w .. 32 w + 31
-__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint32_t* cols, OtArgs a) {
+// rows [128][mp / 32] u32 -> cols [mp] uint4: lane w owns OTs 32 w .. 32 w + 31; the four
+// 32-row groups are transposed in registers (128 words) and each OT's row leaves as one 16-B store
+__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint4* cols, OtArgs a) {
     const uint64_t W = a.mp / 32;
     const uint64_t W_act = (ot_active(a) + 31) / 32;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < W_act; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t x[4][32];
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            uint32_t x[32];
 #pragma unroll
-            for (int r = 0; r < 32; r++) x[r] = rows[(uint64_t)(32 * g + r) * W + w];
-            transpose32(x);   // x[k] bit r = row 32 g + r of OT 32 w + k
-#pragma unroll
-            for (int k = 0; k < 32; k++) cols[(32 * w + k) * 4 + g] = x[k];
+            for (int r = 0; r < 32; r++) x[g][r] = __builtin_nontemporal_load(rows + (uint64_t)(32 * g + r) * W + w);
+            transpose32(x[g]);   // x[g][k] bit r = row 32 g + r of OT 32 w + k
         }
+#pragma unroll
+        for (int k = 0; k < 32; k++) cols[32 * w + k] = make_uint4(x[0][k], x[1][k], x[2][k], x[3][k]);
     }
 }
 
@@ -263,7 +264,7 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
 
 hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_ot_transpose, dim3(ot_grid(a.mp / 32, 256)), dim3(256), 0, stream,
-                       reinterpret_cast<const uint32_t*>(rows), reinterpret_cast<uint32_t*>(cols), a);
+                       reinterpret_cast<const uint32_t*>(rows), cols, a);
     return hipGetLastError();
 }
 

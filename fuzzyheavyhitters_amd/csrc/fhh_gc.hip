@@ -284,21 +284,23 @@ hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uin
     return hipGetLastError();
 }
 
-// bytes (bit 0) -> bit words, zero past n: one lane per byte, a wave ballot per two words
-__global__ void k_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words) {
+// bytes (bit 0) -> bit words, each byte repeated `dup` times (the doubled choices of a BlockPair
+// OT, collect.rs:868), zero past n * dup: one lane per output bit, a wave ballot per two words
+__global__ void k_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; o0 < words * 32;
          o0 += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t o = o0 + lane;
-        const uint64_t v = __ballot(o < n ? (in[o] & 1u) : 0u);
+        const uint64_t v = __ballot(o < n * dup ? (in[o / dup] & 1u) : 0u);
         if (lane < 2 && o0 / 32 + lane < words) out[o0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
     }
 }
 
-hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words, hipStream_t stream) {
+hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words,
+                           hipStream_t stream) {
     const uint64_t blocks = (words * 32 + 255) / 256;
     hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)(blocks < 16384 ? (blocks ? blocks : 1) : 16384)), dim3(256), 0,
-                       stream, in, n, out, words);
+                       stream, in, n, dup, out, words);
     return hipGetLastError();
 }
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, false, stream); }

@@ -1192,23 +1192,30 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 a.gc_out = g.out;
                 a.gc_N = g.N;
                 a.gc_mask = g.mask;
-                if (real_ot && pmode == 1) {
-                    // the FE share conversion by OT extension (collect.rs:437-471): server 0 sends
+                if (real_ot) {
+                    // the share conversion by OT extension (collect.rs:437-471; 846-876 at the last
+                    // level, where a FieldElm travels as a BlockPair = 2 OTs): server 0 sends
                     // (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
-                    HIP_TRY(c0, B.gc_msg[0].ensure(tests * 16));
-                    HIP_TRY(c0, B.gc_msg[1].ensure(tests * 16));
-                    HIP_TRY(c0, B.gc_recv.ensure(tests * 16));
-                    HIP_TRY(c0, launch_ot_fe_messages(a, g.mask, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(),
-                                                      c0->stream));
+                    const uint32_t per = pmode == 1 ? 1 : 2;
+                    const uint64_t m2 = tests * per;
+                    HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
+                    HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
+                    HIP_TRY(c0, B.gc_recv.ensure(m2 * 16));
+                    if (pmode == 1)
+                        HIP_TRY(c0, launch_ot_fe_messages(a, g.mask, B.gc_msg[0].as<uint4>(),
+                                                          B.gc_msg[1].as<uint4>(), c0->stream));
+                    else
+                        HIP_TRY(c0, launch_ot_fe255_messages(a, g.mask, B.gc_msg[0].as<uint4>(),
+                                                             B.gc_msg[1].as<uint4>(), c0->stream));
                     uint32_t* ch = nullptr;
-                    HIP_TRY(c0, ot_choices_buffer(c0, tests, &ch));
-                    HIP_TRY(c0, launch_pack_bits(g.out, tests, ch, ot_padded(tests) / 32, c0->stream));
+                    HIP_TRY(c0, ot_choices_buffer(c0, m2, &ch));
+                    HIP_TRY(c0, launch_pack_bits(g.out, tests, per, ch, ot_padded(m2) / 32, c0->stream));
                     uint32_t sw[4];
                     ot_level_choice(cfg->prf_seed, lv, 1, sw);
                     HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
-                    rc = ot_run(c0, tests, ch, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
+                    rc = ot_run(c0, m2, ch, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
                                 B.gc_recv.as<uint4>(), c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(),
-                                (uint64_t)c0->n, nullptr);
+                                (uint64_t)c0->n * per, nullptr);
                     if (rc) return rc;
                     a.ot_recv = B.gc_recv.as<uint4>();
                 }
@@ -1625,6 +1632,7 @@ int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t*
     const size_t n = ctx->n, K = ctx->K, L = ctx->L, npad = ctx->npad, nw = ctx->nw;
     std::vector<uint8_t> cws(L * K * npad * 16), roots(K * npad * 16);
     std::vector<uint64_t> cwb(L * K * 4 * nw), kidx(K * nw);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // uploads / keygen / bitslicing are async
     HIP_TRY(ctx, hipMemcpy(cws.data(), ctx->cw_seed.p, cws.size(), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(roots.data(), ctx->root_seed.p, roots.size(), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(cwb.data(), ctx->cw_bits.p, cwb.size() * 8, hipMemcpyDeviceToHost));

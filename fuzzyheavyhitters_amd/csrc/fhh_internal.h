@@ -222,8 +222,10 @@ hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, con
 // garbler's OT messages for the FE share conversion; 0/1 bytes -> padded bit words
 hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
                                          uint32_t* choices, uint64_t words, hipStream_t stream);
-hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t* out, uint64_t words, hipStream_t stream);
+hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words,
+                           hipStream_t stream);
 hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
+hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,

@@ -567,6 +567,61 @@ __device__ __forceinline__ void fe255_canon(uint64_t (&x)[4]) {
     }
 }
 
+// BlockPair <-> 4 x u64 little-endian limbs: the value's 32 big-endian bytes, block 0 = bytes
+// 0..15 (limbs 3, 2), block 1 = bytes 16..31 (limbs 1, 0) (field.rs:465-492); a block's 16
+// bytes as four little-endian u32 words
+__device__ __forceinline__ uint4 limbs_to_block(uint64_t hi, uint64_t lo) {
+    return make_uint4(__builtin_bswap32((uint32_t)(hi >> 32)), __builtin_bswap32((uint32_t)hi),
+                      __builtin_bswap32((uint32_t)(lo >> 32)), __builtin_bswap32((uint32_t)lo));
+}
+__device__ __forceinline__ void blockpair_to_limbs(uint4 b0, uint4 b1, uint64_t (&r)[4]) {
+    r[3] = ((uint64_t)__builtin_bswap32(b0.x) << 32) | __builtin_bswap32(b0.y);
+    r[2] = ((uint64_t)__builtin_bswap32(b0.z) << 32) | __builtin_bswap32(b0.w);
+    r[1] = ((uint64_t)__builtin_bswap32(b1.x) << 32) | __builtin_bswap32(b1.y);
+    r[0] = ((uint64_t)__builtin_bswap32(b1.z) << 32) | __builtin_bswap32(b1.w);
+}
+
+// the last level's OT messages (collect.rs:846-866): FieldElm r0 (the k_sim_ot_fe255 PRF),
+// r1 = r0 + 1, each as a BlockPair; two OTs per test (2t: block 0, 2t + 1: block 1), pairs
+// (r0, r1) if the mask bit is set, else (r1, r0)
+__global__ __launch_bounds__(kReduceThreads) void k_ot_fe255_messages(ChildArgs a, uint32_t mask, uint4* x0,
+                                                                      uint4* x1) {
+    const uint64_t base = mix64(a.prf_seed ^ a.level);
+    const uint64_t C_ = child_count(a);
+    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+        const uint64_t bc = mix64(base ^ c);
+        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
+            const uint64_t bi = mix64(bc ^ (a.client_base + i));
+            uint64_t r0[4], r1[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) r0[k] = mix64(bi ^ (uint64_t)k);
+            r0[3] &= 0x7FFFFFFFFFFFFFFFull;
+            fe255_canon(r0);
+            unsigned __int128 acc = (unsigned __int128)r0[0] + 1;
+            r1[0] = (uint64_t)acc;
+#pragma unroll
+            for (int k = 1; k < 4; k++) {
+                acc = (unsigned __int128)r0[k] + (uint64_t)(acc >> 64);
+                r1[k] = (uint64_t)acc;
+            }
+            fe255_canon(r1);
+            const uint64_t* m0 = mask ? r0 : r1;
+            const uint64_t* m1 = mask ? r1 : r0;
+            const size_t t = c * a.gc_N + i;
+            x0[2 * t] = limbs_to_block(m0[3], m0[2]);
+            x0[2 * t + 1] = limbs_to_block(m0[1], m0[0]);
+            x1[2 * t] = limbs_to_block(m1[3], m1[2]);
+            x1[2 * t + 1] = limbs_to_block(m1[1], m1[0]);
+        }
+    }
+}
+
+hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
+    if (a.C == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ot_fe255_messages, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, mask, x0, x1);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[16 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
@@ -579,7 +634,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = 0;
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const bool eq = sim_eq_bit(a, e, c, i);
+            const bool eq = a.ot_recv ? false : sim_eq_bit(a, e, c, i);
             const uint64_t bi = mix64(bc ^ (a.client_base + i));
             uint64_t r0[4];
 #pragma unroll
@@ -596,9 +651,17 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
                 r1[k] = (uint64_t)acc;
             }
             fe255_canon(r1);
+            uint64_t got[4];
+            if (a.ot_recv) {   // FieldElm::try_from(BlockPair): big-endian 32 bytes (field.rs:466-476)
+                const size_t t = c * a.gc_N + i;
+                blockpair_to_limbs(a.ot_recv[2 * t], a.ot_recv[2 * t + 1], got);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) got[k] = eq ? r0[k] : r1[k];
+            }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint64_t x1 = eq ? r0[k] : r1[k];
+                const uint64_t x1 = got[k];
                 v[2 * k] += r1[k] & 0xFFFFFFFFull;
                 v[2 * k + 1] += r1[k] >> 32;
                 v[8 + 2 * k] += x1 & 0xFFFFFFFFull;

@@ -217,7 +217,7 @@ typedef struct fhh_sim_config {
      * equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
      * evaluates), as tree_crawl does with gc_sender (collect.rs:419-482). 1 = the OTs (the
      * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU OT
-     * extension (fhh_ot_*; base OTs ideal; the last level's FieldElm conversion stays ideal).
+     * extension (fhh_ot_*; base OTs ideal; a FieldElm share travels as a BlockPair = 2 OTs).
      * Same sums as 0; fresh garbler key, Delta, mask and base OTs per level, from prf_seed. */
     uint32_t gc;
 } fhh_sim_config;

@@ -129,7 +129,7 @@ def test_sharded_crawl_equals_single_process(oracle, mode):
     assert sorted(final) == sorted(tuple(tuple(int(b) for b in pj) for pj in p) for p in ref.final_paths)
 
 
-def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0):
+def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0, gc=False):
     import sys
     sys.path.insert(0, ROOT)
     import torch
@@ -150,7 +150,7 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_
         c0.set_client_base(rank * n_local)
         c1.set_client_base(rank * n_local)
         res = fhh.sim_crawl(c0, c1, thr, nclients_total=wl_args["n"], mode=mode, prf_seed=7, distributed=True,
-                            host_loop=host_loop, init_capacity=init_capacity)
+                            host_loop=host_loop, init_capacity=init_capacity, gc=gc)
         if rank == 0:
             q.put((res.level_children.tolist(), [c.tolist() for c in res.counts],
                    sorted(tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final)))
@@ -159,8 +159,8 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["count", "fe"])
-@pytest.mark.parametrize("loop", ["device_grow", "host"])
+@pytest.mark.parametrize("mode,loop", [("count", "device_grow"), ("count", "host"), ("fe", "device_grow"),
+                                       ("fe", "host"), ("fe", "device_gc_ot")])
 def test_gpu_two_ranks_allreduce_hook(oracle, mode, loop):
     """Two ranks share one GPU over the host all-reduce hook. device_grow starts the device
     loop at capacity 2 so it aborts and resumes several times: the cross-rank sum of an
@@ -171,7 +171,8 @@ def test_gpu_two_ranks_allreduce_hook(oracle, mode, loop):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    kw = {"host_loop": loop == "host", "init_capacity": 2 if loop == "device_grow" else 0}
+    kw = {"host_loop": loop == "host", "init_capacity": 2 if loop.startswith("device") else 0,
+          "gc": "ot" if loop == "device_gc_ot" else False}
     procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, wl_args, thr, mode, q), kwargs=kw) for r in range(2)]
     for p in procs:
         p.start()

@@ -199,6 +199,60 @@ def plaintext_heavy_hitters(alpha_left: np.ndarray, alpha_right: np.ndarray, thr
     return sorted(frontier)
 
 
+def plaintext_crawl(left: np.ndarray, right: np.ndarray, thr: int, thr_last: int, levels: int | None = None):
+    """Full-size plaintext crawl (no crypto, no oracle): what the two-server protocol computes,
+    level by level in the leader's child order (parents in frontier order x all_bit_vectors,
+    collect.rs:379-391, lib.rs:125-129), keep iff count >= threshold (collect.rs:945-989).
+    A client is inside a node iff in every dim l[:k] <= prefix <= r[:k]; the per-(node, dim)
+    "still equal to l / to r" flags are bit-packed over clients, so a level is a handful of
+    word ops per (child, 64 clients). Returns (per-level child counts, final paths, final
+    counts); paths as tuples of d bit-tuples."""
+    n, d, L = left.shape
+    levels = levels or L
+    nw = (n + 63) // 64
+
+    def pack(a):   # [n] 0/1 -> [nw] u64 over clients
+        b = np.zeros(nw * 64, np.uint8)
+        b[:n] = a
+        return np.packbits(b.reshape(nw, 64), axis=1, bitorder="little").view(np.uint64).reshape(nw)
+
+    ones = np.full(nw, np.uint64(0xFFFFFFFFFFFFFFFF))
+    valid = pack(np.ones(n, np.uint8))
+    # frontier state: alive [F][nw], lo/hi tight [F][d][nw]
+    alive = valid[None, :].copy()
+    lo_t = np.broadcast_to(ones, (1, d, nw)).copy()
+    hi_t = lo_t.copy()
+    paths = [tuple(() for _ in range(d))]
+    counts_per_level = []
+    for k in range(levels):
+        lb = np.stack([pack(left[:, j, k]) for j in range(d)])    # [d][nw]
+        rb = np.stack([pack(right[:, j, k]) for j in range(d)])
+        F = alive.shape[0]
+        C = F << d
+        c_alive = np.repeat(alive, 1 << d, axis=0)                  # child c = f * 2^d + i
+        c_lo = np.repeat(lo_t, 1 << d, axis=0)
+        c_hi = np.repeat(hi_t, 1 << d, axis=0)
+        i_idx = np.tile(np.arange(1 << d), F)
+        for j in range(d):
+            b = ((i_idx >> j) & 1).astype(bool)[:, None]
+            lo, hi = c_lo[:, j], c_hi[:, j]
+            ok = np.where(b, ~hi | rb[j][None, :], ~lo | ~lb[j][None, :])
+            c_alive &= ok
+            c_lo[:, j] = np.where(b, lo & lb[j][None, :], lo & ~lb[j][None, :])
+            c_hi[:, j] = np.where(b, hi & rb[j][None, :], hi & ~rb[j][None, :])
+        cnt = np.bitwise_count(c_alive).sum(axis=1).astype(np.uint64) if C else np.zeros(0, np.uint64)
+        counts_per_level.append(cnt)
+        keep = np.nonzero(cnt >= (thr_last if k == levels - 1 else thr))[0]
+        new_paths = []
+        for c in keep:
+            f, i = divmod(int(c), 1 << d)
+            new_paths.append(tuple(paths[f][j] + ((i >> j) & 1,) for j in range(d)))
+        paths = new_paths
+        alive, lo_t, hi_t = c_alive[keep], c_lo[keep], c_hi[keep]
+        final_counts = cnt[keep]
+    return counts_per_level, paths, [int(v) for v in final_counts]
+
+
 def add_keys_request_bincode(key_idx: np.ndarray, root_seed: np.ndarray, cw_seed: np.ndarray,
                              cw_bits: np.ndarray) -> np.ndarray:
     """Serialize keys (add_keys layout: [n][d][2], [n][d][2][16], [n][d][2][L][16],

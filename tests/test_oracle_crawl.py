@@ -93,3 +93,42 @@ def test_workload_shard_slices_are_consistent():
     b = workload.zipf_workload(180, 64, 1, num_sites=50, seed=11, client_offset=120)
     assert np.array_equal(np.concatenate([a.alpha, b.alpha]), full.alpha)
     assert np.array_equal(np.concatenate([a.root_seeds, b.root_seeds]), full.root_seeds)
+
+
+@pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
+def test_plaintext_crawl_equals_oracle(oracle, kind):
+    """workload.plaintext_crawl (bit-packed, no crypto) reproduces the oracle's per-level
+    counts and final heavy hitters — it is then the full-size check of the GPU crawl."""
+    from fuzzyheavyhitters_amd import workload
+    if kind == "zipf_d1":
+        wl = workload.zipf_workload(300, 40, 1, num_sites=8, seed=3)
+        thr = 0.02
+    else:
+        wl = workload.coords_workload(800, ball_size=3, num_centroids=30, side_km=4.0)
+        thr = 0.01
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    ref = oracle.crawl(k0, k1, thr, mode="count")
+    t, tl = oracle.thresholds(thr, wl.left.shape[0])
+    counts, paths, finals = workload.plaintext_crawl(wl.left, wl.right, t, tl)
+    assert [c.tolist() for c in counts] == [np.asarray(c, np.uint64).tolist() for c in ref.counts]
+    assert paths == [tuple(tuple(int(x) for x in pj) for pj in p) for p in ref.final_paths]
+    assert finals == [int(v) for v in ref.final_values]
+
+
+@pytest.mark.gpu
+def test_gpu_full_size_configs1_equals_plaintext(oracle):
+    """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): every
+    level's child counts, the 222 heavy hitters and their counts from the GPU crawl equal the
+    plaintext crawl (size-independent check; the CPU oracle would take minutes here)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    n = 100_000
+    wl = workload.zipf_workload(n, 512, 1, num_sites=10_000, zipf_s=1.03, seed=0x5EED)
+    c0, c1 = fhh.KeyCollection(512, 1), fhh.KeyCollection(512, 1)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    res = sim_crawl(c0, c1, 0.001, mode="count")
+    t, tl = oracle.thresholds(0.001, n)
+    counts, paths, finals = workload.plaintext_crawl(wl.left, wl.right, t, tl)
+    assert [c.tolist() for c in res.counts] == [c.tolist() for c in counts]
+    assert [tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final] == paths
+    assert [int(r.value) for r in res.final] == finals

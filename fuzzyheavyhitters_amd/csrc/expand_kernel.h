@@ -163,7 +163,123 @@ __host__ __device__ __forceinline__ void aes0_mmo_tab(uint32_t (&s)[NB][4], cons
     }
 }
 
+// ---- AES-128 (zero key) + MMO for sibling counter PAIRS ---------------------------------
+// expand_dir evaluates a seed in both directions at every level: block 2q uses ctr = k
+// (dir 0, left child), block 2q+1 uses ctr = k + 2^64 (dir 1, prg.rs:273-276). Unless byte 8
+// of k is 0xFF (a carry into byte 9), the two counters differ in byte 8 alone, i.e. in one
+// byte of column 2. After round 1 only column 2 differs (MixColumns stays inside the
+// column), and in round 2 each output column takes exactly one byte of column 2
+// (ShiftRows). So the dir-1 block needs 1 table lookup in round 1 and 4 in round 2 instead of
+// 16 + 16; rounds 3..10 are independent. Per pair: 293 lookups instead of 320 (the generic
+// function's compiler CSE reaches 312).
+// A carry in any lane of the wave (probability 1 - (255/256)^64 = 22 % per pair) makes the
+// whole wave recompute the dir-1 block's rounds 1-2 in full (a wave-uniform branch; it is
+// exact for every lane, carry or not), so the output is bit-identical to aes0_mmo_tab.
+template <class Ops, class Tab, int NB>
+__host__ __device__ __forceinline__ void aes0_mmo_pair(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0,
+                                                       uint32_t b1) {
+    static_assert(NB % 2 == 0, "blocks come in (dir 0, dir 1) pairs");
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB / 2; q++) {
+        const uint32_t* a = s[2 * q];
+        const uint32_t* bb = s[2 * q + 1];
+        // round 1: generic for block A, only the column-2 row-0 term differs for block B
+        uint32_t ya[4], yb2;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, a[c]);
+            const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, a[(c + 1) & 3]);
+            const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, a[(c + 2) & 3]);
+            const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, a[(c + 3) & 3]);
+            const uint32_t p = Ops::xor3(t1, t2, t3);
+            ya[c] = Ops::xor3(p, t0, ZERO_RK.w[1][c]);
+            if (c == 2) yb2 = Ops::xor3(p, Tab::template term<0>(tbl, b0, b1, bb[2]), ZERO_RK.w[1][2]);
+        }
+        // round 2: each output column c takes row k = (2 - c) & 3 of column 2
+        uint32_t za[4], zb[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            uint32_t t[4];
+            t[0] = Tab::template term<0>(tbl, b0, b1, ya[c]);
+            t[1] = Tab::template term<1>(tbl, b0, b1, ya[(c + 1) & 3]);
+            t[2] = Tab::template term<2>(tbl, b0, b1, ya[(c + 2) & 3]);
+            t[3] = Tab::template term<3>(tbl, b0, b1, ya[(c + 3) & 3]);
+            const int k = (2 - c) & 3;
+            uint32_t tb;
+            if (k == 0) tb = Tab::template term<0>(tbl, b0, b1, yb2);
+            else if (k == 1) tb = Tab::template term<1>(tbl, b0, b1, yb2);
+            else if (k == 2) tb = Tab::template term<2>(tbl, b0, b1, yb2);
+            else tb = Tab::template term<3>(tbl, b0, b1, yb2);
+            const uint32_t p = Ops::xor3(t[(k + 1) & 3], t[(k + 2) & 3], t[(k + 3) & 3]);
+            za[c] = Ops::xor3(p, t[k], ZERO_RK.w[2][c]);
+            zb[c] = Ops::xor3(p, tb, ZERO_RK.w[2][c]);
+        }
+        // carry into byte 9 somewhere in the wave: B's counter differs in more bytes
+        if (Ops::any((a[2] & 0xFFu) == 0xFFu)) {
+            uint32_t u[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) u[c] = bb[c];
+#pragma unroll
+            for (int r = 1; r <= 2; r++) {
+                uint32_t v[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    v[c] = Ops::xor3(Ops::xor3(Tab::template term<0>(tbl, b0, b1, u[c]),
+                                               Tab::template term<1>(tbl, b0, b1, u[(c + 1) & 3]),
+                                               Tab::template term<2>(tbl, b0, b1, u[(c + 2) & 3])),
+                                     Tab::template term<3>(tbl, b0, b1, u[(c + 3) & 3]), ZERO_RK.w[r][c]);
+#pragma unroll
+                for (int c = 0; c < 4; c++) u[c] = v[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; c++) zb[c] = u[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            x[2 * q][c] = za[c];
+            x[2 * q + 1][c] = zb[c];
+        }
+    }
+#pragma unroll
+    for (int r = 3; r < 10; r++) {
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[b][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[b][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[b][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[b][(c + 3) & 3]);
+                y[b][c] = Ops::xor3(Ops::xor3(t0, t1, t2), t3, ZERO_RK.w[r][c]);
+            }
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[b][c] = y[b][c];
+    }
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint32_t o[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[b][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[b][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[b][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[b][(c + 3) & 3]);
+            o[c] = Ops::xor3(Ops::perm(a1, a0, sel_lo), Ops::perm(a3, a2, sel_hi), ZERO_RK.w[10][c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) s[b][c] ^= o[c];   // MMO feed-forward (prg.rs:227-230)
+    }
+}
+
 struct DevOpsX : DevOps {
+    // wave-uniform "any lane": the carry fallback of aes0_mmo_pair is a scalar branch
+    static __device__ __forceinline__ bool any(bool p) { return __ballot(p) != 0; }
     static __device__ __forceinline__ uint32_t bfe(uint32_t x, uint32_t off, uint32_t w) {
         return (x >> off) & ((1u << w) - 1u);
     }

@@ -30,7 +30,7 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kDefaultVariant = 33;  // 4 tables, 128 KiB, 1024 thr, dynamic items, <= 16 entries per item, nontemporal seed stores (r01 A/B)
+constexpr int kDefaultVariant = 34;  // 4 tables, 128 KiB, 1024 thr, dynamic items, <= 16 entries per item, nontemporal seed stores, sibling-pair AES (r01 A/B)
 
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
 

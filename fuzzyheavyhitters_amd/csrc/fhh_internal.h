@@ -292,10 +292,11 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 }
 // entries per work item (CW reuse and counter traffic vs. end-of-level tail): variant 29 is
 // variant 3 drawing the next item one entry ahead; 30 / 31 are variant 3 with up to 16 / 32
-// entries per item; 32 / 33 store child seeds nontemporally with up to 8 / 16 entries per item
+// entries per item; 32 / 33 store child seeds nontemporally with up to 8 / 16 entries per item;
+// 34 / 35 are 33 / 32 with the sibling-pair AES (aes0_mmo_pair)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33) ? 16u : variant == 31 ? 32u : 8u;
+    return (variant == 30 || variant == 33 || variant == 34) ? 16u : variant == 31 ? 32u : 8u;
 }
 
 }  // namespace fhh

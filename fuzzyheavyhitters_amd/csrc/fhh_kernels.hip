@@ -41,7 +41,7 @@ typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
 
 // NT: child seeds are written with the nontemporal hint — they are read again only at the next
 // level, and 1.3 GB per launch left dirty in L2 costs a writeback at every kernel boundary
-template <class Tab, int NB, bool NT = false>
+template <class Tab, int NB, bool NT = false, bool PAIR = false>
 __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
                                             uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
                                             uint32_t* next = nullptr) {
@@ -88,7 +88,8 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
             }
             if (ahead && e == e_begin && s0 == 0 && lane == 0) *next = atomicAdd(ahead, 1u);
 
-            aes0_mmo_tab<DevOpsX, Tab, NB>(blk, tbl, b0, b1);
+            if constexpr (PAIR) aes0_mmo_pair<DevOpsX, Tab, NB>(blk, tbl, b0, b1);
+            else aes0_mmo_tab<DevOpsX, Tab, NB>(blk, tbl, b0, b1);
 
 #pragma unroll
             for (int q = 0; q < NB / 2; q++) {
@@ -200,11 +201,13 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
     }
 }
 
-// FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores
+// FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores,
+// bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair)
 template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     constexpr bool AHEAD = (FLAGS & 1) != 0;
     constexpr bool NT = (FLAGS & 2) != 0;
+    constexpr bool PAIR = (FLAGS & 4) != 0;
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
@@ -238,8 +241,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         }
         uint32_t nxt = 0;
         if constexpr (PF) expand_item_pf<Tab>(J, item - J.item_begin, tbl, lane, b0, b1);
-        else if constexpr (AHEAD) expand_item<Tab, NB, NT>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
-        else expand_item<Tab, NB, NT>(J, item - J.item_begin, tbl, lane, b0, b1);
+        else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
+        else expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
             uint32_t v = nxt;
             if (!AHEAD && lane == 0) v = atomicAdd(work_counter, 1u);
@@ -281,7 +284,9 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     X(30, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
     X(31, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
     X(32, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
-    X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)
+    X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
+    X(34, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
+    X(35, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)
 
 struct VariantInfo {
     const void* fn;
@@ -312,7 +317,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 7; }
+int expand_variant_count() { return kBsVariant + kBsCount + 9; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

@@ -29,7 +29,41 @@ struct HostOps {
     }
     static uint32_t bfe(uint32_t x, uint32_t off, uint32_t w) { return (x >> off) & ((1u << w) - 1u); }
     static uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+    static bool any(bool p) { return p; }
 };
+
+// aes0_mmo_pair (sibling counters k, k + 2^64 sharing rounds 1-2) == aes0_mmo_tab, including
+// the carry fallback (byte 8 = 0xFF, with longer carry chains into bytes 9..15 and the wrap)
+template <class Tab>
+static int check_pair(std::mt19937_64& rng) {
+    static uint32_t tbl[2 * 256 * 64];
+    for (int i = 0; i < Tab::kWords; i++) tbl[i] = Tab::word(fhh::T0.v, i);
+    int fails = 0;
+    for (int it = 0; it < 4096; it++) {
+        const uint32_t lane = it % 64;
+        uint32_t b0, b1;
+        Tab::bases(lane, b0, b1);
+        uint32_t seed[2][4];
+        for (int q = 0; q < 2; q++)
+            for (int c = 0; c < 4; c++) seed[q][c] = (uint32_t)rng();
+        const int mode = it % 8;   // 0..3 random, 4: byte 8 = FF, 5: bytes 8..11 FF, 6: all upper FF, 7: 8..12 FF
+        if (mode == 4) seed[it & 1][2] |= 0xFFu;
+        if (mode == 5) seed[it & 1][2] = 0xFFFFFFFFu;
+        if (mode == 6) { seed[0][2] = seed[0][3] = 0xFFFFFFFFu; }
+        if (mode == 7) { seed[1][2] = 0xFFFFFFFFu; seed[1][3] |= 0xFFu; }
+        uint32_t s1[4][4], s2[4][4];
+        for (int q = 0; q < 2; q++)
+            for (int dir = 0; dir < 2; dir++) {
+                fhh::prg_ctr(seed[q], dir, s1[2 * q + dir]);
+                fhh::prg_ctr(seed[q], dir, s2[2 * q + dir]);
+            }
+        fhh::aes0_mmo_tab<HostOps, Tab, 4>(s1, tbl, b0, b1);
+        fhh::aes0_mmo_pair<HostOps, Tab, 4>(s2, tbl, b0, b1);
+        if (std::memcmp(s1, s2, sizeof s1)) fails++;
+    }
+    if (fails) std::printf("pair %s: %d failures\n", Tab::kName, fails);
+    return fails;
+}
 
 // every LDS layout of expand_kernel.h: same outputs as the byte-oriented reference, every lane,
 // and lanes that share a ds_read_b32 lane group (32 lanes) hit distinct banks
@@ -160,6 +194,8 @@ int main() {
     fails += check_layout<fhh::Tab4T32<HostOps>>(rng, ref_aes0);
     fails += check_layout<fhh::TabT0R32<HostOps>>(rng, ref_aes0);
     fails += check_layout<fhh::TabT01R32<HostOps>>(rng, ref_aes0);
+    fails += check_pair<fhh::Tab4T32<HostOps>>(rng);
+    fails += check_pair<fhh::TabT0R64<HostOps>>(rng);
     if (fails) { std::printf("FAIL %d\n", fails); return 1; }
     std::printf("OK\n");
     return 0;

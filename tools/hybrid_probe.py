@@ -42,8 +42,14 @@ def main():
         out[i] = time.perf_counter() - t0
 
     out = [0.0, 0.0]
+    for p in pairs:
+        p[0].reset_stats()
+        p[1].reset_stats()
     for i in range(2):
         run(i, out)   # warm
+    blocks = []
+    for p in pairs:   # executed AES blocks of one crawl (both servers)
+        blocks.append(p[0].stats()["aes_blocks"] + p[1].stats()["aes_blocks"])
     for r in range(args.rounds):
         alone = [0.0, 0.0]
         run(0, alone)
@@ -56,13 +62,11 @@ def main():
         for t in th:
             t.join()
         wall = time.perf_counter() - t0
-        blocks = [p[0].stats()["aes_blocks"] for p in pairs]
-        print(f"round {r}: T-table {nA} clients alone {alone[0]*1e3:.1f} ms, bitsliced {nB} alone {alone[1]*1e3:.1f} ms, "
-              f"sum {sum(alone)*1e3:.1f} ms; concurrent wall {wall*1e3:.1f} ms "
+        print(f"round {r}: T-table v{args.vt} {nA} clients alone {alone[0]*1e3:.1f} ms "
+              f"({blocks[0]/alone[0]/1e9:.1f} G/s), bitsliced v{args.vb} {nB} alone {alone[1]*1e3:.1f} ms "
+              f"({blocks[1]/alone[1]/1e9:.1f} G/s); sequential {sum(blocks)/sum(alone)/1e9:.1f} G/s; "
+              f"concurrent wall {wall*1e3:.1f} ms = {sum(blocks)/wall/1e9:.1f} G/s "
               f"(T {both[0]*1e3:.1f}, B {both[1]*1e3:.1f})", flush=True)
-        for p in pairs:
-            p[0].reset_stats()
-            p[1].reset_stats()
 
 
 if __name__ == "__main__":

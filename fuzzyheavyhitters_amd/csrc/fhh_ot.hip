@@ -7,13 +7,15 @@
 //   sender   (base choice s):  q_i = G(k_i^{s_i}) ^ s_i u_i  =>  q_j = t_j ^ r_j s (columns)
 //   sender:    y_j^b = x_j^b ^ H(j, q_j ^ b s)        receiver:  x_j^{r_j} = y_j^{r_j} ^ H(j, t_j)
 //
-// G = AES-128-CTR under the row key (block c -> OTs 128 c .. 128 c + 127), H(j, x) = TCCR(x,
-// tweak_base + j) with pi = AES-128 under the zero key (as fhh_gc.hip). The 128 base OTs are
+// G = AES-128-CTR under the row key (block c -> OTs 128 c .. 128 c + 127), H(j, x) = scuttlebutt's
+// AesHash::cr_hash(j, x) = pi(x) ^ x (the correlation-robust hash ocelot's ALSZ applies to q_j,
+// q_j ^ s and t_j; j is not an input), pi = AES-128 under the zero key (as fhh_gc.hip): the
+// fixed-key AES + feed-forward of k_expand (aes0_mmo_tab, round keys as immediates). The 128 base OTs are
 // ideal (the host hands the sender k_i^{s_i}).
 //
 //   k_ot_recv_expand / k_ot_send_expand  one lane per (row, 128-OT block): 2 / 1 AES
 //   k_ot_transpose                        one lane per 32 OTs: 4 in-register 32x32 transposes
-//   k_ot_send_hash / k_ot_recv_hash       one lane per OT: 2 / 1 TCCR (4 / 2 AES)
+//   k_ot_send_hash / k_ot_recv_hash       one lane per OT: 2 / 1 cr_hash (2 / 1 AES)
 #include "fhh_internal.h"
 #include "aes_keyed.h"
 #include "bitslice.h"
@@ -43,36 +45,6 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
     for (int r = 0; r < 11; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) rk[r][c] = base[4 * r + c];
-}
-
-__device__ __forceinline__ void ot_zero_rk(uint32_t (&rk)[11][4]) {
-#pragma unroll
-    for (int r = 0; r < 11; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) rk[r][c] = ZERO_RK.w[r][c];
-}
-
-template <int NB>
-__device__ __forceinline__ void ot_tccr(uint32_t (&x)[NB][4], uint64_t tw, const uint32_t* tbl, uint32_t b0,
-                                        uint32_t b1, const uint32_t (&zrk)[11][4]) {
-    uint32_t p[NB][4], q[NB][4];
-#pragma unroll
-    for (int k = 0; k < NB; k++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) p[k][c] = x[k][c];
-    aes_rk<OtTab, NB>(p, tbl, b0, b1, zrk);
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-        q[k][0] = p[k][0] ^ (uint32_t)tw;
-        q[k][1] = p[k][1] ^ (uint32_t)(tw >> 32);
-        q[k][2] = p[k][2];
-        q[k][3] = p[k][3];
-    }
-    aes_rk<OtTab, NB>(q, tbl, b0, b1, zrk);
-#pragma unroll
-    for (int k = 0; k < NB; k++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) x[k][c] = q[k][c] ^ p[k][c];
 }
 
 // one lane per (row i, block c); nblk = mp / 128 is a multiple of 64, so a wave's lanes share
@@ -146,13 +118,11 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
     ot_fill(tbl_ot);
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
-    uint32_t zrk[11][4];
-    ot_zero_rk(zrk);
     const uint64_t m = ot_active(a);
     for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
         const uint4 q = a.Qt[j];
         uint32_t h[2][4] = {{q.x, q.y, q.z, q.w}, {q.x ^ a.s[0], q.y ^ a.s[1], q.z ^ a.s[2], q.w ^ a.s[3]}};
-        ot_tccr<2>(h, a.tweak_base + j, tbl_ot, b0, b1, zrk);
+        aes0_mmo_tab<DevOpsX, OtTab, 2>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
         const uint4 x0 = a.x0[j];
         const uint4 x1 = a.x1 ? a.x1[j]
                               : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
@@ -166,13 +136,11 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
     ot_fill(tbl_ot);
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
-    uint32_t zrk[11][4];
-    ot_zero_rk(zrk);
     const uint64_t m = ot_active(a);
     for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
         const uint4 t = a.Tt[j];
         uint32_t h[1][4] = {{t.x, t.y, t.z, t.w}};
-        ot_tccr<1>(h, a.tweak_base + j, tbl_ot, b0, b1, zrk);
+        aes0_mmo_tab<DevOpsX, OtTab, 1>(h, tbl_ot, b0, b1);
         const uint32_t r = (a.choices[j >> 5] >> (j & 31)) & 1u;
         const uint4 y = r ? a.Y1[j] : a.Y0[j];
         a.out[j] = make_uint4(y.x ^ h[0][0], y.y ^ h[0][1], y.z ^ h[0][2], y.w ^ h[0][3]);

@@ -320,7 +320,9 @@ int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t*
  * x_j^{choice_j}. kappa = 128 base OTs are ideal (the receiver's seed pairs base_seeds[i][0..1],
  * the sender's choice bits base_choice; the sender is handed base_seeds[i][s_i]). G = AES-128-CTR
  * under each seed (block c = LE128(c) gives OTs 128 c .. 128 c + 127, bit b of byte b / 8),
- * H(j, x) = TCCR(x, tweak_base + j) as in the GC. x1 == NULL: correlated OT, x1 = x0 ^ delta. */
+ * H(j, x) = scuttlebutt's cr_hash(j, x) = pi(x) ^ x, pi = AES-128 under the zero key (the hash
+ * ocelot's ALSZ applies; j is not an input, so tweak_base is accepted and ignored).
+ * x1 == NULL: correlated OT, x1 = x0 ^ delta. */
 typedef struct fhh_ot_batch {
     uint64_t m;
     const uint32_t* choices_dev;    /* receiver's choice bits, bit j % 32 of word j / 32       */
@@ -330,7 +332,7 @@ typedef struct fhh_ot_batch {
     uint8_t* out_dev;               /* receiver's messages [m][16]                             */
     uint8_t base_seeds[128][2][16];
     uint8_t base_choice[16];
-    uint64_t tweak_base;
+    uint64_t tweak_base;            /* ignored by cr_hash (kept for ABI stability)             */
 } fhh_ot_batch;
 int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* batch);
 /* Host buffers: choices [m] 0/1 bytes; optional transcript u_out [128][ceil(m/128)][16] (the

@@ -761,13 +761,23 @@ void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint
 /* collect.rs:437-471 (FE shares). Published scheme restated: kappa = */
 /* 128 base OTs (ideal here: the sender is handed k_i^{s_i}), G =     */
 /* AES-128-CTR under k (block c = LE128(c) gives OT bits 128c..+127),  */
-/* H(j, x) = TCCR(x, tweak_base + j) as the GC hash. Parity:          */
-/* functional (out_j = x_j^{r_j}); wire format unpinned.              */
+/* H(j, x) = cr_hash(j, x) = pi(x) ^ x (ot_cr_hash; tweak_base is    */
+/* not an input of it). Parity: functional (out_j = x_j^{r_j}); wire  */
+/* format unpinned.                                                   */
 /* ------------------------------------------------------------------ */
 static void ot_prg_block(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
     uint8_t ctr[16] = {0};
     for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
     aes128_encrypt_rk(rk, ctr, out);
+}
+
+/* Correlation-robust hash of the OT extension: scuttlebutt AesHash::cr_hash(i, x) = pi(x) ^ x,
+ * the index i is not an input (ocelot's ALSZ sender/receiver hash q_j, q_j ^ s, t_j with it);
+ * pi = AES-128 under the all-zero key (swanky's fixed AesHash key is not restatable). */
+static void ot_cr_hash(const uint8_t x[16], uint8_t out[16]) {
+    uint8_t px[16];
+    orc_aes128_zero_encrypt(x, px);
+    for (int k = 0; k < 16; k++) out[k] = px[k] ^ x[k];
 }
 
 /* choices: m bits (bit j of byte j/8); x1 NULL -> x1 = x0 ^ delta. Optional transcript:
@@ -818,8 +828,8 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
             if ((t[bit / 8] >> (bit % 8)) & 1) tj[i / 8] |= (uint8_t)(1u << (i % 8));
         }
         for (int k = 0; k < 16; k++) qs[k] = qj[k] ^ s[k];
-        gc_tccr(qj, tweak_base + (uint64_t)j, h0);
-        gc_tccr(qs, tweak_base + (uint64_t)j, h1);
+        ot_cr_hash(qj, h0);
+        ot_cr_hash(qs, h1);
         for (int k = 0; k < 16; k++) {
             const uint8_t a = x0[j * 16 + k];
             const uint8_t b = x1 ? x1[j * 16 + k] : (uint8_t)(a ^ delta[k]);
@@ -829,7 +839,7 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
         if (y0_out) memcpy(y0_out + j * 16, y0, 16);
         if (y1_out) memcpy(y1_out + j * 16, y1, 16);
         const int rj = (choices[j / 8] >> (j % 8)) & 1;
-        gc_tccr(tj, tweak_base + (uint64_t)j, ht);
+        ot_cr_hash(tj, ht);
         for (int k = 0; k < 16; k++) out[j * 16 + k] = (rj ? y1[k] : y0[k]) ^ ht[k];
     }
     if (u_out) memcpy(u_out, U, 128 * nblk * 16);

@@ -215,8 +215,12 @@ __host__ __device__ __forceinline__ void aes0_mmo_pair(uint32_t (&s)[NB][4], con
             za[c] = Ops::xor3(p, t[k], ZERO_RK.w[2][c]);
             zb[c] = Ops::xor3(p, tb, ZERO_RK.w[2][c]);
         }
-        // carry into byte 9 somewhere in the wave: B's counter differs in more bytes
-        if (Ops::any((a[2] & 0xFFu) == 0xFFu)) {
+        // carry into byte 9 somewhere in the wave (byte 8 = 0xFF): B's counter also differs in
+        // byte 9 = row 1 of column 2, which round 1 sends to output column 1. Fix-up exact for
+        // every lane whose carry stops at byte 9 (lanes without a carry cancel to zero): round 1
+        // column 1 gains one lookup pair, round 2 one row-(1 - c) term of column 1 per column.
+        // A carry past byte 9 (bytes 8-9 = 0xFFFF, 1/65536 per lane) redoes rounds 1-2 in full.
+        if (Ops::any((a[2] & 0xFFFFu) == 0xFFFFu)) {
             uint32_t u[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) u[c] = bb[c];
@@ -234,6 +238,14 @@ __host__ __device__ __forceinline__ void aes0_mmo_pair(uint32_t (&s)[NB][4], con
             }
 #pragma unroll
             for (int c = 0; c < 4; c++) zb[c] = u[c];
+        } else if (Ops::any((a[2] & 0xFFu) == 0xFFu)) {
+            const uint32_t yb1 = Ops::xor3(ya[1], Tab::template term<1>(tbl, b0, b1, a[2]),
+                                           Tab::template term<1>(tbl, b0, b1, bb[2]));
+            // output column c takes row k = (1 - c) & 3 of column 1: c = 0 k 1, c = 1 k 0, c = 2 k 3, c = 3 k 2
+            zb[0] = Ops::xor3(zb[0], Tab::template term<1>(tbl, b0, b1, ya[1]), Tab::template term<1>(tbl, b0, b1, yb1));
+            zb[1] = Ops::xor3(zb[1], Tab::template term<0>(tbl, b0, b1, ya[1]), Tab::template term<0>(tbl, b0, b1, yb1));
+            zb[2] = Ops::xor3(zb[2], Tab::template term<3>(tbl, b0, b1, ya[1]), Tab::template term<3>(tbl, b0, b1, yb1));
+            zb[3] = Ops::xor3(zb[3], Tab::template term<2>(tbl, b0, b1, ya[1]), Tab::template term<2>(tbl, b0, b1, yb1));
         }
 #pragma unroll
         for (int c = 0; c < 4; c++) {

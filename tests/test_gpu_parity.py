@@ -127,6 +127,50 @@ def test_level_states_bit_exact(kc, oracle, path, variant):
                 break
 
 
+@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT + 7],
+                         ids=["default-pair-aes", "generic-aes", "bitsliced-pair2"])
+@pytest.mark.parametrize("d", [1, 2])
+def test_prg_counter_carry_seeds(kc, oracle, variant, d):
+    """Root seeds whose byte 8 is 0xFF: the right child's counter (+1 in the upper u64 lane,
+    prg.rs:273-276) carries into byte 9, 11 or wraps bytes 8..15 — the carry fallback of the
+    sibling-pair AES and the bitsliced kernels' carry path — at level 0, every client pattern
+    in every wave. Seeds / t / y of the first levels equal the oracle's."""
+    from fuzzyheavyhitters_amd import workload
+    from fuzzyheavyhitters_amd.collection import sim_eq_count
+    n, L = 200, 32
+    wl = workload.zipf_workload(n, L, d, num_sites=4, seed=99)
+    roots = wl.root_seeds.copy()                      # [n][d][side][server][16]
+    pat = np.arange(n) % 5
+    roots[pat == 1, :, :, :, 8] = 0xFF                 # carry into byte 9
+    roots[pat == 2, :, :, :, 8:12] = 0xFF              # carry into byte 12
+    roots[pat == 3, :, :, :, 8:16] = 0xFF              # upper lane wraps to 0
+    roots[pat == 4, :, 0, :, 8] = 0xFF                 # left keys only
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, roots)
+    c0, c1 = make_pair(kc, wl.left, wl.right, roots)
+    if variant is not None:
+        c0.set_variant(variant)
+        c1.set_variant(variant)
+    c0.tree_init()
+    c1.tree_init()
+    s0, s1 = oracle.tree_init(k0), oracle.tree_init(k1)
+    parents = np.zeros(1, np.uint64)
+    for lvl in range(3):
+        o0, _ = oracle.level_expand(k0, s0, parents, lvl)
+        o1, _ = oracle.level_expand(k1, s1, parents, lvl)
+        C, _ = c0.tree_crawl()
+        c1.tree_crawl()
+        for c, o in ((c0, o0), (c1, o1)):
+            gs, gt, gy = c.export_states()
+            assert np.array_equal(gs, o.seed), f"seeds level {lvl}"
+            assert np.array_equal(gt, o.t) and np.array_equal(gy, o.y), f"t/y level {lvl}"
+        cnt = sim_eq_count(c0, c1, C)
+        keep = cnt >= 1
+        c0.tree_prune(keep)
+        c1.tree_prune(keep)
+        parents = np.nonzero(keep)[0].astype(np.uint64)
+        s0, s1 = o0, o1
+
+
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_sim_crawl_matches_golden(kc, path):
     from fuzzyheavyhitters_amd import sim_crawl

@@ -32,7 +32,7 @@ EXPORTS = [
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
     "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench",
-    "fhh_debug_launch_gaps",
+    "fhh_debug_launch_gaps", "fhh_wave_profile_arm", "fhh_wave_profile_launches",
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
     "fhh_comm_last_error",
@@ -217,6 +217,8 @@ def lib():
         "fhh_device_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i)]),
         "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
         "fhh_debug_launch_gaps": (i, [i, i, i, P(ctypes.c_double)]),
+        "fhh_wave_profile_arm": (i, [i, vp, ctypes.c_uint32]),
+        "fhh_wave_profile_launches": (i, [i, P(ctypes.c_uint32)]),
         "fhh_set_variant": (i, [vp, i]),
         "fhh_variant_info": (i, [i, ctypes.c_char_p, ctypes.c_size_t, P(i), P(i)]),
         "fhh_rccl_load": (i, [ctypes.c_char_p]),

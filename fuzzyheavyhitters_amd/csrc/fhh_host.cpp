@@ -444,25 +444,33 @@ int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
         J.group = 1;
         J.pad_ = 0;
         J.item_begin = 0;
+        J.split = J.n_live;
+        J.group_b = 1;
+        J.e_base = 0;
+        J.pad2_ = 0;
+        J.item_begin_b = 0;
     }
     return FHH_OK;
 }
 
 void finalize_launch(ExpandLaunch& L, int grid, int variant) {
-    uint64_t entry_words = 0;
-    for (uint32_t k = 0; k < L.njobs; k++) entry_words += (uint64_t)L.job[k].n_live * expand_unit(variant, L.job[k].nw);
+    // every job of a launch has the same client count (both servers hold the same clients)
     const uint64_t waves = (uint64_t)grid * (expand_threads(variant) / 64);
-    uint64_t g = entry_words / (2 * waves);
-    if (g < 1) g = 1;
-    if (g > expand_max_group(variant)) g = expand_max_group(variant);
-    uint64_t begin = 0;
+    uint32_t n_live[kMaxJobs] = {};
+    for (uint32_t k = 0; k < L.njobs; k++) n_live[k] = L.job[k].n_live;
+    ItemLayout lay;
+    item_layout(n_live, L.njobs, expand_unit(variant, L.job[0].nw), expand_max_group(variant), waves,
+                expand_tail_split(variant), lay);
     for (uint32_t k = 0; k < L.njobs; k++) {
         ExpandJob& J = L.job[k];
-        J.group = (uint32_t)g;
-        J.item_begin = begin;
-        begin += (uint64_t)expand_unit(variant, J.nw) * ((J.n_live + g - 1) / g);
+        J.group = lay.g;
+        J.group_b = lay.g_b;
+        J.split = lay.split[k];
+        J.item_begin = lay.begin_a[k];
+        J.item_begin_b = lay.begin_b[k];
     }
-    L.total_items = begin;
+    L.items_a = lay.items_a;
+    L.total_items = lay.total;
 }
 
 uint64_t launch_blocks(const fhh_ctx* ctx) {
@@ -1288,6 +1296,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.grid_waves = grid_waves;
         pa.unit = expand_unit(variant, c0->nw);
         pa.max_group = expand_max_group(variant);
+        pa.tail_split = expand_tail_split(variant) ? 1u : 0u;
         HIP_TRY(c0, launch_prune(pa, c0->stream));
         lv++;
         if (lv % kBatch == 0 || lv == levels) {

@@ -45,6 +45,14 @@ struct ExpandJob {
     uint32_t group;         // entries per work item (CW reuse factor)
     uint32_t pad_;
     uint64_t item_begin;
+    // end-of-launch phase (item_layout): entries [split, n_live) as items of group_b entries,
+    // numbered from item_begin_b after every job's bulk items; e_base = first entry of the
+    // segment an item belongs to (set by the kernel)
+    uint32_t split;
+    uint32_t group_b;
+    uint32_t e_base;
+    uint32_t pad2_;
+    uint64_t item_begin_b;
 };
 
 // Device-resident level loop (fhh_sim_crawl with the GPU loop): the frontier sizes live in
@@ -60,16 +68,68 @@ struct LoopCtl {
     uint32_t C;                 // pending children (F << d)
     uint32_t n_live[kMaxDims];  // live entries per dim (same for both servers)
     uint32_t group;             // entries per work item for the next k_expand
-    uint32_t pad_;
+    uint32_t group_b;           // entries per end-phase item
     uint64_t item_begin[kMaxJobs];
     uint64_t total_items;
+    uint64_t items_a;           // bulk items of all jobs precede the end-phase items
+    uint64_t item_begin_b[kMaxJobs];
+    uint32_t split[kMaxJobs];
 };
+
+// k_expand work decomposition, shared by the host (finalize_launch) and the device loop
+// (k_prune, k_loop_init). Bulk: items of g entries x one word unit (64 clients), g sized so
+// each wave gets >= 2 items, capped at max_group. A launch ends when its slowest wave finishes
+// its last item, and with 16-entry items that tail averaged 8.7 % of k_expand's time
+// (tools/tail_profile.py). So about one item per wave of work at the end is re-cut as items
+// of g_b = min(g, kTailGroup) entries, dealt after every job's bulk items. The end phase must
+// not outrun the single work counter (≈ 88 dequeues/µs): 4-entry items at 2 per wave did
+// (8 % slower), hence 8 entries and one item per wave.
+constexpr uint32_t kTailGroup = 8;
+struct ItemLayout {
+    uint32_t g, g_b;
+    uint64_t items_a, total;
+    uint64_t begin_a[kMaxJobs], begin_b[kMaxJobs];
+    uint32_t split[kMaxJobs];
+};
+__host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njobs, uint32_t unit, uint32_t max_group,
+                                            uint64_t grid_waves, bool tail_split, ItemLayout& L) {
+    uint64_t entries = 0;
+    for (uint32_t k = 0; k < njobs; k++) entries += n_live[k];
+    const uint64_t entry_words = entries * unit;
+    uint64_t g = entry_words / (2 * grid_waves);
+    g = g < 1 ? 1 : (g > max_group ? max_group : g);
+    const uint64_t gb = g < kTailGroup ? g : kTailGroup;
+    L.g = (uint32_t)g;
+    L.g_b = (uint32_t)gb;
+    // end-phase entries wanted in all: one item of g_b entries per wave
+    const uint64_t want = (tail_split && gb < g) ? (grid_waves * gb + unit - 1) / unit : 0;
+    for (uint32_t k = 0; k < njobs; k++) {
+        uint32_t split = n_live[k];
+        if (want && entries) {
+            const uint64_t bk = (n_live[k] * want + entries - 1) / entries;   // job's share, rounded up
+            split = bk >= n_live[k] ? 0u : (uint32_t)(n_live[k] - bk);
+        }
+        L.split[k] = split;
+    }
+    uint64_t begin = 0;
+    for (uint32_t k = 0; k < njobs; k++) {
+        L.begin_a[k] = begin;
+        begin += (uint64_t)unit * ((L.split[k] + g - 1) / g);
+    }
+    L.items_a = begin;
+    for (uint32_t k = 0; k < njobs; k++) {
+        L.begin_b[k] = begin;
+        begin += (uint64_t)unit * ((n_live[k] - L.split[k] + gb - 1) / gb);
+    }
+    L.total = begin;
+}
 
 struct ExpandLaunch {
     ExpandJob job[kMaxJobs];
     uint32_t njobs;
     uint32_t jobs_per_ctx;      // = d (LoopCtl::n_live index = job % jobs_per_ctx)
     uint64_t total_items;
+    uint64_t items_a;           // host-driven launches: bulk items (== total_items without a tail phase)
     const LoopCtl* ctl;         // non-null: n_live / group / item_begin / total_items from here
 };
 
@@ -149,6 +209,7 @@ struct PruneArgs {
     uint64_t grid_waves;        // persistent k_expand waves (for the group size)
     uint32_t unit;              // k_expand items per entry group (nw; bitsliced: 4 * ceil(nw / 32))
     uint32_t max_group;         // entries per item cap (8; bitsliced: 1)
+    uint32_t tail_split;        // item_layout end phase (expand_tail_split)
 };
 
 struct KeygenArgs {
@@ -293,10 +354,13 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // entries per work item (CW reuse and counter traffic vs. end-of-level tail): variant 29 is
 // variant 3 drawing the next item one entry ahead; 30 / 31 are variant 3 with up to 16 / 32
 // entries per item; 32 / 33 store child seeds nontemporally with up to 8 / 16 entries per item;
-// 34 / 35 are 33 / 32 with the sibling-pair AES (aes0_mmo_pair)
+// 34 / 35 are 33 / 32 with the sibling-pair AES (aes0_mmo_pair); 36 is 34 + wave timeline;
+// 37 / 38 are 34 / 36 with the end-of-launch phase of small items (item_layout)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34) ? 16u : variant == 31 ? 32u : 8u;
+    return (variant == 30 || variant == 33 || variant == 34 || variant == 36 || variant == 37 || variant == 38)
+               ? 16u : variant == 31 ? 32u : 8u;
 }
+inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }
 
 }  // namespace fhh

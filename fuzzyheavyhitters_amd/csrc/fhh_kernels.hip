@@ -13,6 +13,7 @@
 //   k_keys_from_aos add_key wire layout -> SoA device layout
 #include "fhh_internal.h"
 #include "expand_kernel.h"
+#include "../../include/fhh.h"
 
 namespace fhh {
 
@@ -61,7 +62,7 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
         for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
     }
 
-    const uint32_t e_begin = g * J.group;
+    const uint32_t e_begin = J.e_base + g * J.group;
     const uint32_t e_end = min(e_begin + J.group, J.n_live);
     for (uint32_t e = e_begin; e < e_end; e++) {
         const uint32_t src = J.live[e];
@@ -139,7 +140,7 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
 #pragma unroll
         for (int b = 0; b < 4; b++) cwp[s][b] = J.cw_bits[((krow + s) * 4 + b) * nw + w];
     }
-    const uint32_t e_begin = g * J.group;
+    const uint32_t e_begin = J.e_base + g * J.group;
     const uint32_t e_end = min(e_begin + J.group, J.n_live);
     if (e_begin >= e_end) return;
     uint4 sd[2];
@@ -201,16 +202,27 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
     }
 }
 
+// Wave timeline of the profiling variant (FLAGS bit 3, tools/tail_profile.py): per launch and
+// wave {start after the LDS fill, exit, items} in 100 MHz s_memrealtime ticks, written by lane 0
+// with vector stores into a caller buffer of g_wprof_cap launches; the last wave out bumps the
+// launch index (the same exit detection that re-arms the work counter).
+__device__ uint64_t* g_wprof_buf = nullptr;
+__device__ uint32_t g_wprof_cap = 0;
+__device__ uint32_t g_wprof_launch = 0;
+
 // FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores,
-// bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair)
+// bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline
 template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     constexpr bool AHEAD = (FLAGS & 1) != 0;
     constexpr bool NT = (FLAGS & 2) != 0;
     constexpr bool PAIR = (FLAGS & 4) != 0;
+    constexpr bool PROF = (FLAGS & 8) != 0;
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
+    uint64_t prof_t0 = 0, prof_items = 0;
+    if constexpr (PROF) prof_t0 = wall_clock64();
 
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;
@@ -226,10 +238,16 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         if (lane == 0) v = atomicAdd(work_counter, 1u);
         item = __builtin_amdgcn_readfirstlane(v);
     }
+    const uint64_t items_a = ctl ? ctl->items_a : a.items_a;
     while (item < total) {
+        // bulk items [0, items_a), then the end phase (item_layout): same job order in each
+        const bool tail = item >= items_a;
         uint32_t ji = 0;
         if (ctl) {
-            while (ji + 1 < a.njobs && item >= ctl->item_begin[ji + 1]) ji++;
+            const uint64_t* beg = tail ? ctl->item_begin_b : ctl->item_begin;
+            while (ji + 1 < a.njobs && item >= beg[ji + 1]) ji++;
+        } else if (tail) {
+            while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin_b) ji++;
         } else {
             while (ji + 1 < a.njobs && item >= a.job[ji + 1].item_begin) ji++;
         }
@@ -237,9 +255,21 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         if (ctl) {
             J.n_live = ctl->n_live[ji % a.jobs_per_ctx];
             J.group = ctl->group;
+            J.group_b = ctl->group_b;
+            J.split = ctl->split[ji];
             J.item_begin = ctl->item_begin[ji];
+            J.item_begin_b = ctl->item_begin_b[ji];
+        }
+        if (tail) {
+            J.e_base = J.split;
+            J.group = J.group_b;
+            J.item_begin = J.item_begin_b;
+        } else {
+            J.e_base = 0;
+            J.n_live = J.split;
         }
         uint32_t nxt = 0;
+        if constexpr (PROF) prof_items++;
         if constexpr (PF) expand_item_pf<Tab>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
         else expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
@@ -253,13 +283,40 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     }
     // dynamic mode: every wave drew exactly one item past the end; the last wave to leave
     // re-arms the counter for the next launch (no memset between launches)
+    if constexpr (PROF) {
+        const uint64_t t1 = wall_clock64();
+        const uint32_t L = g_wprof_launch;
+        if (lane == 0 && g_wprof_buf && L < g_wprof_cap) {
+            uint64_t* r = g_wprof_buf + ((uint64_t)L * nwaves + (uint64_t)blockIdx.x * wpb + wave_id_uniform()) * 3;
+            r[0] = prof_t0;
+            r[1] = t1;
+            r[2] = prof_items;
+        }
+    }
     if (work_counter && lane == 0) {
         const uint32_t done = atomicAdd(work_counter + 1, 1u);
         if (done + 1 == (uint32_t)nwaves) {
+            if constexpr (PROF) atomicAdd(&g_wprof_launch, 1u);
             atomicExch(work_counter, 0u);
             atomicExch(work_counter + 1, 0u);
         }
     }
+}
+
+// arm the wave timeline: buf = device buffer of cap launches x grid waves x 3 u64 (NULL disarms)
+extern "C" int fhh_wave_profile_arm(int device, uint64_t* buf, uint32_t cap) {
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    const uint32_t zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wprof_buf), &buf, sizeof buf) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_wprof_cap), &cap, sizeof cap) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_wprof_launch), &zero, sizeof zero) != hipSuccess)
+        return FHH_E_HIP;
+    return FHH_OK;
+}
+
+extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
+    if (hipSetDevice(device) != hipSuccess || !launches) return FHH_E_HIP;
+    return hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_wprof_launch), sizeof *launches) == hipSuccess ? FHH_OK : FHH_E_HIP;
 }
 
 // Variant table (fhh_set_variant). Order matters: index = variant id.
@@ -286,7 +343,10 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     X(32, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
     X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
     X(34, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
-    X(35, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)
+    X(35, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
+    X(36, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 14)   \
+    X(37, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
+    X(38, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 14)
 
 struct VariantInfo {
     const void* fn;
@@ -317,7 +377,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 9; }
+int expand_variant_count() { return kBsVariant + kBsCount + 12; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

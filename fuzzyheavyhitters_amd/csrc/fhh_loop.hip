@@ -151,22 +151,25 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
         a.sizes_out[2] = 1;
         return;
     }
-    // 3. next level's sizes and k_expand work decomposition (as finalize_launch on the host)
-    uint64_t entry_words = 0;
+    // 3. next level's sizes and k_expand work decomposition (item_layout, as finalize_launch)
+    uint32_t job_live[kMaxJobs] = {};
     for (uint32_t j = 0; j < d; j++) {
         ctl->n_live[j] = n_live_new[j];
         a.sizes_out[4 + j] = n_live_new[j];
-        entry_words += (uint64_t)n_live_new[j] * a.unit * a.nctx;
     }
-    uint64_t g = entry_words / (2 * a.grid_waves);
-    g = g < 1 ? 1 : (g > a.max_group ? a.max_group : g);
-    uint64_t begin = 0;
-    for (uint32_t k = 0; k < a.nctx * a.njobs_per_ctx; k++) {
-        ctl->item_begin[k] = begin;
-        begin += (uint64_t)a.unit * ((n_live_new[k % a.njobs_per_ctx] + g - 1) / g);
+    const uint32_t njobs = a.nctx * a.njobs_per_ctx;
+    for (uint32_t k = 0; k < njobs; k++) job_live[k] = n_live_new[k % a.njobs_per_ctx];
+    ItemLayout lay;
+    item_layout(job_live, njobs, a.unit, a.max_group, a.grid_waves, a.tail_split != 0, lay);
+    for (uint32_t k = 0; k < njobs; k++) {
+        ctl->item_begin[k] = lay.begin_a[k];
+        ctl->item_begin_b[k] = lay.begin_b[k];
+        ctl->split[k] = lay.split[k];
     }
-    ctl->group = (uint32_t)g;
-    ctl->total_items = begin;
+    ctl->group = lay.g;
+    ctl->group_b = lay.g_b;
+    ctl->items_a = lay.items_a;
+    ctl->total_items = lay.total;
     ctl->F = nf;
     ctl->C = nf << d;
 }
@@ -219,15 +222,21 @@ __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t ma
         pos0[j] = 0;
         lv[j][0] = 0;
     }
-    uint64_t g = ((uint64_t)unit * nctx * d) / (2 * grid_waves);
-    g = g < 1 ? 1 : (g > max_group ? max_group : g);
-    uint64_t begin = 0;
-    for (uint32_t k = 0; k < nctx * njobs_per_ctx; k++) {
-        ctl->item_begin[k] = begin;
-        begin += (uint64_t)unit * ((1 + g - 1) / g);
+    // level 0: one root entry per job (no end phase: far fewer items than waves)
+    const uint32_t njobs = nctx * njobs_per_ctx;
+    uint32_t job_live[kMaxJobs];
+    for (uint32_t k = 0; k < kMaxJobs; k++) job_live[k] = 1;
+    ItemLayout lay;
+    item_layout(job_live, njobs, unit, max_group, grid_waves, false, lay);
+    for (uint32_t k = 0; k < njobs; k++) {
+        ctl->item_begin[k] = lay.begin_a[k];
+        ctl->item_begin_b[k] = lay.begin_b[k];
+        ctl->split[k] = lay.split[k];
     }
-    ctl->group = (uint32_t)g;
-    ctl->total_items = begin;
+    ctl->group = lay.g;
+    ctl->group_b = lay.g_b;
+    ctl->items_a = lay.items_a;
+    ctl->total_items = lay.total;
 }
 
 hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,

@@ -376,6 +376,11 @@ int fhh_microbench(int device, int which, double* rate);
  * 1 x 1024 (expand -> prune); 3 -> 1 x 1024; 4 / 5 -> alternating a 64 MiB writer (normal /
  * nontemporal stores) with 1 x 1024; 6 / 7 -> as 2 / 4 captured in a hipGraph and replayed. */
 int fhh_debug_launch_gaps(int device, int which, int reps, double* us_per_kernel);
+/* Wave timeline of the profiling k_expand variant 36 (tools/tail_profile.py): arm with a device
+ * buffer of cap launches x grid waves x 3 u64 ({start after the LDS table fill, exit, items},
+ * 100 MHz s_memrealtime ticks; buf NULL disarms); launches = launches recorded so far. */
+int fhh_wave_profile_arm(int device, uint64_t* buf, uint32_t cap);
+int fhh_wave_profile_launches(int device, uint32_t* launches);
 
 /* Device properties the library targets (gfx950). */
 int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus);

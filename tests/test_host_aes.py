@@ -37,3 +37,14 @@ def test_aes_bs_generator_check():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_aes_bs.py"), "--check-only"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_item_layout_host(tmp_path):
+    """k_expand's two-phase work decomposition covers every (job, entry, word) exactly once."""
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "item_layout"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17",
+                    os.path.join(ROOT, "tests", "host", "item_layout_host_test.cpp"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "OK", out.stdout + out.stderr

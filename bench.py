@@ -332,14 +332,30 @@ def main():
         valu_tops = blocks_per_launch * VALU_OPS_PER_BLOCK / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
         hbm_gbps = blocks_per_launch * HBM_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         traffic = None
+        pmc_rates = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_expand.json")
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))
                 if pmc.get("config") == f"n{n_local}_L{args.data_len}_d{args.dims}":
                     traffic = pmc.get("hbm_bytes_per_launch")
+                    # executed (not algorithmic) rates of the profiled k_expand launches, from the
+                    # committed rocprofv3 PMC passes (tools/profile.sh + tools/pmc_summary.py)
+                    t = pmc["k_expand_avg_ns"] * 1e-9
+                    pmc_rates = {
+                        "source": f"profiles/pmc_expand.json ({pmc.get('tag')})",
+                        "valu_lane_ops_per_s": pmc["sq_insts_valu_per_launch"] * 64 / t,
+                        "valu_frac": pmc["sq_insts_valu_per_launch"] * 64 / t / (VALU_PEAK_TOPS * 1e12),
+                        "lds_bytes_per_s": pmc["sq_insts_lds_per_launch"] * 256 / t,
+                        "lds_frac": pmc["sq_insts_lds_per_launch"] * 256 / t / (LDS_PEAK_GBPS * 1e9),
+                        "hbm_bytes_per_s": traffic / t,
+                        "hbm_frac": traffic / t / (HBM_PEAK_GBPS * 1e9),
+                        "lds_insts_per_block": pmc["sq_insts_lds_per_launch"] * 64 / blocks_per_launch,
+                        "valu_insts_per_block": pmc["sq_insts_valu_per_launch"] * 64 / blocks_per_launch,
+                        "effective_clock_ghz": pmc.get("effective_clock_ghz"),
+                    }
             except Exception:
-                traffic = None
+                traffic, pmc_rates = None, None
         out = {
             "metric": "client x prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients",
             "value": blocks / elapsed,
@@ -380,6 +396,7 @@ def main():
             "roofline_hbm": {"achieved": hbm_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": hbm_gbps / HBM_PEAK_GBPS,
                              "algorithmic": f"{HBM_BYTES_PER_BLOCK} B per AES block (SURVEY 8d)"},
+            "pmc_executed": pmc_rates,
         }
         if args.microbench:
             import ctypes

@@ -46,4 +46,48 @@ __device__ __forceinline__ void aes_rk(uint32_t (&s)[NB][4], const uint32_t* tbl
         }
 }
 
+// s <- AES_rk0(s) for blocks [0, Q) and AES_rk1(s) for blocks [Q, 2Q): two uniform key
+// schedules (the OT receiver's row keys k_i^0, k_i^1) with all 2Q blocks in lockstep
+template <class Tab, int Q>
+__device__ __forceinline__ void aes_rk2(uint32_t (&s)[2 * Q][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                        const uint32_t (&rk0)[11][4], const uint32_t (&rk1)[11][4]) {
+    constexpr int NB = 2 * Q;
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[q][c] = s[q][c] ^ (q < Q ? rk0[0][c] : rk1[0][c]);
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                y[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, q < Q ? rk0[r][c] : rk1[r][c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = y[q][c];
+    }
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi),
+                                    q < Q ? rk0[10][c] : rk1[10][c]);
+        }
+}
+
 }  // namespace fhh

@@ -47,50 +47,74 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
         for (int c = 0; c < 4; c++) rk[r][c] = base[4 * r + c];
 }
 
-// one lane per (row i, block c); nblk = mp / 128 is a multiple of 64, so a wave's lanes share
-// the row and its key schedules are uniform (scalar loads)
+// one wave per (row i, kOtSlices consecutive 64-block slices): lane l computes blocks
+// c = c0 + 64 q + l, q < kOtSlices, in lockstep (2 kOtSlices blocks for the receiver's two keys,
+// kOtSlices for the sender). nblk = mp / 128 is a multiple of 64, so a slice is wholly inside or
+// outside the row and the row's key schedules are uniform (scalar loads)
+constexpr int kOtSlices = 2;
 template <bool RECV>
 __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     extern __shared__ uint32_t tbl_ot[];
     ot_fill(tbl_ot);
     uint32_t b0, b1;
-    OtTab::bases(threadIdx.x & 63, b0, b1);
+    const uint32_t lane = threadIdx.x & 63;
+    OtTab::bases(lane, b0, b1);
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
-    const uint64_t total = 128 * nblk;
-    for (uint64_t base = (uint64_t)blockIdx.x * kOtThreads; base < total; base += (uint64_t)gridDim.x * kOtThreads) {
-        const uint64_t idx = base + threadIdx.x;
-        const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(idx / nblk));
-        const uint64_t c = idx - (uint64_t)i * nblk;
-        if (c >= nblk_act) continue;
-        uint32_t s[RECV ? 2 : 1][4];
-#pragma unroll
-        for (int k = 0; k < (RECV ? 2 : 1); k++) {
-            s[k][0] = (uint32_t)c;
-            s[k][1] = (uint32_t)(c >> 32);
-            s[k][2] = 0u;
-            s[k][3] = 0u;
-        }
+    const uint64_t tiles_per_row = (nblk + 64 * kOtSlices - 1) / (64 * kOtSlices);
+    const uint64_t tiles = 128 * tiles_per_row;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
+    for (uint64_t t = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6); t < tiles; t += nwaves) {
+        const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_row));
+        const uint64_t c0 = (t - (uint64_t)i * tiles_per_row) * 64 * kOtSlices;
+        if (c0 >= nblk_act) continue;   // wave-uniform
         if (RECV) {
             uint32_t rk0[11][4], rk1[11][4];
             ld_rk(a.rk + (size_t)i * 44, rk0);
             ld_rk(a.rk + (size_t)(128 + i) * 44, rk1);
-            uint32_t g0[1][4] = {{s[0][0], s[0][1], s[0][2], s[0][3]}};
-            uint32_t g1[1][4] = {{s[0][0], s[0][1], s[0][2], s[0][3]}};
-            aes_rk<OtTab, 1>(g0, tbl_ot, b0, b1, rk0);
-            aes_rk<OtTab, 1>(g1, tbl_ot, b0, b1, rk1);
-            const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
-            a.T[(uint64_t)i * nblk + c] = make_uint4(g0[0][0], g0[0][1], g0[0][2], g0[0][3]);
-            a.U[(uint64_t)i * nblk + c] = make_uint4(g0[0][0] ^ g1[0][0] ^ r.x, g0[0][1] ^ g1[0][1] ^ r.y,
-                                                     g0[0][2] ^ g1[0][2] ^ r.z, g0[0][3] ^ g1[0][3] ^ r.w);
+            uint32_t g[2 * kOtSlices][4];
+#pragma unroll
+            for (int q = 0; q < 2 * kOtSlices; q++) {
+                const uint64_t c = c0 + 64 * (q % kOtSlices) + lane;
+                g[q][0] = (uint32_t)c;
+                g[q][1] = (uint32_t)(c >> 32);
+                g[q][2] = 0u;
+                g[q][3] = 0u;
+            }
+            aes_rk2<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rk0, rk1);
+#pragma unroll
+            for (int q = 0; q < kOtSlices; q++) {
+                const uint64_t c = c0 + 64 * q + lane;
+                if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
+                const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
+                const uint32_t* x0 = g[q];
+                const uint32_t* x1 = g[kOtSlices + q];
+                a.T[(uint64_t)i * nblk + c] = make_uint4(x0[0], x0[1], x0[2], x0[3]);
+                a.U[(uint64_t)i * nblk + c] = make_uint4(x0[0] ^ x1[0] ^ r.x, x0[1] ^ x1[1] ^ r.y,
+                                                         x0[2] ^ x1[2] ^ r.z, x0[3] ^ x1[3] ^ r.w);
+            }
         } else {
             uint32_t rks[11][4];
             ld_rk(a.rk + (size_t)(256 + i) * 44, rks);
-            aes_rk<OtTab, 1>(reinterpret_cast<uint32_t(&)[1][4]>(s), tbl_ot, b0, b1, rks);
+            uint32_t g[kOtSlices][4];
+#pragma unroll
+            for (int q = 0; q < kOtSlices; q++) {
+                const uint64_t c = c0 + 64 * q + lane;
+                g[q][0] = (uint32_t)c;
+                g[q][1] = (uint32_t)(c >> 32);
+                g[q][2] = 0u;
+                g[q][3] = 0u;
+            }
+            aes_rk<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rks);
             const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (si) u = a.U[(uint64_t)i * nblk + c];
-            a.Q[(uint64_t)i * nblk + c] = make_uint4(s[0][0] ^ u.x, s[0][1] ^ u.y, s[0][2] ^ u.z, s[0][3] ^ u.w);
+#pragma unroll
+            for (int q = 0; q < kOtSlices; q++) {
+                const uint64_t c = c0 + 64 * q + lane;
+                if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
+                uint4 u = make_uint4(0, 0, 0, 0);
+                if (si) u = a.U[(uint64_t)i * nblk + c];
+                a.Q[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
+            }
         }
     }
 }
@@ -216,7 +240,7 @@ hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
     static int done = 0;
     hipError_t e = ot_set_lds((const void*)k_ot_expand<true>, &done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128), kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / kOtSlices, kOtThreads)), dim3(kOtThreads), kOtLds,
                        stream, a);
     return hipGetLastError();
 }
@@ -225,7 +249,7 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
     static int done = 0;
     hipError_t e = ot_set_lds((const void*)k_ot_expand<false>, &done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128), kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / kOtSlices, kOtThreads)), dim3(kOtThreads), kOtLds,
                        stream, a);
     return hipGetLastError();
 }

@@ -108,5 +108,9 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
         for C in lc:
             res.counts.append(counts[off:off + int(C)].copy())
             off += int(C)
-    res.final = c0.final_shares()
+    if mode == "fe":
+        # the leader's output: v0 - v1 mod p of the two servers' FieldElm shares (collect.rs:1007-1029)
+        res.final = KeyCollection.final_values(c0.final_shares(), c1.final_shares())
+    else:
+        res.final = c0.final_shares()   # plaintext harness: server 0 holds the counts
     return res

@@ -171,6 +171,25 @@ def test_prg_counter_carry_seeds(kc, oracle, variant, d):
         s0, s1 = o0, o1
 
 
+@pytest.mark.parametrize("d,ball,thr", [(3, 0, 0.01), (3, 1, 0.03), (4, 0, 0.01), (4, 1, 0.03)])
+@pytest.mark.parametrize("mode", ["count", "fe"])
+def test_crawl_three_and_four_dims(kc, oracle, d, ball, thr, mode):
+    """n_dims 3 and 4 (kMaxDims; the reference takes any n_dims, collect.rs:94-119): every
+    level's child counts (or FE sums), the heavy hitters and their values equal the oracle's;
+    ball 1 grows the last levels to 2^d x thousands of children."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(60, 32, d, num_sites=3, seed=11, ball_size=ball)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    ref = oracle.crawl(k0, k1, thr, mode=mode, sim_seed=5)
+    c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
+    res = sim_crawl(c0, c1, thr, mode=mode, prf_seed=5)
+    assert list(res.level_children) == list(ref.n_children)
+    assert np.array_equal(np.concatenate(res.counts), np.concatenate([np.asarray(c, np.uint64) for c in ref.counts]))
+    got = [tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final]
+    assert got == [tuple(tuple(int(x) for x in pj) for pj in p) for p in ref.final_paths]
+    assert [int(r.value) for r in res.final] == [int(v) for v in ref.final_values]
+
+
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_sim_crawl_matches_golden(kc, path):
     from fuzzyheavyhitters_amd import sim_crawl
@@ -184,13 +203,12 @@ def test_sim_crawl_matches_golden(kc, path):
     assert np.array_equal(counts, g["counts"])
     paths = np.array([r.path for r in res.final], np.uint8).reshape(-1, d, L)
     assert np.array_equal(paths, g["final_paths"])
-    if mode == "count":
-        assert [r.value for r in res.final] == [int(x) for x in g["final_values"]]
-    else:
-        # final_shares values are server 0's unreduced FieldElm sums; leader's final_values
+    # count mode: server 0's plaintext counts; fe mode: the leader's final_values of the two
+    # servers' FieldElm shares (sim_crawl applies collect.rs:1007-1029)
+    assert [r.value for r in res.final] == [int(x) for x in g["final_values"]]
+    if mode == "fe":
         from fuzzyheavyhitters_amd import KeyCollection
-        r1 = c1.final_shares()
-        fv = KeyCollection.final_values(res.final, r1)
+        fv = KeyCollection.final_values(c0.final_shares(), c1.final_shares())
         assert [r.value for r in fv] == [int(x) for x in g["final_values"]]
     st = c0.stats()
     assert st["levels"] == L

@@ -95,7 +95,7 @@ def test_workload_shard_slices_are_consistent():
     assert np.array_equal(np.concatenate([a.root_seeds, b.root_seeds]), full.root_seeds)
 
 
-@pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
+@pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2", "zipf_d3_ball1", "zipf_d4_point"])
 def test_plaintext_crawl_equals_oracle(oracle, kind):
     """workload.plaintext_crawl (bit-packed, no crypto) reproduces the oracle's per-level
     counts and final heavy hitters — it is then the full-size check of the GPU crawl."""
@@ -103,6 +103,12 @@ def test_plaintext_crawl_equals_oracle(oracle, kind):
     if kind == "zipf_d1":
         wl = workload.zipf_workload(300, 40, 1, num_sites=8, seed=3)
         thr = 0.02
+    elif kind == "zipf_d3_ball1":
+        wl = workload.zipf_workload(60, 32, 3, num_sites=3, seed=11, ball_size=1)
+        thr = 0.03
+    elif kind == "zipf_d4_point":
+        wl = workload.zipf_workload(60, 32, 4, num_sites=3, seed=11, ball_size=0)
+        thr = 0.01
     else:
         wl = workload.coords_workload(800, ball_size=3, num_centroids=30, side_km=4.0)
         thr = 0.01

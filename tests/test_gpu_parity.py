@@ -190,6 +190,27 @@ def test_crawl_three_and_four_dims(kc, oracle, d, ball, thr, mode):
     assert [int(r.value) for r in res.final] == [int(v) for v in ref.final_values]
 
 
+@pytest.mark.parametrize("L", [1, 2, 7, 37])
+@pytest.mark.parametrize("d", [1, 2])
+@pytest.mark.parametrize("mode", ["count", "fe"])
+def test_crawl_odd_data_len(kc, oracle, L, d, mode):
+    """data_len 1 (only tree_crawl_last), 2, 7 and 37 (not a multiple of 8 or 32): keys of the
+    truncated interval bit strings (l <= r prefixes stay ordered); crawl = oracle."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(65, 40, d, num_sites=4, seed=21, ball_size=2)
+    left = np.ascontiguousarray(wl.left[:, :, :L])
+    right = np.ascontiguousarray(wl.right[:, :, :L])
+    k0, k1 = oracle.gen_keys(left, right, wl.root_seeds)
+    ref = oracle.crawl(k0, k1, 0.03, mode=mode, sim_seed=3)
+    c0, c1 = make_pair(kc, left, right, wl.root_seeds)
+    res = sim_crawl(c0, c1, 0.03, mode=mode, prf_seed=3)
+    assert list(res.level_children) == list(ref.n_children)
+    assert np.array_equal(np.concatenate(res.counts), np.concatenate([np.asarray(c, np.uint64) for c in ref.counts]))
+    got = [tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final]
+    assert got == [tuple(tuple(int(x) for x in pj) for pj in p) for p in ref.final_paths]
+    assert [int(r.value) for r in res.final] == [int(v) for v in ref.final_values]
+
+
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_sim_crawl_matches_golden(kc, path):
     from fuzzyheavyhitters_amd import sim_crawl

@@ -211,13 +211,16 @@ __device__ uint32_t g_wprof_cap = 0;
 __device__ uint32_t g_wprof_launch = 0;
 
 // FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores,
-// bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline
+// bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline,
+// bit 4 = decode the end-phase items of item_layout (only the variants that lay them out:
+// the extra decode state made the 1024-thread kernel spill)
 template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     constexpr bool AHEAD = (FLAGS & 1) != 0;
     constexpr bool NT = (FLAGS & 2) != 0;
     constexpr bool PAIR = (FLAGS & 4) != 0;
     constexpr bool PROF = (FLAGS & 8) != 0;
+    constexpr bool TAIL = (FLAGS & 16) != 0;
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
@@ -238,10 +241,10 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         if (lane == 0) v = atomicAdd(work_counter, 1u);
         item = __builtin_amdgcn_readfirstlane(v);
     }
-    const uint64_t items_a = ctl ? ctl->items_a : a.items_a;
+    const uint64_t items_a = TAIL ? (ctl ? ctl->items_a : a.items_a) : total;
     while (item < total) {
         // bulk items [0, items_a), then the end phase (item_layout): same job order in each
-        const bool tail = item >= items_a;
+        const bool tail = TAIL && item >= items_a;
         uint32_t ji = 0;
         if (ctl) {
             const uint64_t* beg = tail ? ctl->item_begin_b : ctl->item_begin;
@@ -255,18 +258,22 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         if (ctl) {
             J.n_live = ctl->n_live[ji % a.jobs_per_ctx];
             J.group = ctl->group;
-            J.group_b = ctl->group_b;
-            J.split = ctl->split[ji];
             J.item_begin = ctl->item_begin[ji];
-            J.item_begin_b = ctl->item_begin_b[ji];
+            if constexpr (TAIL) {
+                J.group_b = ctl->group_b;
+                J.split = ctl->split[ji];
+                J.item_begin_b = ctl->item_begin_b[ji];
+            }
         }
-        if (tail) {
-            J.e_base = J.split;
-            J.group = J.group_b;
-            J.item_begin = J.item_begin_b;
-        } else {
-            J.e_base = 0;
-            J.n_live = J.split;
+        J.e_base = 0;
+        if constexpr (TAIL) {
+            if (tail) {
+                J.e_base = J.split;
+                J.group = J.group_b;
+                J.item_begin = J.item_begin_b;
+            } else {
+                J.n_live = J.split;
+            }
         }
         uint32_t nxt = 0;
         if constexpr (PROF) prof_items++;
@@ -345,8 +352,11 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(34, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
     X(35, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
     X(36, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 14)   \
-    X(37, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
-    X(38, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 14)
+    X(37, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 22)   \
+    X(38, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 30)   \
+    X(39, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 6)     \
+    X(40, Tab4T32<DevOpsX>, 4, 512, 1, true, false, 6)     \
+    X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)
 
 struct VariantInfo {
     const void* fn;
@@ -377,7 +387,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 12; }
+int expand_variant_count() { return kBsVariant + kBsCount + 15; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

@@ -1,0 +1,43 @@
+"""Register budget of the hot kernel (CPU, hipcc cross-compile): the default k_expand variant
+(kDefaultVariant = 34 in csrc/fhh_host.cpp = X(34, Tab4T32, NB 4, 1024 threads, MINW 1,
+dynamic, FLAGS 6) in csrc/fhh_kernels.hip) must not spill and must keep 4 waves per SIMD.
+A spill once crept in through extra item-decode state and cost 4-8 %."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT_EXPAND = "_ZN3fhh8k_expandINS_7Tab4T32INS_7DevOpsXEEELi4ELi1024ELi1ELb0ELi6EEEvNS_12ExpandLaunchEPj"
+
+
+def _resource_usage(src, tmp_path):
+    r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c",
+                        "-Rpass-analysis=kernel-resource-usage", os.path.join(ROOT, "fuzzyheavyhitters_amd", "csrc", src),
+                        "-o", str(tmp_path / "k.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    usage, cur = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            usage[cur] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z /\[\]]+?):\s+(\S+) \[", line)
+        if m and cur:
+            usage[cur][m.group(1).strip()] = m.group(2)
+    return usage
+
+
+def test_default_expand_variant_does_not_spill(tmp_path):
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    u = _resource_usage("fhh_kernels.hip", tmp_path)
+    assert DEFAULT_EXPAND in u, "default k_expand instantiation not found (variant table changed?)"
+    k = u[DEFAULT_EXPAND]
+    assert k["ScratchSize [bytes/lane]"] == "0", k
+    assert k["VGPRs Spill"] == "0", k
+    assert int(k["Occupancy [waves/SIMD]"]) >= 4, k
+    assert int(k["LDS Size [bytes/block]"]) == 131072, k

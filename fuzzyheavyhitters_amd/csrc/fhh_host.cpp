@@ -714,7 +714,7 @@ int sim_ot_sums_impl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, uint64
     ChildArgs a = child_args(c0, c1);
     a.prf_seed = seed;
     if (last) HIP_TRY(c0, launch_sim_ot_fe255(a, c0->scratch2.as<uint64_t>(), c0->stream));
-    else HIP_TRY(c0, launch_sim_ot_fe(a, c0->scratch2.as<uint64_t>(), c0->stream));
+    else HIP_TRY(c0, launch_sim_ot_fe(a, c0->scratch2.as<uint64_t>(), c0->stream, true));
     std::vector<uint64_t> h(C * per);
     rc = fetch_partials(c0, cfg, c0->scratch2.as<uint64_t>(), C * per, h.data());
     if (rc) return rc;
@@ -1012,6 +1012,8 @@ int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uin
         // a resumed prune reads the (reduced) partials of `level`
         DevBuf npart, nred;
         HIP_TRY(c0, npart.ensure(C_new * 16 * 8));
+        // FE levels add into the partials (k_sim_ot_fe client chunks); k_prune re-zeroes them
+        HIP_TRY(c0, hipMemset(npart.p, 0, C_new * 16 * 8));
         if (B.distributed) HIP_TRY(c0, nred.ensure(C_new * 16 * 8));
         // ... and, multi-rank, the local partials too: the all-reduces of the no-op levels
         // after an abort re-reduce them, which must reproduce the same sums
@@ -1229,7 +1231,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 }
             }
             if (pmode == 0) HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
-            else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream));
+            else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream, false));
             else HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
             // -- cross-rank sum (client-sharded multi-GPU)
             // (the count is the capacity bound: entries past C are never read)
@@ -1297,6 +1299,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.unit = expand_unit(variant, c0->nw);
         pa.max_group = expand_max_group(variant);
         pa.tail_split = expand_tail_split(variant) ? 1u : 0u;
+        pa.zero_partials = (cfg->mode != 0 && !last) ? B.partials.as<uint64_t>() : nullptr;
+        pa.zero_count = (uint64_t)C_cap * 4;
         HIP_TRY(c0, launch_prune(pa, c0->stream));
         lv++;
         if (lv % kBatch == 0 || lv == levels) {

@@ -210,6 +210,11 @@ struct PruneArgs {
     uint32_t unit;              // k_expand items per entry group (nw; bitsliced: 4 * ceil(nw / 32))
     uint32_t max_group;         // entries per item cap (8; bitsliced: 1)
     uint32_t tail_split;        // item_layout end phase (expand_tail_split)
+    // FE levels: k_sim_ot_fe adds its client chunks into the partials by atomics, so a prune that
+    // completes zeroes them for the next level (a memset node would also run after a sticky
+    // abort and wipe the sums the resumed prune re-reads)
+    uint64_t* zero_partials;
+    uint64_t zero_count;
 };
 
 struct KeygenArgs {
@@ -231,7 +236,8 @@ const char* expand_variant_name(int variant);
 int expand_threads(int variant);
 hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream);
 hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream);
-hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream);
+// zero: clear partials first (host-driven launches); the device loop's k_prune clears them instead
+hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream, bool zero);
 hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials /*[C][16]*/, hipStream_t stream);
 hipError_t launch_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][2]*/, hipStream_t stream);
 hipError_t launch_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][8]*/, hipStream_t stream);

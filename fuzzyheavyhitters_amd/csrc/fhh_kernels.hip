@@ -560,16 +560,22 @@ __device__ __forceinline__ bool sim_eq_bit(const ChildArgs& a, const uint32_t (&
     return (eq_word(a, e, i >> 6) >> (i & 63)) & 1;
 }
 
+// grid (children, client chunks of kSimOtChunk): one child per block row would leave the chip
+// at ~3 waves per CU for the usual few hundred children (255 µs per level at configs[1]); the
+// chunks' limb sums meet in partials by 64-bit atomics (zeroed by the launcher)
+constexpr uint32_t kSimOtChunk = 16 * kReduceThreads;
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[4 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
     const uint64_t C_ = child_count(a);
+    const uint32_t i_begin = blockIdx.y * kSimOtChunk;
+    const uint32_t i_end = min(i_begin + kSimOtChunk, a.n);
     for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         const uint64_t bc = mix64(base ^ c);
         uint64_t v[4] = {0, 0, 0, 0};
-        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
+        for (uint32_t i = i_begin + threadIdx.x; i < i_end; i += blockDim.x) {
             uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
             if (r0 >= kFeP) r0 -= kFeP;
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         }
         block_sum_u64<4>(v, red);
         if (threadIdx.x == 0)
-            for (int k = 0; k < 4; k++) partials[c * 4 + k] = v[k];
+            for (int k = 0; k < 4; k++) atomicAdd(reinterpret_cast<unsigned long long*>(partials + c * 4 + k), v[k]);
     }
 }
 
@@ -616,9 +622,14 @@ hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, u
     return hipGetLastError();
 }
 
-hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
+hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream, bool zero) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, partials);
+    if (zero) {
+        const hipError_t e = hipMemsetAsync(partials, 0, (size_t)a.C * 4 * sizeof(uint64_t), stream);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t chunks = a.n ? (a.n + kSimOtChunk - 1) / kSimOtChunk : 1;
+    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(a.C), chunks), dim3(kReduceThreads), 0, stream, a, partials);
     return hipGetLastError();
 }
 

@@ -140,6 +140,10 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
             }
         __syncthreads();
     }
+    // the next FE level's atomically-added partials start from zero (every read of this level's
+    // partials is behind the barriers above; an aborted prune leaves them for its resumption)
+    if (fits && a.zero_partials)
+        for (uint64_t k = threadIdx.x; k < a.zero_count; k += blockDim.x) a.zero_partials[k] = 0;
     if (threadIdx.x != 0) return;
     if (!fits) {
         uint32_t need = 0;

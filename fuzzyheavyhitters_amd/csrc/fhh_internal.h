@@ -363,10 +363,11 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // 34 / 35 are 33 / 32 with the sibling-pair AES (aes0_mmo_pair); 36 is 34 + wave timeline;
 // 37 / 38 are 34 / 36 with the end-of-launch phase of small items (item_layout); 39 / 40 are
 // 34 at 768 / 512 threads (3 / 2 waves per SIMD: a VGPR budget of 168 / 256 lets the
-// scheduler keep more T-table lookups in flight per wave); 41 is 39 drawing the next item ahead
+// scheduler keep more T-table lookups in flight per wave); 41 is 39 drawing the next item ahead;
+// 42 is 34 with the next entry's seeds prefetched under the current entry's AES
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 41))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 42))
                ? 16u : variant == 31 ? 32u : 8u;
 }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }

@@ -124,7 +124,7 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
 }
 
 // NB = 4 with the next entry's seeds / t / y prefetched while the current entry's AES runs.
-template <class Tab>
+template <class Tab, bool NT = false, bool PAIR = false>
 __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
                                                uint32_t b0, uint32_t b1) {
     const uint32_t w = (uint32_t)(local % J.nw);
@@ -179,7 +179,8 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
                 yw[s] = J.src_y[((size_t)src * 2 + s) * nw + w];
             }
         }
-        aes0_mmo_tab<DevOpsX, Tab, 4>(blk, tbl, b0, b1);
+        if constexpr (PAIR) aes0_mmo_pair<DevOpsX, Tab, 4>(blk, tbl, b0, b1);
+        else aes0_mmo_tab<DevOpsX, Tab, 4>(blk, tbl, b0, b1);
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             const uint32_t tmask = 0u - (uint32_t)((ctw[s] >> lane) & 1);
@@ -192,7 +193,12 @@ __device__ __forceinline__ void expand_item_pf(const ExpandJob& J, uint64_t loca
                 out.z = o[2] ^ (cw[s].z & tmask);
                 out.w = o[3] ^ (cw[s].w & tmask);
                 const size_t de = (size_t)(2 * e + dir) * 2 + s;
-                J.dst_seed[de * npad + c] = out;
+                if constexpr (NT) {
+                    v4u32_t o4 = {out.x, out.y, out.z, out.w};
+                    __builtin_nontemporal_store(o4, reinterpret_cast<v4u32_t*>(J.dst_seed + de * npad + c));
+                } else {
+                    J.dst_seed[de * npad + c] = out;
+                }
                 if (lane == 0) {
                     J.dst_t[de * nw + w] = pb[s * 2 + dir] ^ (ctw[s] & cwp[s][dir]);
                     J.dst_y[de * nw + w] = py[s * 2 + dir] ^ (ctw[s] & cwp[s][2 + dir]) ^ cyw[s];
@@ -277,7 +283,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         }
         uint32_t nxt = 0;
         if constexpr (PROF) prof_items++;
-        if constexpr (PF) expand_item_pf<Tab>(J, item - J.item_begin, tbl, lane, b0, b1);
+        if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
         else expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
@@ -356,7 +362,8 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(38, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 30)   \
     X(39, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 6)     \
     X(40, Tab4T32<DevOpsX>, 4, 512, 1, true, false, 6)     \
-    X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)
+    X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)     \
+    X(42, Tab4T32<DevOpsX>, 4, 1024, 1, true, true, 6)
 
 struct VariantInfo {
     const void* fn;
@@ -387,7 +394,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 15; }
+int expand_variant_count() { return kBsVariant + kBsCount + 16; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

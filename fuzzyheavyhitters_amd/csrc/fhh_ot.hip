@@ -14,11 +14,14 @@
 // ideal (the host hands the sender k_i^{s_i}).
 //
 //   k_ot_recv_expand / k_ot_send_expand  one lane per (row, 128-OT block): 2 / 1 AES
-//   k_ot_transpose                        one lane per 32 OTs: 4 in-register 32x32 transposes
+//   k_ot_transpose                        one block per 2048 OTs: LDS-staged 32x32 transposes
 //   k_ot_send_hash / k_ot_recv_hash       one lane per OT: 2 / 1 cr_hash (2 / 1 AES)
 #include "fhh_internal.h"
 #include "aes_keyed.h"
 #include "bitslice.h"
+
+#include <cstdlib>
+#include <cstring>
 
 namespace fhh {
 
@@ -119,9 +122,9 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     }
 }
 
-// rows [128][mp / 32] u32 -> cols [mp] uint4: lane w owns OTs 32 w .. 32 w + 31; the four
-// 32-row groups are transposed in registers (128 words) and each OT's row leaves as one 16-B store
-__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint4* cols, OtArgs a) {
+// The per-lane form (k_ot_transpose_lanes: 128 words per lane, 256 VGPRs, 1 wave/SIMD) stays
+// for same-box A/B runs: FHH_OT_TRANSPOSE=lanes selects it.
+__global__ __launch_bounds__(256) void k_ot_transpose_lanes(const uint32_t* rows, uint4* cols, OtArgs a) {
     const uint64_t W = a.mp / 32;
     const uint64_t W_act = (ot_active(a) + 31) / 32;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < W_act; w += (uint64_t)gridDim.x * blockDim.x) {
@@ -130,10 +133,52 @@ __global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint
         for (int g = 0; g < 4; g++) {
 #pragma unroll
             for (int r = 0; r < 32; r++) x[g][r] = __builtin_nontemporal_load(rows + (uint64_t)(32 * g + r) * W + w);
-            transpose32(x[g]);   // x[g][k] bit r = row 32 g + r of OT 32 w + k
+            transpose32(x[g]);
         }
 #pragma unroll
         for (int k = 0; k < 32; k++) cols[32 * w + k] = make_uint4(x[0][k], x[1][k], x[2][k], x[3][k]);
+    }
+}
+
+// rows [128][mp / 32] u32 -> cols [mp] uint4, one 256-thread block per tile of 64 words
+// (2048 OTs): the tile's 128 x 64 words are staged in LDS by coalesced row loads, thread
+// (g, w) transposes rows 32 g .. 32 g + 31 of word w in registers, writes the 32 results back
+// with pitch 129 words per word-column (conflict-free), and the block stores the 32 KB of
+// output rows contiguously. 33 KB LDS and 160 VGPRs: 3 waves/SIMD, full-line stores. (Holding
+// all 128 rows of a word in one lane took 256 VGPRs, 1 wave/SIMD, and 16-B stores 512 B apart.)
+// mp is a multiple of 8192 (nblk = mp / 128 is a multiple of 64), so W = mp / 32 is a multiple of
+// 64 and every tile lies inside the row matrix.
+constexpr int kTrPitch = 129;
+__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint4* cols, OtArgs a) {
+    __shared__ uint32_t tile[64 * kTrPitch];
+    const uint64_t W = a.mp / 32;
+    const uint64_t W_act = (ot_active(a) + 31) / 32;
+    const uint64_t ntiles = (W_act + 63) / 64;
+    const uint64_t j_act = 32 * W_act;
+    const uint32_t t = threadIdx.x, w = t & 63, g = t >> 6;
+    for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+        const uint64_t w0 = ti * 64;
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            const uint32_t r = 4 * i + g;
+            tile[r * 64 + w] = __builtin_nontemporal_load(rows + (uint64_t)r * W + w0 + w);
+        }
+        __syncthreads();
+        uint32_t x[32];
+#pragma unroll
+        for (int r = 0; r < 32; r++) x[r] = tile[(32 * g + r) * 64 + w];
+        __syncthreads();
+        transpose32(x);   // x[k] bit r = row 32 g + r of OT 32 (w0 + w) + k
+#pragma unroll
+        for (int k = 0; k < 32; k++) tile[w * kTrPitch + 4 * k + g] = x[k];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t j = t + 256 * i, base = (j >> 5) * kTrPitch + 4 * (j & 31);
+            if (32 * w0 + j < j_act)
+                cols[32 * w0 + j] = make_uint4(tile[base], tile[base + 1], tile[base + 2], tile[base + 3]);
+        }
+        __syncthreads();
     }
 }
 
@@ -255,7 +300,21 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_transpose, dim3(ot_grid(a.mp / 32, 256)), dim3(256), 0, stream,
+    static const bool lanes = [] {
+        const char* e = getenv("FHH_OT_TRANSPOSE");
+        return e && strcmp(e, "lanes") == 0;
+    }();
+    if (lanes) {
+        hipLaunchKernelGGL(k_ot_transpose_lanes, dim3(ot_grid(a.mp / 32, 256)), dim3(256), 0, stream,
+                           reinterpret_cast<const uint32_t*>(rows), cols, a);
+        return hipGetLastError();
+    }
+    if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // the tile mapping of k_ot_transpose
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t tiles = a.mp / 2048, cap = (uint64_t)cus * 8;
+    hipLaunchKernelGGL(k_ot_transpose, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(256), 0, stream,
                        reinterpret_cast<const uint32_t*>(rows), cols, a);
     return hipGetLastError();
 }

@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Benchmark of the per-level ibDCF client-key evaluation (BASELINE.json metric:
-"client x prefix key evals/sec (AES blocks/s) + full-crawl wall time").
+"client x prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients").
 
 One step = one full crawl (data_len levels) of the in-process leader + both servers:
 GPU keys already resident in HBM; per level: k_expand for both servers (one launch),
 the plaintext equality count standing in for the GC/OT step, [RCCL all-reduce of the
-per-child partial counts when N > 1], leader keep decision, prune. Workload = configs[1]:
-100k Zipf clients (num_sites 10000, s = 1.03), data_len 512, d = 1, ball 1,
-threshold 0.001; clients are sharded by GPU (weak scaling: --clients per GPU).
+per-child partial counts when N > 1], leader keep decision, prune. Default workload = the
+metric's: 1M Zipf clients IN TOTAL (num_sites 10000, s = 1.03), data_len 512, d = 1, ball 1,
+threshold 0.001, sharded by client over the ranks (strong scaling; at 8 GPUs this is
+configs[2]). `--clients 100000` is configs[1]. The CPU baseline is configs[0] exactly.
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -35,29 +36,51 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(args, n_total):
-    """Oracle restatement (AES-NI, one non-pipelined block per eval_bit, OpenMP over clients)
-    on a bounded sample of the same workload — rank 0, N = 1 only."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def shard(n_total: int, world: int, rank: int):
+    """Contiguous client range of `rank` (strong scaling: the population is fixed)."""
+    base = n_total * rank // world
+    return base, n_total * (rank + 1) // world - base
+
+
+def cpu_baseline(args):
+    """configs[0] exactly — the reference's own CPU configuration (leader.rs:299-443, SURVEY §8d
+    Config A: 1000 Zipf clients over num_sites 10000, s = 1.03, data_len 512, d = 1, ball 1,
+    threshold 0.001) — as a full two-server crawl of the oracle restatement (AES-NI, one
+    non-pipelined block per eval_bit, reference child order, OpenMP over clients). Rank 0, N = 1
+    only; the Rust reference is not buildable here (no cargo, crates not vendored)."""
     from fuzzyheavyhitters_amd import workload
     from oracle import oracle as O
     O.build()
-    n_cpu = min(args.clients, args.cpu_sample_clients)
-    wl = workload.zipf_workload(n_cpu, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
-                                ball_size=args.ball, seed=args.seed)
+    n_cpu, L = 1000, 512
+    wl = workload.zipf_workload(n_cpu, L, 1, num_sites=10_000, zipf_s=1.03, ball_size=1, seed=args.seed)
     k0, k1 = O.gen_keys(wl.left, wl.right, wl.root_seeds)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     t0 = time.perf_counter()
-    res = O.crawl(k0, k1, args.threshold, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds)
+    res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds)
     dt = time.perf_counter() - t0
+    done = len(res.n_children)
     return {
         "value": res.aes_blocks / dt,
         "unit": "AES blocks/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{n_cpu} clients of the same Zipf workload, levels 0..{len(res.n_children) - 1} of "
-                   f"{args.data_len}, both servers, {res.aes_blocks} AES blocks in {dt:.2f} s "
-                   f"(oracle/fhh_oracle.c: AES-NI single block per eval_bit, reference child order, "
-                   f"OpenMP {threads} threads; the Rust reference is not buildable here)"),
+        "cpu_model": cpu_model(),
+        "full_crawl_wall_s": dt if done == L else None,
+        "sample": (f"configs[0]: 1000 Zipf clients (num_sites 10000, s 1.03, seed {args.seed:#x}), data_len 512, d 1, "
+                   f"threshold 0.001 (count 1), levels 0..{done - 1} of {L}, both servers, {sum(res.n_children)} "
+                   f"children, {res.aes_blocks} AES blocks in {dt:.2f} s, {len(res.final_paths)} heavy hitters "
+                   f"(oracle/fhh_oracle.c: AES-NI single block per eval_bit, reference child order, OpenMP "
+                   f"{threads} threads on {cpu_model()})"),
     }
 
 
@@ -89,7 +112,7 @@ def sketch_bench(args, world, rank, local_rank, dist):
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)   # gloo control group: host tensors
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ok = b.ok.cpu().numpy().astype(bool)
@@ -124,7 +147,7 @@ def gc_bench(args, world, rank, local_rank, dist):
     import torch
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import gc
-    G, N, bits = args.gc_groups, args.clients, 2 * args.dims
+    G, N, bits = args.gc_groups, args.gc_clients, 2 * args.dims
     rng = np.random.default_rng(args.seed + rank)
     nw = (N + 63) // 64
     gb = rng.integers(0, 1 << 63, (G, bits, nw), dtype=np.uint64)
@@ -150,7 +173,7 @@ def gc_bench(args, world, rank, local_rank, dist):
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)   # gloo control group: host tensors
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # ground truth: eq = all planes equal at the client's bit
@@ -201,12 +224,25 @@ def gc_bench(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def load_pmc(config: str):
+    """Committed rocprofv3 PMC summary of k_expand for this workload (tools/profile.sh +
+    tools/pmc_summary.py -> profiles/pmc_expand.json, keyed by workload)."""
+    path = os.path.join(ROOT, "profiles", "pmc_expand.json")
+    try:
+        allp = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return allp.get(config)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--clients", type=int, default=100_000, help="clients per GPU")
+    ap.add_argument("--clients", type=int, default=1_000_000,
+                    help="clients in total, sharded over the ranks (strong scaling; 1M = the metric's "
+                         "configuration and, at 8 GPUs, configs[2]; 100000 = configs[1])")
     ap.add_argument("--data-len", type=int, default=512)
     ap.add_argument("--dims", type=int, default=1)
     ap.add_argument("--num-sites", type=int, default=10_000)
@@ -215,18 +251,21 @@ def main():
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
     ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc"],
-                    help="zipf = configs[1] (default); coords = configs[3] (d=2 lat/lon, data_len 16); "
-                         "sketch = configs[4] (sketch + Beaver verification batch); "
-                         "gc = row f1 (garbled-circuit equality tests of one level)")
+                    help="zipf = the metric's Zipf crawl (default 1M clients; --clients 100000 = configs[1]); "
+                         "coords = configs[3] (d=2 lat/lon, data_len 16); sketch = configs[4] (sketch + Beaver "
+                         "verification); gc = row f1 (garbled-circuit equality tests of one level)")
     ap.add_argument("--gc-groups", type=int, default=256, help="--workload gc: children per level")
+    ap.add_argument("--gc-clients", type=int, default=100_000, help="--workload gc: clients per GPU")
     ap.add_argument("--gc", default="none", choices=["none", "ot", "ideal"],
                     help="crawl with the GPU garbled-circuit equality test (mode fe): ot = labels and FE shares "
                          "by GPU OT extension, ideal = ideal OT")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
+    ap.add_argument("--sketch-levels", type=int, default=1,
+                    help="configs[4]: levels verified per step (data_len 1024 -> 1023)")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-sample-clients", type=int, default=4096)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=150.0,
+                    help="upper bound on the configs[0] CPU crawl (it normally completes well inside)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
     ap.add_argument("--variant", type=int, default=-1, help="k_expand variant (-1 = library default)")
@@ -240,13 +279,15 @@ def main():
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
-    import numpy as np
     import torch
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
+        # control plane only (barriers, the communicator id, max-over-ranks timing): gloo on the
+        # host. The data path's one collective is the native RCCL communicator below — one RCCL
+        # communicator per rank, nothing else touches RCCL.
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        dist.init_process_group("gloo")
 
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
@@ -258,8 +299,8 @@ def main():
     if args.gc != "none" and args.mode != "fe":
         args.mode = "fe"   # the GC equality test feeds the OT share conversion (collect.rs:419-482)
 
-    n_local = args.clients
-    n_total = n_local * world
+    n_total = args.clients
+    base, n_local = shard(n_total, world, rank)
     t_gen = time.perf_counter()
     if args.workload == "coords":
         # configs[3]: src/bin/config.json (data_len 16, n_dims 2, ball 1, threshold 0.075)
@@ -267,36 +308,36 @@ def main():
         if args.threshold == 0.001:
             args.threshold = 0.075
         wl = workload.coords_workload(n_local, ball_size=args.ball, zipf_s=args.zipf, seed=args.seed,
-                                      client_offset=rank * n_local)
+                                      client_offset=base)
     else:
         wl = workload.zipf_workload(n_local, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
-                                    ball_size=args.ball, seed=args.seed, client_offset=rank * n_local)
+                                    ball_size=args.ball, seed=args.seed, client_offset=base)
     c0 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     c1 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
     fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    del wl
     if args.variant >= 0:
         c0.set_variant(args.variant)
         c1.set_variant(args.variant)
-    c0.set_client_base(rank * n_local)
-    c1.set_client_base(rank * n_local)
+    c0.set_client_base(base)
+    c1.set_client_base(base)
     c0.set_timing(args.timing_every)
-    log(f"[rank {rank}] workload+keygen {time.perf_counter() - t_gen:.2f}s "
+    log(f"[rank {rank}] {n_local} clients from {base}: workload+keygen {time.perf_counter() - t_gen:.2f}s "
         f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
 
-    comm, collective = None, "none"
+    comm, collective = None, {"kind": "none"}
     if world > 1:
-        # native RCCL all-reduce on the engine stream (no host sync per level); the torch
-        # host-callback path stays available if the communicator cannot be created
-        try:
-            comm = fhh.RcclComm(local_rank)
-            collective = "rccl-native (ncclAllReduce on the engine stream)"
-        except Exception as e:  # pragma: no cover - reported in the JSON line
-            log(f"[rank {rank}] native RCCL comm unavailable ({e}); using torch.distributed callback")
-            collective = "torch.distributed all_reduce (host callback)"
+        # native RCCL all-reduce on the engine stream (no host sync per level); the id travels
+        # over the gloo group
+        comm = fhh.RcclComm(local_rank)
+        nr, rk = comm.info()
+        collective = {"kind": "rccl ncclAllReduce(sum, u64) of per-child partials on the engine stream",
+                      "comm_ranks": nr, "comm_rank": rk}
+        log(f"[rank {rank}] RCCL communicator: {nr} ranks, rank {rk}")
 
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, distributed=world > 1 and comm is None, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc])
+                             record=False, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc])
 
     def barrier():
         if dist is not None:
@@ -317,10 +358,10 @@ def main():
     blocks = s0["aes_blocks"] + s1["aes_blocks"]
     ref_evals = s0["ref_evals"] + s1["ref_evals"]
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        b = torch.tensor([blocks, ref_evals], dtype=torch.int64, device="cuda")
+        b = torch.tensor([blocks, ref_evals], dtype=torch.int64)
         dist.all_reduce(b)
         blocks, ref_evals = int(b[0].item()), int(b[1].item())
 
@@ -328,36 +369,42 @@ def main():
         launches = max(1, s0["expand_launches_timed"])
         avg_launch_s = s0["expand_ms"] / launches / 1e3
         blocks_per_launch = s0["expand_blocks_timed"] / launches
-        lds_gbps = blocks_per_launch * LDS_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        valu_tops = blocks_per_launch * VALU_OPS_PER_BLOCK / avg_launch_s / 1e12 if avg_launch_s > 0 else 0.0
-        hbm_gbps = blocks_per_launch * HBM_BYTES_PER_BLOCK / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        traffic = None
-        pmc_rates = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_expand.json")
-        if os.path.exists(pmc_path):
-            try:
-                pmc = json.load(open(pmc_path))
-                if pmc.get("config") == f"n{n_local}_L{args.data_len}_d{args.dims}":
-                    traffic = pmc.get("hbm_bytes_per_launch")
-                    # executed (not algorithmic) rates of the profiled k_expand launches, from the
-                    # committed rocprofv3 PMC passes (tools/profile.sh + tools/pmc_summary.py)
-                    t = pmc["k_expand_avg_ns"] * 1e-9
-                    pmc_rates = {
-                        "source": f"profiles/pmc_expand.json ({pmc.get('tag')})",
-                        "valu_lane_ops_per_s": pmc["sq_insts_valu_per_launch"] * 64 / t,
-                        "valu_frac": pmc["sq_insts_valu_per_launch"] * 64 / t / (VALU_PEAK_TOPS * 1e12),
-                        "lds_bytes_per_s": pmc["sq_insts_lds_per_launch"] * 256 / t,
-                        "lds_frac": pmc["sq_insts_lds_per_launch"] * 256 / t / (LDS_PEAK_GBPS * 1e9),
-                        "hbm_bytes_per_s": traffic / t,
-                        "hbm_frac": traffic / t / (HBM_PEAK_GBPS * 1e9),
-                        "lds_insts_per_block": pmc["sq_insts_lds_per_launch"] * 64 / blocks_per_launch,
-                        "valu_insts_per_block": pmc["sq_insts_valu_per_launch"] * 64 / blocks_per_launch,
-                        "effective_clock_ghz": pmc.get("effective_clock_ghz"),
-                    }
-            except Exception:
-                traffic, pmc_rates = None, None
+        rate = blocks_per_launch / avg_launch_s if avg_launch_s > 0 else 0.0     # in-kernel blocks/s
+        valu_tops = rate * VALU_OPS_PER_BLOCK / 1e12
+        lds_gbps = rate * LDS_BYTES_PER_BLOCK / 1e9
+        hbm_gbps = rate * HBM_BYTES_PER_BLOCK / 1e9
+        cfg_key = f"n{n_local}_L{args.data_len}_d{args.dims}"
+        pmc = load_pmc(cfg_key) if args.workload == "zipf" and args.variant < 0 else None
+        traffic = pmc_rates = None
+        if pmc:
+            traffic = pmc.get("hbm_bytes_per_launch")
+            t = pmc["k_expand_avg_ns"] * 1e-9
+            lds_exec = pmc["sq_insts_lds_per_launch"] * 64 * 4      # ds_read_b32: 4 B per lane
+            pmc_rates = {
+                "source": f"profiles/pmc_expand.json[{cfg_key}] ({pmc.get('tag')}, rocprofv3 --pmc passes)",
+                "k_expand_avg_us": pmc["k_expand_avg_ns"] / 1e3,
+                "valu_lane_ops_per_s": pmc["sq_insts_valu_per_launch"] * 64 / t,
+                "valu_frac": pmc["sq_insts_valu_per_launch"] * 64 / t / (VALU_PEAK_TOPS * 1e12),
+                "lds_executed_bytes_per_launch": lds_exec,
+                "lds_executed_frac": lds_exec / t / (LDS_PEAK_GBPS * 1e9),
+                "hbm_bytes_per_s": traffic / t,
+                "hbm_frac": traffic / t / (HBM_PEAK_GBPS * 1e9),
+                "lds_insts_per_block": pmc["sq_insts_lds_per_launch"] * 64 / blocks_per_launch,
+                "valu_insts_per_block": pmc["sq_insts_valu_per_launch"] * 64 / blocks_per_launch,
+                "lds_bank_conflict_cycles": pmc.get("sq_lds_bank_conflict"),
+                "effective_clock_ghz": pmc.get("effective_clock_ghz"),
+            }
+        if args.workload == "zipf":
+            wl_name = (f"Zipf ibDCF tree crawl, {n_total} clients, data_len {args.data_len}, d {args.dims}, both "
+                       f"servers in-process" + (" (= configs[2] sharded over 8 GPUs)" if n_total == 1_000_000 else "")
+                       + (" (= configs[1])" if n_total == 100_000 else ""))
+        else:
+            wl_name = "configs[3]: lat/lon l-inf balls (synthetic county-centroid-shaped points), d=2, data_len 16"
+        metric = ("client×prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients"
+                  if n_total == 1_000_000 and args.workload == "zipf" else
+                  f"client×prefix key evals/sec (AES blocks/s) + full-crawl wall time, {n_total} clients")
         out = {
-            "metric": "client x prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients",
+            "metric": metric,
             "value": blocks / elapsed,
             "unit": "AES blocks/s",
             "n_gpus": world,
@@ -365,34 +412,48 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded Zipf workload shaped like leader.rs; random-init keys via GPU keygen)",
+            "data": ("synthetic: seeded Zipf workload shaped like leader.rs (num_sites strings + 8-bit augmentation), "
+                     "keys by GPU keygen, resident in HBM before the timed region"
+                     if args.workload == "zipf" else
+                     "synthetic: Zipf-weighted synthetic county-centroid-shaped points (data/county_centroids.csv "
+                     "not used), keys by GPU keygen"),
             "config": {
-                "workload": ("configs[1]: Zipf clients, data_len 512 ibDCF tree crawl, two in-process servers"
-                             if args.workload == "zipf" else
-                             "configs[3]: lat/lon l-inf balls (county-centroid-shaped points), d=2, data_len 16"),
-                "clients_per_gpu": n_local, "clients_total": n_total, "data_len": args.data_len,
+                "workload": wl_name,
+                "clients_total": n_total, "clients_per_gpu": n_local, "data_len": args.data_len,
                 "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
-                "threshold": args.threshold, "mode": args.mode, "parallelism": f"client-shard x{world}",
-                "collective": collective,
+                "threshold": args.threshold, "mode": args.mode, "gc": args.gc,
+                "parallelism": f"client-shard x{world}", "collective": collective,
+                "variant": args.variant if args.variant >= 0 else "default",
             },
             "full_crawl_wall_s": elapsed / args.steps,
+            "full_crawl_note": "both servers' evaluation fused in one k_expand launch per level, plus the "
+                               "plaintext equality count, leader keep and prune on the GPU",
             "ref_equiv_evals_per_s": ref_evals / elapsed,
             "aes_blocks_per_step": blocks / args.steps,
             "final_heavy_hitters": len(res.final),
             "levels": int(len(res.level_children)),
             "children_total": int(res.level_children.sum()),
             "roofline": {
-                "bound": "lds", "achieved": lds_gbps, "peak": LDS_PEAK_GBPS, "unit": "GB/s",
-                "frac": lds_gbps / LDS_PEAK_GBPS, "traffic": traffic,
-                "kernel": "k_expand", "algorithmic": f"{LDS_BYTES_PER_BLOCK} B of ds_read_b32 T-table lookups per AES block",
+                "bound": "valu", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                "frac": valu_tops / VALU_PEAK_TOPS, "traffic": traffic,
+                "kernel": "k_expand",
+                "algorithmic": (f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d) x blocks per launch / "
+                                f"average launch time (HIP events on the engine stream)"),
+                "peak_basis": "256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md; fhh_microbench)",
                 "avg_launch_us": avg_launch_s * 1e6, "blocks_per_launch": blocks_per_launch,
+                "in_kernel_blocks_per_s": rate,
+                "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE",
             },
-            "roofline_valu": {"achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
-                              "frac": valu_tops / VALU_PEAK_TOPS,
-                              "algorithmic": f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d)"},
+            "roofline_lds": {
+                "achieved_algorithmic": lds_gbps, "peak": LDS_PEAK_GBPS, "unit": "GB/s",
+                "frac_algorithmic": lds_gbps / LDS_PEAK_GBPS,
+                "algorithmic": f"{LDS_BYTES_PER_BLOCK} B of ds_read_b32 T-table lookups per AES block",
+                "frac_executed": pmc_rates["lds_executed_frac"] if pmc_rates else None,
+                "executed": "SQ_INSTS_LDS x 64 lanes x 4 B per launch / rocprof launch time (pmc_executed)",
+            },
             "roofline_hbm": {"achieved": hbm_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": hbm_gbps / HBM_PEAK_GBPS,
                              "algorithmic": f"{HBM_BYTES_PER_BLOCK} B per AES block (SURVEY 8d)"},
@@ -406,11 +467,13 @@ def main():
             fhh.lib().fhh_microbench(local_rank, 1, ctypes.byref(r))
             out["measured_lds_peak_gbps"] = r.value / 1e9
         if world == 1 and not args.no_cpu_baseline and args.workload == "zipf":
-            out["cpu_baseline"] = cpu_baseline(args, n_total)
+            out["cpu_baseline"] = cpu_baseline(args)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if comm is not None:
+        if dist is not None:
+            dist.barrier()
         comm.close()
     if dist is not None:
         dist.barrier()

@@ -35,7 +35,7 @@ EXPORTS = [
     "fhh_debug_launch_gaps", "fhh_wave_profile_arm", "fhh_wave_profile_launches",
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
-    "fhh_comm_last_error",
+    "fhh_comm_info", "fhh_comm_create_hosted", "fhh_comm_last_error",
     "fhh_sketch_at_fe", "fhh_mul_cor_share_fe", "fhh_mul_cor_fe", "fhh_mul_out_share_fe", "fhh_mul_verify_fe",
     "fhh_sim_sketch_verify_fe",
     "fhh_gc_equality_device", "fhh_gc_equality_host", "fhh_ot_extend_device", "fhh_ot_extend_host",
@@ -74,6 +74,14 @@ class FhhSimConfig(ctypes.Structure):
         ("init_capacity", ctypes.c_uint32),
         ("comm", ctypes.c_void_p),
         ("gc", ctypes.c_uint32),
+        ("probe_n_levels", ctypes.c_uint32),
+        ("probe_n_clients", ctypes.c_uint32),
+        ("probe_levels", u32p),
+        ("probe_clients", u64p),
+        ("probe_capacity", ctypes.c_uint64),
+        ("probe_seeds", u8p),
+        ("probe_ty", u8p),
+        ("probe_children", u64p),
     ]
 
 
@@ -227,6 +235,8 @@ def lib():
         "fhh_comm_destroy": (None, [vp]),
         "fhh_comm_allreduce_u64": (i, [vp, vp, vp, u64, vp]),
         "fhh_comm_last_error": (ctypes.c_char_p, []),
+        "fhh_comm_info": (i, [vp, P(i), P(i)]),
+        "fhh_comm_create_hosted": (i, [P(vp), i, i, i, ALLREDUCE_FN, vp]),
         "fhh_sketch_at_fe": (i, [vp, u64, u32, u8p, u64p, u64p, u64p]),
         "fhh_mul_cor_share_fe": (i, [vp, u64, u64p, u64p, u64p, u64p, u64p]),
         "fhh_mul_cor_fe": (i, [u64, u64p, u64p, u64p]),

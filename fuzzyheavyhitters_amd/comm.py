@@ -5,7 +5,8 @@ per-child sums) becomes, with clients sharded over GPUs, one ncclAllReduce(sum, 
 per-child limb partials. The library enqueues it on the engine's own stream, so the
 device-resident level loop runs a whole crawl with no host synchronisation per level.
 
-The unique id is created by rank 0 and broadcast over torch.distributed's default group;
+The unique id is created by rank 0 and broadcast over torch.distributed's default group (the
+bench uses a gloo group for this control traffic, so RCCL carries only the data path);
 RCCL itself is the copy torch already loaded (so one RCCL instance serves the process).
 """
 from __future__ import annotations
@@ -13,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-from ._lib import FhhError, lib, u8p
+from ._lib import ALLREDUCE_FN, FhhError, lib, u8p
 
 
 def _comm_check(rc: int):
@@ -62,6 +63,12 @@ class RcclComm:
         _comm_check(lib().fhh_comm_allreduce_u64(self.handle, ctypes.c_void_p(t.data_ptr()),
                                                  ctypes.c_void_p(t.data_ptr()), t.numel(), ctypes.c_void_p(stream)))
 
+    def info(self):
+        """(ranks, rank) as RCCL reports them for this communicator."""
+        nr, rk = ctypes.c_int(), ctypes.c_int()
+        _comm_check(lib().fhh_comm_info(self.handle, ctypes.byref(nr), ctypes.byref(rk)))
+        return nr.value, rk.value
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             lib().fhh_comm_destroy(self.handle)
@@ -72,3 +79,32 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+class HostedComm(RcclComm):
+    """The level loop's `cfg.comm` path without RCCL (fhh_comm_create_hosted): partials are summed
+    on the host through torch.distributed (e.g. gloo). For multi-rank tests on one GPU, where
+    RCCL cannot place two ranks on one device."""
+
+    def __init__(self, device: int):
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        self.rank, self.world, self.device = dist.get_rank(), dist.get_world_size(), device
+        self.err = None
+
+        def _sum(buf, count, user):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(count,))
+                t = torch.from_numpy(a.view(np.int64).copy())
+                dist.all_reduce(t)
+                a[:] = t.numpy().view(np.uint64)
+                return 0
+            except Exception as e:  # pragma: no cover - surfaced as FHH_E_CALLBACK
+                self.err = e
+                return 1
+
+        self._cb = ALLREDUCE_FN(_sum)
+        h = ctypes.c_void_p()
+        _comm_check(lib().fhh_comm_create_hosted(ctypes.byref(h), self.world, self.rank, device, self._cb, None))
+        self.handle = h

@@ -16,11 +16,17 @@
 
 #include <cstring>
 #include <mutex>
+#include <vector>
 #include <string>
 
 struct fhh_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    // hosted communicator (fhh_comm_create_hosted): the same cfg->comm code path of the level
+    // loop, with the sum done by a host callback instead of RCCL (tests without RCCL ranks)
+    fhh_allreduce_fn hosted = nullptr;
+    void* hosted_user = nullptr;
+    std::vector<uint64_t> host_buf;
 };
 
 namespace {
@@ -34,6 +40,8 @@ struct Rccl {
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
 };
 
 Rccl g_rccl;
@@ -74,7 +82,10 @@ int load_locked(const char* path) {
     r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
     r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string)
+    r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
+    r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(h, "ncclCommUserRank"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string ||
+        !r.comm_count || !r.comm_user_rank)
         return fail(FHH_E_COMM, "librccl lacks an expected symbol");
     g_rccl = r;
     return FHH_OK;
@@ -91,6 +102,25 @@ namespace fhh {
 
 int comm_allreduce(fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t count, hipStream_t stream,
                    std::string* err) {
+    if (c->hosted) {
+        // stream order: wait for the partials, sum on the host, put the result back before the
+        // host returns to enqueue the consumers (blocking copies after the stream drained)
+        c->host_buf.resize(count);
+        if (hipStreamSynchronize(stream) != hipSuccess ||
+            hipMemcpy(c->host_buf.data(), send, count * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+            if (err) *err = "hosted comm: device to host copy failed";
+            return FHH_E_HIP;
+        }
+        if (c->hosted(c->host_buf.data(), count, c->hosted_user) != 0) {
+            if (err) *err = "hosted comm: all-reduce callback failed";
+            return FHH_E_CALLBACK;
+        }
+        if (hipMemcpy(recv, c->host_buf.data(), count * 8, hipMemcpyHostToDevice) != hipSuccess) {
+            if (err) *err = "hosted comm: host to device copy failed";
+            return FHH_E_HIP;
+        }
+        return FHH_OK;
+    }
     const ncclResult_t r = g_rccl.all_reduce(send, recv, count, ncclUint64, ncclSum, c->comm, stream);
     if (r != ncclSuccess) {
         if (err) *err = std::string("ncclAllReduce: ") + g_rccl.error_string(r);
@@ -141,6 +171,18 @@ int fhh_comm_create(fhh_comm** out, int nranks, int rank, const uint8_t id[128],
     return FHH_OK;
 }
 
+int fhh_comm_create_hosted(fhh_comm** out, int nranks, int rank, int device, fhh_allreduce_fn fn, void* user) {
+    if (!out || !fn || nranks < 1 || rank < 0 || rank >= nranks) return fail(FHH_E_ARG, "bad hosted comm arguments");
+    auto* c = new fhh_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    c->hosted = fn;
+    c->hosted_user = user;
+    *out = c;
+    return FHH_OK;
+}
+
 void fhh_comm_destroy(fhh_comm* comm) {
     if (!comm) return;
     if (comm->comm && g_rccl.comm_destroy) {
@@ -157,6 +199,20 @@ int fhh_comm_allreduce_u64(fhh_comm* comm, const uint64_t* send_dev, uint64_t* r
     std::string err;
     const int rc = fhh::comm_allreduce(comm, send_dev, recv_dev, count, static_cast<hipStream_t>(stream), &err);
     if (rc) return fail(rc, err);
+    return FHH_OK;
+}
+
+int fhh_comm_info(fhh_comm* comm, int* nranks, int* rank) {
+    if (!comm || !nranks || !rank) return fail(FHH_E_ARG, "null comm or output");
+    if (comm->hosted) {
+        *nranks = comm->nranks;
+        *rank = comm->rank;
+        return FHH_OK;
+    }
+    ncclResult_t r = g_rccl.comm_count(comm->comm, nranks);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclCommCount");
+    r = g_rccl.comm_user_rank(comm->comm, rank);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclCommUserRank");
     return FHH_OK;
 }
 

@@ -948,6 +948,11 @@ struct LoopBuffers {
     DevBuf reduced;
     bool distributed = false;
     uint64_t* red() const { return distributed ? reduced.as<uint64_t>() : partials.as<uint64_t>(); }
+    // parity probe (cfg->probe_*): per probed level, the gathered states at stride probe_stride
+    static constexpr uint32_t kMaxProbe = 16;
+    DevBuf probe_seed[kMaxProbe], probe_ty[kMaxProbe];
+    uint64_t probe_stride[kMaxProbe] = {};
+    DevBuf probe_C, probe_clients;
     std::vector<DevBuf*> hist_epochs;            // hist rows; a new epoch per F_cap growth
     std::vector<uint32_t*> hist_ptr;             // per level
     uint32_t E_cap = 0, F_cap = 0;
@@ -1073,6 +1078,20 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     HIP_TRY(c0, B.ctl_host.ensure(sizeof(LoopCtl)));
     rc = loop_resize(c0, B, cap0, cap0, levels, 0, false, 0, 0, 1);
     if (rc) return rc;
+    if (cfg->probe_n_levels) {
+        if (cfg->probe_n_levels > LoopBuffers::kMaxProbe || !cfg->probe_levels || !cfg->probe_n_clients ||
+            !cfg->probe_clients || !cfg->probe_seeds || !cfg->probe_ty || !cfg->probe_children)
+            return c0->fail(FHH_E_ARG, "sim_crawl: bad probe arguments");
+        if (c0->tab_bs) return c0->fail(FHH_E_ARG, "sim_crawl: the probe reads the T-table variants' layout");
+        for (uint32_t i = 0; i < cfg->probe_n_clients; i++)
+            if (cfg->probe_clients[i] >= c0->n) return c0->fail(FHH_E_ARG, "sim_crawl: probe client out of range");
+        HIP_TRY(c0, B.probe_C.ensure((size_t)cfg->probe_n_levels * 4));
+        HIP_TRY(c0, hipMemsetAsync(B.probe_C.p, 0, (size_t)cfg->probe_n_levels * 4, c0->stream));
+        HIP_TRY(c0, B.probe_clients.ensure((size_t)cfg->probe_n_clients * 8));
+        HIP_TRY(c0, hipMemcpyAsync(B.probe_clients.p, cfg->probe_clients, (size_t)cfg->probe_n_clients * 8,
+                                   hipMemcpyHostToDevice, c0->stream));
+        HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+    }
     {
         uint32_t* l0[kMaxDims] = {nullptr, nullptr, nullptr, nullptr};
         for (uint32_t j = 0; j < d; j++) l0[j] = B.live[0].as<uint32_t>() + (size_t)j * B.E_cap;
@@ -1123,6 +1142,32 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             HIP_TRY(c0, launch_expand(La, variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
             if (timed) HIP_TRY(c0, timing_end(c0, slot, 0));
             c0->stats.expand_launches++;
+            for (uint32_t k = 0; k < cfg->probe_n_levels; k++) {
+                if (cfg->probe_levels[k] != lv) continue;
+                const size_t per = (size_t)C_cap * cfg->probe_n_clients * d * 2;
+                HIP_TRY(c0, B.probe_seed[k].ensure(2 * per * 16));
+                HIP_TRY(c0, B.probe_ty[k].ensure(2 * per));
+                B.probe_stride[k] = C_cap;
+                ProbeArgs pr{};
+                for (int s = 0; s < 2; s++)
+                    for (uint32_t j = 0; j < d; j++) {
+                        pr.seed[s][j] = cs[s]->tab[j].seed[1 - par].as<uint4>();
+                        pr.t[s][j] = cs[s]->tab[j].t[1 - par].as<uint64_t>();
+                        pr.y[s][j] = cs[s]->tab[j].y[1 - par].as<uint64_t>();
+                    }
+                pr.parent_pos = B.pos[par].as<uint32_t>();
+                pr.clients = B.probe_clients.as<uint64_t>();
+                pr.ctl = B.ctl.as<LoopCtl>();
+                pr.out_seed = B.probe_seed[k].as<uint4>();
+                pr.out_ty = B.probe_ty[k].as<uint8_t>();
+                pr.out_C = B.probe_C.as<uint32_t>() + k;
+                pr.C_cap = C_cap;
+                pr.npad = c0->npad;
+                pr.nw = c0->nw;
+                pr.n_probe = cfg->probe_n_clients;
+                pr.d = d;
+                HIP_TRY(c0, launch_probe_states(pr, c0->stream));
+            }
             // -- equality count / simulated OT sums per child
             ChildArgs a{};
             for (uint32_t j = 0; j < d; j++) {
@@ -1449,6 +1494,25 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             }
         }
         off += C;
+    }
+    if (cfg->probe_n_levels) {
+        std::vector<uint32_t> pC(cfg->probe_n_levels);
+        HIP_TRY(c0, hipMemcpy(pC.data(), B.probe_C.p, pC.size() * 4, hipMemcpyDeviceToHost));
+        const size_t row = (size_t)cfg->probe_n_clients * d * 2;   // states per (server, child)
+        const size_t cap = cfg->probe_capacity;
+        for (uint32_t k = 0; k < cfg->probe_n_levels; k++) {
+            cfg->probe_children[k] = pC[k];
+            const size_t nc = std::min<size_t>(std::min<size_t>(pC[k], cap), B.probe_stride[k]);
+            if (!nc || !B.probe_seed[k].p) continue;
+            for (int s = 0; s < 2; s++) {
+                uint8_t* hs = cfg->probe_seeds + (((size_t)k * 2 + s) * cap) * row * 16;
+                uint8_t* ht = cfg->probe_ty + (((size_t)k * 2 + s) * cap) * row;
+                HIP_TRY(c0, hipMemcpy(hs, B.probe_seed[k].as<uint8_t>() + (size_t)s * B.probe_stride[k] * row * 16,
+                                      nc * row * 16, hipMemcpyDeviceToHost));
+                HIP_TRY(c0, hipMemcpy(ht, B.probe_ty[k].as<uint8_t>() + (size_t)s * B.probe_stride[k] * row, nc * row,
+                                      hipMemcpyDeviceToHost));
+            }
+        }
     }
     pc.mark("readback");
     return FHH_OK;
@@ -1988,6 +2052,8 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     if (cfg->gc && (cfg->mode != 1 || cfg->host_loop))
         return c0->fail(FHH_E_ARG, "sim_crawl: gc needs mode 1 (OT share values) and the device loop");
     if (cfg->gc && 2 * c0->d > (uint32_t)kGcMaxBits) return c0->fail(FHH_E_ARG, "sim_crawl: gc supports d <= 4");
+    if (cfg->probe_n_levels && cfg->host_loop)
+        return c0->fail(FHH_E_ARG, "sim_crawl: the probe instruments the device loop (host_loop = 0)");
     if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");
     if (c0->d != c1->d || c0->L != c1->L) return c0->fail(FHH_E_ARG, "sim_crawl: ctx shapes differ");
     // leader.rs:193-194 and 245-246

@@ -297,6 +297,23 @@ hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,
                               uint32_t* out, uint64_t cap, hipStream_t stream);
+// parity probe of the device loop (fhh_sim_config.probe_*): the pending children's states of a
+// client sample, both servers, gathered between k_expand and the count (fhh_loop.hip)
+struct ProbeArgs {
+    const uint4* seed[2][kMaxDims];     // child tables [E][2][npad] of server s, dim j
+    const uint64_t* t[2][kMaxDims];     // [E][2][nw]
+    const uint64_t* y[2][kMaxDims];
+    const uint32_t* parent_pos;         // [F][d]
+    const uint64_t* clients;            // [n_probe] local client indices (< n)
+    const LoopCtl* ctl;                 // C (0 once aborted)
+    uint4* out_seed;                    // [2][C_cap][n_probe][d][2]
+    uint8_t* out_ty;                    // [2][C_cap][n_probe][d][2]: bit0 t, bit1 y
+    uint32_t* out_C;                    // C of the level (written unless aborted)
+    uint64_t C_cap;
+    uint64_t npad, nw;
+    uint32_t n_probe, d;
+};
+hipError_t launch_probe_states(const ProbeArgs& a, hipStream_t stream);
 hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
                             uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
                             hipStream_t stream);

@@ -209,6 +209,46 @@ hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint
     return hipGetLastError();
 }
 
+// One lane per (server, child, probed client, dim, side): child c's dim-j entry in the child
+// table is 2 * parent_pos[(c >> d) * d + j] + ((c >> j) & 1), as k_eq_count reads it.
+__global__ __launch_bounds__(256) void k_probe_states(ProbeArgs a) {
+    const LoopCtl* ctl = a.ctl;
+    if (ctl->abort) return;   // re-run after the resumption
+    const uint64_t C = ctl->C < a.C_cap ? ctl->C : a.C_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.out_C = ctl->C;
+    const uint32_t d = a.d, mask = (1u << d) - 1;
+    const uint64_t per_c = (uint64_t)a.n_probe * d * 2;
+    const uint64_t total = 2 * C * per_c;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(k & 1);
+        uint64_t r = k >> 1;
+        const uint32_t j = (uint32_t)(r % d);
+        r /= d;
+        const uint32_t i = (uint32_t)(r % a.n_probe);
+        r /= a.n_probe;
+        const uint64_t c = r % C;
+        const uint32_t srv = (uint32_t)(r / C);
+        const uint32_t e = 2 * a.parent_pos[(c >> d) * d + j] + (((uint32_t)(c & mask) >> j) & 1);
+        const uint64_t x = a.clients[i];
+        const size_t row = (size_t)e * 2 + s;
+        const uint4 sd = a.seed[srv][j][row * a.npad + x];
+        const uint64_t tb = (a.t[srv][j][row * a.nw + (x >> 6)] >> (x & 63)) & 1;
+        const uint64_t yb = (a.y[srv][j][row * a.nw + (x >> 6)] >> (x & 63)) & 1;
+        const size_t o = (((size_t)srv * a.C_cap + c) * a.n_probe + i) * d * 2 + (size_t)j * 2 + s;
+        a.out_seed[o] = sd;
+        a.out_ty[o] = (uint8_t)(tb | (yb << 1));
+    }
+}
+
+hipError_t launch_probe_states(const ProbeArgs& a, hipStream_t stream) {
+    const uint64_t most = 2 * a.C_cap * a.n_probe * a.d * 2;
+    const uint64_t blocks = (most + 255) / 256;
+    hipLaunchKernelGGL(k_probe_states, dim3((uint32_t)(blocks < 4096 ? (blocks ? blocks : 1) : 4096)), dim3(256), 0,
+                       stream, a);
+    return hipGetLastError();
+}
+
 __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
                             uint32_t nctx,
                             uint64_t grid_waves, uint32_t* pos0, uint32_t* l0, uint32_t* l1, uint32_t* l2,

@@ -25,6 +25,9 @@ class SimResult:
     level_kept: np.ndarray
     counts: list = field(default_factory=list)     # per level np.ndarray (mode count: counts; fe: v0-v1)
     final: list = field(default_factory=list)      # Result(path, value) from server 0's final_shares
+    # probe: level -> (seeds [2][C][m][d][2][16], t [2][C][m][d][2], y [2][C][m][d][2]) of the
+    # probed clients (server 0, server 1), read inside the device loop right after k_expand
+    probe: dict = field(default_factory=dict)
 
 
 class _TorchAllReduce:
@@ -58,7 +61,7 @@ class _TorchAllReduce:
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
-              init_capacity: int = 0, comm=None, gc=False) -> SimResult:
+              init_capacity: int = 0, comm=None, gc=False, probe: dict | None = None) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
@@ -66,7 +69,11 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     device loop) takes each (child, client) equality bit from the GPU garbled-circuit equality
     test (server 0 garbles, server 1 evaluates) instead of comparing shares: `True` / "ot" with
     the evaluator's labels and the FE shares moved by the GPU OT extension (base OTs ideal),
-    "ideal" with both OTs ideal."""
+    "ideal" with both OTs ideal.
+
+    `probe` (parity tests) = {"levels": [...], "clients": [...], "capacity": C_max}: the device
+    loop gathers those clients' EvalStates of every pending child right after each listed
+    level's k_expand (res.probe)."""
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -98,11 +105,34 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     if record:
         cfg.counts = counts.ctypes.data_as(u64p)
         cfg.counts_capacity = cap
+    if probe:
+        d = c0.n_dims
+        p_lv = np.ascontiguousarray(np.asarray(probe["levels"], np.uint32))
+        p_cl = np.ascontiguousarray(np.asarray(probe["clients"], np.uint64))
+        p_cap = int(probe["capacity"])
+        m = p_cl.size
+        p_seeds = np.zeros((p_lv.size, 2, p_cap, m, d, 2, 16), np.uint8)
+        p_ty = np.zeros((p_lv.size, 2, p_cap, m, d, 2), np.uint8)
+        p_C = np.zeros(p_lv.size, np.uint64)
+        cfg.probe_n_levels = p_lv.size
+        cfg.probe_n_clients = m
+        cfg.probe_levels = p_lv.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+        cfg.probe_clients = p_cl.ctypes.data_as(u64p)
+        cfg.probe_capacity = p_cap
+        cfg.probe_seeds = p_seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        cfg.probe_ty = p_ty.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        cfg.probe_children = p_C.ctypes.data_as(u64p)
     rc = lib().fhh_sim_crawl(c0.handle, c1.handle, ctypes.byref(cfg))
     if ar is not None and ar.err is not None:
         raise ar.err
     check(rc, c0.handle)
     res = SimResult(lc, lk)
+    if probe:
+        for k, lv in enumerate(p_lv):
+            C = int(p_C[k])
+            if C > p_cap:
+                raise ValueError(f"probe: level {lv} has {C} children > capacity {p_cap}")
+            res.probe[int(lv)] = (p_seeds[k, :, :C], p_ty[k, :, :C] & 1, p_ty[k, :, :C] >> 1)
     if record:
         off = 0
         for C in lc:

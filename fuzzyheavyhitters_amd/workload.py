@@ -46,9 +46,7 @@ def _add_small(bits: np.ndarray, delta: int, sign: int) -> np.ndarray:
     pad = nwords * 64 - W
     b = np.concatenate([np.zeros(bits.shape[:-1] + (pad,), np.uint8), bits], axis=-1)
     # pack big-endian into u64 words (word 0 most significant)
-    words = np.zeros(bits.shape[:-1] + (nwords,), np.uint64)
-    for k in range(64):
-        words |= b[..., k::64].astype(np.uint64) << np.uint64(63 - k)
+    words = np.packbits(b, axis=-1, bitorder="big").view(">u8").astype(np.uint64)
     carry = np.full(bits.shape[:-1], np.uint64(delta), np.uint64)
     for wi in range(nwords - 1, -1, -1):
         x = words[..., wi]
@@ -61,10 +59,8 @@ def _add_small(bits: np.ndarray, delta: int, sign: int) -> np.ndarray:
         words[..., wi] = nx
     if sign > 0 and np.any(carry) or (sign > 0 and pad and np.any(words[..., 0] >> np.uint64(64 - pad))):
         raise ValueError("carry out of add_bitstrings: the reference panics on this input (ibDCF.rs:182)")
-    out = np.zeros_like(b)
-    for k in range(64):
-        out[..., k::64] = ((words >> np.uint64(63 - k)) & np.uint64(1)).astype(np.uint8)
-    return out[..., pad:]
+    out = np.unpackbits(np.ascontiguousarray(words.astype(">u8")).view(np.uint8), axis=-1, bitorder="big")
+    return np.ascontiguousarray(out[..., pad:])
 
 
 def l_inf_ball_bounds(alpha: np.ndarray, ball: int):

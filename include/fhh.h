@@ -185,6 +185,14 @@ void fhh_comm_destroy(fhh_comm* comm);
  * (hipStream_t; NULL = the null stream). Asynchronous. */
 int fhh_comm_allreduce_u64(fhh_comm* comm, const uint64_t* send_dev, uint64_t* recv_dev, uint64_t count,
                            void* stream);
+/* A communicator without RCCL: fhh_comm_allreduce_u64 and the level loop's cfg->comm path
+ * drain the stream, copy the partials to a host buffer, call fn(host_buf, count, user) to sum
+ * them in place across ranks (e.g. over gloo), and copy the result back. For tests of the
+ * comm path where RCCL ranks are not available (one GPU shared by several ranks). */
+int fhh_comm_create_hosted(fhh_comm** out, int nranks, int rank, int device, fhh_allreduce_fn fn, void* user);
+/* The rank count and rank RCCL itself reports for the communicator (ncclCommCount /
+ * ncclCommUserRank) — what the bench records as the ranks the collective saw. */
+int fhh_comm_info(fhh_comm* comm, int* nranks, int* rank);
 /* Last error of the calling thread's fhh_rccl_* / fhh_comm_* call. */
 const char* fhh_comm_last_error(void);
 
@@ -220,6 +228,23 @@ typedef struct fhh_sim_config {
      * extension (fhh_ot_*; base OTs ideal; a FieldElm share travels as a BlockPair = 2 OTs).
      * Same sums as 0; fresh garbler key, Delta, mask and base OTs per level, from prf_seed. */
     uint32_t gc;
+    /* parity probe of the device loop (tests; probe_n_levels = 0 disables it): right after level
+     * probe_levels[k]'s k_expand, the pending children's EvalStates (ibDCF.rs:24-30) of the
+     * local clients probe_clients[0..probe_n_clients) are gathered from both servers' tables.
+     *   probe_seeds    [probe_n_levels][2 server][probe_capacity][probe_n_clients][d][2 side][16]
+     *   probe_ty       [probe_n_levels][2][probe_capacity][probe_n_clients][d][2]: bit0 t, bit1 y
+     *   probe_children [probe_n_levels]: C of that level (children past probe_capacity are not
+     *                  copied; the caller checks C <= capacity)
+     * Child order is the crawl's (parent order x all_bit_vectors), as fhh_export_states. The
+     * gather is a separate kernel between k_expand and the count: the timed path is unchanged. */
+    uint32_t probe_n_levels;   /* <= 16 */
+    uint32_t probe_n_clients;
+    const uint32_t* probe_levels;
+    const uint64_t* probe_clients;
+    uint64_t probe_capacity;
+    uint8_t* probe_seeds;
+    uint8_t* probe_ty;
+    uint64_t* probe_children;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x

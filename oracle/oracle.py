@@ -211,6 +211,35 @@ def level_expand(keys: ServerKeys, st: States, parent_idx, level: int, nthreads:
     return out, int(blocks)
 
 
+def subset_keys(keys: ServerKeys, clients) -> ServerKeys:
+    """The keys of a client sample (in the given order)."""
+    idx = np.asarray(clients, np.int64)
+    return ServerKeys(np.ascontiguousarray(keys.key_idx[idx]), np.ascontiguousarray(keys.root_seed[idx]),
+                      np.ascontiguousarray(keys.cw_seed[idx]), np.ascontiguousarray(keys.cw_bits[idx]))
+
+
+def replay_states(keys0: ServerKeys, keys1: ServerKeys, keeps, want_levels, nthreads: int = 0):
+    """The crawl's expansion (collect.rs:379-391) for the clients in keys0/keys1 along a GIVEN
+    frontier: level l expands the children kept at level l - 1 (keeps[l - 1], a bool mask over
+    that level's children, e.g. from the run under test, decided over all clients). The EvalStates
+    of every child depend only on the client's own keys and the child's path, so a client sample
+    evaluated on the full run's frontier must reproduce that run's states exactly.
+    Returns {level: (States server 0, States server 1)} for the levels in want_levels."""
+    want = set(int(x) for x in want_levels)
+    out = {}
+    s0, s1 = tree_init(keys0), tree_init(keys1)
+    parents = np.zeros(1, np.uint64)
+    for lv in range(max(want) + 1):
+        c0, _ = level_expand(keys0, s0, parents, lv, nthreads)
+        c1, _ = level_expand(keys1, s1, parents, lv, nthreads)
+        if lv in want:
+            out[lv] = (c0, c1)
+        if lv < len(keeps):
+            parents = np.nonzero(np.asarray(keeps[lv], bool))[0].astype(np.uint64)
+        s0, s1 = c0, c1
+    return out
+
+
 def share_bits(st: States) -> np.ndarray:
     """collect.rs:393-418: [C][n][2d], left dims then right dims."""
     e = st.t ^ st.y                       # [C][n][d][2]
@@ -330,6 +359,7 @@ class CrawlResult:
     aes_blocks: int = 0
     states0: list = field(default_factory=list)     # optional: per level States
     states1: list = field(default_factory=list)
+    level_states: dict = field(default_factory=dict)   # keep_levels: level -> (States0, States1)
 
 
 def thresholds(frac: float, nclients: int):
@@ -341,9 +371,11 @@ def thresholds(frac: float, nclients: int):
 
 def crawl(keys0: ServerKeys, keys1: ServerKeys, threshold: float, mode: str = "count", sim_seed: int = 0,
           nthreads: int = 0, keep_states: bool = False, levels: int | None = None,
-          max_seconds: float | None = None) -> CrawlResult:
+          max_seconds: float | None = None, keep_levels=None) -> CrawlResult:
     """max_seconds bounds the run (CPU-baseline sampling): stops after the level that
-    crosses it; res.n_children then covers only the levels done."""
+    crosses it; res.n_children then covers only the levels done. keep_levels: record the
+    children's States only at these levels (res.level_states[level] = (States0, States1))."""
+    keep_set = set(int(x) for x in keep_levels) if keep_levels is not None else set()
     import time
     t_start = time.perf_counter()
     n, d, _, L = keys0.cw_bits.shape
@@ -383,6 +415,8 @@ def crawl(keys0: ServerKeys, keys1: ServerKeys, threshold: float, mode: str = "c
         if keep_states:
             res.states0.append(c0)
             res.states1.append(c1)
+        if level in keep_set:
+            res.level_states[level] = (c0, c1)
         child_paths = []
         for p in paths:
             for i in range(1 << d):

@@ -1,0 +1,71 @@
+"""bench.py's multi-rank plan on the CPU: the strong-scaling shard of the 1M-client population
+(configs[2] at 8 ranks), the per-rank workload slices, and the max-over-ranks / sum-over-ranks
+aggregation over a gloo world of 2 (the control group bench.py uses at N > 1)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.mark.parametrize("n,world", [(1_000_000, 8), (1_000_000, 3), (100_000, 2), (7, 4), (1000, 1)])
+def test_shard_covers_population(n, world):
+    import bench
+    ranges = [bench.shard(n, world, r) for r in range(world)]
+    assert ranges[0][0] == 0
+    for (b0, n0), (b1, _) in zip(ranges, ranges[1:]):
+        assert b0 + n0 == b1
+    assert sum(k for _, k in ranges) == n
+    assert max(k for _, k in ranges) - min(k for _, k in ranges) <= 1
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from fuzzyheavyhitters_amd import workload
+        n = 1000
+        base, k = bench.shard(n, world, rank)
+        wl = workload.zipf_workload(k, 64, 1, num_sites=50, seed=0x5EED, client_offset=base)
+        parts = [None] * world
+        dist.all_gather_object(parts, (base, wl.left, wl.root_seeds))
+        elapsed = torch.tensor([0.5 + rank], dtype=torch.float64)
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        blocks = torch.tensor([10 * (rank + 1)], dtype=torch.int64)
+        dist.all_reduce(blocks)
+        if rank == 0:
+            q.put((parts, float(elapsed.item()), int(blocks.item())))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_plan_and_aggregation():
+    import socket
+    from fuzzyheavyhitters_amd import workload
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    parts, elapsed, blocks = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = workload.zipf_workload(1000, 64, 1, num_sites=50, seed=0x5EED)
+    assert [b for b, _, _ in parts] == [0, 500]
+    assert np.array_equal(np.concatenate([l for _, l, _ in parts]), full.left)
+    assert np.array_equal(np.concatenate([r for _, _, r in parts]), full.root_seeds)
+    assert elapsed == 1.5 and blocks == 30

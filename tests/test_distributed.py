@@ -129,7 +129,8 @@ def test_sharded_crawl_equals_single_process(oracle, mode):
     assert sorted(final) == sorted(tuple(tuple(int(b) for b in pj) for pj in p) for p in ref.final_paths)
 
 
-def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0, gc=False):
+def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0, gc=False,
+                hosted_comm=False):
     import sys
     sys.path.insert(0, ROOT)
     import torch
@@ -149,8 +150,12 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_
         fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
         c0.set_client_base(rank * n_local)
         c1.set_client_base(rank * n_local)
-        res = fhh.sim_crawl(c0, c1, thr, nclients_total=wl_args["n"], mode=mode, prf_seed=7, distributed=True,
-                            host_loop=host_loop, init_capacity=init_capacity, gc=gc)
+        comm = fhh.HostedComm(0) if hosted_comm else None
+        if comm is not None:
+            assert comm.info() == (world, rank)
+        res = fhh.sim_crawl(c0, c1, thr, nclients_total=wl_args["n"], mode=mode, prf_seed=7,
+                            distributed=comm is None, comm=comm, host_loop=host_loop, init_capacity=init_capacity,
+                            gc=gc)
         if rank == 0:
             q.put((res.level_children.tolist(), [c.tolist() for c in res.counts],
                    sorted(tuple(tuple(int(b) for b in pj) for pj in r.path) for r in res.final)))
@@ -160,19 +165,23 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,loop", [("count", "device_grow"), ("count", "host"), ("fe", "device_grow"),
-                                       ("fe", "host"), ("fe", "device_gc_ot")])
+                                       ("fe", "host"), ("fe", "device_gc_ot"), ("count", "comm_grow"),
+                                       ("fe", "comm_grow"), ("fe", "comm_host")])
 def test_gpu_two_ranks_allreduce_hook(oracle, mode, loop):
     """Two ranks share one GPU over the host all-reduce hook. device_grow starts the device
     loop at capacity 2 so it aborts and resumes several times: the cross-rank sum of an
-    aborted level must not be applied twice (out-of-place reduction)."""
+    aborted level must not be applied twice (out-of-place reduction). comm_* drive the level
+    loop's native-communicator path (cfg.comm, the path bench.py takes at N > 1) with a hosted
+    communicator (fhh_comm_create_hosted: the sum over gloo instead of RCCL, which cannot put two
+    ranks on one GPU)."""
     from fuzzyheavyhitters_amd import workload
     wl_args = {"n": 256, "L": 48, "d": 1, "sites": 6, "seed": 77}
     thr = 0.02
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    kw = {"host_loop": loop == "host", "init_capacity": 2 if loop.startswith("device") else 0,
-          "gc": "ot" if loop == "device_gc_ot" else False}
+    kw = {"host_loop": loop in ("host", "comm_host"), "init_capacity": 2 if loop.endswith("grow") else 0,
+          "gc": "ot" if loop == "device_gc_ot" else False, "hosted_comm": loop.startswith("comm")}
     procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, wl_args, thr, mode, q), kwargs=kw) for r in range(2)]
     for p in procs:
         p.start()

@@ -1,0 +1,113 @@
+"""Parity that sees the AES at the timed sizes.
+
+The heavy-hitter output does not depend on any AES block (the PRG's control bits are constant
+after the nibble mask, prg.rs:96-105), so full-size count checks cannot catch a
+wrong seed. Here the device loop's own k_expand states are read back (the probe of
+fhh_sim_config, a gather kernel between k_expand and the count) for a sample of clients that
+touches every 64-client word — hence every work item and every wave of the persistent launch —
+and compared with the oracle (oracle.replay_states: eval_bit, ibDCF.rs:208-227, with
+expand_dir, prg.rs:92-122) evaluated for just those clients along the same surviving paths.
+
+configs[0] (the reference's own CPU configuration, leader.rs:299-443: 1000 Zipf clients,
+num_sites 10000, s = 1.03, data_len 512, threshold 0.001) is run exactly, on both sides.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def sample_clients(n: int, word_step: int = 1, seed: int = 7) -> np.ndarray:
+    """One client per `word_step`-th 64-client word at a varying lane, plus the edges (first and
+    last words, the partial last word)."""
+    nw = (n + 63) // 64
+    rng = np.random.default_rng(seed)
+    w = np.arange(0, nw, word_step)
+    c = np.minimum(w * 64 + rng.integers(0, 64, w.size), n - 1)
+    edges = [0, 1, 63, 64, 65, n - 1, n - 2, ((n - 1) // 64) * 64, max(0, n - 65)]
+    return np.unique(np.concatenate([c, np.array([e for e in edges if 0 <= e < n])])).astype(np.uint64)
+
+
+def keeps_from_counts(res, thr: int, thr_last: int):
+    L = len(res.counts)
+    return [np.asarray(res.counts[lv]) >= (thr_last if lv == L - 1 else thr) for lv in range(L)]
+
+
+def assert_probe_equal(res, ref, clients_sel=None):
+    for lv, (seeds, t, y) in res.probe.items():
+        o0, o1 = ref[lv]
+        for s, o in ((0, o0), (1, o1)):
+            os_, ot, oy = o.seed, o.t, o.y
+            if clients_sel is not None:
+                os_, ot, oy = os_[:, clients_sel], ot[:, clients_sel], oy[:, clients_sel]
+            assert seeds[s].shape == os_.shape, f"level {lv} server {s}: {seeds[s].shape} vs {os_.shape}"
+            bad = np.nonzero(np.any(seeds[s] != os_, axis=-1))
+            assert bad[0].size == 0, (f"level {lv} server {s}: {bad[0].size} seeds differ, first (child, "
+                                      f"client, dim, side) = {[int(b[0]) for b in bad]}")
+            assert np.array_equal(t[s], ot), f"level {lv} server {s}: t bits differ"
+            assert np.array_equal(y[s], oy), f"level {lv} server {s}: y bits differ"
+
+
+def crawl_with_probe(n, L, levels, clients, cap, seed=0x5EED, num_sites=10_000, threshold=0.001):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(n, L, 1, num_sites=num_sites, zipf_s=1.03, ball_size=1, seed=seed)
+    c0, c1 = fhh.KeyCollection(L, 1), fhh.KeyCollection(L, 1)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    res = fhh.sim_crawl(c0, c1, threshold, mode="count",
+                        probe={"levels": levels, "clients": clients, "capacity": cap})
+    return wl, c0, c1, res
+
+
+@pytest.mark.parametrize("n,word_step", [(100_000, 1), (1_000_000, 8)], ids=["configs1-100k", "1M"])
+def test_sampled_states_bit_exact_full_size(oracle, n, word_step):
+    """configs[1] (100k clients) and the metric's 1M clients, data_len 512, seed 0x5EED: the
+    default k_expand's seeds / t / y of every child at levels 0, 1, a middle level, L-2 and
+    L-1 equal the oracle's for a client in every word (configs[1]) / every 8th word (1M)."""
+    L = 512
+    clients = sample_clients(n, word_step)
+    levels = [0, 1, 256, L - 2, L - 1]
+    wl, c0, c1, res = crawl_with_probe(n, L, levels, clients, cap=1024)
+    thr = max(1, int(0.001 * n))
+    keeps = keeps_from_counts(res, thr, thr)
+    k0, k1 = oracle.gen_keys(wl.left[clients.astype(np.int64)], wl.right[clients.astype(np.int64)],
+                             wl.root_seeds[clients.astype(np.int64)])
+    ref = oracle.replay_states(k0, k1, keeps, levels)
+    assert set(res.probe) == set(levels)
+    for lv in levels:
+        assert res.probe[lv][0].shape[1] == res.level_children[lv] > 0
+    assert_probe_equal(res, ref)
+    if n > 100_000:
+        return   # 1M: the plaintext recount takes minutes in numpy (tools/verify_full.py runs it)
+    # the crawl itself (AES-independent) still matches the plaintext recount
+    from fuzzyheavyhitters_amd import workload
+    cnt, paths, _ = workload.plaintext_crawl(wl.left, wl.right, thr, thr)
+    assert [len(c) for c in cnt] == [int(x) for x in res.level_children]
+    assert all(np.array_equal(a, np.asarray(b)) for a, b in zip(cnt, res.counts))
+    got = sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in res.final)
+    assert got == sorted(paths)
+
+
+def test_configs0_gpu_equals_oracle(oracle):
+    """configs[0] exactly (leader.rs:299-443, SURVEY §8d Config A): 1000 Zipf clients over
+    num_sites 10000 (s = 1.03), data_len 512, d = 1, ball 1, threshold 0.001 -> count threshold
+    max(1, 1) = 1, so every non-empty node survives. GPU device loop vs the oracle's crawl
+    (reference child order): every level's child count, counts and keep masks, the heavy
+    hitters and their counts, and the EvalStates of every client at levels 0, 255 and 511."""
+    n, L = 1000, 512
+    levels = [0, 255, L - 1]
+    clients = np.arange(n, dtype=np.uint64)
+    wl, c0, c1, res = crawl_with_probe(n, L, levels, clients, cap=4096)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    ores = oracle.crawl(k0, k1, 0.001, mode="count", keep_levels=levels)
+    assert list(res.level_children) == list(ores.n_children)
+    assert sum(ores.n_children) > 100_000            # ~4.9e5 children summed
+    for lv in range(L):
+        assert np.array_equal(res.counts[lv], ores.counts[lv]), f"counts level {lv}"
+        assert int(res.level_kept[lv]) == int(ores.keeps[lv].sum()), f"keep mask level {lv}"
+    got = [(tuple(tuple(int(b) for b in p) for p in r.path), int(r.value)) for r in res.final]
+    exp = [(tuple(tuple(int(x) for x in p) for p in fp), int(v)) for fp, v in zip(ores.final_paths, ores.final_values)]
+    assert got == exp
+    assert_probe_equal(res, ores.level_states)
+    st = c0.stats()
+    assert st["aes_blocks"] * 2 == ores.aes_blocks

@@ -121,6 +121,22 @@ def test_plaintext_crawl_equals_oracle(oracle, kind):
     assert finals == [int(v) for v in ref.final_values]
 
 
+def test_replay_states_on_client_sample(oracle):
+    """oracle.replay_states (the checker of the full-size GPU probe) on a client sample, driven
+    by the full crawl's keep masks, reproduces the full crawl's states of those clients."""
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(300, 48, 1, num_sites=6, seed=9)
+    k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    levels = [0, 7, 46, 47]
+    full = oracle.crawl(k0, k1, 0.02, mode="count", keep_levels=levels)
+    sel = np.array([0, 5, 63, 64, 199, 299])
+    ref = oracle.replay_states(oracle.subset_keys(k0, sel), oracle.subset_keys(k1, sel), full.keeps, levels)
+    for lv in levels:
+        for a, b in zip(ref[lv], full.level_states[lv]):
+            assert np.array_equal(a.seed, b.seed[:, sel]) and np.array_equal(a.t, b.t[:, sel])
+            assert np.array_equal(a.y, b.y[:, sel])
+
+
 @pytest.mark.gpu
 def test_gpu_full_size_configs1_equals_plaintext(oracle):
     """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): every

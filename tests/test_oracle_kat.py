@@ -123,7 +123,9 @@ def test_ibdcf_semantics_exhaustive(oracle, nbits):
 def test_bitstring_utils(oracle):
     o = oracle
     assert o.u32_to_bits(5, 21) == [True, False, True, False, True]
-    assert o.msb_u32_to_bits(5, 21) == [True, False, True, False, True][::-1] or True
+    # lib.rs:56-76: u32_to_bits is LSB first, MSB_u32_to_bits MSB first (6 = 0b00110)
+    assert o.u32_to_bits(5, 6) == [False, True, True, False, False]
+    assert o.msb_u32_to_bits(5, 6) == [False, False, True, True, False]
     assert o.bits_to_u32(o.msb_u32_to_bits(7, 77)) == 77
     assert o.add_bitstrings([True, True], [True]) == [True, False, False]
     assert o.subtract_bitstrings([False, False], [False, True]) == [True, True]

@@ -4,7 +4,7 @@ kernel stats, per-kernel PMC means, and profiles/pmc_expand.json for bench.py's
 roofline.traffic: HBM bytes per k_expand launch = FETCH_SIZE x 2 (gfx950 reports half of a
 16-B/lane streaming read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB x 1024.
 
-    python tools/pmc_summary.py <tag> [--config n100000_L512_d1]
+    python tools/pmc_summary.py <tag> [--config n1000000_L512_d1]
 """
 import collections
 import csv
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     tag = sys.argv[1]
-    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "n100000_L512_d1"
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "n1000000_L512_d1"
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -58,7 +58,16 @@ def main():
             res["sq_lds_bank_conflict"] = ex["SQ_LDS_BANK_CONFLICT"]["mean_per_dispatch"]
         if "GRBM_GUI_ACTIVE" in ex and res["k_expand_avg_ns"]:
             res["effective_clock_ghz"] = ex["GRBM_GUI_ACTIVE"]["mean_per_dispatch"] / 8 / res["k_expand_avg_ns"]
-        json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_expand.json"), "w"), indent=1)
+        # profiles/pmc_expand.json holds one entry per workload (bench.py looks up its own)
+        path = os.path.join(ROOT, "profiles", "pmc_expand.json")
+        try:
+            allp = json.load(open(path))
+        except (OSError, ValueError):
+            allp = {}
+        if "config" in allp:          # the single-entry format of r01
+            allp = {allp["config"]: allp}
+        allp[config] = res
+        json.dump(allp, open(path, "w"), indent=1)
         print(json.dumps(res, indent=1))
     print(json.dumps(stats, indent=1))
 

@@ -12,7 +12,8 @@
 //                2 ciphertexts per AND gate (4 TCCR = 8 AES), its active input labels, the
 //                evaluator's active labels (ideal OT: the labels an OT extension would deliver)
 //                and the output decoding bit
-//   k_gc_eval    one lane per test: 2 TCCR (4 AES) per AND gate, output bit = colour ^ decode
+//   k_gc_eval    one lane per test: 2 TCCR (4 AES) per AND gate, output bit = colour ^ decode,
+//                optionally also ballot-packed as the FE-share OT's choice words
 //
 // Both use the 4-table / 32-replica LDS T-table (conflict-free, as k_expand) and SoA outputs, so
 // a wave's 64 lanes read and write 64 consecutive 16-B blocks.
@@ -127,7 +128,9 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
                 bz[c] = s[0][c] ^ s[1][c] ^ D[c];   // z_k = NOT(x_k ^ y_k): free XOR, NOT = ^Delta
             }
             st_blk(a.gb_labels, k, n, t, x);
-            if (a.ev_ot) st_blk(a.ev_labels, t, B, k, y);   // OT sender input x0 = zero label
+            // OT sender input x0 = zero label, at OT index (g B + k) Npad + i: the evaluator's share
+            // planes are then the OT's choice bits as they stand (no repacking)
+            if (a.ev_ot) st_blk(a.ev_labels, g * B + k, (uint64_t)a.nw * 64, i, y);
             else st_blk(a.ev_labels, k, n, t, y);
             if (k == 0) {
 #pragma unroll
@@ -169,49 +172,82 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     }
 }
 
+// spread 32 bits to 64: bit k -> bits 2k and 2k + 1 (the doubled choices of a BlockPair OT)
+__device__ __forceinline__ uint64_t spread2(uint32_t x) {
+    uint64_t v = x;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+    return v | (v << 1);
+}
+
+// Waves step over aligned 64-test slices (t0 wave-uniform), so with out_packed set the wave's
+// ballot of its output bits is directly the OT choice words of tests t0 .. t0 + 63 (dup = 2:
+// each bit twice, collect.rs:868) — no separate byte-to-bit pass.
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
     extern __shared__ uint32_t tbl_gc[];
     gc_fill(tbl_gc);
+    const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;
-    GcTab::bases(threadIdx.x & 63, b0, b1);
+    GcTab::bases(lane, b0, b1);
     uint32_t zrk[11][4];
     zero_rk(zrk);
     const uint64_t n = a.G * a.N;
     const uint64_t n_act = gc_active(a);
-    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
-        uint32_t acc[4], x[4], y[4];
-        ld_blk(a.gb_labels, 0, n, t, x);
-        if (a.ev_ot) ld_blk(a.ev_labels, t, B, 0, y);
-        else ld_blk(a.ev_labels, 0, n, t, y);
+    const uint64_t Npad = (uint64_t)a.nw * 64;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + (threadIdx.x & ~63u); t0 < n_act;
+         t0 += (uint64_t)gridDim.x * kGcThreads) {
+        const uint64_t t = t0 + lane;
+        uint32_t bit = 0;
+        if (t < n_act) {
+            const uint64_t g = t / a.N;
+            const uint32_t i = (uint32_t)(t - g * a.N);
+            uint32_t acc[4], x[4], y[4];
+            ld_blk(a.gb_labels, 0, n, t, x);
+            if (a.ev_ot) ld_blk(a.ev_labels, g * B, Npad, i, y);
+            else ld_blk(a.ev_labels, 0, n, t, y);
 #pragma unroll
-        for (int c = 0; c < 4; c++) acc[c] = x[c] ^ y[c];   // NOT is free for the evaluator
+            for (int c = 0; c < 4; c++) acc[c] = x[c] ^ y[c];   // NOT is free for the evaluator
 #pragma unroll
-        for (int k = 1; k < B; k++) {
-            uint32_t h[2][4], TG[4], TE[4];
-            ld_blk(a.gb_labels, k, n, t, x);
-            if (a.ev_ot) ld_blk(a.ev_labels, t, B, k, y);
-            else ld_blk(a.ev_labels, k, n, t, y);
-            ld_blk(a.tables, 2 * (k - 1), n, t, TG);
-            ld_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
+            for (int k = 1; k < B; k++) {
+                uint32_t h[2][4], TG[4], TE[4];
+                ld_blk(a.gb_labels, k, n, t, x);
+                if (a.ev_ot) ld_blk(a.ev_labels, g * B + k, Npad, i, y);
+                else ld_blk(a.ev_labels, k, n, t, y);
+                ld_blk(a.tables, 2 * (k - 1), n, t, TG);
+                ld_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                h[0][c] = acc[c];
-                h[1][c] = x[c] ^ y[c];
+                for (int c = 0; c < 4; c++) {
+                    h[0][c] = acc[c];
+                    h[1][c] = x[c] ^ y[c];
+                }
+                const uint32_t sa = acc[0] & 1u, sb = h[1][0] & 1u;
+                const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
+                const uint64_t tw[2] = {j, j + 1};
+                tccr<2>(h, tw, tbl_gc, b0, b1, zrk);
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t wg = h[0][c] ^ (sa ? TG[c] : 0u);
+                    const uint32_t we = h[1][c] ^ (sb ? (TE[c] ^ acc[c]) : 0u);
+                    acc[c] = wg ^ we;
+                }
             }
-            const uint32_t sa = acc[0] & 1u, sb = h[1][0] & 1u;
-            const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
-            const uint64_t tw[2] = {j, j + 1};
-            tccr<2>(h, tw, tbl_gc, b0, b1, zrk);
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t wg = h[0][c] ^ (sa ? TG[c] : 0u);
-                const uint32_t we = h[1][c] ^ (sb ? (TE[c] ^ acc[c]) : 0u);
-                acc[c] = wg ^ we;
+            ld_blk(a.gb_labels, B, n, t, x);   // mask wire
+            bit = ((acc[0] ^ x[0]) & 1u) ^ a.decode[t];
+            a.out[t] = (uint8_t)bit;
+        }
+        if (a.out_packed) {
+            const uint64_t v = __ballot(bit);
+            if (a.out_dup == 1) {
+                if (lane < 2) a.out_packed[t0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
+            } else if (lane < 4) {
+                const uint64_t w = spread2((uint32_t)(v >> (32 * (lane >> 1))));
+                a.out_packed[t0 / 16 + lane] = (uint32_t)(w >> (32 * (lane & 1)));
             }
         }
-        ld_blk(a.gb_labels, B, n, t, x);   // mask wire
-        a.out[t] = (uint8_t)(((acc[0] ^ x[0]) & 1u) ^ a.decode[t]);
     }
 }
 
@@ -254,55 +290,6 @@ static hipError_t gc_dispatch(const GcArgs& a, bool garble, hipStream_t stream) 
 
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, true, stream); }
 
-// evaluator's label-OT choice bits: OT index o = t * bits + j (test-major, so the active tests'
-// OTs are a prefix), bit = plane[g][j][i] with t = g * N + i; zero past G * N * bits. One lane per
-// OT (32-bit index math: the host keeps G * N * bits < 2^32), a wave ballot forms two words.
-__global__ void k_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
-                                         uint32_t* choices, uint64_t words) {
-    const uint32_t m = (uint32_t)(G * N * bits);
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; o0 < words * 32;
-         o0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t o = (uint32_t)o0 + lane;
-        uint32_t bit = 0;
-        if (o0 + lane < m) {
-            const uint32_t t = o / bits, j = o - t * bits;
-            const uint32_t g = t / N;
-            bit = plane_bit(planes, g, bits, j, nw, t - g * N);
-        }
-        const uint64_t v = __ballot(bit);
-        if (lane < 2 && o0 / 32 + lane < words) choices[o0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
-    }
-}
-
-hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
-                                         uint32_t* choices, uint64_t words, hipStream_t stream) {
-    if (G * N * bits >= (1ull << 32)) return hipErrorInvalidValue;
-    const uint64_t blocks = (words * 32 + 255) / 256;
-    hipLaunchKernelGGL(k_ot_choices_from_planes, dim3((unsigned)(blocks < 16384 ? (blocks ? blocks : 1) : 16384)),
-                       dim3(256), 0, stream, planes, G, N, nw, bits, choices, words);
-    return hipGetLastError();
-}
-
-// bytes (bit 0) -> bit words, each byte repeated `dup` times (the doubled choices of a BlockPair
-// OT, collect.rs:868), zero past n * dup: one lane per output bit, a wave ballot per two words
-__global__ void k_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words) {
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; o0 < words * 32;
-         o0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t o = o0 + lane;
-        const uint64_t v = __ballot(o < n * dup ? (in[o / dup] & 1u) : 0u);
-        if (lane < 2 && o0 / 32 + lane < words) out[o0 / 32 + lane] = (uint32_t)(v >> (32 * lane));
-    }
-}
-
-hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words,
-                           hipStream_t stream) {
-    const uint64_t blocks = (words * 32 + 255) / 256;
-    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)(blocks < 16384 ? (blocks ? blocks : 1) : 16384)), dim3(256), 0,
-                       stream, in, n, dup, out, words);
-    return hipGetLastError();
-}
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream) { return gc_dispatch(a, false, stream); }
 
 }  // namespace fhh

@@ -1196,7 +1196,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
                 HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
                 HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
-                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * tests * 16));
+                // OT mode: the evaluator's zero labels at OT index (g bits + j) npad + i
+                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * C_cap * c0->npad * 16));
                 HIP_TRY(c0, B.gc_decode.ensure(tests));
                 HIP_TRY(c0, B.gc_out.ensure(tests));
                 ChildArgs pa = a;
@@ -1228,20 +1229,27 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     // the evaluator's input labels by OT extension (gb_set_fancy_inputs /
                     // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1 receives the
                     // labels of its share bits, server 0 sends (zero label, zero label ^ Delta)
-                    const uint64_t m1 = tests * bits;
-                    uint32_t* ch = nullptr;
-                    HIP_TRY(c0, ot_choices_buffer(c0, m1, &ch));
-                    HIP_TRY(c0, launch_ot_choices_from_planes(B.gc_planes[1].as<uint64_t>(), C_cap, (uint32_t)c0->n,
-                                                              (uint32_t)c0->nw, bits, ch, ot_padded(m1) / 32,
-                                                              c0->stream));
+                    // OT index (g bits + j) npad + i: the choice bits are server 1's share planes
+                    // [C][bits][nw] as they stand (m1 is a multiple of 128: npad of 64, bits even)
+                    const uint64_t m1 = (uint64_t)C_cap * bits * c0->npad;
+                    const uint32_t* ch = B.gc_planes[1].as<uint32_t>();
                     uint32_t sw[4];
                     ot_level_choice(cfg->prf_seed, lv, 0, sw);
                     HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 0, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
                     HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
                     rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(),
-                                c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * bits, nullptr);
+                                c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits,
+                                nullptr);
                     if (rc) return rc;
                     g.ev_labels = B.gc_evact.as<uint4>();
+                }
+                const uint32_t per2 = pmode == 1 ? 1 : 2;   // OTs per test of the share conversion
+                if (real_ot) {
+                    // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
+                    uint32_t* ch = nullptr;
+                    HIP_TRY(c0, ot_choices_buffer(c0, tests * per2, &ch));
+                    g.out_packed = ch;
+                    g.out_dup = per2;
                 }
                 HIP_TRY(c0, launch_gc_eval(g, c0->stream));
                 a.gc_out = g.out;
@@ -1251,7 +1259,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     // the share conversion by OT extension (collect.rs:437-471; 846-876 at the last
                     // level, where a FieldElm travels as a BlockPair = 2 OTs): server 0 sends
                     // (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
-                    const uint32_t per = pmode == 1 ? 1 : 2;
+                    const uint32_t per = per2;
                     const uint64_t m2 = tests * per;
                     HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
                     HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
@@ -1262,9 +1270,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     else
                         HIP_TRY(c0, launch_ot_fe255_messages(a, g.mask, B.gc_msg[0].as<uint4>(),
                                                              B.gc_msg[1].as<uint4>(), c0->stream));
-                    uint32_t* ch = nullptr;
-                    HIP_TRY(c0, ot_choices_buffer(c0, m2, &ch));
-                    HIP_TRY(c0, launch_pack_bits(g.out, tests, per, ch, ot_padded(m2) / 32, c0->stream));
+                    const uint32_t* ch = g.out_packed;
                     uint32_t sw[4];
                     ot_level_choice(cfg->prf_seed, lv, 1, sw);
                     HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
@@ -2442,13 +2448,8 @@ int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
     const uint64_t mp = ot_padded(b->m), words = (b->m + 31) / 32;
     HIP_TRY(ctx, hipMemsetAsync(ch, 0, mp / 8, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ch, b->choices_dev, words * 4, hipMemcpyDeviceToDevice, ctx->stream));
-    if (b->m % 32) {   // clear the bits past m in the last word
-        std::vector<uint32_t> last(1);
-        HIP_TRY(ctx, hipMemcpyAsync(last.data(), ch + words - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        last[0] &= (1u << (b->m % 32)) - 1;
-        HIP_TRY(ctx, hipMemcpy(ch + words - 1, last.data(), 4, hipMemcpyHostToDevice));
-    }
+    // clear the bits past m in the last word, in stream order on the device
+    if (b->m % 32) HIP_TRY(ctx, launch_mask_word(ch + words - 1, (1u << (b->m % 32)) - 1, ctx->stream));
     const uint32_t* rk = nullptr;
     rc = ot_host_keys(ctx, &b->base_seeds[0][0][0], b->base_choice, &rk);
     if (rc) return rc;

@@ -183,7 +183,12 @@ struct GcArgs {
     const LoopCtl* ctl;          // non-null (level loop): groups = min(G, ctl->C), 0 once aborted;
                                  // G * N stays the SoA stride
     uint32_t ev_ot;              // 1: ev_labels holds the evaluator's ZERO labels (OT sender input)
-                                 // test-major [n][bits]; k_gc_eval then reads its OT'd labels there
+                                 // at OT index (g bits + j) Npad + i (Npad = 64 nw: the evaluator's
+                                 // share planes are the choice bits); k_gc_eval reads its OT'd
+                                 // labels there
+    uint32_t out_dup;            // out_packed: each output bit repeated out_dup (1 or 2) times
+    uint32_t* out_packed;        // non-null: k_gc_eval also writes the outputs as bit words
+                                 // (tests t0.. of a 64-aligned wave slice; the FE-share OT choices)
 };
 
 struct PruneArgs {
@@ -283,14 +288,11 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream);
+// *word &= mask (one lane; the tail of a choice-bit buffer)
+hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream);
 hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, const uint32_t s[4], uint32_t* rk,
                                 hipStream_t stream);
-// GC + OT glue (level loop): evaluator's choice bits (OT index t * bits + j) from its share planes;
-// garbler's OT messages for the FE share conversion; 0/1 bytes -> padded bit words
-hipError_t launch_ot_choices_from_planes(const uint64_t* planes, uint64_t G, uint32_t N, uint32_t nw, uint32_t bits,
-                                         uint32_t* choices, uint64_t words, hipStream_t stream);
-hipError_t launch_pack_bits(const uint8_t* in, uint64_t n, uint32_t dup, uint32_t* out, uint64_t words,
-                           hipStream_t stream);
+// GC + OT glue (level loop): the garbler's OT messages for the FE share conversion
 hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
 hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
@@ -381,10 +383,12 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // 37 / 38 are 34 / 36 with the end-of-launch phase of small items (item_layout); 39 / 40 are
 // 34 at 768 / 512 threads (3 / 2 waves per SIMD: a VGPR budget of 168 / 256 lets the
 // scheduler keep more T-table lookups in flight per wave); 41 is 39 drawing the next item ahead;
-// 42 is 34 with the next entry's seeds prefetched under the current entry's AES
+// 42 is 34 with the next entry's seeds prefetched under the current entry's AES; 43 / 44 are
+// DIAGNOSTIC builds of 34 that store no / only the dir-0 child seeds (HBM-write A/B; their states
+// are incomplete by design and no product path selects them)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 42))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 44))
                ? 16u : variant == 31 ? 32u : 8u;
 }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }

@@ -42,7 +42,10 @@ typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
 
 // NT: child seeds are written with the nontemporal hint — they are read again only at the next
 // level, and 1.3 GB per launch left dirty in L2 costs a writeback at every kernel boundary
-template <class Tab, int NB, bool NT = false, bool PAIR = false>
+// STORE (diagnostic A/B only, never a product variant): 0 = every child seed, 1 = none (a store
+// guarded by an output value that never occurs, so the AES stays live), 2 = dir-0 children only
+// (about the half that survives a prune) — the HBM-write share of k_expand's time and power
+template <class Tab, int NB, bool NT = false, bool PAIR = false, int STORE = 0>
 __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
                                             uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
                                             uint32_t* next = nullptr) {
@@ -105,7 +108,10 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
                     out.z = o[2] ^ (cw[s].z & tmask);
                     out.w = o[3] ^ (cw[s].w & tmask);
                     const size_t de = (size_t)(2 * e + dir) * 2 + s;
-                    if constexpr (NT) {
+                    const bool st = STORE == 0 || (STORE == 2 && dir == 0) ||
+                                    (STORE == 1 && (out.x ^ out.y ^ out.z ^ out.w) == 0x5EED5EEDu && out.x == 0);
+                    if (!st) {
+                    } else if constexpr (NT) {
                         v4u32_t o4 = {out.x, out.y, out.z, out.w};
                         __builtin_nontemporal_store(o4, reinterpret_cast<v4u32_t*>(J.dst_seed + de * npad + c));
                     } else {
@@ -227,6 +233,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     constexpr bool PAIR = (FLAGS & 4) != 0;
     constexpr bool PROF = (FLAGS & 8) != 0;
     constexpr bool TAIL = (FLAGS & 16) != 0;
+    constexpr int STORE = (FLAGS >> 5) & 3;   // diagnostic variants 43 / 44 only
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
@@ -284,8 +291,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         uint32_t nxt = 0;
         if constexpr (PROF) prof_items++;
         if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
-        else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
-        else expand_item<Tab, NB, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
+        else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
+        else expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
             uint32_t v = nxt;
             if (!AHEAD && lane == 0) v = atomicAdd(work_counter, 1u);
@@ -363,7 +370,9 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(39, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 6)     \
     X(40, Tab4T32<DevOpsX>, 4, 512, 1, true, false, 6)     \
     X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)     \
-    X(42, Tab4T32<DevOpsX>, 4, 1024, 1, true, true, 6)
+    X(42, Tab4T32<DevOpsX>, 4, 1024, 1, true, true, 6)      \
+    X(43, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 38)    \
+    X(44, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 70)
 
 struct VariantInfo {
     const void* fn;
@@ -394,7 +403,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 16; }
+int expand_variant_count() { return kBsVariant + kBsCount + 18; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

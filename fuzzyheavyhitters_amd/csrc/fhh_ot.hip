@@ -20,8 +20,6 @@
 #include "aes_keyed.h"
 #include "bitslice.h"
 
-#include <cstdlib>
-#include <cstring>
 
 namespace fhh {
 
@@ -119,24 +117,6 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
                 a.Q[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
             }
         }
-    }
-}
-
-// The per-lane form (k_ot_transpose_lanes: 128 words per lane, 256 VGPRs, 1 wave/SIMD) stays
-// for same-box A/B runs: FHH_OT_TRANSPOSE=lanes selects it.
-__global__ __launch_bounds__(256) void k_ot_transpose_lanes(const uint32_t* rows, uint4* cols, OtArgs a) {
-    const uint64_t W = a.mp / 32;
-    const uint64_t W_act = (ot_active(a) + 31) / 32;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < W_act; w += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t x[4][32];
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-#pragma unroll
-            for (int r = 0; r < 32; r++) x[g][r] = __builtin_nontemporal_load(rows + (uint64_t)(32 * g + r) * W + w);
-            transpose32(x[g]);
-        }
-#pragma unroll
-        for (int k = 0; k < 32; k++) cols[32 * w + k] = make_uint4(x[0][k], x[1][k], x[2][k], x[3][k]);
     }
 }
 
@@ -272,12 +252,23 @@ static hipError_t ot_set_lds(const void* fn, int* done) {
     return e;
 }
 
+// CU count of the current device, queried once per device (the level loop launches these
+// kernels thousands of times per crawl)
+static int device_cus() {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
 static int ot_grid(uint64_t items, int threads) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t need = (items + threads - 1) / threads;
-    const uint64_t cap = (uint64_t)cus * (threads >= 1024 ? 4 : 16);
+    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 4 : 16);
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 
@@ -300,22 +291,19 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream) {
-    static const bool lanes = [] {
-        const char* e = getenv("FHH_OT_TRANSPOSE");
-        return e && strcmp(e, "lanes") == 0;
-    }();
-    if (lanes) {
-        hipLaunchKernelGGL(k_ot_transpose_lanes, dim3(ot_grid(a.mp / 32, 256)), dim3(256), 0, stream,
-                           reinterpret_cast<const uint32_t*>(rows), cols, a);
-        return hipGetLastError();
-    }
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // the tile mapping of k_ot_transpose
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t tiles = a.mp / 2048, cap = (uint64_t)cus * 8;
+    const uint64_t tiles = a.mp / 2048, cap = (uint64_t)device_cus() * 8;
     hipLaunchKernelGGL(k_ot_transpose, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(256), 0, stream,
                        reinterpret_cast<const uint32_t*>(rows), cols, a);
+    return hipGetLastError();
+}
+
+__global__ void k_mask_word(uint32_t* word, uint32_t mask) {
+    if (threadIdx.x == 0) *word &= mask;
+}
+
+hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream) {
+    hipLaunchKernelGGL(k_mask_word, dim3(1), dim3(64), 0, stream, word, mask);
     return hipGetLastError();
 }
 

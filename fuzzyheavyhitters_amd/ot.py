@@ -4,27 +4,38 @@ collect.rs:437-471), backed by fhh_ot.hip. Both parties run in one process; the 
 are ideal. See include/fhh.h (fhh_ot_batch) for the exact construction."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from ._lib import check, lib, ptr
 
 
 def ot_extend(kc, choices, x0, x1=None, delta=None, base_seeds=None, base_choice=None, tweak_base: int = 0,
-              transcript: bool = False, seed: int = 0):
+              transcript: bool = False, seed: int | None = None):
     """m OTs: returns the receiver's messages out [m][16] with out[j] = (x1 if choices[j] else x0)[j]
     (x1 None: correlated OT, x1 = x0 ^ delta). With transcript, also (U [128][ceil(m/128)][16],
-    Y0, Y1 [m][16]) — the two protocol messages."""
+    Y0, Y1 [m][16]) — the two protocol messages.
+
+    The base-OT material (the receiver's seed pairs, the sender's choice bits) must be fresh for
+    every batch, as the reference's OtSender/OtReceiver::init per batch draws it
+    (collect.rs:454-471): the row PRG restarts at counter 0, so reused material repeats the pads
+    and U ^ U' would reveal the receiver's choices. When omitted it is drawn from os.urandom;
+    `seed` (tests only) makes it reproducible instead."""
     ch = np.ascontiguousarray(np.asarray(choices).astype(np.uint8) & 1)
     m = ch.size
     a0 = np.ascontiguousarray(x0, np.uint8).reshape(m, 16)
     a1 = None if x1 is None else np.ascontiguousarray(x1, np.uint8).reshape(m, 16)
     if a1 is None and delta is None:
         raise ValueError("ot_extend: x1 or delta required")
-    rng = np.random.default_rng(seed)
-    seeds = (rng.integers(0, 256, (128, 2, 16), dtype=np.uint8) if base_seeds is None
+    def fresh(k):
+        if seed is not None:
+            return np.random.default_rng([seed, k]).integers(0, 256, (128 * 2 * 16,) if k == 0 else (16,),
+                                                            dtype=np.uint8)
+        return np.frombuffer(os.urandom(128 * 2 * 16 if k == 0 else 16), np.uint8).copy()
+    seeds = (fresh(0).reshape(128, 2, 16) if base_seeds is None
              else np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16))
-    s = (rng.integers(0, 256, 16, dtype=np.uint8) if base_choice is None
-         else np.frombuffer(bytes(base_choice), np.uint8).copy())
+    s = fresh(1) if base_choice is None else np.frombuffer(bytes(base_choice), np.uint8).copy()
     d = np.frombuffer(bytes(delta), np.uint8).copy() if delta is not None else np.zeros(16, np.uint8)
     out = np.zeros((m, 16), np.uint8)
     nb = (m + 127) // 128

@@ -347,7 +347,13 @@ int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t*
  * under each seed (block c = LE128(c) gives OTs 128 c .. 128 c + 127, bit b of byte b / 8),
  * H(j, x) = scuttlebutt's cr_hash(j, x) = pi(x) ^ x, pi = AES-128 under the zero key (the hash
  * ocelot's ALSZ applies; j is not an input, so tweak_base is accepted and ignored).
- * x1 == NULL: correlated OT, x1 = x0 ^ delta. */
+ * x1 == NULL: correlated OT, x1 = x0 ^ delta.
+ * The base material (base_seeds, base_choice) MUST be fresh for every batch — the reference
+ * re-runs OtSender/OtReceiver::init per batch (collect.rs:454-471) — because the row PRG restarts
+ * at counter 0: two batches on the same material repeat the pads, and U ^ U' reveals r ^ r'.
+ * Device buffers: the call runs on the ctx's own (non-blocking) stream, so choices_dev / x0_dev /
+ * x1_dev must be complete when it is made (synchronise the stream that produced them); it returns
+ * after out_dev is complete. */
 typedef struct fhh_ot_batch {
     uint64_t m;
     const uint32_t* choices_dev;    /* receiver's choice bits, bit j % 32 of word j / 32       */

@@ -60,3 +60,54 @@ def test_gpu_ot_bit_exact(oracle, m):
         assert np.array_equal(y0, ey0) and np.array_equal(y1, ey1)
         want = np.where(ch[:, None] == 1, x0 ^ np.frombuffer(delta, np.uint8) if corr else x1, x0)
         assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [33, 1000, 8193])
+def test_gpu_ot_extend_device_buffers(oracle, m):
+    """fhh_ot_extend_device on device buffers (torch tensors on cuda:0): the choice words carry
+    garbage past bit m, which the call clears in stream order; outputs equal the oracle's."""
+    import ctypes
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd._lib import FhhOtBatch, check, lib
+    ch, x0, x1, seeds, s, _ = _inputs(m, 3 * m)
+    words = (m + 31) // 32
+    cw = np.zeros(words * 32, np.uint8)
+    cw[:m] = ch
+    cw[m:] = 1                                            # garbage past m
+    packed = np.packbits(cw.reshape(words, 32), axis=1, bitorder="little").view(np.uint32).reshape(words)
+    kc = fhh.KeyCollection(8, 1)
+    d_ch = torch.from_numpy(packed.view(np.int32).copy()).cuda()
+    d_x0 = torch.from_numpy(x0.copy()).cuda()
+    d_x1 = torch.from_numpy(x1.copy()).cuda()
+    d_out = torch.zeros((m, 16), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    b = FhhOtBatch()
+    b.m = m
+    b.choices_dev = d_ch.data_ptr()
+    b.x0_dev = d_x0.data_ptr()
+    b.x1_dev = d_x1.data_ptr()
+    b.out_dev = d_out.data_ptr()
+    ctypes.memmove(b.base_seeds, seeds.tobytes(), 128 * 2 * 16)
+    ctypes.memmove(b.base_choice, s, 16)
+    check(lib().fhh_ot_extend_device(kc.handle, ctypes.byref(b)), kc.handle)
+    got = d_out.cpu().numpy()
+    exp = oracle.ot_extend(ch, x0, x1, None, seeds, s)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(got, np.where(ch[:, None] == 1, x1, x0))
+
+
+@pytest.mark.gpu
+def test_gpu_ot_default_base_material_is_fresh():
+    """Without explicit base material every batch draws its own (os.urandom): the receiver's
+    message U differs between two batches on the same choices, the outputs are still right."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import ot
+    ch, x0, x1, _, _, _ = _inputs(500, 5)
+    kc = fhh.KeyCollection(8, 1)
+    a, ua, _, _ = ot.ot_extend(kc, ch, x0, x1, transcript=True)
+    b, ub, _, _ = ot.ot_extend(kc, ch, x0, x1, transcript=True)
+    want = np.where(ch[:, None] == 1, x1, x0)
+    assert np.array_equal(a, want) and np.array_equal(b, want)
+    assert not np.array_equal(ua, ub)

@@ -85,18 +85,30 @@ def cpu_baseline(args):
 
 
 def sketch_bench(args, world, rank, local_rank, dist):
-    """configs[4]: one step = one level of sketch verification (main.rs:14-70) for
-    --sketch-keys keys per GPU x --sketch-nodes frontier nodes, both servers in-process:
-    sketch_at (AES-128-CTR PrgStream + 3 FE inner products per key), MulState cor/out shares,
-    verify. Inputs resident in HBM. Keys shard by GPU (weak scaling, no collective: each key's
-    check is independent; the leader gathers accept bits only)."""
+    """configs[4]: one step = the sketch verification of a whole data_len-level crawl
+    (--sketch-levels, default 1024): levels 0..L-2 over FE (sketch_at + MulState with the level's
+    triples, main.rs:14-70 verify_sketches per level, batched in one call) and the last level over
+    FieldElm (sketch_at_last + MulState<FieldElm>), for --sketch-keys keys per GPU x
+    --sketch-nodes frontier nodes, both servers in-process. Inputs resident in HBM: the one-hot
+    vectors are the same at every level (the work is not: every level has its own PrgStream and
+    triples). Keys shard by GPU (weak scaling, no collective: every key's check is independent)."""
     import numpy as np
     import torch
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S
+    L = max(1, args.sketch_levels)
     wl = S.sketch_workload(args.sketch_keys, args.sketch_nodes, seed=args.seed + rank, bad_fraction=0.01)
     kc = fhh.KeyCollection(8, 1, device=local_rank)
     b = S.DeviceSketchBatch(wl, device=local_rank)
+    if L > 1:
+        S.deal_triples(kc, b, levels=L - 1, seed=args.seed + 17 * rank)
+    wl255 = S.sketch_workload255(args.sketch_keys, args.sketch_nodes, seed=args.seed + 1000 + rank, bad_fraction=0.01)
+    b255 = S.DeviceSketchBatch255(wl255, device=local_rank)
+
+    def step():
+        if L > 1:
+            S.sim_sketch_verify(kc, b, level=0, n_levels=L - 1)
+        S.sim_sketch_verify_fe255(kc, b255, level=L - 1)
 
     def barrier():
         if dist is not None:
@@ -104,33 +116,40 @@ def sketch_bench(args, world, rank, local_rank, dist):
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        S.sim_sketch_verify(kc, b)
+        step()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        S.sim_sketch_verify(kc, b)
+        step()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)   # gloo control group: host tensors
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ok = b.ok.cpu().numpy().astype(bool)
-    assert np.array_equal(ok, wl.honest), "sketch verification disagrees with the workload's ground truth"
+    ok = b.ok.cpu().numpy().astype(bool)[: max(L - 1, 1)]
+    assert (L == 1 or np.array_equal(ok, np.broadcast_to(wl.honest, ok.shape))), \
+        "FE sketch verification disagrees with the workload's ground truth"
+    ok255 = b255.ok.cpu().numpy().astype(bool)
+    assert np.array_equal(ok255, wl255.honest), "FieldElm sketch verification disagrees with the ground truth"
     keys = args.sketch_keys * world * args.steps
-    elems = keys * args.sketch_nodes * 2   # both servers
-    blocks = keys * 2 * ((args.sketch_nodes + 4) // 2)
+    elems = keys * args.sketch_nodes * 2 * L   # both servers, every level
+    blocks = keys * 2 * ((L - 1) * ((args.sketch_nodes + 4) // 2) + 2 * (args.sketch_nodes + 3))
     if rank == 0:
         print(json.dumps({
-            "metric": "sketch key x node evaluations/sec (configs[4] sketch + Beaver verification)",
+            "metric": "sketch key x node evaluations/sec (configs[4] sketch + Beaver verification, all levels)",
             "value": elems / elapsed, "unit": "key-node evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64 (GF(2^62-2^30-1))",
-            "data": "synthetic one-hot frontier vectors, MAC keys and Beaver triples (sketch.rs:84-150 shape)",
-            "config": {"workload": "configs[4]: sketch_at + MulState verify, both servers in-process",
-                       "keys_per_gpu": args.sketch_keys, "nodes": args.sketch_nodes, "parallelism": f"key-shard x{world}"},
-            "keys_verified_per_s": keys / elapsed, "aes_blocks_per_s": blocks / elapsed,
-            "accepted": int(ok.sum()), "rejected": int((~ok).sum()),
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64 (GF(2^62-2^30-1)) + 8 x u32 (GF(2^255-19))",
+            "data": ("synthetic one-hot frontier vectors (the same at every level), MAC keys, and Beaver triples "
+                     "dealt per level on the GPU (sketch.rs:84-150 shape)"),
+            "config": {"workload": f"configs[4]: {L - 1} FE levels + 1 FieldElm level of sketch_at + MulState "
+                                   f"verify, both servers in-process",
+                       "keys_per_gpu": args.sketch_keys, "nodes": args.sketch_nodes, "levels": L,
+                       "parallelism": f"key-shard x{world}"},
+            "keys_verified_per_s": keys * L / elapsed, "aes_blocks_per_s": blocks / elapsed,
+            "ms_per_level": elapsed / args.steps / L * 1e3,
+            "accepted_per_level": int(wl.honest.sum()), "rejected_per_level": int((~wl.honest).sum()),
         }), flush=True)
     if dist is not None:
         dist.barrier()
@@ -259,10 +278,13 @@ def main():
     ap.add_argument("--gc", default="none", choices=["none", "ot", "ideal"],
                     help="crawl with the GPU garbled-circuit equality test (mode fe): ot = labels and FE shares "
                          "by GPU OT extension, ideal = ideal OT")
+    ap.add_argument("--base-ot", action="store_true",
+                    help="--gc ot: real Chou-Orlandi base OTs for every level's OT extensions (host threads, "
+                         "overlapped with the crawl) instead of ideal ones")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
-    ap.add_argument("--sketch-levels", type=int, default=1,
-                    help="configs[4]: levels verified per step (data_len 1024 -> 1023)")
+    ap.add_argument("--sketch-levels", type=int, default=1024,
+                    help="configs[4]: data_len levels verified per step (L-1 over FE, the last over FieldElm)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=150.0,
                     help="upper bound on the configs[0] CPU crawl (it normally completes well inside)")
@@ -337,7 +359,8 @@ def main():
 
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc])
+                             record=False, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc],
+                             base_ot=args.base_ot)
 
     def barrier():
         if dist is not None:
@@ -425,6 +448,7 @@ def main():
                 "clients_total": n_total, "clients_per_gpu": n_local, "data_len": args.data_len,
                 "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
                 "threshold": args.threshold, "mode": args.mode, "gc": args.gc,
+                "base_ot": "chou-orlandi (host)" if args.base_ot else ("ideal" if args.gc == "ot" else None),
                 "parallelism": f"client-shard x{world}", "collective": collective,
                 "variant": args.variant if args.variant >= 0 else "default",
             },
@@ -433,6 +457,7 @@ def main():
                                "plaintext equality count, leader keep and prune on the GPU",
             "ref_equiv_evals_per_s": ref_evals / elapsed,
             "aes_blocks_per_step": blocks / args.steps,
+            "base_ot_ms_per_step": s0.get("base_ot_ms", 0.0) / args.steps if args.base_ot else None,
             "final_heavy_hitters": len(res.final),
             "levels": int(len(res.level_children)),
             "children_total": int(res.level_children.sum()),

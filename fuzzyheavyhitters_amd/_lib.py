@@ -37,7 +37,10 @@ EXPORTS = [
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
     "fhh_comm_info", "fhh_comm_create_hosted", "fhh_comm_last_error",
     "fhh_sketch_at_fe", "fhh_mul_cor_share_fe", "fhh_mul_cor_fe", "fhh_mul_out_share_fe", "fhh_mul_verify_fe",
-    "fhh_sim_sketch_verify_fe",
+    "fhh_sim_sketch_verify_fe", "fhh_sketch_at_fe255", "fhh_mul_cor_share_fe255", "fhh_mul_cor_fe255",
+    "fhh_mul_out_share_fe255", "fhh_mul_verify_fe255", "fhh_sim_sketch_verify_fe255", "fhh_deal_triples_fe",
+    "fhh_co15_sender_start", "fhh_co15_receiver", "fhh_co15_sender_finish", "fhh_base_ot_co15",
+    "fhh_base_ot_last_error",
     "fhh_gc_equality_device", "fhh_gc_equality_host", "fhh_ot_extend_device", "fhh_ot_extend_host",
 ]
 
@@ -52,6 +55,7 @@ class FhhStats(ctypes.Structure):
         ("levels", ctypes.c_uint64),
         ("keygen_ms", ctypes.c_double),
         ("expand_launches_timed", ctypes.c_uint64),
+        ("base_ot_ms", ctypes.c_double),
     ]
 
 
@@ -82,11 +86,12 @@ class FhhSimConfig(ctypes.Structure):
         ("probe_seeds", u8p),
         ("probe_ty", u8p),
         ("probe_children", u64p),
+        ("base_ot", ctypes.c_uint32),
     ]
 
 
 SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_ot.hip", "fhh_loop.hip",
-           "fhh_microbench.hip", "fhh_host.cpp", "fhh_comm.cpp")
+           "fhh_microbench.hip", "fhh_host.cpp", "fhh_comm.cpp", "fhh_base_ot.cpp")
 
 
 class FhhSketchBatch(ctypes.Structure):
@@ -103,6 +108,30 @@ class FhhSketchBatch(ctypes.Structure):
         ("sketch_dev", ctypes.c_void_p * 2),
         ("ok_dev", ctypes.c_void_p),
         ("out_shares_dev", ctypes.c_void_p),
+        ("level", ctypes.c_uint32),
+        ("n_levels", ctypes.c_uint32),
+        ("triples_levels", ctypes.c_uint32),
+        ("pad_", ctypes.c_uint32),
+        ("x_level_stride", ctypes.c_uint64),
+    ]
+
+
+class FhhSketchBatch255(ctypes.Structure):
+    _fields_ = [
+        ("n_keys", ctypes.c_uint64),
+        ("n_nodes", ctypes.c_uint32),
+        ("force_sequential", ctypes.c_uint32),
+        ("seeds_dev", ctypes.c_void_p),
+        ("x_dev", ctypes.c_void_p * 2),
+        ("kx_dev", ctypes.c_void_p * 2),
+        ("mac_dev", ctypes.c_void_p * 2),
+        ("mac2_dev", ctypes.c_void_p * 2),
+        ("triples_dev", ctypes.c_void_p * 2),
+        ("sketch_dev", ctypes.c_void_p * 2),
+        ("ok_dev", ctypes.c_void_p),
+        ("out_shares_dev", ctypes.c_void_p),
+        ("level", ctypes.c_uint32),
+        ("pad_", ctypes.c_uint32),
     ]
 
 
@@ -158,8 +187,8 @@ def build(verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
         res = list(ex.map(compile_one, SOURCES))
-    r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *[o for o, _ in res], "-ldl", "-o",
-                        LIB_PATH], capture_output=True, text=True)
+    r = subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", *[o for o, _ in res], "-ldl", "-lcrypto",
+                        "-o", LIB_PATH], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc link failed:\n" + r.stdout + r.stderr)
     if verbose:
@@ -243,6 +272,18 @@ def lib():
         "fhh_mul_out_share_fe": (i, [vp, i, u64, u64p, u64p, u64p, u64p, u64p, u64p]),
         "fhh_mul_verify_fe": (i, [u64, u64p, u64p, u8p]),
         "fhh_sim_sketch_verify_fe": (i, [vp, P(FhhSketchBatch)]),
+        "fhh_sketch_at_fe255": (i, [vp, u64, u32, u8p, u32p, u32p, u32p]),
+        "fhh_mul_cor_share_fe255": (i, [vp, u64, u32p, u32p, u32p, u32p, u32p]),
+        "fhh_mul_cor_fe255": (i, [u64, u32p, u32p, u32p]),
+        "fhh_mul_out_share_fe255": (i, [vp, i, u64, u32p, u32p, u32p, u32p, u32p, u32p]),
+        "fhh_mul_verify_fe255": (i, [u64, u32p, u32p, u8p]),
+        "fhh_sim_sketch_verify_fe255": (i, [vp, P(FhhSketchBatch255)]),
+        "fhh_deal_triples_fe": (i, [vp, u64, u32, u64, vp, vp]),
+        "fhh_co15_sender_start": (i, [u8p, u8p]),
+        "fhh_co15_receiver": (i, [u32, u8p, u8p, u8p, u8p, u8p]),
+        "fhh_co15_sender_finish": (i, [u32, u8p, u8p, u8p]),
+        "fhh_base_ot_co15": (i, [u32, u8p, u8p, u8p, u8p]),
+        "fhh_base_ot_last_error": (ctypes.c_char_p, []),
         "fhh_gc_equality_device": (i, [vp, P(FhhGcBatch)]),
         "fhh_ot_extend_device": (i, [vp, P(FhhOtBatch)]),
         "fhh_ot_extend_host": (i, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u64, u8p, u8p, u8p, u8p]),

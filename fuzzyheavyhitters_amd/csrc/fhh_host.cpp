@@ -16,7 +16,12 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -938,6 +943,68 @@ struct PhaseClock {
     }
 };
 
+// Host producer of the real base OTs (fhh_sim_config.base_ot): worker threads compute instances
+// 0, 1, ... (level l's OT extensions are 2 l and 2 l + 1) with their key schedules
+// [3][128][44] (receiver k_i^0, k_i^1; sender k_i^{s_i}); wait(k) blocks until k is done.
+struct BaseOtProducer {
+    uint32_t instances;
+    uint8_t seed[32];
+    std::vector<uint8_t> choices;
+    std::vector<uint32_t> rk;                     // [instances][3][128][44]
+    std::vector<uint8_t> done;
+    std::atomic<uint32_t> next{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    int rc = FHH_OK;
+    std::string err;
+    std::vector<std::thread> workers;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double busy_ms = 0;                            // wall time until the last instance finished
+    BaseOtProducer(uint32_t n, const uint8_t s[32], std::vector<uint8_t> ch)
+        : instances(n), choices(std::move(ch)), rk((size_t)n * 3 * 128 * 44), done(n, 0) {
+        std::memcpy(seed, s, 32);
+        unsigned nt = std::thread::hardware_concurrency();
+        if (const char* e = std::getenv("OMP_NUM_THREADS")) nt = (unsigned)std::atoi(e);
+        nt = std::max(1u, std::min(nt ? nt : 1u, 64u));
+        for (unsigned w = 0; w < nt; w++) workers.emplace_back([this] { work(); });
+    }
+    ~BaseOtProducer() {
+        next = instances;   // stop handing out work
+        for (auto& t : workers) t.join();
+    }
+    void work() {
+        std::vector<uint8_t> pairs(128 * 32), chosen(128 * 16);
+        for (;;) {
+            const uint32_t k = next.fetch_add(1);
+            if (k >= instances) return;
+            std::string e;
+            const int r = base_ot_instance(k, seed, &choices[(size_t)k * 16], pairs.data(), chosen.data(), &e);
+            if (!r)
+                for (int i = 0; i < 128; i++) {
+                    uint32_t w[11][4];
+                    for (int b = 0; b < 3; b++) {
+                        host_key_schedule(b < 2 ? &pairs[((size_t)i * 2 + b) * 16] : &chosen[(size_t)i * 16], w);
+                        std::memcpy(&rk[(((size_t)k * 3 + b) * 128 + i) * 44], w, 44 * 4);
+                    }
+                }
+            std::lock_guard<std::mutex> lk(mu);
+            if (r && !rc) {
+                rc = r;
+                err = e;
+            }
+            done[k] = 1;
+            busy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            cv.notify_all();
+        }
+    }
+    int wait(uint32_t k) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done[k] != 0 || rc != FHH_OK; });
+        return rc;
+    }
+    const uint32_t* schedules(uint32_t k) const { return &rk[(size_t)k * 3 * 128 * 44]; }
+};
+
 struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
     DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
@@ -953,6 +1020,11 @@ struct LoopBuffers {
     DevBuf probe_seed[kMaxProbe], probe_ty[kMaxProbe];
     uint64_t probe_stride[kMaxProbe] = {};
     DevBuf probe_C, probe_clients;
+    // cfg->base_ot: the key schedules [levels][2 OTs][3][128][44] of the real base OTs
+    bool base_ot = false;
+    DevBuf base_rk;
+    std::unique_ptr<BaseOtProducer> bot;
+    std::vector<uint8_t> bot_uploaded;   // per instance
     std::vector<DevBuf*> hist_epochs;            // hist rows; a new epoch per F_cap growth
     std::vector<uint32_t*> hist_ptr;             // per level
     uint32_t E_cap = 0, F_cap = 0;
@@ -963,6 +1035,20 @@ struct LoopBuffers {
         for (auto* b : hist_epochs) delete b;
     }
 };
+
+// wait for base-OT instance k and copy its key schedules to the device (once; a resumed level
+// reuses them). The copy is from pageable memory, so it has left the host buffer on return.
+int upload_base_ot(fhh_ctx* c0, LoopBuffers& B, uint32_t k) {
+    if (B.bot_uploaded.empty()) B.bot_uploaded.assign(B.bot->instances, 0);
+    if (B.bot_uploaded[k]) return FHH_OK;
+    const int rc = B.bot->wait(k);
+    if (rc) return c0->fail(rc, "base OTs: " + B.bot->err);
+    const size_t words = (size_t)3 * 128 * 44;
+    HIP_TRY(c0, hipMemcpyAsync(B.base_rk.as<uint32_t>() + (size_t)k * words, B.bot->schedules(k), words * 4,
+                               hipMemcpyHostToDevice, c0->stream));
+    B.bot_uploaded[k] = 1;
+    return FHH_OK;
+}
 
 uint32_t next_pow2(uint32_t v) {
     uint32_t p = 1;
@@ -1078,6 +1164,27 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     HIP_TRY(c0, B.ctl_host.ensure(sizeof(LoopCtl)));
     rc = loop_resize(c0, B, cap0, cap0, levels, 0, false, 0, 0, 1);
     if (rc) return rc;
+    if (cfg->gc == 2 && cfg->base_ot) {
+        // the two OT extensions of every level each start with 128 Chou–Orlandi base OTs
+        // (AlszSender/AlszReceiver::init, collect.rs:454-471): host threads produce them in level
+        // order while this thread enqueues the crawl, which waits only for the level it is about
+        // to enqueue; the sender's base choice bits are the per-level words the ideal mode uses
+        std::vector<uint8_t> choices((size_t)2 * levels * 16);
+        for (uint32_t lv = 0; lv < levels; lv++)
+            for (uint32_t salt = 0; salt < 2; salt++) {
+                uint32_t sw[4];
+                ot_level_choice(cfg->prf_seed, lv, salt, sw);
+                std::memcpy(&choices[((size_t)lv * 2 + salt) * 16], sw, 16);
+            }
+        uint8_t seed[32];
+        for (int k = 0; k < 4; k++) {
+            const uint64_t z = host_mix64(cfg->prf_seed ^ (0x626173655f6f74ull + (uint64_t)k));
+            std::memcpy(seed + 8 * k, &z, 8);
+        }
+        HIP_TRY(c0, B.base_rk.ensure((size_t)2 * levels * 3 * 128 * 44 * 4));
+        B.bot = std::make_unique<BaseOtProducer>(2 * levels, seed, std::move(choices));
+        B.base_ot = true;
+    }
     if (cfg->probe_n_levels) {
         if (cfg->probe_n_levels > LoopBuffers::kMaxProbe || !cfg->probe_levels || !cfg->probe_n_clients ||
             !cfg->probe_clients || !cfg->probe_seeds || !cfg->probe_ty || !cfg->probe_children)
@@ -1235,11 +1342,17 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     const uint32_t* ch = B.gc_planes[1].as<uint32_t>();
                     uint32_t sw[4];
                     ot_level_choice(cfg->prf_seed, lv, 0, sw);
-                    HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 0, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    const uint32_t* rk1 = c0->ot_rk.as<uint32_t>();
+                    if (B.base_ot) {
+                        rc = upload_base_ot(c0, B, 2 * lv);
+                        if (rc) return rc;
+                        rk1 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 0) * 3 * 128 * 44;
+                    } else {
+                        HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 0, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    }
                     HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
-                    rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(),
-                                c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits,
-                                nullptr);
+                    rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(), rk1, sw, 0,
+                                B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits, nullptr);
                     if (rc) return rc;
                     g.ev_labels = B.gc_evact.as<uint4>();
                 }
@@ -1273,10 +1386,17 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     const uint32_t* ch = g.out_packed;
                     uint32_t sw[4];
                     ot_level_choice(cfg->prf_seed, lv, 1, sw);
-                    HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
+                    if (B.base_ot) {
+                        rc = upload_base_ot(c0, B, 2 * lv + 1);
+                        if (rc) return rc;
+                        rk2 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 1) * 3 * 128 * 44;
+                    } else {
+                        HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
+                    }
                     rc = ot_run(c0, m2, ch, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
-                                B.gc_recv.as<uint4>(), c0->ot_rk.as<uint32_t>(), sw, 0, B.ctl.as<LoopCtl>(),
-                                (uint64_t)c0->n * per, nullptr);
+                                B.gc_recv.as<uint4>(), rk2, sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * per,
+                                nullptr);
                     if (rc) return rc;
                     a.ot_recv = B.gc_recv.as<uint4>();
                 }
@@ -1387,6 +1507,11 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 (void)per_level_per;
             }
         }
+    }
+    if (B.bot) {
+        const int brc = B.bot->wait(B.bot->instances - 1);
+        if (brc) return c0->fail(brc, "base OTs: " + B.bot->err);
+        c0->stats.base_ot_ms += B.bot->busy_ms;
     }
     c0->loop_cap_hint = std::max(B.E_cap, B.F_cap);   // the next crawl starts at this size
     pc.mark("loop");
@@ -2279,6 +2404,7 @@ static int mul_fe_host(fhh_ctx* ctx, uint32_t mode, int server_idx, uint64_t n, 
     a.n = n;
     a.mode = mode;
     a.server_idx = server_idx ? 1 : 0;
+    a.triples_levels = 1;
     HIP_TRY(ctx, launch_mul_fe(a, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(out, dout.p, n * 8 * out_words, hipMemcpyDeviceToHost, ctx->stream));
     return sync(ctx);
@@ -2329,8 +2455,179 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
         if (!b->mac_dev[s] || !b->mac2_dev[s] || !b->triples_dev[s] || !b->sketch_dev[s] ||
             (b->n_nodes && (!b->x_dev[s] || !b->kx_dev[s])))
             return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: NULL buffer");
+    const uint32_t nl = b->n_levels ? b->n_levels : 1;
+    const uint32_t tl = b->triples_levels ? b->triples_levels : 1;
+    if (b->triples_levels && b->level + nl > tl)
+        return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: levels past the triples held");
+    for (uint32_t k = 0; k < nl; k++) {
+        const uint32_t lv = b->level + k;
+        for (int s = 0; s < 2; s++) {
+            SketchArgs a{};
+            a.seeds = b->seeds_dev;
+            a.x = b->x_dev[s] + (size_t)k * b->x_level_stride;
+            a.kx = b->kx_dev[s] + (size_t)k * b->x_level_stride;
+            a.out = b->sketch_dev[s];
+            a.n_keys = b->n_keys;
+            a.n_nodes = b->n_nodes;
+            a.force_sequential = b->force_sequential;
+            a.level = lv;
+            HIP_TRY(ctx, launch_sketch_fe(a, ctx->stream));
+        }
+        VerifyArgs v{};
+        for (int s = 0; s < 2; s++) {
+            v.sketch[s] = b->sketch_dev[s];
+            v.mac[s] = b->mac_dev[s];
+            v.mac2[s] = b->mac2_dev[s];
+            v.triples[s] = b->triples_dev[s];
+        }
+        v.ok = b->ok_dev + (size_t)k * b->n_keys;
+        v.out_shares = b->out_shares_dev ? b->out_shares_dev + (size_t)k * 2 * b->n_keys : nullptr;
+        v.n = b->n_keys;
+        v.level = b->triples_levels ? lv : 0;
+        v.triples_levels = tl;
+        HIP_TRY(ctx, launch_verify_fe(v, ctx->stream));
+    }
+    return sync(ctx);
+}
+
+int fhh_deal_triples_fe(fhh_ctx* ctx, uint64_t n, uint32_t levels, uint64_t seed, uint64_t* triples0_dev,
+                        uint64_t* triples1_dev) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!triples0_dev || !triples1_dev) return ctx->fail(FHH_E_ARG, "deal_triples_fe: NULL buffer");
+    HIP_TRY(ctx, launch_deal_triples_fe(n, levels, seed, triples0_dev, triples1_dev, ctx->stream));
+    return sync(ctx);
+}
+
+// ---- U = FieldElm (the last level) -----------------------------------------------------------
+int fhh_sketch_at_fe255(fhh_ctx* ctx, uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint32_t* x,
+                        const uint32_t* kx, uint32_t* sketch6) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (n_keys == 0) return FHH_OK;
+    if (!seeds || !sketch6 || (n_nodes && (!x || !kx))) return ctx->fail(FHH_E_ARG, "sketch_at_fe255: NULL buffer");
+    const size_t vb = (size_t)n_keys * n_nodes * 32;
+    DevBuf ds, dx, dkx, dout;
+    HIP_TRY(ctx, ds.ensure(n_keys * 16));
+    HIP_TRY(ctx, dx.ensure(vb));
+    HIP_TRY(ctx, dkx.ensure(vb));
+    HIP_TRY(ctx, dout.ensure(n_keys * 192));
+    HIP_TRY(ctx, hipMemcpyAsync(ds.p, seeds, n_keys * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (vb) {
+        HIP_TRY(ctx, hipMemcpyAsync(dx.p, x, vb, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(dkx.p, kx, vb, hipMemcpyHostToDevice, ctx->stream));
+    }
+    Sketch255Args a{};
+    a.seeds = ds.as<uint8_t>();
+    a.x = dx.as<uint32_t>();
+    a.kx = dkx.as<uint32_t>();
+    a.out = dout.as<uint32_t>();
+    a.n_keys = n_keys;
+    a.n_nodes = n_nodes;
+    HIP_TRY(ctx, launch_sketch_fe255(a, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(sketch6, dout.p, n_keys * 192, hipMemcpyDeviceToHost, ctx->stream));
+    return sync(ctx);
+}
+
+static int mul_fe255_host(fhh_ctx* ctx, uint32_t mode, int server_idx, uint64_t n, const uint32_t* sketch6,
+                          const uint32_t* mac, const uint32_t* mac2, const uint32_t* triples9, const uint32_t* cor6,
+                          uint32_t* out) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (n == 0) return FHH_OK;
+    if (!sketch6 || !mac || !mac2 || !triples9 || !out || (mode == 1 && !cor6))
+        return ctx->fail(FHH_E_ARG, "mul_fe255: NULL buffer");
+    DevBuf dsk, dm, dm2, dt, dc, dout;
+    const size_t out_bytes = mode == 0 ? 192 : 32;
+    HIP_TRY(ctx, dsk.ensure(n * 192));
+    HIP_TRY(ctx, dm.ensure(n * 32));
+    HIP_TRY(ctx, dm2.ensure(n * 32));
+    HIP_TRY(ctx, dt.ensure(n * 288));
+    HIP_TRY(ctx, dc.ensure(n * 192));
+    HIP_TRY(ctx, dout.ensure(n * out_bytes));
+    HIP_TRY(ctx, hipMemcpyAsync(dsk.p, sketch6, n * 192, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dm.p, mac, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dm2.p, mac2, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dt.p, triples9, n * 288, hipMemcpyHostToDevice, ctx->stream));
+    if (mode == 1) HIP_TRY(ctx, hipMemcpyAsync(dc.p, cor6, n * 192, hipMemcpyHostToDevice, ctx->stream));
+    Mul255Args a{};
+    a.sketch = dsk.as<uint32_t>();
+    a.mac = dm.as<uint32_t>();
+    a.mac2 = dm2.as<uint32_t>();
+    a.triples = dt.as<uint32_t>();
+    a.cor = dc.as<uint32_t>();
+    a.out = dout.as<uint32_t>();
+    a.n = n;
+    a.mode = mode;
+    a.server_idx = server_idx ? 1 : 0;
+    HIP_TRY(ctx, launch_mul_fe255(a, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(out, dout.p, n * out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return sync(ctx);
+}
+
+int fhh_mul_cor_share_fe255(fhh_ctx* ctx, uint64_t n, const uint32_t* sketch6, const uint32_t* mac_key,
+                            const uint32_t* mac_key2, const uint32_t* triples9, uint32_t* cor_share6) {
+    return mul_fe255_host(ctx, 0, 0, n, sketch6, mac_key, mac_key2, triples9, nullptr, cor_share6);
+}
+
+int fhh_mul_out_share_fe255(fhh_ctx* ctx, int server_idx, uint64_t n, const uint32_t* sketch6,
+                            const uint32_t* mac_key, const uint32_t* mac_key2, const uint32_t* triples9,
+                            const uint32_t* cor6, uint32_t* out) {
+    return mul_fe255_host(ctx, 1, server_idx, n, sketch6, mac_key, mac_key2, triples9, cor6, out);
+}
+
+int fhh_mul_cor_fe255(uint64_t n, const uint32_t* share0, const uint32_t* share1, uint32_t* cor6) {
+    if (n && (!share0 || !share1 || !cor6)) {
+        g_err = "mul_cor_fe255: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < 6 * n; i++) {   // MulState::cor (mpc.rs:160-180)
+        uint32_t a[8], b[8], o[8];
+        std::memcpy(a, share0 + 8 * i, 32);
+        std::memcpy(b, share1 + 8 * i, 32);
+        fe255_canonm(a);
+        fe255_canonm(b);
+        fe255_addm(a, b, o);
+        std::memcpy(cor6 + 8 * i, o, 32);
+    }
+    return FHH_OK;
+}
+
+int fhh_mul_verify_fe255(uint64_t n, const uint32_t* out0, const uint32_t* out1, uint8_t* ok) {
+    if (n && (!out0 || !out1 || !ok)) {
+        g_err = "mul_verify_fe255: NULL buffer";
+        return FHH_E_ARG;
+    }
+    for (uint64_t i = 0; i < n; i++) {   // MulState::verify (mpc.rs:214-220)
+        uint32_t a[8], b[8], o[8];
+        std::memcpy(a, out0 + 8 * i, 32);
+        std::memcpy(b, out1 + 8 * i, 32);
+        fe255_canonm(a);
+        fe255_canonm(b);
+        fe255_addm(a, b, o);
+        uint32_t nz = 0;
+        for (int k = 0; k < 8; k++) nz |= o[k];
+        ok[i] = nz == 0;
+    }
+    return FHH_OK;
+}
+
+int fhh_sim_sketch_verify_fe255(fhh_ctx* ctx, const fhh_sketch_batch255* b) {
+    CTX_CHECK(ctx);
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (!b) return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe255: NULL batch");
+    if (b->n_keys == 0) return FHH_OK;
+    if (!b->seeds_dev || !b->ok_dev) return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe255: NULL buffer");
+    for (int s = 0; s < 2; s++)
+        if (!b->mac_dev[s] || !b->mac2_dev[s] || !b->triples_dev[s] || !b->sketch_dev[s] ||
+            (b->n_nodes && (!b->x_dev[s] || !b->kx_dev[s])))
+            return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe255: NULL buffer");
     for (int s = 0; s < 2; s++) {
-        SketchArgs a{};
+        Sketch255Args a{};
         a.seeds = b->seeds_dev;
         a.x = b->x_dev[s];
         a.kx = b->kx_dev[s];
@@ -2338,9 +2635,10 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
         a.n_keys = b->n_keys;
         a.n_nodes = b->n_nodes;
         a.force_sequential = b->force_sequential;
-        HIP_TRY(ctx, launch_sketch_fe(a, ctx->stream));
+        a.level = b->level;
+        HIP_TRY(ctx, launch_sketch_fe255(a, ctx->stream));
     }
-    VerifyArgs v{};
+    Verify255Args v{};
     for (int s = 0; s < 2; s++) {
         v.sketch[s] = b->sketch_dev[s];
         v.mac[s] = b->mac_dev[s];
@@ -2350,7 +2648,7 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
     v.ok = b->ok_dev;
     v.out_shares = b->out_shares_dev;
     v.n = b->n_keys;
-    HIP_TRY(ctx, launch_verify_fe(v, ctx->stream));
+    HIP_TRY(ctx, launch_verify_fe255(v, ctx->stream));
     return sync(ctx);
 }
 

@@ -290,6 +290,9 @@ hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream);
 // *word &= mask (one lane; the tail of a choice-bit buffer)
 hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream);
+// the 128 Chou–Orlandi base OTs of OT extension k (fhh_base_ot.cpp)
+int base_ot_instance(uint64_t k, const uint8_t seed[32], const uint8_t choices[16], uint8_t* pairs, uint8_t* chosen,
+                     std::string* err);
 hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, const uint32_t s[4], uint32_t* rk,
                                 hipStream_t stream);
 // GC + OT glue (level loop): the garbler's OT messages for the FE share conversion
@@ -329,17 +332,51 @@ struct SketchArgs {
     uint64_t n_keys;
     uint32_t n_nodes;
     uint32_t force_sequential;   // 1: every key takes the sequential-stream path (tests)
+    uint32_t level;              // the level's stream seed = seed with bytes 12..15 ^= level
+};
+// U = FieldElm: values as 8 x u32 little-endian limbs
+struct Sketch255Args {
+    const uint8_t* seeds;
+    const uint32_t* x;      // [n_keys][n_nodes][8]
+    const uint32_t* kx;
+    uint32_t* out;          // [n_keys][6][8]
+    uint64_t n_keys;
+    uint32_t n_nodes;
+    uint32_t force_sequential;
+    uint32_t level;
+};
+struct Mul255Args {
+    const uint32_t* sketch;   // [n][6][8]
+    const uint32_t* mac;      // [n][8]
+    const uint32_t* mac2;     // [n][8]
+    const uint32_t* triples;  // [n][9][8]
+    const uint32_t* cor;      // [n][6][8] (mode 1)
+    uint32_t* out;            // mode 0: [n][6][8]; mode 1: [n][8]
+    uint64_t n;
+    uint32_t mode;
+    uint32_t server_idx;
+};
+struct Verify255Args {
+    const uint32_t* sketch[2];
+    const uint32_t* mac[2];
+    const uint32_t* mac2[2];
+    const uint32_t* triples[2];
+    uint8_t* ok;
+    uint32_t* out_shares;     // [2][n][8] or null
+    uint64_t n;
 };
 struct MulArgs {
     const uint64_t* sketch;   // [n][6]
     const uint64_t* mac;      // [n]
     const uint64_t* mac2;     // [n]
-    const uint64_t* triples;  // [n][3][a, b, c]
+    const uint64_t* triples;  // [n][triples_levels][3][a, b, c]
     const uint64_t* cor;      // [n][6] (mode 1)
     uint64_t* out;            // mode 0: [n][6] cor share; mode 1: [n] out share
     uint64_t n;
     uint32_t mode;
     uint32_t server_idx;
+    uint32_t level;           // the level's triples (MulState::new's triples[3 level ..], mpc.rs:94-98)
+    uint32_t triples_levels;  // levels the triple arrays hold (>= 1)
 };
 struct VerifyArgs {
     const uint64_t* sketch[2];
@@ -349,10 +386,17 @@ struct VerifyArgs {
     uint8_t* ok;              // [n]
     uint64_t* out_shares;     // [2][n] or null
     uint64_t n;
+    uint32_t level;
+    uint32_t triples_levels;
 };
 hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream);
 hipError_t launch_mul_fe(const MulArgs& a, hipStream_t stream);
 hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream);
+hipError_t launch_deal_triples_fe(uint64_t n, uint32_t levels, uint64_t seed, uint64_t* t0, uint64_t* t1,
+                                  hipStream_t stream);
+hipError_t launch_sketch_fe255(const Sketch255Args& a, hipStream_t stream);
+hipError_t launch_mul_fe255(const Mul255Args& a, hipStream_t stream);
+hipError_t launch_verify_fe255(const Verify255Args& a, hipStream_t stream);
 
 // ---- bitsliced k_expand (fhh_expand_bs.hip) -------------------------------------------------
 // Variant kBsVariant selects it; seeds (CW, root, prefix tables) are then stored per key row as

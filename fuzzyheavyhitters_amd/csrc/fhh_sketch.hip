@@ -10,6 +10,8 @@
 //                 wave that sees one falls back to the sequential stream for that key.
 //   k_mul_fe      MulState::cor_share / out_share per key (one lane per key).
 //   k_verify_fe   MulState::cor + out shares of both servers + verify, fused (in-process).
+//   k_sketch_fe255 / k_mul_fe255 / k_verify_fe255: the same for U = FieldElm (GF(2^255 - 19)),
+//                 the last level's sketch_at_last (sketch.rs:202-245).
 #include "fhh_internal.h"
 #include "expand_kernel.h"
 #include "aes_tables.h"
@@ -152,6 +154,7 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
         uint32_t seed[4];
 #pragma unroll
         for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
+        seed[3] ^= a.level;   // the level's stream (bytes 12..15; level 0 = the seed itself)
         uint32_t rk[11][4];
         key_schedule(seed, rk, tbl, lane & 31);
         const uint64_t* x = a.x + kk * F;
@@ -307,7 +310,7 @@ __device__ __forceinline__ uint64_t out_share_fe(const MulView& m, int server_id
 __global__ __launch_bounds__(256) void k_mul_fe(MulArgs a) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
         const MulView m = mul_view(a.sketch + 6 * i, a.mac[i], a.mac2[i]);
-        const uint64_t* tr = a.triples + 9 * i;
+        const uint64_t* tr = a.triples + 9 * (i * a.triples_levels + a.level);
         if (a.mode == 0) {
             for (int t = 0; t < 3; t++) {
                 a.out[6 * i + t] = fe_subc(m.xs[t], fe_canon_dev(tr[3 * t]));
@@ -326,14 +329,14 @@ __global__ __launch_bounds__(256) void k_verify_fe(VerifyArgs a) {
         uint64_t cor[6] = {0, 0, 0, 0, 0, 0};
         for (int s = 0; s < 2; s++) {
             m[s] = mul_view(a.sketch[s] + 6 * i, a.mac[s][i], a.mac2[s][i]);
-            const uint64_t* tr = a.triples[s] + 9 * i;
+            const uint64_t* tr = a.triples[s] + 9 * (i * a.triples_levels + a.level);
             for (int t = 0; t < 3; t++) {
                 cor[t] = fe_addc(cor[t], fe_subc(m[s].xs[t], fe_canon_dev(tr[3 * t])));
                 cor[3 + t] = fe_addc(cor[3 + t], fe_subc(m[s].ys[t], fe_canon_dev(tr[3 * t + 1])));
             }
         }
-        const uint64_t o0 = out_share_fe(m[0], 0, a.triples[0] + 9 * i, cor);
-        const uint64_t o1 = out_share_fe(m[1], 1, a.triples[1] + 9 * i, cor);
+        const uint64_t o0 = out_share_fe(m[0], 0, a.triples[0] + 9 * (i * a.triples_levels + a.level), cor);
+        const uint64_t o1 = out_share_fe(m[1], 1, a.triples[1] + 9 * (i * a.triples_levels + a.level), cor);
         if (a.out_shares) {
             a.out_shares[i] = o0;
             a.out_shares[a.n + i] = o1;
@@ -356,6 +359,361 @@ hipError_t launch_mul_fe(const MulArgs& a, hipStream_t stream) {
 hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_verify_fe, dim3(grid_for(a.n)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+// ---- dealer (harness): TripleShare::new (mpc.rs:18-45) for n keys x levels x 3 triples ------
+// a = a0 + a1, b = b0 + b1 with random shares, c = a b shared as c0 random, c1 = c - c0; the
+// randomness is a mix64 PRF of (seed, key, level, triple, word) (the reference: thread_rng).
+__device__ __forceinline__ uint64_t deal_mix(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_deal_triples_fe(uint64_t n, uint32_t levels, uint64_t seed, uint64_t* t0,
+                                                         uint64_t* t1) {
+    const uint64_t total = n * levels * 3;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t base = deal_mix(seed ^ deal_mix(q));
+        uint64_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = fe_canon_dev(deal_mix(base ^ (uint64_t)k) & ((1ull << 62) - 1));
+        const uint64_t a = fe_addc(w[0], w[1]), b = fe_addc(w[2], w[3]);
+        const uint64_t c = fe_mulc(a, b);
+        t0[3 * q] = w[0];
+        t0[3 * q + 1] = w[2];
+        t0[3 * q + 2] = w[4];
+        t1[3 * q] = w[1];
+        t1[3 * q + 1] = w[3];
+        t1[3 * q + 2] = fe_subc(c, w[4]);
+    }
+}
+
+hipError_t launch_deal_triples_fe(uint64_t n, uint32_t levels, uint64_t seed, uint64_t* t0, uint64_t* t1,
+                                  hipStream_t stream) {
+    const uint64_t total = n * levels * 3;
+    if (total == 0) return hipSuccess;
+    const uint64_t b = (total + 255) / 256;
+    hipLaunchKernelGGL(k_deal_triples_fe, dim3((unsigned)(b < 65535 ? b : 65535)), dim3(256), 0, stream, n, levels,
+                       seed, t0, t1);
+    return hipGetLastError();
+}
+
+// ---- U = FieldElm (the last level, sketch_at_last, sketch.rs:202-245) ----------------------
+// FieldElm::from_rng = num-bigint gen_biguint_below(p) (field.rs:367-372): 32 keystream bytes
+// per attempt as 8 little-endian u32 digits, top digit >> 1, redraw while >= p (probability
+// 19 / 2^255). Draw m is keystream blocks 2m, 2m + 1 while nothing was redrawn (the stream is
+// byte-continuous). Segment lane l of a key produces draws l, l + LPK, ... (rand1..3 for m < 3,
+// then node m - 3), both blocks of a draw in lockstep; a segment that sees a draw >= p falls
+// back to the sequential stream for its key.
+using Fe8 = uint32_t[8];
+
+__device__ __forceinline__ void ld8(const uint32_t* p, uint32_t (&v)[8]) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(uint32_t* p, const uint32_t (&v)[8]) {
+    reinterpret_cast<uint4*>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<uint4*>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+template <int LPK>
+__device__ __forceinline__ void seg_fe255_sum(uint32_t (&v)[8]) {
+#pragma unroll
+    for (int off = LPK / 2; off > 0; off >>= 1) {
+        uint32_t o[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] = __shfl_xor(v[k], off, 64);
+        fe255_addm(v, o, v);
+    }
+}
+
+// draw m (two blocks) of a key's stream: the 8 digits, top one shifted
+__device__ __forceinline__ void fe255_draw_blocks(uint64_t m, const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                                  const uint32_t (&rk)[11][4], uint32_t (&d)[8]) {
+    uint32_t st[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint64_t b = 2 * m + h;
+        st[h][0] = 0u;
+        st[h][1] = 0u;
+        st[h][2] = __builtin_bswap32((uint32_t)(b >> 32));
+        st[h][3] = __builtin_bswap32((uint32_t)b);
+    }
+    aes_rk<SkTab, 2>(st, tbl, b0, b1, rk);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        d[k] = st[0][k];
+        d[4 + k] = st[1][k];
+    }
+    d[7] >>= 1;
+}
+
+template <int KPW>
+__global__ __launch_bounds__(kSketchThreads) void k_sketch_fe255(Sketch255Args a) {
+    constexpr int LPK = 64 / KPW;
+    __shared__ uint32_t tbl[SkTab::kWords];
+    for (int i = threadIdx.x; i < SkTab::kWords; i += kSketchThreads) tbl[i] = SkTab::word(c_T0_sk.v, i);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t seg = lane / LPK, sl = lane % LPK;
+    uint32_t b0, b1;
+    SkTab::bases(lane, b0, b1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kSketchThreads / 64);
+    const uint64_t F = a.n_nodes;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kSketchThreads / 64) + (threadIdx.x >> 6);
+    for (uint64_t kbase = wave * KPW; kbase < a.n_keys; kbase += nwaves * KPW) {
+        const uint64_t k = kbase + seg;
+        const bool kact = k < a.n_keys;
+        const uint64_t kk = kact ? k : kbase;
+        uint32_t seed[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
+        seed[3] ^= a.level;
+        uint32_t rk[11][4];
+        key_schedule(seed, rk, tbl, lane & 31);
+        const uint32_t* x = a.x + kk * F * 8;
+        const uint32_t* kx = a.kx + kk * F * 8;
+        uint32_t acc[3][8], rnd[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc[0][q] = acc[1][q] = acc[2][q] = rnd[q] = 0;
+        bool rej = false;
+        if (!a.force_sequential) {
+            for (uint64_t m = sl; m < F + 3; m += LPK) {
+                uint32_t xv[8], kxv[8], r[8];
+                if (m >= 3) {
+                    ld8(x + 8 * (m - 3), xv);
+                    ld8(kx + 8 * (m - 3), kxv);
+                }
+                fe255_draw_blocks(m, tbl, b0, b1, rk, r);
+                rej |= fe255_geq_p(r);
+                if (m < 3) {   // rand1..3 live on segment lanes 0..2 (LPK >= 4)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) rnd[q] = r[q];
+                    continue;
+                }
+                fe255_canonm(xv);
+                fe255_canonm(kxv);
+                uint32_t r2[8], t[8];
+                fe255_mulm(r, r, r2);
+                fe255_mulm(xv, r, t);
+                fe255_addm(acc[0], t, acc[0]);
+                fe255_mulm(xv, r2, t);
+                fe255_addm(acc[1], t, acc[1]);
+                fe255_mulm(kxv, r, t);
+                fe255_addm(acc[2], t, acc[2]);
+            }
+        }
+        const uint64_t rej_mask = __ballot(rej);
+        const uint64_t seg_bits = (LPK == 64 ? ~0ull : ((1ull << LPK) - 1)) << (seg * LPK);
+        const bool key_rej = a.force_sequential || (rej_mask & seg_bits) != 0;
+#pragma unroll
+        for (int i = 0; i < 3; i++) seg_fe255_sum<LPK>(acc[i]);
+        uint32_t r3[3][8];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r3[i][q] = __shfl(rnd[q], seg * LPK + i, 64);
+        if (kact && sl == 0) {
+            uint32_t* o = a.out + 48 * k;
+            if (!key_rej) {
+#pragma unroll
+                for (int i = 0; i < 3; i++) st8(o + 8 * i, acc[i]);
+#pragma unroll
+                for (int i = 0; i < 3; i++) st8(o + 8 * (3 + i), r3[i]);
+            } else {
+                // sequential stream with redraws (field.rs:367-372) for this key
+                uint64_t m = 0;
+                auto draw = [&](uint32_t (&v)[8]) {
+                    for (;;) {
+                        fe255_draw_blocks(m++, tbl, b0, b1, rk, v);
+                        if (!fe255_geq_p(v)) return;
+                    }
+                };
+                uint32_t q[3][8], s[3][8];
+#pragma unroll
+                for (int i = 0; i < 3; i++) draw(q[i]);
+#pragma unroll
+                for (int i = 0; i < 3; i++)
+#pragma unroll
+                    for (int w = 0; w < 8; w++) s[i][w] = 0;
+                for (uint64_t j = 0; j < F; j++) {
+                    uint32_t r[8], r2[8], t[8], xv[8], kxv[8];
+                    draw(r);
+                    ld8(x + 8 * j, xv);
+                    ld8(kx + 8 * j, kxv);
+                    fe255_canonm(xv);
+                    fe255_canonm(kxv);
+                    fe255_mulm(r, r, r2);
+                    fe255_mulm(xv, r, t);
+                    fe255_addm(s[0], t, s[0]);
+                    fe255_mulm(xv, r2, t);
+                    fe255_addm(s[1], t, s[1]);
+                    fe255_mulm(kxv, r, t);
+                    fe255_addm(s[2], t, s[2]);
+                }
+#pragma unroll
+                for (int i = 0; i < 3; i++) st8(o + 8 * i, s[i]);
+#pragma unroll
+                for (int i = 0; i < 3; i++) st8(o + 8 * (3 + i), q[i]);
+            }
+        }
+    }
+}
+
+constexpr int kSketch255KeysPerWave = 4;   // 16 lanes per key
+
+hipError_t launch_sketch_fe255(const Sketch255Args& a, hipStream_t stream) {
+    if (a.n_keys == 0) return hipSuccess;
+    int cus = 256, dev = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* fn = reinterpret_cast<const void*>(&k_sketch_fe255<kSketch255KeysPerWave>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSketchThreads, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const uint64_t waves_needed = (a.n_keys + kSketch255KeysPerWave - 1) / kSketch255KeysPerWave;
+    uint64_t blocks = (waves_needed + 3) / 4;
+    const uint64_t cap = (uint64_t)cus * per_cu;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_sketch_fe255<kSketch255KeysPerWave>, dim3((unsigned)blocks), dim3(kSketchThreads), 0, stream,
+                       a);
+    return hipGetLastError();
+}
+
+// MulState (mpc.rs:83-220) for U: xs = [r_x, k, r_x], ys = [r_x, k, k], zs = [-r2_x, -k2, -r_kx]
+struct MulView255 {
+    uint32_t xs[3][8], ys[3][8], zs[3][8], rs[3][8];
+};
+
+__device__ __forceinline__ void mul_view255(const uint32_t* sk, const uint32_t* mac_p, const uint32_t* mac2_p,
+                                            MulView255& m) {
+    uint32_t rx[8], r2x[8], rkx[8], mac[8], mac2[8];
+    ld8(sk, rx);
+    ld8(sk + 8, r2x);
+    ld8(sk + 16, rkx);
+    ld8(mac_p, mac);
+    ld8(mac2_p, mac2);
+    fe255_canonm(rx); fe255_canonm(r2x); fe255_canonm(rkx); fe255_canonm(mac); fe255_canonm(mac2);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        m.xs[0][q] = rx[q];  m.ys[0][q] = rx[q];
+        m.xs[1][q] = mac[q]; m.ys[1][q] = mac[q];
+        m.xs[2][q] = rx[q];  m.ys[2][q] = mac[q];
+    }
+    fe255_negm(r2x, m.zs[0]);
+    fe255_negm(mac2, m.zs[1]);
+    fe255_negm(rkx, m.zs[2]);
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        ld8(sk + 8 * (3 + i), m.rs[i]);
+        fe255_canonm(m.rs[i]);
+    }
+}
+
+__device__ __forceinline__ void out_share_fe255(const MulView255& m, int server_idx, const uint32_t* tr,
+                                                const uint32_t (&cor)[6][8], uint32_t (&out)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) out[q] = 0;
+    for (int i = 0; i < 3; i++) {
+        uint32_t ta[8], tb[8], tc[8], term[8], t[8];
+        ld8(tr + 8 * (3 * i), ta);
+        ld8(tr + 8 * (3 * i + 1), tb);
+        ld8(tr + 8 * (3 * i + 2), tc);
+        fe255_canonm(ta); fe255_canonm(tb); fe255_canonm(tc);
+        if (server_idx) {
+            fe255_mulm(cor[i], cor[3 + i], term);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) term[q] = 0;
+        }
+        fe255_mulm(cor[i], tb, t);
+        fe255_addm(term, t, term);
+        fe255_mulm(cor[3 + i], ta, t);
+        fe255_addm(term, t, term);
+        fe255_addm(term, tc, term);
+        fe255_addm(term, m.zs[i], term);
+        fe255_mulm(term, m.rs[i], t);
+        fe255_addm(out, t, out);
+    }
+}
+
+__device__ __forceinline__ void cor_share255(const MulView255& m, const uint32_t* tr, uint32_t (&d)[6][8]) {
+    for (int i = 0; i < 3; i++) {
+        uint32_t ta[8], tb[8];
+        ld8(tr + 8 * (3 * i), ta);
+        ld8(tr + 8 * (3 * i + 1), tb);
+        fe255_canonm(ta);
+        fe255_canonm(tb);
+        fe255_subm(m.xs[i], ta, d[i]);
+        fe255_subm(m.ys[i], tb, d[3 + i]);
+    }
+}
+
+// mode 0: cor_share -> out [n][6][8]; mode 1: out_share -> out [n][8]
+__global__ __launch_bounds__(256) void k_mul_fe255(Mul255Args a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        MulView255 m;
+        mul_view255(a.sketch + 48 * i, a.mac + 8 * i, a.mac2 + 8 * i, m);
+        const uint32_t* tr = a.triples + 72 * i;
+        if (a.mode == 0) {
+            uint32_t d[6][8];
+            cor_share255(m, tr, d);
+            for (int q = 0; q < 6; q++) st8(a.out + 48 * i + 8 * q, d[q]);
+        } else {
+            uint32_t cor[6][8], o[8];
+            for (int q = 0; q < 6; q++) {
+                ld8(a.cor + 48 * i + 8 * q, cor[q]);
+                fe255_canonm(cor[q]);
+            }
+            out_share_fe255(m, a.server_idx, tr, cor, o);
+            st8(a.out + 8 * i, o);
+        }
+    }
+}
+
+// both servers in one process (main.rs:14-70 at the last level): cor shares, cor, out shares, verify
+__global__ __launch_bounds__(256) void k_verify_fe255(Verify255Args a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        MulView255 m[2];
+        uint32_t cor[6][8];
+        for (int s = 0; s < 2; s++) {
+            mul_view255(a.sketch[s] + 48 * i, a.mac[s] + 8 * i, a.mac2[s] + 8 * i, m[s]);
+            uint32_t d[6][8];
+            cor_share255(m[s], a.triples[s] + 72 * i, d);
+            for (int q = 0; q < 6; q++) {
+                if (s == 0) {
+                    for (int w = 0; w < 8; w++) cor[q][w] = d[q][w];
+                } else {
+                    fe255_addm(cor[q], d[q], cor[q]);   // MulState::cor (mpc.rs:160-180)
+                }
+            }
+        }
+        uint32_t o0[8], o1[8], sum[8];
+        out_share_fe255(m[0], 0, a.triples[0] + 72 * i, cor, o0);
+        out_share_fe255(m[1], 1, a.triples[1] + 72 * i, cor, o1);
+        if (a.out_shares) {
+            st8(a.out_shares + 8 * i, o0);
+            st8(a.out_shares + 8 * (a.n + i), o1);
+        }
+        fe255_addm(o0, o1, sum);   // MulState::verify (mpc.rs:214-220)
+        uint32_t nz = 0;
+        for (int w = 0; w < 8; w++) nz |= sum[w];
+        a.ok[i] = nz == 0 ? 1 : 0;
+    }
+}
+
+hipError_t launch_mul_fe255(const Mul255Args& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mul_fe255, dim3(grid_for(a.n)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_fe255(const Verify255Args& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify_fe255, dim3(grid_for(a.n)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

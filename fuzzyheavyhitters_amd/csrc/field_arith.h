@@ -87,4 +87,110 @@ __host__ __device__ inline bool fe255_ge_u32(const uint32_t* v8, uint32_t t) {
     return v8[0] >= t;
 }
 
+// ---- canonical GF(2^255 - 19) arithmetic on 8 x u32 little-endian limbs (FieldElm's lazy ops
+// are exact BigUint add / mul then one reduce, field.rs:337-349: the same value mod p) --------
+__host__ __device__ inline bool fe255_geq_p(const uint32_t (&a)[8]) {
+    if (a[7] != 0x7FFFFFFFu) return a[7] > 0x7FFFFFFFu;
+    for (int k = 6; k >= 1; k--)
+        if (a[k] != 0xFFFFFFFFu) return false;
+    return a[0] >= 0xFFFFFFEDu;
+}
+
+// r < 2^256 (= 2 p + 38) -> r mod p
+__host__ __device__ inline void fe255_sub_p_twice(uint32_t (&r)[8]) {
+    const uint32_t P[8] = {0xFFFFFFEDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                           0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+        if (!fe255_geq_p(r)) break;
+        uint64_t borrow = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t v = (uint64_t)r[k] - P[k] - borrow;
+            r[k] = (uint32_t)v;
+            borrow = (v >> 63) & 1;
+        }
+    }
+}
+
+// x = lo + 2^256 hi (16 limbs) -> x mod p, folding 2^256 = 38 (mod p)
+__host__ __device__ inline void fe255_fold16(const uint32_t (&x)[16], uint32_t (&out)[8]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)x[k] + (uint64_t)x[8 + k] * 38u + c;
+        out[k] = (uint32_t)v;
+        c = v >> 32;
+    }
+    c *= 38u;   // < 39 * 38
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)out[k] + c;
+        out[k] = (uint32_t)v;
+        c = v >> 32;
+    }
+    if (c) {    // wrapped past 2^256 once more: the remainder is tiny, add 38
+        uint64_t cc = 38;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t v = (uint64_t)out[k] + cc;
+            out[k] = (uint32_t)v;
+            cc = v >> 32;
+        }
+    }
+    fe255_sub_p_twice(out);
+}
+
+__host__ __device__ inline void fe255_mulm(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&out)[8]) {
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t v = (uint64_t)a[i] * b[j] + x[i + j] + c;
+            x[i + j] = (uint32_t)v;
+            c = v >> 32;
+        }
+        x[i + 8] = (uint32_t)c;
+    }
+    fe255_fold16(x, out);
+}
+
+__host__ __device__ inline void fe255_addm(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&out)[8]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)a[k] + b[k] + c;
+        out[k] = (uint32_t)v;
+        c = v >> 32;
+    }
+    // a, b < p: the sum < 2 p < 2^256, no carry out
+    fe255_sub_p_twice(out);
+}
+
+__host__ __device__ inline void fe255_negm(const uint32_t (&a)[8], uint32_t (&out)[8]) {
+    const uint32_t P[8] = {0xFFFFFFEDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                           0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)P[k] - a[k] - borrow;
+        out[k] = (uint32_t)v;
+        borrow = (v >> 63) & 1;
+    }
+    fe255_sub_p_twice(out);   // a = 0 gives p -> 0
+}
+
+__host__ __device__ inline void fe255_subm(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&out)[8]) {
+    uint32_t nb[8];
+    fe255_negm(b, nb);
+    fe255_addm(a, nb, out);
+}
+
+// any value < 2^256 -> canonical
+__host__ __device__ inline void fe255_canonm(uint32_t (&a)[8]) { fe255_sub_p_twice(a); }
+
 }  // namespace fhh

@@ -100,6 +100,7 @@ class DeviceGcBatch:
         self.ev_labels = torch.empty((bits, n, 16), dtype=u8, device=dev)
         self.decode = torch.empty(n, dtype=u8, device=dev)
         self.out = torch.empty(n, dtype=u8, device=dev)
+        torch.cuda.synchronize(dev)   # the library runs on its own stream
         self.mask, self.key, self.delta = int(mask) & 1, _block(label_key), _block(delta)
         self.label_nonce, self.gate_base = label_nonce, gate_base
 

@@ -61,7 +61,8 @@ class _TorchAllReduce:
 def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
-              init_capacity: int = 0, comm=None, gc=False, probe: dict | None = None) -> SimResult:
+              init_capacity: int = 0, comm=None, gc=False, probe: dict | None = None,
+              base_ot: bool = False) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
@@ -85,6 +86,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.host_loop = 1 if host_loop else 0
     cfg.init_capacity = init_capacity
     cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2}[gc]
+    cfg.base_ot = 1 if base_ot else 0   # gc = "ot": Chou–Orlandi base OTs on the host (else ideal)
     ar = None
     if comm is not None:
         cfg.comm = comm.handle

@@ -13,7 +13,9 @@
  *    The reference panics (unwrap/assert, collect.rs:83,919,932,946,967,1008,1012); a
  *    caller that wants that behaviour aborts on nonzero.
  *  - All buffers are caller-owned HOST memory unless the name ends in `_dev` (device
- *    pointer on the ctx's GPU). The ctx owns its device memory and its HIP stream.
+ *    pointer on the ctx's GPU). The ctx owns its device memory and its HIP stream, a
+ *    non-blocking stream: `_dev` inputs must be complete when a call is made (synchronise the
+ *    stream that produced them), and a call returns after its `_dev` outputs are complete.
  *  - A ctx may be used from any thread, but not concurrently (the reference wraps the
  *    collection in a Mutex, server.rs:49). Calls are synchronous w.r.t. the host.
  *  - Key order: client-major, then dim j in [0,d), then (left, right) — the order of
@@ -245,6 +247,10 @@ typedef struct fhh_sim_config {
     uint8_t* probe_seeds;
     uint8_t* probe_ty;
     uint64_t* probe_children;
+    /* gc = 2: 0 = ideal base OTs (seed pairs derived on the device per level); 1 = real base OTs:
+     * Chou–Orlandi (fhh_base_ot_co15) for both OT extensions of every level, computed on host
+     * threads before the crawl (time in fhh_stats.base_ot_ms), uploaded as key schedules. */
+    uint32_t base_ot;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x
@@ -289,11 +295,63 @@ typedef struct fhh_sketch_batch {
     const uint64_t* mac_dev[2];       /* [n] shares of the MAC key k                       */
     const uint64_t* mac2_dev[2];      /* [n] shares of k^2                                 */
     const uint64_t* triples_dev[2];   /* [n][9]                                            */
-    uint64_t* sketch_dev[2];          /* out [n][6]                                        */
-    uint8_t* ok_dev;                  /* out [n]                                           */
-    uint64_t* out_shares_dev;         /* out [2][n] or NULL                                */
+    uint64_t* sketch_dev[2];          /* out [n][6] (the last level verified)              */
+    uint8_t* ok_dev;                  /* out [n_levels][n]                                 */
+    uint64_t* out_shares_dev;         /* out [n_levels][2][n] or NULL                      */
+    /* level batching (main.rs:14-70 runs verify_sketches once per level; SketchDPFKey::triples
+     * holds TRIPLES_PER_LEVEL = 3 per level, sketch.rs:120-126, and MulState::new takes
+     * triples[3 level .. 3 level + 3], mpc.rs:94-98): levels [level, level + n_levels) in one call. */
+    uint32_t level;                   /* first level                                       */
+    uint32_t n_levels;                /* 0 = 1                                             */
+    uint32_t triples_levels;          /* triples_dev is [n][triples_levels][9] (0 = 1)     */
+    uint32_t pad_;
+    uint64_t x_level_stride;          /* elements between levels' x / kx (0: same vectors) */
 } fhh_sketch_batch;
+/* Level l's PrgStream seed is the key's seed with bytes 12..15 XORed with l (little-endian; level 0
+ * = the seed itself): a harness convention — the reference's rand_stream is a collection-wide
+ * stream (collect.rs:35,57) whose per-level use is in the absent dpf/sketch glue. */
 int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* batch);
+
+/* Leader-side dealer for benches / tests: TripleShare::new (mpc.rs:18-45) for n keys x levels x
+ * TRIPLES_PER_LEVEL, both servers' shares written to device buffers [n][levels][9] (a, b, c per
+ * triple; a = a0 + a1, b = b0 + b1, c0 + c1 = a b). Randomness: a mix64 PRF of seed (the
+ * reference draws thread_rng). */
+int fhh_deal_triples_fe(fhh_ctx* ctx, uint64_t n, uint32_t levels, uint64_t seed, uint64_t* triples0_dev,
+                        uint64_t* triples1_dev);
+
+/* ---- the last level, U = FieldElm (sketch_at_last, sketch.rs:202-245; MulState<FieldElm>) ----
+ * FieldElm values are 8 x u32 little-endian limbs (any value < 2^256 is accepted as input, reduced
+ * mod p = 2^255 - 19; outputs canonical). FieldElm::from_rng = num-bigint 0.3.3
+ * gen_biguint_below(p) (field.rs:367-372): 32 stream bytes per attempt as 8 LE u32 digits, the top
+ * digit >> 1, redrawn while >= p — num-bigint is not vendored: this digit order is an ASSUMPTION
+ * (parity unpinned). sketch6 [n][6][8], mac / mac2 [n][8], triples9 [n][9][8]
+ * (triples_last: 3 TripleShares {a, b, c}), cor_share6 / cor6 [n][6][8], out [n][8]. */
+int fhh_sketch_at_fe255(fhh_ctx* ctx, uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint32_t* x,
+                        const uint32_t* kx, uint32_t* sketch6);
+int fhh_mul_cor_share_fe255(fhh_ctx* ctx, uint64_t n, const uint32_t* sketch6, const uint32_t* mac_key,
+                            const uint32_t* mac_key2, const uint32_t* triples9, uint32_t* cor_share6);
+int fhh_mul_cor_fe255(uint64_t n, const uint32_t* share0, const uint32_t* share1, uint32_t* cor6);
+int fhh_mul_out_share_fe255(fhh_ctx* ctx, int server_idx, uint64_t n, const uint32_t* sketch6,
+                            const uint32_t* mac_key, const uint32_t* mac_key2, const uint32_t* triples9,
+                            const uint32_t* cor6, uint32_t* out);
+int fhh_mul_verify_fe255(uint64_t n, const uint32_t* out0, const uint32_t* out1, uint8_t* ok);
+typedef struct fhh_sketch_batch255 {
+    uint64_t n_keys;
+    uint32_t n_nodes;
+    uint32_t force_sequential;
+    const uint8_t* seeds_dev;         /* [n][16]                                           */
+    const uint32_t* x_dev[2];         /* per server [n][n_nodes][8]                        */
+    const uint32_t* kx_dev[2];
+    const uint32_t* mac_dev[2];       /* [n][8] shares of mac_key_last                     */
+    const uint32_t* mac2_dev[2];      /* [n][8] shares of mac_key2_last                    */
+    const uint32_t* triples_dev[2];   /* [n][9][8] triples_last                            */
+    uint32_t* sketch_dev[2];          /* out [n][6][8]                                     */
+    uint8_t* ok_dev;                  /* out [n]                                           */
+    uint32_t* out_shares_dev;         /* out [2][n][8] or NULL                             */
+    uint32_t level;                   /* stream seed = seed with bytes 12..15 ^= level     */
+    uint32_t pad_;
+} fhh_sketch_batch255;
+int fhh_sim_sketch_verify_fe255(fhh_ctx* ctx, const fhh_sketch_batch255* batch);
 
 /* ---- garbled-circuit equality test -------------------------------------
  * multiple_gb_equality_test / multiple_ev_equality_test (equalitytest.rs:25-219): per test,
@@ -372,6 +430,21 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
                        const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                        uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out);
 
+/* ---- base OTs (the OT extension's init, collect.rs:454-471) -------------------------------
+ * Chou–Orlandi "simplest OT" over NIST P-256 (ocelot runs it over Ristretto; not vendored, so the
+ * group and the wire format differ: functionality only). Points are 65-byte uncompressed SEC1;
+ * scalars are derived from the 32-byte seeds (pass fresh randomness per batch). The base-OT
+ * sender ends with key pairs keys[count][2][16], the receiver with keys[count][16] =
+ * pair[c_i] (choices: bit i % 8 of byte i / 8). */
+int fhh_co15_sender_start(const uint8_t seed[32], uint8_t A_out[65]);
+int fhh_co15_receiver(uint32_t count, const uint8_t A[65], const uint8_t* choices, const uint8_t seed[32],
+                      uint8_t* B_out, uint8_t* keys);
+int fhh_co15_sender_finish(uint32_t count, const uint8_t seed[32], const uint8_t* B, uint8_t* keys);
+/* Both parties in one process (derives the two parties' seeds from `seed`). */
+int fhh_base_ot_co15(uint32_t count, const uint8_t* choices, const uint8_t seed[32], uint8_t* sender_keys,
+                     uint8_t* receiver_keys);
+const char* fhh_base_ot_last_error(void);
+
 /* ---- statistics ------------------------------------------------------------------------ */
 
 typedef struct fhh_stats {
@@ -383,6 +456,7 @@ typedef struct fhh_stats {
     uint64_t levels;            /* crawled levels                                        */
     double keygen_ms;
     uint64_t expand_launches_timed; /* k_expand launches covered by expand_ms             */
+    double base_ot_ms;          /* host time of the real base OTs (fhh_sim_config.base_ot) */
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);

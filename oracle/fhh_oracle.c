@@ -634,6 +634,287 @@ void orc_sketch_verify_fe_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t
 }
 
 /* ------------------------------------------------------------------ */
+/* Row a9, last level: sketch_at_last (sketch.rs:202-245) and MulState  */
+/* (mpc.rs:83-222) for U = FieldElm (BigUint mod p = 2^255 - 19,       */
+/* field.rs:14-30,312-372). Values: 8 x u32 little-endian limbs.       */
+/* FieldElm's lazy ops are exact BigUint add / mul followed by one     */
+/* reduce (field.rs:337-349), so every result equals the same          */
+/* expression computed mod p — which is how it is computed here.       */
+/* ------------------------------------------------------------------ */
+static const uint32_t P255[8] = {0xFFFFFFEDu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+
+static int fe255_geq_p(const uint32_t a[8]) {
+    for (int k = 7; k >= 0; k--) {
+        if (a[k] > P255[k]) return 1;
+        if (a[k] < P255[k]) return 0;
+    }
+    return 1;
+}
+
+/* a (< 2^256) -> a mod p, assuming a < 2 p + 2^255 (one or two subtractions) */
+static void fe255_canon(uint32_t a[8]) {
+    for (int it = 0; it < 3 && fe255_geq_p(a); it++) {
+        uint64_t borrow = 0;
+        for (int k = 0; k < 8; k++) {
+            const uint64_t v = (uint64_t)a[k] - P255[k] - borrow;
+            a[k] = (uint32_t)v;
+            borrow = (v >> 63) & 1;
+        }
+    }
+}
+
+/* 16-limb product -> mod p: x = lo + 2^256 hi == lo + 38 hi (2^256 = 38 mod p) */
+static void fe255_reduce16(const uint32_t x[16], uint32_t out[8]) {
+    uint64_t t[9];
+    uint64_t c = 0;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)x[k] + (uint64_t)x[8 + k] * 38u + c;
+        t[k] = v & 0xFFFFFFFFu;
+        c = v >> 32;
+    }
+    t[8] = c;   /* < 39 */
+    /* fold t[8] * 2^256 again */
+    uint32_t r[8];
+    c = t[8] * 38u;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = t[k] + c;
+        r[k] = (uint32_t)v;
+        c = v >> 32;
+    }
+    if (c) {   /* a carry out of 2^256 once more (only for r near 2^256) */
+        uint64_t cc = 38;
+        for (int k = 0; k < 8 && cc; k++) {
+            const uint64_t v = (uint64_t)r[k] + cc;
+            r[k] = (uint32_t)v;
+            cc = v >> 32;
+        }
+    }
+    /* r < 2^256 = 2 p + 38: at most two subtractions of p (the top bit may be set) */
+    for (int it = 0; it < 2; it++) {
+        if (!fe255_geq_p(r)) break;
+        uint64_t borrow = 0;
+        for (int k = 0; k < 8; k++) {
+            const uint64_t v = (uint64_t)r[k] - P255[k] - borrow;
+            r[k] = (uint32_t)v;
+            borrow = (v >> 63) & 1;
+        }
+    }
+    memcpy(out, r, 32);
+}
+
+void orc_fe255_mul(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+    uint32_t x[16] = {0};
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < 8; j++) {
+            const uint64_t v = (uint64_t)a[i] * b[j] + x[i + j] + c;
+            x[i + j] = (uint32_t)v;
+            c = v >> 32;
+        }
+        x[i + 8] = (uint32_t)c;
+    }
+    fe255_reduce16(x, out);
+}
+
+void orc_fe255_add(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+    uint32_t x[16] = {0};
+    uint64_t c = 0;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)a[k] + b[k] + c;
+        x[k] = (uint32_t)v;
+        c = v >> 32;
+    }
+    x[8] = (uint32_t)c;
+    fe255_reduce16(x, out);
+}
+
+/* p - a for canonical a (the Group::negate of field.rs:361-364 gives p for a = 0: equal mod p) */
+void orc_fe255_neg(const uint32_t a[8], uint32_t out[8]) {
+    uint32_t r[8];
+    uint64_t borrow = 0;
+    for (int k = 0; k < 8; k++) {
+        const uint64_t v = (uint64_t)P255[k] - a[k] - borrow;
+        r[k] = (uint32_t)v;
+        borrow = (v >> 63) & 1;
+    }
+    fe255_canon(r);
+    memcpy(out, r, 32);
+}
+
+void orc_fe255_sub(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {   /* field.rs:352-359 */
+    uint32_t nb[8];
+    orc_fe255_neg(b, nb);
+    orc_fe255_add(a, nb, out);
+}
+
+/* FieldElm::from_rng (field.rs:367-372) = num-bigint 0.3.3 `gen_biguint_below(p)` (not vendored;
+ * its published algorithm): loop { n = gen_biguint(bits(p) = 255); if n < p { return n } }, with
+ * gen_biguint = ceil(255 / 32) = 8 u32 digits filled by `Rng::fill` (rand 0.7: fill_bytes of the
+ * digits' 32 bytes, each digit little-endian), then the top digit >>= 32 - 255 % 32 = 1
+ * (`gen_bits`). ASSUMPTION (parity unpinned): that digit fill order and the shift — num-bigint
+ * is absent here, so no reference output pins them. The PrgStream is byte-continuous
+ * (apply_keystream), so a draw is keystream bytes [32 m, 32 m + 32) = blocks 2 m, 2 m + 1. */
+static void fe255_from_stream(const uint8_t rk[176], uint64_t* pos /* in 32-B draws */, uint32_t out[8]) {
+    for (;;) {
+        uint8_t bytes[32];
+        for (int h = 0; h < 2; h++) {
+            const uint64_t b = 2 * *pos + h;
+            uint8_t ctr[16] = {0};
+            for (int i = 0; i < 8; i++) ctr[15 - i] = (uint8_t)(b >> (8 * i));
+            aes128_encrypt_rk(rk, ctr, bytes + 16 * h);
+        }
+        (*pos)++;
+        uint32_t d[8];
+        for (int k = 0; k < 8; k++)
+            d[k] = (uint32_t)bytes[4 * k] | ((uint32_t)bytes[4 * k + 1] << 8) | ((uint32_t)bytes[4 * k + 2] << 16) |
+                   ((uint32_t)bytes[4 * k + 3] << 24);
+        d[7] >>= 1;
+        if (!fe255_geq_p(d)) {
+            memcpy(out, d, 32);
+            return;
+        }
+    }
+}
+
+/* one draw of the FieldElm stream for tests: draw number m (no redraw applied) */
+void orc_fe255_stream_draw(const uint8_t seed[16], uint64_t m, uint32_t out[8]) {
+    oracle_init();
+    uint8_t rk[176];
+    key_expand(seed, rk);
+    uint8_t bytes[32];
+    for (int h = 0; h < 2; h++) {
+        const uint64_t b = 2 * m + h;
+        uint8_t ctr[16] = {0};
+        for (int i = 0; i < 8; i++) ctr[15 - i] = (uint8_t)(b >> (8 * i));
+        aes128_encrypt_rk(rk, ctr, bytes + 16 * h);
+    }
+    for (int k = 0; k < 8; k++)
+        out[k] = (uint32_t)bytes[4 * k] | ((uint32_t)bytes[4 * k + 1] << 8) | ((uint32_t)bytes[4 * k + 2] << 16) |
+                 ((uint32_t)bytes[4 * k + 3] << 24);
+    out[7] >>= 1;
+}
+
+/* sketch_at_last (sketch.rs:202-245), one key: rand1..3 = from_rng, then per (x, kx):
+ * r = from_rng; r2 = r * r; r_x += x r; r2_x += x r2; r_kx += kx r; reduce.
+ * x, kx [n_nodes][8]; out6 [6][8] canonical {r_x, r2_x, r_kx, rand1, rand2, rand3}. */
+void orc_sketch_fe255(const uint8_t seed[16], uint32_t n_nodes, const uint32_t* x, const uint32_t* kx, uint32_t* out6) {
+    oracle_init();
+    uint8_t rk[176];
+    key_expand(seed, rk);
+    uint64_t pos = 0;
+    uint32_t rnd[3][8], acc[3][8];
+    memset(acc, 0, sizeof acc);
+    for (int i = 0; i < 3; i++) fe255_from_stream(rk, &pos, rnd[i]);
+    for (uint32_t j = 0; j < n_nodes; j++) {
+        uint32_t r[8], r2[8], t[8], xj[8], kxj[8];
+        fe255_from_stream(rk, &pos, r);
+        orc_fe255_mul(r, r, r2);
+        memcpy(xj, x + 8 * (size_t)j, 32);
+        memcpy(kxj, kx + 8 * (size_t)j, 32);
+        orc_fe255_mul(xj, r, t);
+        orc_fe255_add(acc[0], t, acc[0]);
+        orc_fe255_mul(xj, r2, t);
+        orc_fe255_add(acc[1], t, acc[1]);
+        orc_fe255_mul(kxj, r, t);
+        orc_fe255_add(acc[2], t, acc[2]);
+    }
+    memcpy(out6, acc, 96);
+    memcpy(out6 + 24, rnd, 96);
+}
+
+void orc_sketch_fe255_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint32_t* x,
+                            const uint32_t* kx, uint32_t* out6, int nthreads) {
+    oracle_init();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < (int64_t)n_keys; i++)
+        orc_sketch_fe255(seeds + 16 * i, n_nodes, x + (uint64_t)i * n_nodes * 8, kx + (uint64_t)i * n_nodes * 8,
+                         out6 + 48 * i);
+}
+
+/* MulState::new (mpc.rs:83-140) for U: xs = [r_x, k, r_x], ys = [r_x, k, k],
+ * zs = [-r2_x, -k2, -r_kx], rs = [rand1, rand2, rand3]. */
+static void mul_state255(const uint32_t* sk6, const uint32_t* mac, const uint32_t* mac2, uint32_t xs[3][8],
+                         uint32_t ys[3][8], uint32_t zs[3][8], uint32_t rs[3][8]) {
+    memcpy(xs[0], sk6, 32);     memcpy(ys[0], sk6, 32);     orc_fe255_neg(sk6 + 8, zs[0]);
+    memcpy(xs[1], mac, 32);     memcpy(ys[1], mac, 32);     orc_fe255_neg(mac2, zs[1]);
+    memcpy(xs[2], sk6, 32);     memcpy(ys[2], mac, 32);     orc_fe255_neg(sk6 + 16, zs[2]);
+    for (int i = 0; i < 3; i++) memcpy(rs[i], sk6 + 8 * (3 + i), 32);
+}
+
+/* MulState::cor_share (mpc.rs:142-158): triples9 [3 triples][a, b, c][8]; out6 [d0 d1 d2 e0 e1 e2][8] */
+void orc_mul_cor_share_fe255(const uint32_t* sk6, const uint32_t* mac, const uint32_t* mac2, const uint32_t* triples9,
+                             uint32_t* out6) {
+    uint32_t xs[3][8], ys[3][8], zs[3][8], rs[3][8];
+    mul_state255(sk6, mac, mac2, xs, ys, zs, rs);
+    for (int i = 0; i < 3; i++) {
+        orc_fe255_sub(xs[i], triples9 + 8 * (3 * i), out6 + 8 * i);
+        orc_fe255_sub(ys[i], triples9 + 8 * (3 * i + 1), out6 + 8 * (3 + i));
+    }
+}
+
+/* MulState::out_share (mpc.rs:182-212): sum_i r_i ([server 1] d e + d b + e a + c + z) */
+void orc_mul_out_share_fe255(int server_idx, const uint32_t* sk6, const uint32_t* mac, const uint32_t* mac2,
+                             const uint32_t* triples9, const uint32_t* cor6, uint32_t* out) {
+    uint32_t xs[3][8], ys[3][8], zs[3][8], rs[3][8];
+    mul_state255(sk6, mac, mac2, xs, ys, zs, rs);
+    uint32_t acc[8] = {0};
+    for (int i = 0; i < 3; i++) {
+        const uint32_t* d = cor6 + 8 * i;
+        const uint32_t* e = cor6 + 8 * (3 + i);
+        const uint32_t* a = triples9 + 8 * (3 * i);
+        const uint32_t* b = triples9 + 8 * (3 * i + 1);
+        const uint32_t* c = triples9 + 8 * (3 * i + 2);
+        uint32_t term[8] = {0}, t[8];
+        if (server_idx) orc_fe255_mul(d, e, term);
+        orc_fe255_mul(d, b, t);
+        orc_fe255_add(term, t, term);
+        orc_fe255_mul(e, a, t);
+        orc_fe255_add(term, t, term);
+        orc_fe255_add(term, c, term);
+        orc_fe255_add(term, zs[i], term);
+        orc_fe255_mul(term, rs[i], t);
+        orc_fe255_add(acc, t, acc);
+    }
+    memcpy(out, acc, 32);
+}
+
+/* main.rs:14-70 verify_sketches at the last level, both servers: ok[n] (and out_shares [2][n][8]) */
+void orc_sketch_verify_fe255_batch(uint64_t n_keys, uint32_t n_nodes, const uint8_t* seeds, const uint32_t* x0,
+                                   const uint32_t* kx0, const uint32_t* x1, const uint32_t* kx1,
+                                   const uint32_t* mac /*[2][n][8]*/, const uint32_t* mac2 /*[2][n][8]*/,
+                                   const uint32_t* triples /*[2][n][9][8]*/, uint8_t* ok,
+                                   uint32_t* out_shares /*[2][n][8]*/, int nthreads) {
+    oracle_init();
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t i = 0; i < (int64_t)n_keys; i++) {
+        uint32_t sk[2][48], cs[2][48], cor[48], o[2][8], sum[8];
+        const uint32_t* xs[2] = {x0, x1};
+        const uint32_t* kxs[2] = {kx0, kx1};
+        for (int s = 0; s < 2; s++)
+            orc_sketch_fe255(seeds + 16 * i, n_nodes, xs[s] + (uint64_t)i * n_nodes * 8,
+                             kxs[s] + (uint64_t)i * n_nodes * 8, sk[s]);
+        for (int s = 0; s < 2; s++)
+            orc_mul_cor_share_fe255(sk[s], mac + (s * n_keys + i) * 8, mac2 + (s * n_keys + i) * 8,
+                                    triples + (s * n_keys + i) * 72, cs[s]);
+        for (int k = 0; k < 6; k++) orc_fe255_add(cs[0] + 8 * k, cs[1] + 8 * k, cor + 8 * k);   /* MulState::cor */
+        for (int s = 0; s < 2; s++)
+            orc_mul_out_share_fe255(s, sk[s], mac + (s * n_keys + i) * 8, mac2 + (s * n_keys + i) * 8,
+                                    triples + (s * n_keys + i) * 72, cor, o[s]);
+        orc_fe255_add(o[0], o[1], sum);   /* MulState::verify (mpc.rs:214-220) */
+        int zero = 1;
+        for (int k = 0; k < 8; k++) zero &= sum[k] == 0;
+        ok[i] = (uint8_t)zero;
+        if (out_shares) {
+            memcpy(out_shares + 8 * i, o[0], 32);
+            memcpy(out_shares + 8 * (n_keys + i), o[1], 32);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* Row f1: garbled-circuit equality test (equalitytest.rs:25-219).    */
 /* Third-party algorithm: swanky `fancy-garbling` @553ede0 (not       */
 /* vendored). Restated from the published schemes it implements:     */

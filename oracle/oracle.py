@@ -526,6 +526,85 @@ def prg_stream_u64(seed: bytes, pos: int) -> int:
     return int(lib().orc_prg_stream_u64(_p(s), ctypes.c_uint64(pos)))
 
 
+u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def fe255_stream_draw(seed: bytes, m: int) -> int:
+    """Draw m of the FieldElm stream before rejection (num-bigint gen_biguint(255), see the C)."""
+    s = np.frombuffer(bytes(seed), np.uint8).copy()
+    out = np.zeros(8, np.uint32)
+    lib().orc_fe255_stream_draw(_p(s), ctypes.c_uint64(m), _p(out, u32p))
+    return limbs_to_int(out)
+
+
+def int_to_limbs8(v: int) -> np.ndarray:
+    return np.array([(v >> (32 * k)) & 0xFFFFFFFF for k in range(8)], np.uint32)
+
+
+def limbs_to_int(a) -> int:
+    return sum(int(x) << (32 * k) for k, x in enumerate(np.asarray(a, np.uint64).ravel()))
+
+
+def fe255_op(op: str, a: int, b: int = 0) -> int:
+    """orc_fe255_{mul,add,sub,neg} on Python ints (canonical inputs)."""
+    x, y, o = int_to_limbs8(a), int_to_limbs8(b), np.zeros(8, np.uint32)
+    f = getattr(lib(), "orc_fe255_" + op)
+    if op == "neg":
+        f(_p(x, u32p), _p(o, u32p))
+    else:
+        f(_p(x, u32p), _p(y, u32p), _p(o, u32p))
+    return limbs_to_int(o)
+
+
+def sketch_fe255(seeds: np.ndarray, x: np.ndarray, kx: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """sketch_at_last (sketch.rs:202-245), U = FieldElm: x / kx [n][nodes][8] u32 LE limbs ->
+    [n][6][8] canonical {r_x, r2_x, r_kx, rand1, rand2, rand3}."""
+    seeds = np.ascontiguousarray(seeds, np.uint8)
+    x = np.ascontiguousarray(x, np.uint32)
+    kx = np.ascontiguousarray(kx, np.uint32)
+    n, F = x.shape[:2]
+    out = np.zeros((n, 6, 8), np.uint32)
+    lib().orc_sketch_fe255_batch(ctypes.c_uint64(n), ctypes.c_uint32(F), _p(seeds), _p(x, u32p), _p(kx, u32p),
+                                 _p(out, u32p), ctypes.c_int(nthreads))
+    return out
+
+
+def mul_cor_share_fe255(sketch6, mac, mac2, triples9) -> np.ndarray:
+    """MulState::new + cor_share (mpc.rs:83-158), U = FieldElm: [n][6][8]."""
+    sk, m, m2, tr = (np.ascontiguousarray(a, np.uint32) for a in (sketch6, mac, mac2, triples9))
+    n = sk.shape[0]
+    out = np.zeros((n, 6, 8), np.uint32)
+    for i in range(n):
+        lib().orc_mul_cor_share_fe255(_p(sk[i], u32p), _p(m[i], u32p), _p(m2[i], u32p), _p(tr[i], u32p),
+                                      _p(out[i], u32p))
+    return out
+
+
+def mul_out_share_fe255(server_idx: int, sketch6, mac, mac2, triples9, cor6) -> np.ndarray:
+    """MulState::out_share (mpc.rs:182-212), U = FieldElm: [n][8]."""
+    sk, m, m2, tr, c = (np.ascontiguousarray(a, np.uint32) for a in (sketch6, mac, mac2, triples9, cor6))
+    n = sk.shape[0]
+    out = np.zeros((n, 8), np.uint32)
+    for i in range(n):
+        lib().orc_mul_out_share_fe255(int(server_idx), _p(sk[i], u32p), _p(m[i], u32p), _p(m2[i], u32p),
+                                      _p(tr[i], u32p), _p(c[i], u32p), _p(out[i], u32p))
+    return out
+
+
+def sketch_verify_fe255(seeds, x0, kx0, x1, kx1, mac, mac2, triples, nthreads: int = 0):
+    """main.rs:14-70 at the last level (U = FieldElm), both servers: (ok [n], out_shares [2][n][8])."""
+    x0, kx0, x1, kx1 = (np.ascontiguousarray(a, np.uint32) for a in (x0, kx0, x1, kx1))
+    mac, mac2, triples = (np.ascontiguousarray(a, np.uint32) for a in (mac, mac2, triples))
+    n, F = x0.shape[:2]
+    ok = np.zeros(n, np.uint8)
+    outs = np.zeros((2, n, 8), np.uint32)
+    lib().orc_sketch_verify_fe255_batch(ctypes.c_uint64(n), ctypes.c_uint32(F),
+                                        _p(np.ascontiguousarray(seeds, np.uint8)), _p(x0, u32p), _p(kx0, u32p),
+                                        _p(x1, u32p), _p(kx1, u32p), _p(mac, u32p), _p(mac2, u32p),
+                                        _p(triples, u32p), _p(ok), _p(outs, u32p), ctypes.c_int(nthreads))
+    return ok.astype(bool), outs
+
+
 def sketch_fe(seeds: np.ndarray, x: np.ndarray, kx: np.ndarray, nthreads: int = 0) -> np.ndarray:
     """sketch_at (sketch.rs:157-200), T = FE, for [n] keys -> [n][6] canonical."""
     seeds = np.ascontiguousarray(seeds, np.uint8)

@@ -145,11 +145,12 @@ def _sig(res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gc_mode", ["ideal", "ot"])
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15"])
 @pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
 def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
     """tree_crawl with the GC equality test (collect.rs:419-482) gives the same FE sums, keep
-    decisions and heavy hitters as the plaintext-equality harness, level by level."""
+    decisions and heavy hitters as the plaintext-equality harness, level by level; "ot+co15" runs
+    both OT extensions of every level on real Chou–Orlandi base OTs (host threads)."""
     from fuzzyheavyhitters_amd import sim_crawl, workload
     if kind == "zipf_d1":
         wl = workload.zipf_workload(3000, 64, 1, num_sites=40, seed=5)
@@ -159,9 +160,12 @@ def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
         thr = 0.01
     c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
     plain = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9)
-    with_gc = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9, gc=gc_mode, init_capacity=2)
+    with_gc = sim_crawl(c0, c1, thr, mode="fe", prf_seed=9, gc=gc_mode.split("+")[0], init_capacity=2,
+                        base_ot=gc_mode.endswith("co15"))
     assert _sig(with_gc) == _sig(plain)
     assert len(with_gc.final) > 0
+    if gc_mode.endswith("co15"):
+        assert c0.stats()["base_ot_ms"] > 0
 
 
 @pytest.mark.gpu

@@ -111,3 +111,52 @@ def test_gpu_ot_default_base_material_is_fresh():
     want = np.where(ch[:, None] == 1, x1, x0)
     assert np.array_equal(a, want) and np.array_equal(b, want)
     assert not np.array_equal(ua, ub)
+
+
+def _co15(count, choices, seed):
+    import ctypes
+    from fuzzyheavyhitters_amd._lib import lib, u8p
+    ch = np.packbits(np.asarray(choices, np.uint8), bitorder="little")
+    sk = np.zeros((count, 2, 16), np.uint8)
+    rk = np.zeros((count, 16), np.uint8)
+    sd = np.frombuffer(seed, np.uint8).copy()
+    rc = lib().fhh_base_ot_co15(count, ch.ctypes.data_as(u8p), sd.ctypes.data_as(u8p), sk.ctypes.data_as(u8p),
+                                rk.ctypes.data_as(u8p))
+    assert rc == 0, lib().fhh_base_ot_last_error()
+    return sk, rk
+
+
+def test_co15_base_ot_functionality():
+    """Chou–Orlandi base OTs (the OT extension's init, collect.rs:454-471; host code in libfhh.so,
+    no GPU): the receiver's key is the sender's key of its choice and differs from the other one;
+    the split-party entry points give the same keys as the in-process call; a non-point is
+    rejected."""
+    import ctypes
+    from fuzzyheavyhitters_amd._lib import lib, u8p
+    rng = np.random.default_rng(9)
+    choices = rng.integers(0, 2, 128, dtype=np.uint8)
+    seed = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    sk, rk = _co15(128, choices, seed)
+    assert np.array_equal(rk, sk[np.arange(128), choices])
+    assert not np.any(np.all(rk == sk[np.arange(128), 1 - choices], axis=1))
+    assert len({bytes(k) for k in sk.reshape(-1, 16)}) == 256          # all sender keys distinct
+    sk2, rk2 = _co15(128, choices, bytes([seed[0] ^ 1]) + seed[1:])
+    assert not np.array_equal(sk, sk2)                                  # fresh seed, fresh keys
+    # split parties
+    sa = rng.integers(0, 256, 32, dtype=np.uint8)
+    sb = rng.integers(0, 256, 32, dtype=np.uint8)
+    A = np.zeros(65, np.uint8)
+    assert lib().fhh_co15_sender_start(sa.ctypes.data_as(u8p), A.ctypes.data_as(u8p)) == 0
+    ch = np.packbits(choices[:40], bitorder="little")
+    B = np.zeros((40, 65), np.uint8)
+    kr = np.zeros((40, 16), np.uint8)
+    assert lib().fhh_co15_receiver(40, A.ctypes.data_as(u8p), ch.ctypes.data_as(u8p), sb.ctypes.data_as(u8p),
+                                   B.ctypes.data_as(u8p), kr.ctypes.data_as(u8p)) == 0
+    ks = np.zeros((40, 2, 16), np.uint8)
+    assert lib().fhh_co15_sender_finish(40, sa.ctypes.data_as(u8p), B.ctypes.data_as(u8p),
+                                        ks.ctypes.data_as(u8p)) == 0
+    assert np.array_equal(kr, ks[np.arange(40), choices[:40]])
+    bad = A.copy()
+    bad[1:] ^= 0x5A                                                      # not on the curve
+    assert lib().fhh_co15_receiver(1, bad.ctypes.data_as(u8p), ch.ctypes.data_as(u8p), sb.ctypes.data_as(u8p),
+                                   B.ctypes.data_as(u8p), kr.ctypes.data_as(u8p)) != 0

@@ -152,6 +152,185 @@ def test_gpu_sim_sketch_verify(oracle, force_sequential):
     S.sim_sketch_verify(kc, b, force_sequential=force_sequential)
     ok_exp, outs_exp = oracle.sketch_verify_fe(wl.seeds, wl.x[0], wl.kx[0], wl.x[1], wl.kx[1], np.stack(wl.mac),
                                                np.stack(wl.mac2), np.stack(wl.triples))
-    assert np.array_equal(b.ok.cpu().numpy().astype(bool), ok_exp)
-    assert np.array_equal(b.out_shares.cpu().numpy().view(np.uint64), outs_exp)
+    assert np.array_equal(b.ok[0].cpu().numpy().astype(bool), ok_exp)        # [levels][n], one level
+    assert np.array_equal(b.out_shares[0].cpu().numpy().view(np.uint64), outs_exp)
     assert np.array_equal(ok_exp, wl.honest)
+
+
+# ---- U = FieldElm: the last level (sketch_at_last, sketch.rs:202-245; MulState<FieldElm>) ------
+P255 = (1 << 255) - 19
+
+
+def _py_stream255(seed: bytes):
+    """FieldElm::from_rng = num-bigint 0.3.3 gen_biguint_below(p) on PrgStream (field.rs:367-372):
+    each attempt takes the next 32 keystream bytes as 8 little-endian u32 digits, the top digit
+    shifted right by 1 (255 bits); redraw while >= p. (num-bigint is not vendored: the digit order
+    is the assumption DESIGN.md §5.2 records.)"""
+    enc = _openssl_aes(seed)
+    blk = 0
+    while True:
+        raw = enc(blk.to_bytes(16, "big")) + enc((blk + 1).to_bytes(16, "big"))
+        blk += 2
+        d = [int.from_bytes(raw[4 * k:4 * k + 4], "little") for k in range(8)]
+        d[7] >>= 1
+        v = sum(x << (32 * k) for k, x in enumerate(d))
+        if v < P255:
+            yield v
+
+
+def _py_sketch255(seed: bytes, x, kx):
+    st = _py_stream255(seed)
+    r1, r2, r3 = next(st), next(st), next(st)
+    rx = r2x = rkx = 0
+    for xi, kxi in zip(x, kx):
+        r = next(st)
+        # lazy BigUint ops, one reduce at the end (field.rs:337-349)
+        rx += xi * r
+        r2x += xi * (r * r)
+        rkx += kxi * r
+    return [rx % P255, r2x % P255, rkx % P255, r1, r2, r3]
+
+
+def _ints(a):
+    from fuzzyheavyhitters_amd.sketch import fe8_to_int
+    a = np.asarray(a)
+    return [fe8_to_int(a[idx]) for idx in np.ndindex(a.shape[:-1])]
+
+
+def test_fe255_oracle_arith_vs_python(oracle):
+    rng = np.random.default_rng(17)
+    vals = [0, 1, 2, 19, P255 - 1, P255 - 2, (1 << 254), (1 << 255) - 20, (1 << 128) + 7]
+    vals += [int.from_bytes(rng.bytes(32), "little") % P255 for _ in range(40)]
+    for a in vals:
+        assert oracle.fe255_op("neg", a) == (-a) % P255
+        for b in vals[::3]:
+            assert oracle.fe255_op("mul", a, b) == a * b % P255
+            assert oracle.fe255_op("add", a, b) == (a + b) % P255
+            assert oracle.fe255_op("sub", a, b) == (a - b) % P255
+
+
+def test_fe255_stream_matches_openssl_ctr(oracle):
+    rng = np.random.default_rng(4)
+    for _ in range(4):
+        seed = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+        st = _py_stream255(seed)
+        for m in range(5):
+            assert oracle.fe255_stream_draw(seed, m) == next(st)   # no redraw at these odds (19 / 2^255)
+
+
+def test_sketch_fe255_oracle_vs_python(oracle):
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(10, 7, seed=12, bad_fraction=0.3)
+    got = oracle.sketch_fe255(wl.seeds, wl.x[1], wl.kx[1])
+    for i in range(10):
+        exp = _py_sketch255(bytes(wl.seeds[i]), _ints(wl.x[1][i]), _ints(wl.kx[1][i]))
+        assert _ints(got[i]) == exp
+
+
+def test_beaver_identities_fe255(oracle):
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(120, 11, seed=6, bad_fraction=0.25)
+    args = (wl.seeds, wl.x[0], wl.kx[0], wl.x[1], wl.kx[1], np.stack(wl.mac), np.stack(wl.mac2), np.stack(wl.triples))
+    ok, _ = oracle.sketch_verify_fe255(*args)
+    assert ok[wl.honest].all() and not ok[~wl.honest].any()
+    t = np.stack(wl.triples).copy()
+    t[1, :, 2, 0] ^= 1                       # c of the first triple off by one on server 1
+    ok2, _ = oracle.sketch_verify_fe255(*args[:7], t)
+    assert not ok2.any()
+    mac = np.stack(wl.mac).copy()
+    mac[0, :, 0] ^= 4                        # a wrong MAC-key share
+    ok3, _ = oracle.sketch_verify_fe255(*args[:5], mac, *args[6:])
+    assert not ok3[wl.honest].any()
+
+
+def test_split_steps_equal_fused_fe255(oracle):
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(30, 9, seed=3, bad_fraction=0.3)
+    sk = [oracle.sketch_fe255(wl.seeds, wl.x[s], wl.kx[s]) for s in range(2)]
+    cs = [oracle.mul_cor_share_fe255(sk[s], wl.mac[s], wl.mac2[s], wl.triples[s]) for s in range(2)]
+    cor = np.array([[S.int_to_fe8((a + b) % P255) for a, b in zip(_ints(cs[0][i]), _ints(cs[1][i]))]
+                    for i in range(30)], np.uint32)
+    o = [oracle.mul_out_share_fe255(s, sk[s], wl.mac[s], wl.mac2[s], wl.triples[s], cor) for s in range(2)]
+    ok = np.array([(a + b) % P255 == 0 for a, b in zip(_ints(o[0]), _ints(o[1]))])
+    ok_f, outs = oracle.sketch_verify_fe255(wl.seeds, wl.x[0], wl.kx[0], wl.x[1], wl.kx[1], np.stack(wl.mac),
+                                            np.stack(wl.mac2), np.stack(wl.triples))
+    assert np.array_equal(ok, ok_f) and np.array_equal(ok, wl.honest)
+    assert np.array_equal(o[0], outs[0]) and np.array_equal(o[1], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_keys,n_nodes", [(1, 0), (3, 1), (5, 2), (9, 13), (70, 63), (64, 64), (130, 125),
+                                            (600, 40)])
+def test_gpu_sketch_at_fe255_bit_exact(oracle, n_keys, n_nodes):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(n_keys, n_nodes, seed=n_keys * 5 + n_nodes, bad_fraction=0.1)
+    kc = fhh.KeyCollection(8, 1)
+    for s in range(2):
+        got = S.sketch_at_fe255(kc, wl.seeds, wl.x[s], wl.kx[s])
+        exp = oracle.sketch_fe255(wl.seeds, wl.x[s], wl.kx[s])
+        assert np.array_equal(got, exp), f"server {s}"
+
+
+@pytest.mark.gpu
+def test_gpu_mul_steps_fe255_bit_exact(oracle):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(200, 17, seed=23, bad_fraction=0.2)
+    kc = fhh.KeyCollection(8, 1)
+    sk = [S.sketch_at_fe255(kc, wl.seeds, wl.x[s], wl.kx[s]) for s in range(2)]
+    cs = [S.mul_cor_share_fe255(kc, sk[s], wl.mac[s], wl.mac2[s], wl.triples[s]) for s in range(2)]
+    for s in range(2):
+        assert np.array_equal(cs[s], oracle.mul_cor_share_fe255(sk[s], wl.mac[s], wl.mac2[s], wl.triples[s]))
+    cor = S.mul_cor_fe255(cs[0], cs[1])
+    o = [S.mul_out_share_fe255(kc, s, sk[s], wl.mac[s], wl.mac2[s], wl.triples[s], cor) for s in range(2)]
+    for s in range(2):
+        assert np.array_equal(o[s], oracle.mul_out_share_fe255(s, sk[s], wl.mac[s], wl.mac2[s], wl.triples[s], cor))
+    assert np.array_equal(S.mul_verify_fe255(o[0], o[1]), wl.honest)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force_sequential", [False, True], ids=["parallel", "sequential-stream"])
+def test_gpu_sim_sketch_verify_fe255(oracle, force_sequential):
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload255(700, 45, seed=98, bad_fraction=0.1)
+    kc = fhh.KeyCollection(8, 1)
+    b = S.DeviceSketchBatch255(wl)
+    S.sim_sketch_verify_fe255(kc, b, force_sequential=force_sequential)
+    ok_exp, outs_exp = oracle.sketch_verify_fe255(wl.seeds, wl.x[0], wl.kx[0], wl.x[1], wl.kx[1], np.stack(wl.mac),
+                                                  np.stack(wl.mac2), np.stack(wl.triples))
+    assert np.array_equal(b.ok.cpu().numpy().astype(bool), ok_exp)
+    assert np.array_equal(b.out_shares.cpu().numpy().view(np.uint32), outs_exp)
+    assert np.array_equal(ok_exp, wl.honest)
+
+
+@pytest.mark.gpu
+def test_gpu_sketch_verify_level_batch(oracle):
+    """Levels [2, 7) in one call (configs[4] runs data_len - 1 = 1023 such levels): level l uses
+    the stream of seed ^ l (bytes 12..15) and the dealt triples[l] (TripleShare::new per level,
+    MulState::new's triples[3 l ..], mpc.rs:94-98); every level's ok bits and out shares equal
+    the oracle's for that level, and the dealt triples satisfy c0 + c1 = (a0 + a1)(b0 + b1)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    wl = S.sketch_workload(500, 19, seed=41, bad_fraction=0.1)
+    kc = fhh.KeyCollection(8, 1)
+    b = S.DeviceSketchBatch(wl)
+    S.deal_triples(kc, b, levels=8, seed=77)
+    S.sim_sketch_verify(kc, b, level=2, n_levels=5)
+    tr = [t.cpu().numpy().view(np.uint64) for t in b.triples]           # [n][8][9]
+    a = (tr[0][..., 0::3] + tr[1][..., 0::3]) % np.uint64(P)
+    bb = (tr[0][..., 1::3] + tr[1][..., 1::3]) % np.uint64(P)
+    c = (tr[0][..., 2::3] + tr[1][..., 2::3]) % np.uint64(P)
+    for idx in [(0, 0, 0), (3, 5, 2), (499, 7, 1)]:
+        assert int(a[idx]) * int(bb[idx]) % P == int(c[idx])
+    ok = b.ok.cpu().numpy()
+    outs = b.out_shares.cpu().numpy().view(np.uint64)
+    for k, lv in enumerate(range(2, 7)):
+        seeds = wl.seeds.copy()
+        seeds[:, 12:16] ^= np.frombuffer(np.uint32(lv).tobytes(), np.uint8)
+        ok_e, outs_e = oracle.sketch_verify_fe(seeds, wl.x[0], wl.kx[0], wl.x[1], wl.kx[1], np.stack(wl.mac),
+                                               np.stack(wl.mac2), np.stack([tr[0][:, lv], tr[1][:, lv]]))
+        assert np.array_equal(ok[k].astype(bool), ok_e), f"level {lv}"
+        assert np.array_equal(outs[k], outs_e), f"level {lv}"
+        assert np.array_equal(ok_e, wl.honest)

@@ -429,10 +429,13 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // scheduler keep more T-table lookups in flight per wave); 41 is 39 drawing the next item ahead;
 // 42 is 34 with the next entry's seeds prefetched under the current entry's AES; 43 / 44 are
 // DIAGNOSTIC builds of 34 that store no / only the dir-0 child seeds (HBM-write A/B; their states
-// are incomplete by design and no product path selects them)
+// are incomplete by design and no product path selects them); 45 / 46 / 47 / 48 are the hybrid:
+// 34 with the last 2 / 4 / 6 / 8 of each workgroup's 16 waves running the pair-sliced VALU AES
+// (expand_ps.h) on the same items; 49 runs every wave as a VALU wave (the test variant that
+// pins expand_item_ps: in 45-48 which items the VALU waves take depends on timing)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 44))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 49))
                ? 16u : variant == 31 ? 32u : 8u;
 }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }

@@ -13,6 +13,7 @@
 //   k_keys_from_aos add_key wire layout -> SoA device layout
 #include "fhh_internal.h"
 #include "expand_kernel.h"
+#include "expand_ps.h"
 #include "../../include/fhh.h"
 
 namespace fhh {
@@ -225,7 +226,8 @@ __device__ uint32_t g_wprof_launch = 0;
 // FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores,
 // bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline,
 // bit 4 = decode the end-phase items of item_layout (only the variants that lay them out:
-// the extra decode state made the 1024-thread kernel spill)
+// the extra decode state made the 1024-thread kernel spill), bits 7-11 = NBS: the last NBS waves
+// of every workgroup are VALU waves (expand_item_ps, pair-sliced AES) — the hybrid variants
 template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     constexpr bool AHEAD = (FLAGS & 1) != 0;
@@ -234,6 +236,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     constexpr bool PROF = (FLAGS & 8) != 0;
     constexpr bool TAIL = (FLAGS & 16) != 0;
     constexpr int STORE = (FLAGS >> 5) & 3;   // diagnostic variants 43 / 44 only
+    constexpr int NBS = (FLAGS >> 7) & 31;
+    static_assert(NBS <= THR / 64, "hybrid: NBS VALU waves out of THR / 64");
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
     __syncthreads();
@@ -243,6 +247,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;
     Tab::bases(lane, b0, b1);
+    const bool valu_wave = NBS > 0 && wave_id_uniform() >= (uint32_t)(THR / 64 - NBS);
     const uint64_t wpb = THR / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     // sizes: kernel arguments (host-driven crawl) or LoopCtl (device-resident loop)
@@ -290,7 +295,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         }
         uint32_t nxt = 0;
         if constexpr (PROF) prof_items++;
-        if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
+        if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
+        else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
         else expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
@@ -321,6 +327,28 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             atomicExch(work_counter + 1, 0u);
         }
     }
+}
+
+// test hook: AES_0 of 1024 blocks through the hybrid's pair-sliced data path (k_debug_aes_ps);
+// in / out are host arrays of 1024 x 16 bytes
+extern "C" int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out) {
+    if (!in || !out) return FHH_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    uint4 *din = nullptr, *dout = nullptr;
+    if (hipMalloc(&din, 16384) != hipSuccess) return FHH_E_NOMEM;
+    if (hipMalloc(&dout, 16384) != hipSuccess) {
+        (void)hipFree(din);
+        return FHH_E_NOMEM;
+    }
+    hipError_t e = hipMemcpy(din, in, 16384, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_debug_aes_ps, dim3(1), dim3(64), 0, 0, din, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, 16384, hipMemcpyDeviceToHost);
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return e == hipSuccess ? FHH_OK : FHH_E_HIP;
 }
 
 // arm the wave timeline: buf = device buffer of cap launches x grid waves x 3 u64 (NULL disarms)
@@ -372,7 +400,12 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)     \
     X(42, Tab4T32<DevOpsX>, 4, 1024, 1, true, true, 6)      \
     X(43, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 38)    \
-    X(44, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 70)
+    X(44, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 70)   \
+    X(45, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (2 << 7)) \
+    X(46, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (4 << 7)) \
+    X(47, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (6 << 7)) \
+    X(48, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (8 << 7)) \
+    X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7))
 
 struct VariantInfo {
     const void* fn;
@@ -403,7 +436,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 18; }
+int expand_variant_count() { return kBsVariant + kBsCount + 23; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

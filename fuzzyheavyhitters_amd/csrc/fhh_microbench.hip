@@ -66,6 +66,98 @@ __global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters)
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Mixed lookup paths: NL dependent chains through the per-lane-replica LDS table (as
+// k_lds_peak / k_expand) and NG dependent chains through a read-only global table of
+// `gbytes` bytes (4-byte entries, L1/L2 resident), issued as buffer_load_dword with a
+// data-dependent offset. Measures whether the vector-memory path adds lookup throughput
+// beside a saturated LDS (fhh_microbench_gather).
+template <int NL, int NG>
+__global__ __launch_bounds__(512) void k_gather_mix(const uint32_t* __restrict__ gtab, uint32_t gmask,
+                                                    uint32_t* out, uint32_t iters) {
+    __shared__ uint32_t tbl[256 * 64];
+    for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) tbl[i] = (uint32_t)i * 2654435761u;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(gtab), 0, (int)((gmask + 1) * 4), 0x00020000);
+    const uint32_t lb = (threadIdx.x & 63) * 4;
+    uint32_t x[NL > 0 ? NL : 1], y[NG > 0 ? NG : 1];
+#pragma unroll
+    for (int k = 0; k < (NL > 0 ? NL : 1); k++) x[k] = threadIdx.x * 31 + k * 77;
+#pragma unroll
+    for (int k = 0; k < (NG > 0 ? NG : 1); k++) y[k] = threadIdx.x * 131 + k * 7919 + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) {
+            const uint32_t a = __builtin_amdgcn_perm(lb, x[k], 0x0C0C0104u);
+            x[k] = *(const uint32_t*)((const char*)tbl + a);
+        }
+#pragma unroll
+        for (int k = 0; k < NG; k++)
+            y[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((y[k] & gmask) << 2), 0, 0);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < NL; k++) acc ^= x[k];
+#pragma unroll
+    for (int k = 0; k < NG; k++) acc ^= y[k];
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Can VALU-only waves add work beside LDS-bound waves in the same workgroup? 1024-thread
+// workgroups (4 waves/SIMD, <= 128 VGPRs); waves 0 .. 15-NB run k_expand-shaped lookup chains
+// (one ds_read_b32 + one v_perm + one v_bitop3 per lookup, ~ the T-table's 1.7 VALU per
+// lookup), waves 16-NB .. 15 run independent v_bitop3 chains over 48 live words (a bitsliced
+// AES's shape) until the lookup waves are done (LDS flag). counts[0] += lookups,
+// counts[1] += bitop3 lane-ops (fhh_microbench_hybrid).
+template <int NB>
+__global__ __launch_bounds__(1024) void k_hybrid_mix(unsigned long long* counts, uint32_t iters) {
+    __shared__ uint32_t tbl[256 * 64];
+    __shared__ uint32_t done;
+    for (int i = threadIdx.x; i < 256 * 64; i += blockDim.x) tbl[i] = (uint32_t)i * 2654435761u;
+    if (threadIdx.x == 0) done = 0;
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    if (w < 16 - NB) {
+        const uint32_t lb = (threadIdx.x & 63) * 4;
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = threadIdx.x * 31 + k * 77;
+        for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t a = __builtin_amdgcn_perm(lb, x[k], 0x0C0C0104u);
+                const uint32_t v = *(const uint32_t*)((const char*)tbl + a);
+                x[k] = __builtin_amdgcn_bitop3_b32(v, x[k], x[(k + 1) & 7], 0x96);
+            }
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc ^= x[k];
+        if (acc == 0x12345678u) counts[2] = acc;
+        __atomic_fetch_add(&done, 1u, __ATOMIC_RELAXED);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&counts[0], (unsigned long long)iters * 8 * 64);
+    } else {
+        uint32_t x[48];
+#pragma unroll
+        for (int k = 0; k < 48; k++) x[k] = threadIdx.x * (k + 3) + k * 0x9e3779b9u + blockIdx.x;
+        uint32_t n = 0;
+        while (__atomic_load_n(&done, __ATOMIC_RELAXED) < (uint32_t)(64 * (16 - NB))) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+#pragma unroll
+                for (int k = 0; k < 48; k++)
+                    x[k] = __builtin_amdgcn_bitop3_b32(x[k], x[(k + 1 + r) % 48], x[(k + 17 + r) % 48], 0x6A);
+            }
+            n++;
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 48; k++) acc ^= x[k];
+        if (acc == 0x12345678u) counts[2] = acc;
+        if ((threadIdx.x & 63) == 0) atomicAdd(&counts[1], (unsigned long long)n * 4 * 48 * 64);
+    }
+}
+
 // launch-gap probe: a kernel that only touches its dynamic LDS (so the LDS allocation is
 // real) and, from one lane, one word of global memory
 __global__ void k_gap_probe(uint32_t* out, uint32_t tag) {
@@ -206,5 +298,96 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
     (void)hipEventDestroy(b);
     (void)hipFree(out);
     *rate = ops / (ms * 1e-3);
+    return FHH_OK;
+}
+
+// Lookup throughput of the LDS and vector-memory gather paths, alone and mixed
+// (k_gather_mix<NL, NG>): combo 0..8 = (NL, NG) in the table below; gbytes = global table
+// span (256 .. 65536). rate = lookups per second over the chip (both paths).
+extern "C" int fhh_microbench_gather(int device, int combo, uint32_t gbytes, double* rate) {
+    static const int kCombos[][2] = {{8, 0}, {0, 8}, {0, 16}, {8, 1}, {8, 2}, {8, 4}, {6, 2}, {4, 4}, {12, 2}};
+    if (!rate || combo < 0 || combo >= (int)(sizeof kCombos / sizeof kCombos[0]) || gbytes < 256 ||
+        gbytes > 65536 || (gbytes & (gbytes - 1)))
+        return FHH_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return FHH_E_HIP;
+    uint32_t* out = nullptr;
+    uint32_t* g = nullptr;
+    if (hipMalloc(&out, 4) != hipSuccess) return FHH_E_NOMEM;
+    if (hipMalloc(&g, 65536) != hipSuccess) {
+        (void)hipFree(out);
+        return FHH_E_NOMEM;
+    }
+    {
+        uint32_t h[16384];
+        for (uint32_t i = 0; i < 16384; i++) h[i] = i * 2654435761u + 12345u;
+        (void)hipMemcpy(g, h, sizeof h, hipMemcpyHostToDevice);
+    }
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const int nl = kCombos[combo][0], ng = kCombos[combo][1];
+    const uint32_t gmask = gbytes / 4 - 1;
+    const int blocks = cus * 2;
+    const uint32_t iters = 4096;
+    float ms = 0.f;
+    hipError_t e = hipSuccess;
+    for (int rep = 0; rep < 3 && e == hipSuccess; rep++) {
+        (void)hipEventRecord(a, 0);
+#define FHH_GM(L, G) \
+    if (nl == L && ng == G) hipLaunchKernelGGL((fhh::k_gather_mix<L, G>), dim3(blocks), dim3(512), 0, 0, g, gmask, out, iters);
+        FHH_GM(8, 0) FHH_GM(0, 8) FHH_GM(0, 16) FHH_GM(8, 1) FHH_GM(8, 2) FHH_GM(8, 4) FHH_GM(6, 2) FHH_GM(4, 4)
+        FHH_GM(12, 2)
+#undef FHH_GM
+        (void)hipEventRecord(b, 0);
+        e = hipEventSynchronize(b);
+        (void)hipEventElapsedTime(&ms, a, b);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(out);
+    (void)hipFree(g);
+    if (e != hipSuccess) return FHH_E_HIP;
+    *rate = (double)blocks * 512 * iters * (nl + ng) / (ms * 1e-3);
+    return FHH_OK;
+}
+
+// k_hybrid_mix with nb VALU-only waves (0, 2, 4, 6, 8) per 16-wave workgroup; rates[0] =
+// LDS lookups/s, rates[1] = v_bitop3 lane-ops/s, chip-wide, over the kernel time.
+extern "C" int fhh_microbench_hybrid(int device, int nb, double* rates) {
+    if (!rates || (nb != 0 && nb != 2 && nb != 4 && nb != 6 && nb != 8)) return FHH_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return FHH_E_HIP;
+    unsigned long long* c = nullptr;
+    if (hipMalloc(&c, 32) != hipSuccess) return FHH_E_NOMEM;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const uint32_t iters = 8192;
+    float ms = 0.f;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipError_t e = hipSuccess;
+    for (int rep = 0; rep < 3 && e == hipSuccess; rep++) {
+        (void)hipMemset(c, 0, 32);
+        (void)hipEventRecord(a, 0);
+#define FHH_HM(N) \
+    if (nb == N) hipLaunchKernelGGL((fhh::k_hybrid_mix<N>), dim3(cus), dim3(1024), 0, 0, c, iters);
+        FHH_HM(0) FHH_HM(2) FHH_HM(4) FHH_HM(6) FHH_HM(8)
+#undef FHH_HM
+        (void)hipEventRecord(b, 0);
+        e = hipEventSynchronize(b);
+        (void)hipEventElapsedTime(&ms, a, b);
+        if (e == hipSuccess) e = hipMemcpy(h, c, 32, hipMemcpyDeviceToHost);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(c);
+    if (e != hipSuccess) return FHH_E_HIP;
+    rates[0] = (double)h[0] / (ms * 1e-3);
+    rates[1] = (double)h[1] / (ms * 1e-3);
     return FHH_OK;
 }

@@ -475,6 +475,16 @@ int fhh_set_timing(fhh_ctx* ctx, int enabled);
  * which = 0 -> v_xor_b32 lane-ops/s; which = 1 -> ds_read_b32 bytes/s (k_expand pattern);
  * 2 -> v_bitop3_b32 lane-ops/s; 3 -> v_bitop3_b32 at 2 waves/SIMD; 4 -> v_xor_b32 at 2 waves/SIMD. */
 int fhh_microbench(int device, int which, double* rate);
+// Lookup throughput (lookups/s, chip-wide) of k_gather_mix<NL, NG>: NL chains through the
+// per-lane LDS table beside NG chains through a global table of gbytes (power of two,
+// 256..65536); combo 0..8 = (8,0) (0,8) (0,16) (8,1) (8,2) (8,4) (6,2) (4,4) (12,2).
+int fhh_microbench_gather(int device, int combo, uint32_t gbytes, double* rate);
+// k_hybrid_mix: nb (0, 2, 4, 6, 8) of a 16-wave workgroup's waves run v_bitop3 chains while
+// the others run LDS lookup chains; rates[0] = lookups/s, rates[1] = bitop3 lane-ops/s.
+int fhh_microbench_hybrid(int device, int nb, double* rates);
+// Test hook of the hybrid k_expand's VALU waves: AES-128 (zero key, no feed-forward) of 1024
+// blocks (in / out: 1024 x 16 B host arrays) through the pair-sliced data path of expand_ps.h.
+int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out);
 /* Device time per kernel of `reps` back-to-back launches of an empty kernel on one stream
  * (launch-overhead probe for the level loop): which = 0 -> 256 x 1024 threads, 4 KiB LDS;
  * 1 -> 256 x 1024, 128 KiB LDS (k_expand's footprint); 2 -> alternating 256 x 1024 / 128 KiB and

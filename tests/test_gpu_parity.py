@@ -72,11 +72,14 @@ BS_VARIANT = 14   # bitsliced k_expand (csrc/fhh_expand_bs.hip): seeds stored bi
 DIAGNOSTIC_VARIANTS = (43, 44)   # store no / half of the child seeds (HBM A/B only, fhh_internal.h)
 
 GENERIC_AES_VARIANT = 33   # T-table k_expand with the generic AES (the default, 34, shares rounds 1-2 of sibling pairs)
+HYBRID_VARIANT = 46        # T-table waves + 4 pair-sliced VALU waves per workgroup (expand_ps.h)
+VALU_ONLY_VARIANT = 49     # every wave a pair-sliced VALU wave: pins expand_item_ps deterministically
 
 
 @pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT, BS_VARIANT + 2, BS_VARIANT + 7,
-                                     BS_VARIANT + 10],
-                         ids=["default", "generic-aes", "bitsliced", "bitsliced-pair", "bitsliced-pair2", "pair2-carry4"])
+                                     BS_VARIANT + 10, HYBRID_VARIANT, VALU_ONLY_VARIANT],
+                         ids=["default", "generic-aes", "bitsliced", "bitsliced-pair", "bitsliced-pair2", "pair2-carry4",
+                              "hybrid", "pair-sliced-only"])
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_level_states_bit_exact(kc, oracle, path, variant):
     """Every level: EvalState seeds/t/y of all children, share planes and equality counts
@@ -129,8 +132,8 @@ def test_level_states_bit_exact(kc, oracle, path, variant):
                 break
 
 
-@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT + 7],
-                         ids=["default-pair-aes", "generic-aes", "bitsliced-pair2"])
+@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT + 7, VALU_ONLY_VARIANT],
+                         ids=["default-pair-aes", "generic-aes", "bitsliced-pair2", "pair-sliced-only"])
 @pytest.mark.parametrize("d", [1, 2])
 def test_prg_counter_carry_seeds(kc, oracle, variant, d):
     """Root seeds whose byte 8 is 0xFF: the right child's counter (+1 in the upper u64 lane,
@@ -382,3 +385,29 @@ def test_every_expand_variant_bit_exact(kc, oracle):
                 f"variant {v} ({buf.value}) states"
         v += 1
     assert v >= 8
+
+
+def test_pair_sliced_aes_data_path(oracle):
+    """The hybrid k_expand's VALU waves (expand_ps.h): 1024 blocks through the ballot /
+    v_writelane scatter, the generated pair-sliced AES (DPP swaps, lane-parity round keys) and
+    the two 32x32 transposes equal AES-128 under the zero key (no feed-forward) block by block.
+    Dir-1 units carry the dir-0 block + 1 in the upper u64 lane, as PRG counters do, plus
+    the all-ones / carry patterns."""
+    import ctypes
+    from fuzzyheavyhitters_amd import lib
+    rng = np.random.default_rng(11)
+    blk = rng.integers(0, 256, (16, 64, 16), dtype=np.uint8)
+    blk[0, :4] = 0
+    blk[0, 4:8] = 0xFF
+    blk[2, :8, 8:] = 0xFF                 # upper lane wraps for the dir-1 unit
+    for u in range(1, 16, 2):             # dir-1 unit: same bytes 0..7, upper u64 + 1
+        hi = blk[u - 1, :, 8:].copy().view("<u8")[:, 0] + np.uint64(1)
+        blk[u] = blk[u - 1]
+        blk[u, :, 8:] = hi.reshape(-1, 1).view(np.uint8)
+    inp = np.ascontiguousarray(blk.reshape(1024, 16))
+    out = np.zeros_like(inp)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    assert lib().fhh_debug_aes_ps(0, inp.ctypes.data_as(u8p), out.ctypes.data_as(u8p)) == 0
+    exp = np.array([np.frombuffer(oracle.aes0(bytes(b)), np.uint8) for b in inp])
+    bad = np.nonzero(np.any(out != exp, axis=1))[0]
+    assert bad.size == 0, f"{bad.size} blocks differ, first {bad[:8].tolist()}"

@@ -291,6 +291,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
     ap.add_argument("--variant", type=int, default=-1, help="k_expand variant (-1 = library default)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 rehearsal on fewer GPUs than ranks: ranks share devices (local_rank mod the "
+                         "device count) and the per-level all-reduce runs through the hosted communicator "
+                         "(the same cfg.comm path, partials summed by gloo) instead of RCCL, which cannot "
+                         "place two ranks on one GPU. Never a measurement.")
     ap.add_argument("--timing-every", type=int, default=1,
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
     args = ap.parse_args()
@@ -302,6 +307,8 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
     import torch
+    if args.rehearse:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
@@ -348,7 +355,11 @@ def main():
         f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
 
     comm, collective = None, {"kind": "none"}
-    if world > 1:
+    if world > 1 and args.rehearse:
+        comm = fhh.HostedComm(local_rank)
+        collective = {"kind": "REHEARSAL: hosted communicator (gloo all-reduce of the partials), not RCCL",
+                      "comm_ranks": world, "comm_rank": rank}
+    elif world > 1:
         # native RCCL all-reduce on the engine stream (no host sync per level); the id travels
         # over the gloo group
         comm = fhh.RcclComm(local_rank)
@@ -484,6 +495,9 @@ def main():
                              "algorithmic": f"{HBM_BYTES_PER_BLOCK} B per AES block (SURVEY 8d)"},
             "pmc_executed": pmc_rates,
         }
+        if args.rehearse:
+            out["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s), hosted all-reduce: "
+                                "checks the N>1 path (sharding, per-level partial sums, timing), not a measurement")
         if args.microbench:
             import ctypes
             r = ctypes.c_double()

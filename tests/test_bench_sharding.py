@@ -69,3 +69,33 @@ def test_two_rank_plan_and_aggregation():
     assert np.array_equal(np.concatenate([l for _, l, _ in parts]), full.left)
     assert np.array_equal(np.concatenate([r for _, _, r in parts]), full.root_seeds)
     assert elapsed == 1.5 and blocks == 30
+
+
+def _bench_line(cmd):
+    import json
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal_equals_one_rank():
+    """bench.py's N > 1 path end to end on one GPU: two torchrun ranks share the device
+    (--rehearse: the per-level all-reduce through the hosted communicator, RCCL cannot put two
+    ranks on one GPU). The sharded crawl must recover exactly the single-rank run's frontier and
+    heavy hitters, and the JSON line must aggregate over both ranks."""
+    import random
+    import sys as _sys
+    common = ["--clients", "20000", "--data-len", "128", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"]
+    one = _bench_line([_sys.executable, "-u", "bench.py", *common])
+    port = str(29600 + random.randrange(300))
+    two = _bench_line([_sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                       "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2", "--rehearse",
+                       *common])
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["collective"]["comm_ranks"] == 2 and "rehearsal" in two
+    for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
+        assert two[k] == one[k], k
+    assert two["config"]["clients_total"] == one["config"]["clients_total"] == 20000

@@ -97,6 +97,8 @@ def sketch_bench(args, world, rank, local_rank, dist):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S
     L = max(1, args.sketch_levels)
+    if fhh.lib().fhh_sketch_set_impl(args.sketch_impl) != 0:
+        raise SystemExit(f"--sketch-impl {args.sketch_impl}: no such k_sketch_fe form")
     wl = S.sketch_workload(args.sketch_keys, args.sketch_nodes, seed=args.seed + rank, bad_fraction=0.01)
     kc = fhh.KeyCollection(8, 1, device=local_rank)
     b = S.DeviceSketchBatch(wl, device=local_rank)
@@ -146,7 +148,7 @@ def sketch_bench(args, world, rank, local_rank, dist):
             "config": {"workload": f"configs[4]: {L - 1} FE levels + 1 FieldElm level of sketch_at + MulState "
                                    f"verify, both servers in-process",
                        "keys_per_gpu": args.sketch_keys, "nodes": args.sketch_nodes, "levels": L,
-                       "parallelism": f"key-shard x{world}"},
+                       "sketch_impl": args.sketch_impl, "parallelism": f"key-shard x{world}"},
             "keys_verified_per_s": keys * L / elapsed, "aes_blocks_per_s": blocks / elapsed,
             "ms_per_level": elapsed / args.steps / L * 1e3,
             "accepted_per_level": int(wl.honest.sum()), "rejected_per_level": int((~wl.honest).sum()),
@@ -282,6 +284,8 @@ def main():
                     help="--gc ot: real Chou-Orlandi base OTs for every level's OT extensions (host threads, "
                          "overlapped with the crawl) instead of ideal ones")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
+    ap.add_argument("--sketch-impl", type=int, default=0,
+                    help="k_sketch_fe form: 0 = on-the-fly schedule / 1024 threads (default), 1 = r01 kernel")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
     ap.add_argument("--sketch-levels", type=int, default=1024,
                     help="configs[4]: data_len levels verified per step (L-1 over FE, the last over FieldElm)")

@@ -90,4 +90,71 @@ __device__ __forceinline__ void aes_rk2(uint32_t (&s)[2 * Q][4], const uint32_t*
         }
 }
 
+// s <- AES_key(s) for NB blocks under ONE per-lane key, the schedule expanded on the fly (one
+// round key live instead of 44 words: the sketch kernels' per-key PrgStream, where a lane's key
+// differs from its neighbours' and a stored schedule would cost 44 VGPRs). Per round: SubWord of
+// RotWord(w3) through the same tables (4 lookups), rcon, the w0..w3 chain (FIPS-197 5.2).
+template <class Tab>
+__device__ __forceinline__ uint32_t sub_rot_word(uint32_t w3, const uint32_t* tbl, uint32_t b0, uint32_t b1) {
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+    const uint32_t r = (w3 >> 8) | (w3 << 24);   // RotWord on the little-endian column word
+    const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, r);
+    const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, r);
+    const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, r);
+    const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, r);
+    return DevOpsX::perm(a1, a0, sel_lo) | DevOpsX::perm(a3, a2, sel_hi);
+}
+
+template <class Tab, int NB>
+__device__ __forceinline__ void aes_otf(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                        const uint32_t (&key)[4]) {
+    uint32_t k[4] = {key[0], key[1], key[2], key[3]};
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[q][c] = s[q][c] ^ k[c];
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k[0] ^= sub_rot_word<Tab>(k[3], tbl, b0, b1) ^ rcon;
+        k[1] ^= k[0];
+        k[2] ^= k[1];
+        k[3] ^= k[2];
+        rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11Bu : 0u);
+        uint32_t y[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                y[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, k[c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = y[q][c];
+    }
+    k[0] ^= sub_rot_word<Tab>(k[3], tbl, b0, b1) ^ rcon;   // rcon(10) = 0x36
+    k[1] ^= k[0];
+    k[2] ^= k[1];
+    k[3] ^= k[2];
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi), k[c]);
+        }
+}
+
 }  // namespace fhh

@@ -17,6 +17,7 @@
 #include "aes_tables.h"
 #include "field_arith.h"
 #include "aes_keyed.h"
+#include "../../include/fhh.h"
 
 namespace fhh {
 
@@ -96,6 +97,16 @@ __device__ __forceinline__ void ks_block(uint64_t b, const uint32_t* tbl, uint32
     d1 = (uint64_t)s[0][2] | ((uint64_t)s[0][3] << 32);
 }
 
+// the same with the schedule expanded on the fly (k_sketch_fe's default form)
+template <class Tab>
+__device__ __forceinline__ void ks_block_otf(uint64_t b, const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                             const uint32_t (&key)[4], uint64_t& d0, uint64_t& d1) {
+    uint32_t s[1][4] = {{0u, 0u, __builtin_bswap32((uint32_t)(b >> 32)), __builtin_bswap32((uint32_t)b)}};
+    aes_otf<Tab, 1>(s, tbl, b0, b1, key);
+    d0 = (uint64_t)s[0][0] | ((uint64_t)s[0][1] << 32);
+    d1 = (uint64_t)s[0][2] | ((uint64_t)s[0][3] << 32);
+}
+
 // draw `pos` of the key's stream (value v = low 62 bits): rand1..3 or node j = pos - 3
 __device__ __forceinline__ void sketch_draw(uint64_t pos, uint64_t v, uint64_t xv, uint64_t kxv, uint64_t F,
                                             int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1, uint64_t& rx,
@@ -115,6 +126,42 @@ __device__ __forceinline__ void sketch_draw(uint64_t pos, uint64_t v, uint64_t x
     }
 }
 
+// v mod p for any v < 2^128 (three folds of 2^62 = 2^30 + 1, then canonical)
+__device__ __forceinline__ uint64_t fe_red128(unsigned __int128 v) {
+    const uint64_t mask = (1ull << 62) - 1;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const unsigned __int128 h = v >> 62;
+        v = (v & mask) + h + (h << 30);
+    }
+    const uint64_t h = (uint64_t)(v >> 62);
+    uint64_t r = ((uint64_t)v & mask) + h + (h << 30);
+    if (r >= kFeP_) r -= kFeP_;
+    if (r >= kFeP_) r -= kFeP_;
+    return r;
+}
+
+// sketch_draw with the three inner-product terms accumulated unreduced: a pass adds at most 4
+// products (< 2^124 each, canonical x and a 62-bit draw) to an accumulator that starts below
+// 2^62, so one fe_red128 per accumulator per pass replaces a reduction per product
+__device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint64_t xv, uint64_t kxv, uint64_t F,
+                                                 int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1,
+                                                 unsigned __int128& ax, unsigned __int128& a2x,
+                                                 unsigned __int128& akx) {
+    if (pos < 3) {
+        rej |= v >= kFeP_;
+        if (h == 0) rnd0 = v;
+        else rnd1 = v;
+    } else if (pos < F + 3) {
+        rej |= v >= kFeP_;
+        const uint64_t r2 = fe_mulc(v, v);
+        xv = fe_canon_dev(xv);
+        ax += (unsigned __int128)xv * v;
+        a2x += (unsigned __int128)xv * r2;
+        akx += (unsigned __int128)fe_canon_dev(kxv) * v;
+    }
+}
+
 __device__ __forceinline__ uint64_t wave_fe_sum(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fe_addc(v, __shfl_xor(v, off, 64));
@@ -129,24 +176,66 @@ __device__ __forceinline__ uint64_t seg_fe_sum(uint64_t v) {
     return v;
 }
 
+// The sequential PrgStream with FE::from_rng redraws (field.rs:252-264) for one key, one lane:
+// the path of a key whose parallel draws hit a value >= p (P ~ 2^-32 per draw) and of the
+// force_sequential tests. Out of line so its registers do not weigh on the parallel loop.
+template <class Tab>
+__device__ __noinline__ void sketch_sequential_otf(const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                                   const uint32_t (&seed)[4], const uint64_t* x, const uint64_t* kx,
+                                                   uint64_t F, uint64_t* o) {
+    const uint64_t mask = (1ull << 62) - 1;
+    uint64_t pos = 0, cur_b = ~0ull, d[2] = {0, 0};
+    auto draw = [&]() -> uint64_t {
+        for (;;) {
+            const uint64_t b = pos >> 1;
+            if (b != cur_b) {
+                ks_block_otf<Tab>(b, tbl, b0, b1, seed, d[0], d[1]);
+                cur_b = b;
+            }
+            const uint64_t v = d[pos & 1] & mask;
+            pos++;
+            if (v < kFeP_) return v;
+        }
+    };
+    const uint64_t q1 = draw(), q2 = draw(), q3 = draw();
+    uint64_t sx = 0, s2x = 0, skx = 0;
+    for (uint64_t j = 0; j < F; j++) {
+        const uint64_t r = draw();
+        const uint64_t r2 = fe_mulc(r, r);
+        const uint64_t xv = fe_canon_dev(x[j]), kxv = fe_canon_dev(kx[j]);
+        sx = fe_addc(sx, fe_mulc(xv, r));
+        s2x = fe_addc(s2x, fe_mulc(xv, r2));
+        skx = fe_addc(skx, fe_mulc(kxv, r));
+    }
+    o[0] = sx;
+    o[1] = s2x;
+    o[2] = skx;
+    o[3] = q1;
+    o[4] = q2;
+    o[5] = q3;
+}
+
 // KPW keys per wave, LPK = 64 / KPW lanes per key: lane l of a key's segment produces keystream
 // blocks l, l + LPK, ... two per pass in lockstep, with the pass's (x, kx) loads issued first.
-// The key schedule is per lane (each segment has its own key).
-template <int KPW>
-__global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
+// The key differs per segment, so the schedule is per lane: OTF = false keeps all 11 round keys
+// in VGPRs (r01: T0 + rotations, 256 threads, 157 VGPRs, 3 waves/SIMD); OTF = true expands it on
+// the fly per pass (4 extra lookups per round, shared by the pass's two blocks), which with the
+// four-table LDS layout (one v_perm per lookup) fits 1024 threads x <= 128 VGPRs.
+template <int KPW, class Tab = SkTab, int THR = kSketchThreads, bool OTF = false, int NBP = 2>
+__global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
     constexpr int LPK = 64 / KPW;
-    __shared__ uint32_t tbl[SkTab::kWords];
-    for (int i = threadIdx.x; i < SkTab::kWords; i += kSketchThreads) tbl[i] = SkTab::word(c_T0_sk.v, i);
+    __shared__ uint32_t tbl[Tab::kWords];
+    for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0_sk.v, i);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t seg = lane / LPK, sl = lane % LPK;
     uint32_t b0, b1;
-    SkTab::bases(lane, b0, b1);
+    Tab::bases(lane, b0, b1);
     const uint64_t mask = (1ull << 62) - 1;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kSketchThreads / 64);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (THR / 64);
     const uint64_t F = a.n_nodes;
     const uint64_t nb = (F + 3 + 1) / 2;   // draws 0..F+2
-    const uint64_t wave = (uint64_t)blockIdx.x * (kSketchThreads / 64) + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (THR / 64) + (threadIdx.x >> 6);
     for (uint64_t kbase = wave * KPW; kbase < a.n_keys; kbase += nwaves * KPW) {
         const uint64_t k = kbase + seg;
         const bool kact = k < a.n_keys;
@@ -155,45 +244,63 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
         seed[3] ^= a.level;   // the level's stream (bytes 12..15; level 0 = the seed itself)
-        uint32_t rk[11][4];
-        key_schedule(seed, rk, tbl, lane & 31);
+        uint32_t rk[OTF ? 1 : 11][4];
+        if constexpr (!OTF) key_schedule(seed, rk, tbl, lane & 31);
         const uint64_t* x = a.x + kk * F;
         const uint64_t* kx = a.kx + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
         bool rej = false;
         if (!a.force_sequential) {
-            for (uint64_t bb = sl; bb < nb; bb += 2 * LPK) {
-                uint64_t xv[4] = {0, 0, 0, 0}, kxv[4] = {0, 0, 0, 0};
+            for (uint64_t bb = sl; bb < nb; bb += NBP * LPK) {
+                // the pass's (x, kx) loads go ahead of the AES at 2 blocks per pass; at 4 their 32
+                // registers would be live across it, so they follow it (other waves hide the latency)
+                uint64_t xv[2 * NBP] = {}, kxv[2 * NBP] = {};
+                auto load_xkx = [&]() {
 #pragma unroll
-                for (int q = 0; q < 2; q++)
+                    for (int q = 0; q < NBP; q++)
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const uint64_t pos = 2 * (bb + LPK * q) + h;
-                        if (pos >= 3 && pos < F + 3) {
-                            xv[2 * q + h] = x[pos - 3];
-                            kxv[2 * q + h] = kx[pos - 3];
+                        for (int h = 0; h < 2; h++) {
+                            const uint64_t pos = 2 * (bb + LPK * q) + h;
+                            if (pos >= 3 && pos < F + 3) {
+                                xv[2 * q + h] = x[pos - 3];
+                                kxv[2 * q + h] = kx[pos - 3];
+                            }
                         }
-                    }
-                uint32_t st[2][4];
+                };
+                if constexpr (NBP <= 2) load_xkx();
+                uint32_t st[NBP][4];
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
+                for (int q = 0; q < NBP; q++) {
                     const uint64_t b = bb + LPK * q;
                     st[q][0] = 0u;
                     st[q][1] = 0u;
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
                     st[q][3] = __builtin_bswap32((uint32_t)b);
                 }
-                aes_rk<SkTab, 2>(st, tbl, b0, b1, rk);
+                if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
+                else aes_rk<Tab, NBP>(st, tbl, b0, b1, rk);
+                if constexpr (NBP > 2) load_xkx();
+                unsigned __int128 ax = rx, a2x = r2x, akx = rkx;
 #pragma unroll
-                for (int q = 0; q < 2; q++) {
+                for (int q = 0; q < NBP; q++) {
                     const uint64_t b = bb + LPK * q;
                     if (b >= nb) break;
                     const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
                                             (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
 #pragma unroll
-                    for (int h = 0; h < 2; h++)
-                        sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1, rx,
-                                    r2x, rkx);
+                    for (int h = 0; h < 2; h++) {
+                        if constexpr (OTF)
+                            sketch_draw_lazy(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0,
+                                             rnd1, ax, a2x, akx);
+                        else
+                            sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
+                                        rx, r2x, rkx);
+                    }
+                }
+                if constexpr (OTF) {
+                    rx = fe_red128(ax);
+                    r2x = fe_red128(a2x);
+                    rkx = fe_red128(akx);
                 }
             }
         }
@@ -215,6 +322,8 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
             o[3] = rand1;
             o[4] = rand2;
             o[5] = rand3;
+        } else if (kact && key_rej && sl == 0 && OTF) {
+            sketch_sequential_otf<Tab>(tbl, b0, b1, seed, x, kx, F, a.out + 6 * k);
         } else if (kact && key_rej && sl == 0) {
             // sequential PrgStream with FE::from_rng redraws (field.rs:252-264) for this key
             uint64_t pos = 0, cur_b = ~0ull, d[2] = {0, 0};
@@ -222,7 +331,7 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
                 for (;;) {
                     const uint64_t b = pos >> 1;
                     if (b != cur_b) {
-                        ks_block(b, tbl, b0, b1, rk, d[0], d[1]);
+                        if constexpr (!OTF) ks_block(b, tbl, b0, b1, rk, d[0], d[1]);
                         cur_b = b;
                     }
                     const uint64_t v = d[pos & 1] & mask;
@@ -252,21 +361,44 @@ __global__ __launch_bounds__(kSketchThreads) void k_sketch_fe(SketchArgs a) {
 }
 
 constexpr int kSketchKeysPerWave = 4;
+// default form: 8 keys per wave (8 lanes per key: at 256 nodes 130 blocks fill 9 passes of 16
+// slots, 90 % of the slots), four-table LDS layout, 1024 threads, schedule on the fly
+constexpr int kSketchKpwOtf = 8;
+constexpr int kSketchThreadsOtf = 1024;
+constexpr int kSketchNbpOtf = 2;   // 4 blocks per pass (16 keys per wave) spills at 128 VGPRs: 0.88 vs 0.66 ms/level
+using SkTab4 = Tab4T32<DevOpsX>;
 
-hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
-    if (a.n_keys == 0) return hipSuccess;
+template <class K>
+static hipError_t launch_sketch_kernel(K kern, int thr, int kpw, const SketchArgs& a, hipStream_t stream) {
     int cus = 256, dev = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* fn = reinterpret_cast<const void*>(&k_sketch_fe<kSketchKeysPerWave>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kSketchThreads, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), thr, 0) !=
+            hipSuccess || per_cu < 1)
         per_cu = 1;
-    const uint64_t waves_needed = (a.n_keys + kSketchKeysPerWave - 1) / kSketchKeysPerWave;
-    uint64_t blocks = (waves_needed + 3) / 4;
+    const uint64_t wpb = thr / 64;
+    const uint64_t waves_needed = (a.n_keys + kpw - 1) / kpw;
+    uint64_t blocks = (waves_needed + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)cus * per_cu;   // one resident wave set; keys are strided over it
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL(k_sketch_fe<kSketchKeysPerWave>, dim3((unsigned)blocks), dim3(kSketchThreads), 0, stream, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(thr), 0, stream, a);
     return hipGetLastError();
+}
+
+// impl (fhh_sketch_set_impl): 0 = default (on-the-fly schedule, 1024 threads), 1 = the r01 kernel
+static int g_sketch_impl = 0;
+extern "C" int fhh_sketch_set_impl(int impl) {
+    if (impl < 0 || impl > 1) return FHH_E_ARG;
+    g_sketch_impl = impl;
+    return FHH_OK;
+}
+
+hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
+    if (a.n_keys == 0) return hipSuccess;
+    if (g_sketch_impl == 1)
+        return launch_sketch_kernel(k_sketch_fe<kSketchKeysPerWave>, kSketchThreads, kSketchKeysPerWave, a, stream);
+    return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, true, kSketchNbpOtf>,
+                                kSketchThreadsOtf, kSketchKpwOtf, a, stream);
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

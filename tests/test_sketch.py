@@ -109,10 +109,19 @@ def test_split_steps_equal_fused(oracle):
 
 
 # ---- HIP path (through the C ABI) against the oracle -----------------------------------------
+@pytest.fixture(params=[0, 1], ids=["otf-1024", "r01-256"])
+def sketch_impl(request):
+    """both k_sketch_fe forms (fhh_sketch_set_impl): on-the-fly schedule (default) and r01's"""
+    from fuzzyheavyhitters_amd import lib
+    assert lib().fhh_sketch_set_impl(request.param) == 0
+    yield request.param
+    lib().fhh_sketch_set_impl(0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_keys,n_nodes", [(1, 0), (3, 1), (5, 2), (70, 63), (64, 64), (130, 125), (257, 300),
-                                            (2000, 40)])
-def test_gpu_sketch_at_bit_exact(oracle, n_keys, n_nodes):
+                                            (2000, 40), (1001, 256)])
+def test_gpu_sketch_at_bit_exact(oracle, n_keys, n_nodes, sketch_impl):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S
     wl = S.sketch_workload(n_keys, n_nodes, seed=n_keys * 7 + n_nodes, bad_fraction=0.1)
@@ -143,7 +152,7 @@ def test_gpu_mul_steps_bit_exact(oracle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("force_sequential", [False, True], ids=["parallel", "sequential-stream"])
-def test_gpu_sim_sketch_verify(oracle, force_sequential):
+def test_gpu_sim_sketch_verify(oracle, force_sequential, sketch_impl):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S
     wl = S.sketch_workload(3000, 77, seed=99, bad_fraction=0.1)

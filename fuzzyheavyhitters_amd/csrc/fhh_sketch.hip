@@ -148,18 +148,18 @@ __device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint6
                                                  int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1,
                                                  unsigned __int128& ax, unsigned __int128& a2x,
                                                  unsigned __int128& akx) {
-    if (pos < 3) {
-        rej |= v >= kFeP_;
-        if (h == 0) rnd0 = v;
-        else rnd1 = v;
-    } else if (pos < F + 3) {
-        rej |= v >= kFeP_;
-        const uint64_t r2 = fe_mulc(v, v);
-        xv = fe_canon_dev(xv);
-        ax += (unsigned __int128)xv * v;
-        a2x += (unsigned __int128)xv * r2;
-        akx += (unsigned __int128)fe_canon_dev(kxv) * v;
-    }
+    // branch-free (pos depends on the lane): out-of-range positions carry x = kx = 0 (the loads
+    // are skipped), so their products vanish; a divergent branch here would keep the compiler from
+    // interleaving the pass's four independent draws
+    const bool is_rand = pos < 3, live = pos < F + 3;
+    rej |= live && v >= kFeP_;
+    rnd0 = (is_rand && h == 0) ? v : rnd0;
+    rnd1 = (is_rand && h == 1) ? v : rnd1;
+    const uint64_t r2 = fe_mulc(v, v);
+    xv = fe_canon_dev(xv);
+    ax += (unsigned __int128)xv * v;
+    a2x += (unsigned __int128)xv * r2;
+    akx += (unsigned __int128)fe_canon_dev(kxv) * v;
 }
 
 __device__ __forceinline__ uint64_t wave_fe_sum(uint64_t v) {
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
 #pragma unroll
                 for (int q = 0; q < NBP; q++) {
                     const uint64_t b = bb + LPK * q;
-                    if (b >= nb) break;
+                    if (!OTF && b >= nb) break;   // OTF: positions past the stream are no-ops
                     const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
                                             (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
 #pragma unroll

@@ -11,6 +11,9 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfhh.so")
+# same-box A/B of two builds (tools/ab_builds.sh): load another copy of the library instead
+if os.environ.get("FHH_LIB_PATH"):
+    LIB_PATH = os.environ["FHH_LIB_PATH"]
 _CSRC = os.path.join(_HERE, "csrc")
 _LIB = None
 

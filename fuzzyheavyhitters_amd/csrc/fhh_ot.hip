@@ -52,9 +52,11 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
 // c = c0 + 64 q + l, q < kOtSlices, in lockstep (2 kOtSlices blocks for the receiver's two keys,
 // kOtSlices for the sender). nblk = mp / 128 is a multiple of 64, so a slice is wholly inside or
 // outside the row and the row's key schedules are uniform (scalar loads)
-constexpr int kOtSlices = 2;
+// slices per wave: the receiver runs 2 keys x 2 slices, the sender 1 key x 4 slices — 4 blocks per
+// lane in lockstep either way (the sender at 2 had half the lookups in flight)
 template <bool RECV>
 __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
+    constexpr int kOtSlices = RECV ? 2 : 4;
     extern __shared__ uint32_t tbl_ot[];
     ot_fill(tbl_ot);
     uint32_t b0, b1;
@@ -276,7 +278,7 @@ hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
     static int done = 0;
     hipError_t e = ot_set_lds((const void*)k_ot_expand<true>, &done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / kOtSlices, kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 2, kOtThreads)), dim3(kOtThreads), kOtLds,
                        stream, a);
     return hipGetLastError();
 }
@@ -285,7 +287,7 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
     static int done = 0;
     hipError_t e = ot_set_lds((const void*)k_ot_expand<false>, &done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / kOtSlices, kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), kOtLds,
                        stream, a);
     return hipGetLastError();
 }

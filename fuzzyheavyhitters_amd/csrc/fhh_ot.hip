@@ -49,14 +49,15 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
 }
 
 // one wave per (row i, kOtSlices consecutive 64-block slices): lane l computes blocks
-// c = c0 + 64 q + l, q < kOtSlices, in lockstep (2 kOtSlices blocks for the receiver's two keys,
-// kOtSlices for the sender). nblk = mp / 128 is a multiple of 64, so a slice is wholly inside or
-// outside the row and the row's key schedules are uniform (scalar loads)
-// slices per wave: the receiver runs 2 keys x 2 slices, the sender 1 key x 4 slices — 4 blocks per
-// lane in lockstep either way (the sender at 2 had half the lookups in flight)
+// c = c0 + 64 q + l, q < kOtSlices, in lockstep. nblk = mp / 128 is a multiple of 64, so a slice
+// is wholly inside or outside the row and the row's key schedules are uniform (scalar loads)
 template <bool RECV>
 __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
-    constexpr int kOtSlices = RECV ? 2 : 4;
+    // 4 slices per wave (4 blocks per lane in lockstep). The receiver runs its two row keys one
+    // after the other over the same 4 blocks (T = G(k0) is stored, U = T ^ G(k1) ^ r): only one
+    // 44-word schedule is live in SGPRs at a time (both at once spilled it into VGPRs: 128 VGPRs
+    // plus scratch)
+    constexpr int kOtSlices = 4;
     extern __shared__ uint32_t tbl_ot[];
     ot_fill(tbl_ot);
     uint32_t b0, b1;
@@ -64,51 +65,56 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     OtTab::bases(lane, b0, b1);
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
-    const uint64_t tiles_per_row = (nblk + 64 * kOtSlices - 1) / (64 * kOtSlices);
+    // the active tiles (rows x 64 kOtSlices blocks) in contiguous runs per wave: consecutive tiles
+    // of a wave share a row, so its key schedules (scalar loads, re-issued per tile to keep the
+    // SGPR budget) hit the scalar cache instead of going to L2 as grid-strided tiles did
+    const uint64_t tiles_per_row = (nblk_act + 64 * kOtSlices - 1) / (64 * kOtSlices);
     const uint64_t tiles = 128 * tiles_per_row;
     const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
-    for (uint64_t t = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6); t < tiles; t += nwaves) {
+    const uint64_t wave = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6);
+    const uint64_t run = (tiles + nwaves - 1) / nwaves;
+    const uint64_t t_end = min(tiles, (wave + 1) * run);
+    for (uint64_t t = wave * run; t < t_end; t++) {
         const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_row));
         const uint64_t c0 = (t - (uint64_t)i * tiles_per_row) * 64 * kOtSlices;
         if (c0 >= nblk_act) continue;   // wave-uniform
-        if (RECV) {
-            uint32_t rk0[11][4], rk1[11][4];
-            ld_rk(a.rk + (size_t)i * 44, rk0);
-            ld_rk(a.rk + (size_t)(128 + i) * 44, rk1);
-            uint32_t g[2 * kOtSlices][4];
+        uint32_t g[kOtSlices][4];
 #pragma unroll
-            for (int q = 0; q < 2 * kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * (q % kOtSlices) + lane;
-                g[q][0] = (uint32_t)c;
-                g[q][1] = (uint32_t)(c >> 32);
-                g[q][2] = 0u;
-                g[q][3] = 0u;
+        for (int q = 0; q < kOtSlices; q++) {
+            const uint64_t c = c0 + 64 * q + lane;
+            g[q][0] = (uint32_t)c;
+            g[q][1] = (uint32_t)(c >> 32);
+            g[q][2] = 0u;
+            g[q][3] = 0u;
+        }
+        {
+            uint32_t rk[11][4];
+            ld_rk(a.rk + (size_t)(RECV ? i : 256 + i) * 44, rk);
+            aes_rk<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rk);   // G(k_i^0) (receiver) / G(k_i^{s_i})
+        }
+        if (RECV) {
+            uint32_t g1[kOtSlices][4];
+#pragma unroll
+            for (int q = 0; q < kOtSlices; q++) {
+                const uint64_t c = c0 + 64 * q + lane;
+                if (c0 + 64 * q < nblk_act) a.T[(uint64_t)i * nblk + c] = make_uint4(g[q][0], g[q][1], g[q][2], g[q][3]);
+                g1[q][0] = (uint32_t)c;
+                g1[q][1] = (uint32_t)(c >> 32);
+                g1[q][2] = 0u;
+                g1[q][3] = 0u;
             }
-            aes_rk2<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rk0, rk1);
+            uint32_t rk[11][4];
+            ld_rk(a.rk + (size_t)(128 + i) * 44, rk);
+            aes_rk<OtTab, kOtSlices>(g1, tbl_ot, b0, b1, rk);   // G(k_i^1)
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
                 const uint64_t c = c0 + 64 * q + lane;
                 if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
                 const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
-                const uint32_t* x0 = g[q];
-                const uint32_t* x1 = g[kOtSlices + q];
-                a.T[(uint64_t)i * nblk + c] = make_uint4(x0[0], x0[1], x0[2], x0[3]);
-                a.U[(uint64_t)i * nblk + c] = make_uint4(x0[0] ^ x1[0] ^ r.x, x0[1] ^ x1[1] ^ r.y,
-                                                         x0[2] ^ x1[2] ^ r.z, x0[3] ^ x1[3] ^ r.w);
+                a.U[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ g1[q][0] ^ r.x, g[q][1] ^ g1[q][1] ^ r.y,
+                                                         g[q][2] ^ g1[q][2] ^ r.z, g[q][3] ^ g1[q][3] ^ r.w);
             }
         } else {
-            uint32_t rks[11][4];
-            ld_rk(a.rk + (size_t)(256 + i) * 44, rks);
-            uint32_t g[kOtSlices][4];
-#pragma unroll
-            for (int q = 0; q < kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * q + lane;
-                g[q][0] = (uint32_t)c;
-                g[q][1] = (uint32_t)(c >> 32);
-                g[q][2] = 0u;
-                g[q][3] = 0u;
-            }
-            aes_rk<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rks);
             const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
@@ -170,15 +176,31 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
     const uint64_t m = ot_active(a);
-    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
-        const uint4 q = a.Qt[j];
-        uint32_t h[2][4] = {{q.x, q.y, q.z, q.w}, {q.x ^ a.s[0], q.y ^ a.s[1], q.z ^ a.s[2], q.w ^ a.s[3]}};
-        aes0_mmo_tab<DevOpsX, OtTab, 2>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
-        const uint4 x0 = a.x0[j];
-        const uint4 x1 = a.x1 ? a.x1[j]
-                              : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
-        a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
-        a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
+    const uint64_t G = (uint64_t)gridDim.x * kOtThreads;
+    // two OTs per lane per pass (OTs j and j + G: coalesced either way), 4 blocks in lockstep
+    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += 2 * G) {
+        uint32_t h[4][4];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t jj = j + u * G;
+            const uint4 q = jj < m ? a.Qt[jj] : make_uint4(0, 0, 0, 0);
+            h[2 * u][0] = q.x; h[2 * u][1] = q.y; h[2 * u][2] = q.z; h[2 * u][3] = q.w;
+            h[2 * u + 1][0] = q.x ^ a.s[0]; h[2 * u + 1][1] = q.y ^ a.s[1];
+            h[2 * u + 1][2] = q.z ^ a.s[2]; h[2 * u + 1][3] = q.w ^ a.s[3];
+        }
+        aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t jj = j + u * G;
+            if (jj >= m) break;
+            const uint4 x0 = a.x0[jj];
+            const uint4 x1 = a.x1 ? a.x1[jj]
+                                  : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+            const uint32_t* h0 = h[2 * u];
+            const uint32_t* h1 = h[2 * u + 1];
+            a.Y0[jj] = make_uint4(x0.x ^ h0[0], x0.y ^ h0[1], x0.z ^ h0[2], x0.w ^ h0[3]);
+            a.Y1[jj] = make_uint4(x1.x ^ h1[0], x1.y ^ h1[1], x1.z ^ h1[2], x1.w ^ h1[3]);
+        }
     }
 }
 
@@ -188,13 +210,26 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
     const uint64_t m = ot_active(a);
-    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += (uint64_t)gridDim.x * kOtThreads) {
-        const uint4 t = a.Tt[j];
-        uint32_t h[1][4] = {{t.x, t.y, t.z, t.w}};
-        aes0_mmo_tab<DevOpsX, OtTab, 1>(h, tbl_ot, b0, b1);
-        const uint32_t r = (a.choices[j >> 5] >> (j & 31)) & 1u;
-        const uint4 y = r ? a.Y1[j] : a.Y0[j];
-        a.out[j] = make_uint4(y.x ^ h[0][0], y.y ^ h[0][1], y.z ^ h[0][2], y.w ^ h[0][3]);
+    const uint64_t G = (uint64_t)gridDim.x * kOtThreads;
+    // four OTs per lane per pass (j + u G), 4 blocks in lockstep (one block per lane starved the
+    // LDS pipe: 70 G blocks/s)
+    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += 4 * G) {
+        uint32_t h[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t jj = j + u * G;
+            const uint4 t = jj < m ? a.Tt[jj] : make_uint4(0, 0, 0, 0);
+            h[u][0] = t.x; h[u][1] = t.y; h[u][2] = t.z; h[u][3] = t.w;
+        }
+        aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t jj = j + u * G;
+            if (jj >= m) break;
+            const uint32_t r = (a.choices[jj >> 5] >> (jj & 31)) & 1u;
+            const uint4 y = r ? a.Y1[jj] : a.Y0[jj];
+            a.out[jj] = make_uint4(y.x ^ h[u][0], y.y ^ h[u][1], y.z ^ h[u][2], y.w ^ h[u][3]);
+        }
     }
 }
 
@@ -278,7 +313,7 @@ hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
     static int done = 0;
     hipError_t e = ot_set_lds((const void*)k_ot_expand<true>, &done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 2, kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), kOtLds,
                        stream, a);
     return hipGetLastError();
 }

@@ -111,3 +111,37 @@ def test_configs0_gpu_equals_oracle(oracle):
     assert_probe_equal(res, ores.level_states)
     st = c0.stats()
     assert st["aes_blocks"] * 2 == ores.aes_blocks
+
+
+@pytest.mark.parametrize("thr_frac,levels", [(0.075, [0, 5, 9, 13]), (0.01, [0, 7, 14, 15])],
+                         ids=["config-threshold", "deep"])
+def test_configs3_sampled_states_bit_exact(oracle, thr_frac, levels):
+    """configs[3] at its full size (src/bin/config.json: 1M clients, d = 2 lat/lon, data_len 16,
+    ball 1, threshold 0.075 — the synthetic centroids keep no node past level 13 there, so a
+    0.01 run crawls to the leaves too): the d = 2 path (dim-prefix dedup, per-dim entry tables, a
+    node = a pair of entries) at 1M clients. The probe reads every child's per-dim states for a
+    client in every 8th word at four non-empty levels and the oracle replays them; the counts of
+    every level equal the plaintext recount."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 1_000_000, 16
+    wl = workload.coords_workload(n, ball_size=1, seed=0x5EED)
+    c0, c1 = fhh.KeyCollection(L, 2), fhh.KeyCollection(L, 2)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    clients = sample_clients(n, 8)
+    res = fhh.sim_crawl(c0, c1, thr_frac, mode="count",
+                        probe={"levels": levels, "clients": clients, "capacity": 4096})
+    thr = max(1, int(thr_frac * n))
+    keeps = keeps_from_counts(res, thr, thr)
+    sel = clients.astype(np.int64)
+    k0, k1 = oracle.gen_keys(wl.left[sel], wl.right[sel], wl.root_seeds[sel])
+    ref = oracle.replay_states(k0, k1, keeps, levels)
+    assert set(res.probe) == set(levels)
+    assert all(int(res.level_children[lv]) > 0 for lv in levels)
+    assert_probe_equal(res, ref)
+    cnt, paths, _ = workload.plaintext_crawl(wl.left, wl.right, thr, thr)
+    assert [len(c) for c in cnt] == [int(x) for x in res.level_children]
+    assert all(np.array_equal(a, np.asarray(b)) for a, b in zip(cnt, res.counts))
+    got = sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in res.final)
+    assert got == sorted(paths)
+    print("configs[3] children per level:", [int(x) for x in res.level_children], "heavy hitters:", len(got))

@@ -25,7 +25,6 @@ namespace fhh {
 __constant__ WordTable c_T0_gc = T0;
 using GcTab = Tab4T32<DevOpsX>;
 constexpr int kGcThreads = 1024;
-constexpr size_t kGcLds = (size_t)GcTab::kWords * 4;
 
 __device__ __forceinline__ void gc_fill(uint32_t* tbl) {
     for (int i = threadIdx.x; i < GcTab::kWords; i += blockDim.x) tbl[i] = GcTab::word(c_T0_gc.v, i);
@@ -90,7 +89,7 @@ __device__ __forceinline__ void ld_blk(const uint4* base, uint64_t row, uint64_t
 
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
-    extern __shared__ uint32_t tbl_gc[];
+    __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
     gc_fill(tbl_gc);
     uint32_t b0, b1;
     GcTab::bases(threadIdx.x & 63, b0, b1);
@@ -188,7 +187,7 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x) {
 // each bit twice, collect.rs:868) — no separate byte-to-bit pass.
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
-    extern __shared__ uint32_t tbl_gc[];
+    __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
     gc_fill(tbl_gc);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;
@@ -253,13 +252,6 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
 
 template <int B>
 static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
-    const void* fn = garble ? (const void*)k_gc_garble<B> : (const void*)k_gc_eval<B>;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[garble]) {
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGcLds);
-        if (e != hipSuccess) return e;
-        attr_set[garble] = true;
-    }
     int dev = 0, cus = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -268,8 +260,8 @@ static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     const uint64_t n = a.G * a.N;
     const uint64_t need = (n + kGcThreads - 1) / kGcThreads;
     const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
-    if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), kGcLds, stream, a);
-    else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), kGcLds, stream, a);
+    if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
     return hipGetLastError();
 }
 

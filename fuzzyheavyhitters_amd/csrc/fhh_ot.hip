@@ -26,7 +26,6 @@ namespace fhh {
 __constant__ WordTable c_T0_ot = T0;
 using OtTab = Tab4T32<DevOpsX>;
 constexpr int kOtThreads = 1024;
-constexpr size_t kOtLds = (size_t)OtTab::kWords * 4;
 
 __device__ __forceinline__ void ot_fill(uint32_t* tbl) {
     for (int i = threadIdx.x; i < OtTab::kWords; i += blockDim.x) tbl[i] = OtTab::word(c_T0_ot.v, i);
@@ -58,7 +57,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     // 44-word schedule is live in SGPRs at a time (both at once spilled it into VGPRs: 128 VGPRs
     // plus scratch)
     constexpr int kOtSlices = 4;
-    extern __shared__ uint32_t tbl_ot[];
+    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
     ot_fill(tbl_ot);
     uint32_t b0, b1;
     const uint32_t lane = threadIdx.x & 63;
@@ -171,7 +170,7 @@ __global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint
 }
 
 __global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
-    extern __shared__ uint32_t tbl_ot[];
+    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
     ot_fill(tbl_ot);
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
@@ -205,7 +204,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
 }
 
 __global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
-    extern __shared__ uint32_t tbl_ot[];
+    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
     ot_fill(tbl_ot);
     uint32_t b0, b1;
     OtTab::bases(threadIdx.x & 63, b0, b1);
@@ -282,13 +281,6 @@ hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, con
     return hipGetLastError();
 }
 
-static hipError_t ot_set_lds(const void* fn, int* done) {
-    if (*done) return hipSuccess;
-    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOtLds);
-    if (e == hipSuccess) *done = 1;
-    return e;
-}
-
 // CU count of the current device, queried once per device (the level loop launches these
 // kernels thousands of times per crawl)
 static int device_cus() {
@@ -310,19 +302,13 @@ static int ot_grid(uint64_t items, int threads) {
 }
 
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
-    static int done = 0;
-    hipError_t e = ot_set_lds((const void*)k_ot_expand<true>, &done);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
                        stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
-    static int done = 0;
-    hipError_t e = ot_set_lds((const void*)k_ot_expand<false>, &done);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), kOtLds,
+    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
                        stream, a);
     return hipGetLastError();
 }
@@ -345,18 +331,12 @@ hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream) {
 }
 
 hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream) {
-    static int done = 0;
-    hipError_t e = ot_set_lds((const void*)k_ot_send_hash, &done);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_send_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), kOtLds, stream, a);
+    hipLaunchKernelGGL(k_ot_send_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream) {
-    static int done = 0;
-    hipError_t e = ot_set_lds((const void*)k_ot_recv_hash, &done);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_ot_recv_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), kOtLds, stream, a);
+    hipLaunchKernelGGL(k_ot_recv_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), 0, stream, a);
     return hipGetLastError();
 }
 

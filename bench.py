@@ -285,7 +285,8 @@ def main():
                          "overlapped with the crawl) instead of ideal ones")
     ap.add_argument("--sketch-keys", type=int, default=100_000, help="configs[4] sketch_batch_size (per GPU)")
     ap.add_argument("--sketch-impl", type=int, default=0,
-                    help="k_sketch_fe form: 0 = on-the-fly schedule / 1024 threads (default), 1 = r01 kernel")
+                    help="k_sketch_fe form: 0 = round keys in LDS / 1024 threads (default), 1 = r01 kernel, "
+                         "2 = round keys expanded on the fly")
     ap.add_argument("--sketch-nodes", type=int, default=256, help="frontier nodes per sketched vector")
     ap.add_argument("--sketch-levels", type=int, default=1024,
                     help="configs[4]: data_len levels verified per step (L-1 over FE, the last over FieldElm)")

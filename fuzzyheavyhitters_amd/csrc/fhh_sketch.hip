@@ -221,10 +221,15 @@ __device__ __noinline__ void sketch_sequential_otf(const uint32_t* tbl, uint32_t
 // in VGPRs (r01: T0 + rotations, 256 threads, 157 VGPRs, 3 waves/SIMD); OTF = true expands it on
 // the fly per pass (4 extra lookups per round, shared by the pass's two blocks), which with the
 // four-table LDS layout (one v_perm per lookup) fits 1024 threads x <= 128 VGPRs.
-template <int KPW, class Tab = SkTab, int THR = kSketchThreads, bool OTF = false, int NBP = 2>
+// SCHED 2: the schedule is computed once per key (every lane of the segment, through the tables)
+// and kept in LDS beside the tables (16 waves x KPW keys x 176 B = 22.5 KiB at KPW 8); a round
+// reads it with one broadcast ds_read_b128 instead of 4 lookups + the SubWord chain per pass.
+template <int KPW, class Tab = SkTab, int THR = kSketchThreads, int SCHED = 0, int NBP = 2>
 __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
+    constexpr bool OTF = SCHED >= 1;   // lazy sums, out-of-line fallback, key expanded through Tab
     constexpr int LPK = 64 / KPW;
     __shared__ uint32_t tbl[Tab::kWords];
+    __shared__ uint4 rks_lds[SCHED == 2 ? THR / 64 : 1][SCHED == 2 ? KPW : 1][11];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0_sk.v, i);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -246,6 +251,19 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
         seed[3] ^= a.level;   // the level's stream (bytes 12..15; level 0 = the seed itself)
         uint32_t rk[OTF ? 1 : 11][4];
         if constexpr (!OTF) key_schedule(seed, rk, tbl, lane & 31);
+        const uint4* rkl = rks_lds[SCHED == 2 ? (threadIdx.x >> 6) : 0][SCHED == 2 ? seg : 0];
+        if constexpr (SCHED == 2) {
+            uint32_t full[11][4];
+            key_schedule_tab<Tab>(seed, full, tbl, b0, b1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the previous key's reads are done
+            if (sl == 0) {
+                uint4* w = rks_lds[threadIdx.x >> 6][seg];
+#pragma unroll
+                for (int r = 0; r < 11; r++) w[r] = make_uint4(full[r][0], full[r][1], full[r][2], full[r][3]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
         const uint64_t* x = a.x + kk * F;
         const uint64_t* kx = a.kx + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
@@ -277,7 +295,8 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
                     st[q][3] = __builtin_bswap32((uint32_t)b);
                 }
-                if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
+                if constexpr (SCHED == 2) aes_lds_rk<Tab, NBP>(st, tbl, b0, b1, rkl);
+                else if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
                 else aes_rk<Tab, NBP>(st, tbl, b0, b1, rk);
                 if constexpr (NBP > 2) load_xkx();
                 unsigned __int128 ax = rx, a2x = r2x, akx = rkx;
@@ -362,7 +381,7 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
 
 constexpr int kSketchKeysPerWave = 4;
 // default form: 8 keys per wave (8 lanes per key: at 256 nodes 130 blocks fill 9 passes of 16
-// slots, 90 % of the slots), four-table LDS layout, 1024 threads, schedule on the fly
+// slots, 90 % of the slots), four-table LDS layout, 1024 threads, round keys in LDS
 constexpr int kSketchKpwOtf = 8;
 constexpr int kSketchThreadsOtf = 1024;
 constexpr int kSketchNbpOtf = 2;   // 4 blocks per pass (16 keys per wave) spills at 128 VGPRs: 0.88 vs 0.66 ms/level
@@ -385,10 +404,11 @@ static hipError_t launch_sketch_kernel(K kern, int thr, int kpw, const SketchArg
     return hipGetLastError();
 }
 
-// impl (fhh_sketch_set_impl): 0 = default (on-the-fly schedule, 1024 threads), 1 = the r01 kernel
+// impl (fhh_sketch_set_impl): 0 = default (schedule once per key in LDS, 1024 threads), 1 = the
+// r01 kernel, 2 = the schedule expanded on the fly per pass (1.8 % slower than 0)
 static int g_sketch_impl = 0;
 extern "C" int fhh_sketch_set_impl(int impl) {
-    if (impl < 0 || impl > 1) return FHH_E_ARG;
+    if (impl < 0 || impl > 2) return FHH_E_ARG;
     g_sketch_impl = impl;
     return FHH_OK;
 }
@@ -397,7 +417,10 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     if (a.n_keys == 0) return hipSuccess;
     if (g_sketch_impl == 1)
         return launch_sketch_kernel(k_sketch_fe<kSketchKeysPerWave>, kSketchThreads, kSketchKeysPerWave, a, stream);
-    return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, true, kSketchNbpOtf>,
+    if (g_sketch_impl == 2)
+        return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, 1, kSketchNbpOtf>,
+                                    kSketchThreadsOtf, kSketchKpwOtf, a, stream);
+    return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, 2, kSketchNbpOtf>,
                                 kSketchThreadsOtf, kSketchKpwOtf, a, stream);
 }
 

@@ -319,9 +319,10 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* batch);
  * reference draws thread_rng). */
 int fhh_deal_triples_fe(fhh_ctx* ctx, uint64_t n, uint32_t levels, uint64_t seed, uint64_t* triples0_dev,
                         uint64_t* triples1_dev);
-/* k_sketch_fe implementation for A/B (process-wide): 0 = default (round keys expanded on the fly,
- * four-table LDS layout, 1024 threads), 1 = the r01 kernel (stored schedule, 256 threads). Both
- * are bit-identical; FHH_E_ARG for any other value. */
+/* k_sketch_fe implementation for A/B (process-wide): 0 = default (four-table LDS layout, 1024
+ * threads, each key's round keys computed once into LDS), 1 = the r01 kernel (schedule in
+ * registers, 256 threads), 2 = as 0 with the round keys expanded on the fly per pass. All are
+ * bit-identical; FHH_E_ARG for any other value. */
 int fhh_sketch_set_impl(int impl);
 
 /* ---- the last level, U = FieldElm (sketch_at_last, sketch.rs:202-245; MulState<FieldElm>) ----

@@ -109,9 +109,9 @@ def test_split_steps_equal_fused(oracle):
 
 
 # ---- HIP path (through the C ABI) against the oracle -----------------------------------------
-@pytest.fixture(params=[0, 1], ids=["otf-1024", "r01-256"])
+@pytest.fixture(params=[0, 1, 2], ids=["lds-sched", "r01-256", "otf-1024"])
 def sketch_impl(request):
-    """both k_sketch_fe forms (fhh_sketch_set_impl): on-the-fly schedule (default) and r01's"""
+    """every k_sketch_fe form (fhh_sketch_set_impl): round keys in LDS (default), r01's, on the fly"""
     from fuzzyheavyhitters_amd import lib
     assert lib().fhh_sketch_set_impl(request.param) == 0
     yield request.param

@@ -432,10 +432,11 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // are incomplete by design and no product path selects them); 45 / 46 / 47 / 48 are the hybrid:
 // 34 with the last 2 / 4 / 6 / 8 of each workgroup's 16 waves running the pair-sliced VALU AES
 // (expand_ps.h) on the same items; 49 runs every wave as a VALU wave (the test variant that
-// pins expand_item_ps: in 45-48 which items the VALU waves take depends on timing)
+// pins expand_item_ps: in 45-48 which items the VALU waves take depends on timing); 50 is 34 with
+// ordinary (write-back) child-seed stores instead of nontemporal ones (the power-bound A/B)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 49))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 50))
                ? 16u : variant == 31 ? 32u : 8u;
 }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }

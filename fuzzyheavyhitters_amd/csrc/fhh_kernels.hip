@@ -405,7 +405,8 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(46, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (4 << 7)) \
     X(47, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (6 << 7)) \
     X(48, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (8 << 7)) \
-    X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7))
+    X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7)) \
+    X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)
 
 struct VariantInfo {
     const void* fn;
@@ -436,7 +437,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 23; }
+int expand_variant_count() { return kBsVariant + kBsCount + 24; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

@@ -138,17 +138,22 @@ def test_replay_states_on_client_sample(oracle):
 
 
 @pytest.mark.gpu
-def test_gpu_full_size_configs1_equals_plaintext(oracle):
+@pytest.mark.parametrize("mode,gc", [("count", False), ("fe", False), ("fe", "ot")],
+                         ids=["count", "fe", "fe-gc-ot"])
+def test_gpu_full_size_configs1_equals_plaintext(oracle, mode, gc):
     """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): every
     level's child counts, the 222 heavy hitters and their counts from the GPU crawl equal the
-    plaintext crawl (size-independent check; the CPU oracle would take minutes here)."""
+    plaintext crawl (size-independent check; the CPU oracle would take minutes here) — in count
+    mode, in FE mode (simulated OT shares summed in FE, the last level in FieldElm, the leader's
+    v0 - v1) and with the real protocol's garbled-circuit equality test + OT extension in every
+    level (25.6 M equality tests and 77 M OTs per full level)."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sim_crawl, workload
     n = 100_000
     wl = workload.zipf_workload(n, 512, 1, num_sites=10_000, zipf_s=1.03, seed=0x5EED)
     c0, c1 = fhh.KeyCollection(512, 1), fhh.KeyCollection(512, 1)
     fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
-    res = sim_crawl(c0, c1, 0.001, mode="count")
+    res = sim_crawl(c0, c1, 0.001, mode=mode, gc=gc)
     t, tl = oracle.thresholds(0.001, n)
     counts, paths, finals = workload.plaintext_crawl(wl.left, wl.right, t, tl)
     assert [c.tolist() for c in res.counts] == [c.tolist() for c in counts]

@@ -366,7 +366,10 @@ def main():
                       "comm_ranks": world, "comm_rank": rank}
     elif world > 1:
         # native RCCL all-reduce on the engine stream (no host sync per level); the id travels
-        # over the gloo group
+        # over the gloo group. One node (the driver's torchrun --nnodes=1): RCCL's bootstrap
+        # sockets stay on loopback unless the environment says otherwise (the data path is xGMI)
+        if int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world:
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         comm = fhh.RcclComm(local_rank)
         nr, rk = comm.info()
         collective = {"kind": "rccl ncclAllReduce(sum, u64) of per-child partials on the engine stream",

@@ -49,3 +49,13 @@ def test_create_fails_cleanly_without_gpu(fhh):
     rc = lib.fhh_create(ctypes.byref(h), 8, 1, 0)
     assert rc != 0
     assert lib.fhh_last_error(None)
+
+
+def test_sketch_impl_switch_validates(fhh):
+    """fhh_sketch_set_impl (the k_sketch_fe A/B switch) accepts 0..2 and rejects the rest; no GPU
+    call is made."""
+    lib = fhh.lib()
+    assert lib.fhh_sketch_set_impl(3) != 0
+    assert lib.fhh_sketch_set_impl(-1) != 0
+    for impl in (1, 2, 0):
+        assert lib.fhh_sketch_set_impl(impl) == 0

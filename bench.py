@@ -158,6 +158,66 @@ def sketch_bench(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def bincode_bench(args, world, rank, local_rank, dist):
+    """Row f4: the add_keys RPC payload (rpc.rs:12-15, bincode 1.x legacy encoding of
+    Vec<Vec<(ibDCFKey, ibDCFKey)>>) of --clients clients per GPU (data_len 512, d 1: 10 265 B per
+    key, ibDCFbench.csv) decoded straight into the device layout by fhh_add_keys_bincode. One step =
+    one server's payload from host memory to decoded device keys (the H2D copy included, since the
+    payload arrives in host memory from the RPC layer). Keys from GPU keygen, serialized once on
+    the host before the timed region."""
+    import numpy as np
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n = args.clients
+    wl = workload.zipf_workload(n, args.data_len, args.dims, num_sites=args.num_sites, zipf_s=args.zipf,
+                                ball_size=args.ball, seed=args.seed + rank)
+    c0 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
+    c1 = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    ki, rs, cw, cb = c0.export_keys()
+    req = workload.add_keys_request_bincode(ki, rs, cw, cb)
+    del c1, wl
+
+    def step():
+        c = fhh.KeyCollection(args.data_len, args.dims, device=local_rank)
+        t0 = time.perf_counter()
+        c.add_keys_bincode(req)   # pageable host memory, as a deserializer hands it over
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return c, dt
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    times = []
+    for _ in range(args.steps):
+        c, dt = step()
+        times.append(dt)
+    # check the last decode against the keys it came from (bit-exact round trip)
+    k2 = c.export_keys()
+    assert all(np.array_equal(a, b) for a, b in zip(k2, (ki, rs, cw, cb))), "bincode round trip differs"
+    elapsed = sum(times)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        nbytes = req.size * world * args.steps
+        print(json.dumps({
+            "metric": "add_keys payload decoded to device keys (bincode, host memory in)", "value": nbytes / elapsed / 1e9,
+            "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic: GPU-keygen ibDCF keys serialized as AddKeysRequest.keys",
+            "config": {"workload": f"row f4: {n} clients x {args.dims} dims x 2 keys, data_len {args.data_len}",
+                       "payload_bytes": int(req.size), "bytes_per_key": 25 + 20 * args.data_len,
+                       "parallelism": f"client-shard x{world}"},
+            "keys_per_s": n * args.dims * 2 * world * args.steps / elapsed,
+        }), flush=True)
+    return 0
+
+
 def gc_bench(args, world, rank, local_rank, dist):
     """Row f1: one step = the garbled-circuit equality tests of one crawl level at configs[1]
     scale (--gc-groups children x --clients clients per GPU, 2d-bit share strings):
@@ -271,10 +331,11 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
-    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc"],
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc", "bincode"],
                     help="zipf = the metric's Zipf crawl (default 1M clients; --clients 100000 = configs[1]); "
                          "coords = configs[3] (d=2 lat/lon, data_len 16); sketch = configs[4] (sketch + Beaver "
-                         "verification); gc = row f1 (garbled-circuit equality tests of one level)")
+                         "verification); gc = row f1 (garbled-circuit equality tests of one level); "
+                         "bincode = row f4 (add_keys payload decoded on the GPU, --clients per GPU)")
     ap.add_argument("--gc-groups", type=int, default=256, help="--workload gc: children per level")
     ap.add_argument("--gc-clients", type=int, default=100_000, help="--workload gc: clients per GPU")
     ap.add_argument("--gc", default="none", choices=["none", "ot", "ideal"],
@@ -330,6 +391,8 @@ def main():
         return sketch_bench(args, world, rank, local_rank, dist)
     if args.workload == "gc":
         return gc_bench(args, world, rank, local_rank, dist)
+    if args.workload == "bincode":
+        return bincode_bench(args, world, rank, local_rank, dist)
     if args.gc != "none" and args.mode != "fe":
         args.mode = "fe"   # the GC equality test feeds the OT share conversion (collect.rs:419-482)
 

@@ -34,7 +34,7 @@ EXPORTS = [
     "fhh_node_sums_fe255", "fhh_tree_prune", "fhh_tree_prune_last", "fhh_frontier_size",
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
-    "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench", "fhh_microbench_gather", "fhh_microbench_hybrid", "fhh_debug_aes_ps", "fhh_sketch_set_impl",
+    "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench", "fhh_microbench_gather", "fhh_microbench_hybrid", "fhh_debug_aes_ps", "fhh_sketch_set_impl", "fhh_sketch_plan",
     "fhh_debug_launch_gaps", "fhh_wave_profile_arm", "fhh_wave_profile_launches",
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
@@ -260,6 +260,8 @@ def lib():
         "fhh_microbench_hybrid": (i, [i, i, P(ctypes.c_double)]),
         "fhh_debug_aes_ps": (i, [i, u8p, u8p]),
         "fhh_sketch_set_impl": (i, [i]),
+        "fhh_sketch_plan": (i, [u64, u32, u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int)]),
         "fhh_debug_launch_gaps": (i, [i, i, i, P(ctypes.c_double)]),
         "fhh_wave_profile_arm": (i, [i, vp, ctypes.c_uint32]),
         "fhh_wave_profile_launches": (i, [i, P(ctypes.c_uint32)]),

@@ -334,6 +334,12 @@ struct SketchArgs {
     uint32_t force_sequential;   // 1: every key takes the sequential-stream path (tests)
     uint32_t level;              // the level's stream seed = seed with bytes 12..15 ^= level
 };
+// k_sketch_fe launch plan: keys [0, n_main) at lpk_main lanes per key, the rest at lpk_tail
+struct SketchPlan {
+    uint64_t n_main;
+    int lpk_main, lpk_tail;
+};
+SketchPlan plan_sketch(uint64_t n_keys, uint32_t n_nodes, uint64_t resident_waves);
 // U = FieldElm: values as 8 x u32 little-endian limbs
 struct Sketch255Args {
     const uint8_t* seeds;

@@ -404,11 +404,93 @@ static hipError_t launch_sketch_kernel(K kern, int thr, int kpw, const SketchArg
     return hipGetLastError();
 }
 
-// impl (fhh_sketch_set_impl): 0 = default (schedule once per key in LDS, 1024 threads), 1 = the
-// r01 kernel, 2 = the schedule expanded on the fly per pass (1.8 % slower than 0)
+// The default form with the key-to-wave granularity chosen per launch. Keys are strided over one
+// resident wave set (W = CUs x 16 waves), a task = KPW keys of LPK = 64 / KPW lanes each, so a
+// launch takes ceil(tasks / W) rounds of ceil(ceil(nb / LPK) / NBP) passes. At configs[4] (100k
+// keys, 256 nodes, nb = 130) LPK 8 alone needs 3.05 rounds: the fourth runs 212 of 4096 waves for
+// as long as a full round (the kernel is latency-bound, a lone wave is not faster), 36 passes where
+// 24.8 would do. plan_sketch splits such a launch: R full LPK-8 rounds, then the remaining keys in
+// one launch with the LPK that needs the fewest passes (LPK 64: 1 round of 2 passes), 29 in all.
+template <int KPW>
+static hipError_t launch_sketch_lds(const SketchArgs& a, hipStream_t stream) {
+    return launch_sketch_kernel(k_sketch_fe<KPW, SkTab4, kSketchThreadsOtf, 2, kSketchNbpOtf>, kSketchThreadsOtf, KPW,
+                                a, stream);
+}
+
+static hipError_t launch_sketch_lpk(int lpk, const SketchArgs& a, hipStream_t stream) {
+    if (a.n_keys == 0) return hipSuccess;
+    switch (lpk) {
+        case 8: return launch_sketch_lds<8>(a, stream);
+        case 16: return launch_sketch_lds<4>(a, stream);
+        case 32: return launch_sketch_lds<2>(a, stream);
+        default: return launch_sketch_lds<1>(a, stream);
+    }
+}
+
+// resident waves of the LDS-schedule kernel on the current device (cached per device)
+static uint64_t sketch_resident_waves() {
+    static uint64_t cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) {
+        int cus = 256, per_cu = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(k_sketch_fe<8, SkTab4, kSketchThreadsOtf, 2, kSketchNbpOtf>),
+                kSketchThreadsOtf, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        cache[dev] = (uint64_t)(cus > 0 ? cus : 256) * per_cu * (kSketchThreadsOtf / 64);
+    }
+    return cache[dev];
+}
+
+// cost in passes of one launch of n keys at LPK lanes per key (+ half a pass per round for the key
+// schedule, the reductions and the stores)
+static double sketch_launch_cost(uint64_t n, uint64_t nb, int lpk, uint64_t W) {
+    if (n == 0) return 0.0;
+    const uint64_t kpw = 64 / lpk, tasks = (n + kpw - 1) / kpw, rounds = (tasks + W - 1) / W;
+    const uint64_t passes = ((nb + lpk - 1) / lpk + kSketchNbpOtf - 1) / kSketchNbpOtf;
+    return (double)rounds * ((double)passes + 0.5);
+}
+
+SketchPlan plan_sketch(uint64_t n_keys, uint32_t n_nodes, uint64_t W) {
+    static const int kLpk[4] = {8, 16, 32, 64};
+    const uint64_t nb = ((uint64_t)n_nodes + 4) / 2;
+    SketchPlan best{n_keys, 8, 8};
+    double best_cost = sketch_launch_cost(n_keys, nb, 8, W);
+    for (int L : kLpk) {   // one launch (ties keep the smaller LPK: less redundant schedule work)
+        const double c = sketch_launch_cost(n_keys, nb, L, W);
+        if (c < best_cost) best_cost = c, best = SketchPlan{n_keys, L, L};
+    }
+    for (int Lm : kLpk) {   // R full rounds at Lm, the rest at Lt (+ half a pass for the second launch)
+        const uint64_t kpw = 64 / Lm, R = n_keys / kpw / W;
+        if (R == 0) continue;
+        const uint64_t n_main = R * W * kpw;
+        if (n_main >= n_keys) continue;
+        for (int Lt : kLpk) {
+            const double c = sketch_launch_cost(n_main, nb, Lm, W) + sketch_launch_cost(n_keys - n_main, nb, Lt, W) + 0.5;
+            if (c < best_cost) best_cost = c, best = SketchPlan{n_main, Lm, Lt};
+        }
+    }
+    return best;
+}
+
+extern "C" int fhh_sketch_plan(uint64_t n_keys, uint32_t n_nodes, uint64_t resident_waves, uint64_t* n_main,
+                               int* lpk_main, int* lpk_tail) {
+    if (!n_main || !lpk_main || !lpk_tail || resident_waves == 0) return FHH_E_ARG;
+    const SketchPlan p = plan_sketch(n_keys, n_nodes, resident_waves);
+    *n_main = p.n_main;
+    *lpk_main = p.lpk_main;
+    *lpk_tail = p.lpk_tail;
+    return FHH_OK;
+}
+
+// impl (fhh_sketch_set_impl): 0 = default (schedule once per key in LDS, 1024 threads, planned
+// key granularity), 1 = the r01 kernel, 2 = the schedule expanded on the fly per pass, 3 = the
+// default kernel at LPK 8 for every key (the form before plan_sketch)
 static int g_sketch_impl = 0;
 extern "C" int fhh_sketch_set_impl(int impl) {
-    if (impl < 0 || impl > 2) return FHH_E_ARG;
+    if (impl < 0 || impl > 3) return FHH_E_ARG;
     g_sketch_impl = impl;
     return FHH_OK;
 }
@@ -420,8 +502,19 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     if (g_sketch_impl == 2)
         return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, 1, kSketchNbpOtf>,
                                     kSketchThreadsOtf, kSketchKpwOtf, a, stream);
-    return launch_sketch_kernel(k_sketch_fe<kSketchKpwOtf, SkTab4, kSketchThreadsOtf, 2, kSketchNbpOtf>,
-                                kSketchThreadsOtf, kSketchKpwOtf, a, stream);
+    if (g_sketch_impl == 3) return launch_sketch_lpk(8, a, stream);
+    const SketchPlan p = plan_sketch(a.n_keys, a.n_nodes, sketch_resident_waves());
+    SketchArgs m = a;
+    m.n_keys = p.n_main;
+    hipError_t e = launch_sketch_lpk(p.lpk_main, m, stream);
+    if (e != hipSuccess || p.n_main == a.n_keys) return e;
+    SketchArgs t = a;   // the tail: the same launch on the keys past n_main
+    t.seeds = a.seeds + 16 * p.n_main;
+    t.x = a.x ? a.x + p.n_main * a.n_nodes : nullptr;
+    t.kx = a.kx ? a.kx + p.n_main * a.n_nodes : nullptr;
+    t.out = a.out + 6 * p.n_main;
+    t.n_keys = a.n_keys - p.n_main;
+    return launch_sketch_lpk(p.lpk_tail, t, stream);
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

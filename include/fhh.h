@@ -320,10 +320,16 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* batch);
 int fhh_deal_triples_fe(fhh_ctx* ctx, uint64_t n, uint32_t levels, uint64_t seed, uint64_t* triples0_dev,
                         uint64_t* triples1_dev);
 /* k_sketch_fe implementation for A/B (process-wide): 0 = default (four-table LDS layout, 1024
- * threads, each key's round keys computed once into LDS), 1 = the r01 kernel (schedule in
- * registers, 256 threads), 2 = as 0 with the round keys expanded on the fly per pass. All are
- * bit-identical; FHH_E_ARG for any other value. */
+ * threads, each key's round keys computed once into LDS, lanes per key chosen per launch by
+ * fhh_sketch_plan), 1 = the r01 kernel (schedule in registers, 256 threads), 2 = 8 lanes per key
+ * with the round keys expanded on the fly per pass, 3 = 0 at 8 lanes per key for every key. All
+ * are bit-identical; FHH_E_ARG for any other value. */
 int fhh_sketch_set_impl(int impl);
+/* The default form's launch plan for n_keys keys of n_nodes nodes on `resident_waves` waves (CUs x
+ * 16 on MI355X): keys [0, *n_main) run at *lpk_main lanes per key, the rest in a second launch at
+ * *lpk_tail (host-only arithmetic, no device call). */
+int fhh_sketch_plan(uint64_t n_keys, uint32_t n_nodes, uint64_t resident_waves, uint64_t* n_main, int* lpk_main,
+                    int* lpk_tail);
 
 /* ---- the last level, U = FieldElm (sketch_at_last, sketch.rs:202-245; MulState<FieldElm>) ----
  * FieldElm values are 8 x u32 little-endian limbs (any value < 2^256 is accepted as input, reduced

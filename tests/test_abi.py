@@ -52,10 +52,40 @@ def test_create_fails_cleanly_without_gpu(fhh):
 
 
 def test_sketch_impl_switch_validates(fhh):
-    """fhh_sketch_set_impl (the k_sketch_fe A/B switch) accepts 0..2 and rejects the rest; no GPU
+    """fhh_sketch_set_impl (the k_sketch_fe A/B switch) accepts 0..3 and rejects the rest; no GPU
     call is made."""
     lib = fhh.lib()
-    assert lib.fhh_sketch_set_impl(3) != 0
+    assert lib.fhh_sketch_set_impl(4) != 0
     assert lib.fhh_sketch_set_impl(-1) != 0
-    for impl in (1, 2, 0):
+    for impl in (1, 2, 3, 0):
         assert lib.fhh_sketch_set_impl(impl) == 0
+
+
+def sketch_plan(lib, n, nodes, waves=4096):
+    import ctypes
+    nm, lm, lt = ctypes.c_uint64(), ctypes.c_int(), ctypes.c_int()
+    assert lib.fhh_sketch_plan(n, nodes, waves, ctypes.byref(nm), ctypes.byref(lm), ctypes.byref(lt)) == 0
+    return nm.value, lm.value, lt.value
+
+
+def test_sketch_plan(fhh):
+    """k_sketch_fe's launch plan (host arithmetic): configs[4] (100k keys x 256 nodes on 4096 waves)
+    runs 3 full rounds at 8 lanes per key and the 1 696 keys left at 64 (29 passes instead of the 36
+    of 8 lanes throughout); small launches take one launch at the lanes-per-key with the fewest
+    passes; every plan covers the keys exactly once with a power-of-two lanes-per-key."""
+    lib = fhh.lib()
+    assert sketch_plan(lib, 100_000, 256) == (98_304, 8, 64)
+    assert sketch_plan(lib, 98_304, 256) == (98_304, 8, 8)       # whole rounds: one launch
+    assert sketch_plan(lib, 1001, 256) == (1001, 64, 64)         # one round of 2 passes
+    assert sketch_plan(lib, 1, 0) == (1, 8, 8)
+    assert sketch_plan(lib, 40_000, 256)[0] < 40_000             # the GPU test's split case
+    for n in (1, 7, 64, 4095, 4097, 32_768, 33_000, 100_000, 250_001, 1_000_000):
+        for nodes in (0, 1, 13, 256, 1000):
+            n_main, lm, lt = sketch_plan(lib, n, nodes)
+            assert 0 < n_main <= n and lm in (8, 16, 32, 64) and lt in (8, 16, 32, 64)
+            if n_main < n:   # a split: whole rounds of the main launch
+                assert n_main % (4096 * (64 // lm)) == 0
+    import ctypes
+    x = ctypes.c_uint64()
+    y = ctypes.c_int()
+    assert lib.fhh_sketch_plan(10, 10, 0, ctypes.byref(x), ctypes.byref(y), ctypes.byref(y)) != 0

@@ -109,9 +109,10 @@ def test_split_steps_equal_fused(oracle):
 
 
 # ---- HIP path (through the C ABI) against the oracle -----------------------------------------
-@pytest.fixture(params=[0, 1, 2], ids=["lds-sched", "r01-256", "otf-1024"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["lds-sched", "r01-256", "otf-1024", "lds-sched-lpk8"])
 def sketch_impl(request):
-    """every k_sketch_fe form (fhh_sketch_set_impl): round keys in LDS (default), r01's, on the fly"""
+    """every k_sketch_fe form (fhh_sketch_set_impl): round keys in LDS with the planned lanes per key
+    (default), r01's, on the fly, round keys in LDS at 8 lanes per key throughout"""
     from fuzzyheavyhitters_amd import lib
     assert lib().fhh_sketch_set_impl(request.param) == 0
     yield request.param
@@ -120,7 +121,7 @@ def sketch_impl(request):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_keys,n_nodes", [(1, 0), (3, 1), (5, 2), (70, 63), (64, 64), (130, 125), (257, 300),
-                                            (2000, 40), (1001, 256)])
+                                            (2000, 40), (1001, 256), (40000, 256)])
 def test_gpu_sketch_at_bit_exact(oracle, n_keys, n_nodes, sketch_impl):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S

@@ -35,7 +35,7 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kDefaultVariant = 34;  // 4 tables, 128 KiB, 1024 thr, dynamic items, <= 16 entries per item, nontemporal seed stores, sibling-pair AES (r01 A/B)
+constexpr int kDefaultVariant = 51;  // 4 tables, 128 KiB, 1024 thr, dynamic items (first one static, multi-word on narrow levels), <= 16 entries per item, nontemporal seed stores, sibling-pair AES (r02 A/B vs 34)
 
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
 
@@ -148,7 +148,7 @@ struct fhh_ctx {
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> last_hist;
 
     DevBuf scratch, scratch2;
-    DevBuf ot_buf[8], ot_rk;                     // OT extension scratch (T U Q Tt Qt Y0 Y1 choices)
+    DevBuf ot_buf[8], ot_rk;                     // OT extension scratch (T U Q - - Y0 Y1 choices)
     std::vector<uint32_t> ot_rk_host;            // key schedules staged for ot_rk
     std::vector<PinnedBuf*> stage;   // pinned staging for async H2D, recycled at every sync
     size_t stage_used = 0;
@@ -447,7 +447,7 @@ int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
         J.npad = (uint32_t)ctx->npad;
         J.nw = (uint32_t)ctx->nw;
         J.group = 1;
-        J.pad_ = 0;
+        J.wpi = 1;
         J.item_begin = 0;
         J.split = J.n_live;
         J.group_b = 1;
@@ -465,9 +465,11 @@ void finalize_launch(ExpandLaunch& L, int grid, int variant) {
     for (uint32_t k = 0; k < L.njobs; k++) n_live[k] = L.job[k].n_live;
     ItemLayout lay;
     item_layout(n_live, L.njobs, expand_unit(variant, L.job[0].nw), expand_max_group(variant), waves,
-                expand_tail_split(variant), lay);
+                expand_tail_split(variant), lay, expand_max_wpi(variant));
+    L.wpi = lay.wpi;
     for (uint32_t k = 0; k < L.njobs; k++) {
         ExpandJob& J = L.job[k];
+        J.wpi = lay.wpi;
         J.group = lay.g;
         J.group_b = lay.g_b;
         J.split = lay.split[k];
@@ -890,7 +892,6 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
     for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
-    for (int k = 3; k < 5; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(mp * 16));
     for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
     OtArgs a{};
     a.m = m;
@@ -901,8 +902,6 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     a.T = ctx->ot_buf[0].as<uint4>();
     a.U = ctx->ot_buf[1].as<uint4>();
     a.Q = ctx->ot_buf[2].as<uint4>();
-    a.Tt = ctx->ot_buf[3].as<uint4>();
-    a.Qt = ctx->ot_buf[4].as<uint4>();
     a.x0 = x0;
     a.x1 = x1;
     if (delta_words)
@@ -915,10 +914,8 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     a.per_group = per_group;
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
-    HIP_TRY(ctx, launch_ot_transpose(a.Q, a.Qt, a, ctx->stream));
-    HIP_TRY(ctx, launch_ot_send_hash(a, ctx->stream));       // sender -> receiver: Y0, Y1
-    HIP_TRY(ctx, launch_ot_transpose(a.T, a.Tt, a, ctx->stream));
-    HIP_TRY(ctx, launch_ot_recv_hash(a, ctx->stream));
+    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1
+    HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     if (tr) {
         tr->U = a.U;
         tr->Y0 = a.Y0;
@@ -1204,6 +1201,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         for (uint32_t j = 0; j < d; j++) l0[j] = B.live[0].as<uint32_t>() + (size_t)j * B.E_cap;
         for (uint32_t j = d; j < kMaxDims; j++) l0[j] = l0[0];
         HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, expand_unit(variant, c0->nw), expand_max_group(variant),
+                                     expand_max_wpi(variant),
                                      d, 2, grid_waves, B.pos[0].as<uint32_t>(), l0, c0->stream));
     }
     pc.mark("setup");
@@ -1470,6 +1468,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.unit = expand_unit(variant, c0->nw);
         pa.max_group = expand_max_group(variant);
         pa.tail_split = expand_tail_split(variant) ? 1u : 0u;
+        pa.max_wpi = expand_max_wpi(variant);
         pa.zero_partials = (cfg->mode != 0 && !last) ? B.partials.as<uint64_t>() : nullptr;
         pa.zero_count = (uint64_t)C_cap * 4;
         HIP_TRY(c0, launch_prune(pa, c0->stream));

@@ -43,7 +43,7 @@ struct ExpandJob {
     uint32_t npad;
     uint32_t nw;
     uint32_t group;         // entries per work item (CW reuse factor)
-    uint32_t pad_;
+    uint32_t wpi;           // words (64-client units) per work item (item_layout; 1 = one word)
     uint64_t item_begin;
     // end-of-launch phase (item_layout): entries [split, n_live) as items of group_b entries,
     // numbered from item_begin_b after every job's bulk items; e_base = first entry of the
@@ -69,6 +69,8 @@ struct LoopCtl {
     uint32_t n_live[kMaxDims];  // live entries per dim (same for both servers)
     uint32_t group;             // entries per work item for the next k_expand
     uint32_t group_b;           // entries per end-phase item
+    uint32_t wpi;               // words per bulk item (item_layout)
+    uint32_t pad_;
     uint64_t item_begin[kMaxJobs];
     uint64_t total_items;
     uint64_t items_a;           // bulk items of all jobs precede the end-phase items
@@ -84,15 +86,22 @@ struct LoopCtl {
 // of g_b = min(g, kTailGroup) entries, dealt after every job's bulk items. The end phase must
 // not outrun the single work counter (≈ 88 dequeues/µs): 4-entry items at 2 per wave did
 // (8 % slower), hence 8 entries and one item per wave.
+// Words per item (max_wpi > 1, no end phase): when the frontier is narrow (d = 2 at data_len 16,
+// or the first levels of any crawl) a group holds only a few entries, so one-word items are too
+// small for the single counter — configs[3] at 1M clients made 62 500 items of ~2.5 entries per
+// level and k_expand ran at the counter's 88 items/µs (25 G blocks/s). A bulk item then spans
+// wpi = max_group / (entries per group) consecutive words (64-client units), lowered until the
+// launch still has 2 items per wave; wide levels (groups of ≥ max_group / 2 entries) keep wpi = 1.
 constexpr uint32_t kTailGroup = 8;
 struct ItemLayout {
-    uint32_t g, g_b;
+    uint32_t g, g_b, wpi;
     uint64_t items_a, total;
     uint64_t begin_a[kMaxJobs], begin_b[kMaxJobs];
     uint32_t split[kMaxJobs];
 };
 __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njobs, uint32_t unit, uint32_t max_group,
-                                            uint64_t grid_waves, bool tail_split, ItemLayout& L) {
+                                            uint64_t grid_waves, bool tail_split, ItemLayout& L,
+                                            uint32_t max_wpi = 1) {
     uint64_t entries = 0;
     for (uint32_t k = 0; k < njobs; k++) entries += n_live[k];
     const uint64_t entry_words = entries * unit;
@@ -101,6 +110,19 @@ __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njo
     const uint64_t gb = g < kTailGroup ? g : kTailGroup;
     L.g = (uint32_t)g;
     L.g_b = (uint32_t)gb;
+    uint64_t wpi = 1;
+    if (max_wpi > 1 && !tail_split) {
+        uint64_t groups = 0;
+        for (uint32_t k = 0; k < njobs; k++) groups += (n_live[k] + g - 1) / g;
+        if (groups) {
+            const uint64_t e_eff = entries / groups;   // >= 1: every group holds an entry
+            wpi = e_eff >= max_group ? 1 : max_group / e_eff;
+            if (wpi > max_wpi) wpi = max_wpi;
+            while (wpi > 1 && groups * ((unit + wpi - 1) / wpi) < 2 * grid_waves) wpi--;
+        }
+    }
+    L.wpi = (uint32_t)wpi;
+    const uint64_t units = (unit + wpi - 1) / wpi;   // bulk items per entry group
     // end-phase entries wanted in all: one item of g_b entries per wave
     const uint64_t want = (tail_split && gb < g) ? (grid_waves * gb + unit - 1) / unit : 0;
     for (uint32_t k = 0; k < njobs; k++) {
@@ -114,7 +136,7 @@ __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njo
     uint64_t begin = 0;
     for (uint32_t k = 0; k < njobs; k++) {
         L.begin_a[k] = begin;
-        begin += (uint64_t)unit * ((L.split[k] + g - 1) / g);
+        begin += units * ((L.split[k] + g - 1) / g);
     }
     L.items_a = begin;
     for (uint32_t k = 0; k < njobs; k++) {
@@ -130,6 +152,8 @@ struct ExpandLaunch {
     uint32_t jobs_per_ctx;      // = d (LoopCtl::n_live index = job % jobs_per_ctx)
     uint64_t total_items;
     uint64_t items_a;           // host-driven launches: bulk items (== total_items without a tail phase)
+    uint32_t wpi;               // host-driven launches: words per bulk item (item_layout)
+    uint32_t pad_;
     const LoopCtl* ctl;         // non-null: n_live / group / item_begin / total_items from here
 };
 
@@ -215,6 +239,7 @@ struct PruneArgs {
     uint32_t unit;              // k_expand items per entry group (nw; bitsliced: 4 * ceil(nw / 32))
     uint32_t max_group;         // entries per item cap (8; bitsliced: 1)
     uint32_t tail_split;        // item_layout end phase (expand_tail_split)
+    uint32_t max_wpi;           // item_layout words-per-item cap (expand_max_wpi)
     // FE levels: k_sim_ot_fe adds its client chunks into the partials by atomics, so a prune that
     // completes zeroes them for the next level (a memset node would also run after a sticky
     // abort and wipe the sums the resumed prune re-reads)
@@ -266,7 +291,7 @@ int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
 // IKNP / ALSZ OT extension (row f1's OT): m OTs of 16-B messages; base OTs ideal (the sender's
 // key schedules are those of k_i^{s_i}). Bit matrices are [128 rows][mp / 128] uint4 blocks,
-// transposed to [mp] uint4 per-OT rows. With ctl set (level loop) only the first
+// read per OT by the hashes (transposed on the fly). With ctl set (level loop) only the first
 // per_group * min(groups, ctl->C) OTs run.
 struct OtArgs {
     uint64_t m;                  // OTs (capacity)
@@ -275,7 +300,6 @@ struct OtArgs {
     uint32_t s[4];               // sender's base choice bits
     const uint32_t* choices;     // [mp / 32] receiver's choice bits (0 past m)
     uint4 *T, *U, *Q;            // [128][mp / 128]
-    uint4 *Tt, *Qt;              // [mp]
     const uint4 *x0, *x1;        // [m]; x1 == nullptr: x1 = x0 ^ delta (correlated OT)
     uint32_t delta[4];
     uint4 *Y0, *Y1, *out;        // [m]
@@ -285,9 +309,9 @@ struct OtArgs {
 };
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
-hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream);
-hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream);
-hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream);
+// the hashes reading T / Q in row form with the transpose fused in (no Tt / Qt pass)
+hipError_t launch_ot_send_hash_rows(const OtArgs& a, hipStream_t stream);
+hipError_t launch_ot_recv_hash_rows(const OtArgs& a, hipStream_t stream);
 // *word &= mask (one lane; the tail of a choice-bit buffer)
 hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream);
 // the 128 Chou–Orlandi base OTs of OT extension k (fhh_base_ot.cpp)
@@ -319,9 +343,9 @@ struct ProbeArgs {
     uint32_t n_probe, d;
 };
 hipError_t launch_probe_states(const ProbeArgs& a, hipStream_t stream);
-hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
-                            uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
-                            hipStream_t stream);
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t max_wpi,
+                            uint32_t njobs_per_ctx, uint32_t nctx, uint64_t grid_waves, uint32_t* pos0,
+                            uint32_t* live0[kMaxDims], hipStream_t stream);
 
 // ---- sketch + Beaver verification (fhh_sketch.hip), FE values as u64 (any representation) ----
 struct SketchArgs {
@@ -442,9 +466,12 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // ordinary (write-back) child-seed stores instead of nontemporal ones (the power-bound A/B)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 50))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 51))
                ? 16u : variant == 31 ? 32u : 8u;
 }
+// 51 is 34 with multi-word items on narrow levels and each wave's first item taken statically
+// (k_expand FLAGS bit 12): the only variant whose item_layout may set wpi > 1
+inline uint32_t expand_max_wpi(int variant) { return variant == 51 ? 16u : 1u; }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }
 
 }  // namespace fhh

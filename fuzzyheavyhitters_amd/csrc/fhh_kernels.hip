@@ -46,12 +46,11 @@ typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
 // STORE (diagnostic A/B only, never a product variant): 0 = every child seed, 1 = none (a store
 // guarded by an output value that never occurs, so the AES stays live), 2 = dir-0 children only
 // (about the half that survives a prune) — the HBM-write share of k_expand's time and power
+// (entry group g, word w): clients 64 w .. 64 w + 63 of entries [e_base + g group, + group)
 template <class Tab, int NB, bool NT = false, bool PAIR = false, int STORE = 0>
-__device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
-                                            uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
-                                            uint32_t* next = nullptr) {
-    const uint32_t w = (uint32_t)(local % J.nw);
-    const uint32_t g = (uint32_t)(local / J.nw);
+__device__ __forceinline__ void expand_item_wg(const ExpandJob& J, uint32_t w, uint32_t g, const uint32_t* tbl,
+                                               uint32_t lane, uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
+                                               uint32_t* next = nullptr) {
     const uint32_t c = w * 64 + lane;
     const size_t npad = J.npad, nw = J.nw;
 
@@ -128,6 +127,14 @@ __device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, 
             }
         }
     }
+}
+
+template <class Tab, int NB, bool NT = false, bool PAIR = false, int STORE = 0>
+__device__ __forceinline__ void expand_item(const ExpandJob& J, uint64_t local, const uint32_t* tbl, uint32_t lane,
+                                            uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
+                                            uint32_t* next = nullptr) {
+    expand_item_wg<Tab, NB, NT, PAIR, STORE>(J, (uint32_t)(local % J.nw), (uint32_t)(local / J.nw), tbl, lane, b0, b1,
+                                             ahead, next);
 }
 
 // NB = 4 with the next entry's seeds / t / y prefetched while the current entry's AES runs.
@@ -227,7 +234,10 @@ __device__ uint32_t g_wprof_launch = 0;
 // bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline,
 // bit 4 = decode the end-phase items of item_layout (only the variants that lay them out:
 // the extra decode state made the 1024-thread kernel spill), bits 7-11 = NBS: the last NBS waves
-// of every workgroup are VALU waves (expand_item_ps, pair-sliced AES) — the hybrid variants
+// of every workgroup are VALU waves (expand_item_ps, pair-sliced AES) — the hybrid variants,
+// bit 12 = MW: a bulk item may span wpi consecutive words (item_layout, narrow levels), and each
+// wave's first item is its wave index instead of a counter draw (the counter then hands out items
+// from nwaves on: 4 096 simultaneous first draws cost ≈ 46 µs at the counter's 88 per µs)
 template <class Tab, int NB, int THR, int MINW, bool PF = false, int FLAGS = 0>
 __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* work_counter) {
     constexpr bool AHEAD = (FLAGS & 1) != 0;
@@ -237,6 +247,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     constexpr bool TAIL = (FLAGS & 16) != 0;
     constexpr int STORE = (FLAGS >> 5) & 3;   // diagnostic variants 43 / 44 only
     constexpr int NBS = (FLAGS >> 7) & 31;
+    constexpr bool MW = (FLAGS & 4096) != 0;
+    static_assert(!(MW && (AHEAD || TAIL || NBS > 0 || PF)), "MW: plain dynamic items only");
     static_assert(NBS <= THR / 64, "hybrid: NBS VALU waves out of THR / 64");
     __shared__ uint32_t tbl[Tab::kWords];
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
@@ -254,7 +266,10 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     const LoopCtl* ctl = a.ctl;
     const uint64_t total = ctl ? (ctl->abort ? 0 : ctl->total_items) : a.total_items;
     uint64_t item = work_counter ? 0 : (uint64_t)blockIdx.x * wpb + wave_id_uniform();
-    if (work_counter) {
+    const uint64_t draw_base = MW ? nwaves : 0;   // counter value v -> item v + draw_base
+    if (MW) {
+        item = (uint64_t)blockIdx.x * wpb + wave_id_uniform();
+    } else if (work_counter) {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(work_counter, 1u);
         item = __builtin_amdgcn_readfirstlane(v);
@@ -295,14 +310,22 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
         }
         uint32_t nxt = 0;
         if constexpr (PROF) prof_items++;
-        if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
+        if constexpr (MW) {
+            // bulk item = (entry group, chunk of wpi words): local = group * ceil(nw / wpi) + chunk
+            // (wpi = 1 is the one-word item of the other variants: grp = local / nw, w = local % nw)
+            const uint32_t wpi = __builtin_amdgcn_readfirstlane(ctl ? ctl->wpi : a.wpi);
+            const uint32_t local = (uint32_t)(item - J.item_begin);   // < 2^32: groups x nw
+            const uint32_t nwi = (J.nw + wpi - 1) / wpi;
+            const uint32_t grp = local / nwi, w0 = (local % nwi) * wpi, w1 = min(J.nw, w0 + wpi);
+            for (uint32_t w = w0; w < w1; w++) expand_item_wg<Tab, NB, NT, PAIR, STORE>(J, w, grp, tbl, lane, b0, b1);
+        } else if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
         else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
         else expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (work_counter) {
             uint32_t v = nxt;
             if (!AHEAD && lane == 0) v = atomicAdd(work_counter, 1u);
-            item = __builtin_amdgcn_readfirstlane(v);
+            item = (uint64_t)__builtin_amdgcn_readfirstlane(v) + draw_base;
         } else {
             item += nwaves;
         }
@@ -406,7 +429,8 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(47, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (6 << 7)) \
     X(48, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (8 << 7)) \
     X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7)) \
-    X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)
+    X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)      \
+    X(51, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096)
 
 struct VariantInfo {
     const void* fn;
@@ -437,7 +461,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 24; }
+int expand_variant_count() { return kBsVariant + kBsCount + 25; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

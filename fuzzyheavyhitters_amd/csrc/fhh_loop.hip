@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
     const uint32_t njobs = a.nctx * a.njobs_per_ctx;
     for (uint32_t k = 0; k < njobs; k++) job_live[k] = n_live_new[k % a.njobs_per_ctx];
     ItemLayout lay;
-    item_layout(job_live, njobs, a.unit, a.max_group, a.grid_waves, a.tail_split != 0, lay);
+    item_layout(job_live, njobs, a.unit, a.max_group, a.grid_waves, a.tail_split != 0, lay, a.max_wpi);
     for (uint32_t k = 0; k < njobs; k++) {
         ctl->item_begin[k] = lay.begin_a[k];
         ctl->item_begin_b[k] = lay.begin_b[k];
@@ -172,6 +172,7 @@ __global__ __launch_bounds__(kPruneThreads) void k_prune(PruneArgs a) {
     }
     ctl->group = lay.g;
     ctl->group_b = lay.g_b;
+    ctl->wpi = lay.wpi;
     ctl->items_a = lay.items_a;
     ctl->total_items = lay.total;
     ctl->F = nf;
@@ -249,7 +250,8 @@ hipError_t launch_probe_states(const ProbeArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-__global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
+__global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t max_wpi,
+                            uint32_t njobs_per_ctx,
                             uint32_t nctx,
                             uint64_t grid_waves, uint32_t* pos0, uint32_t* l0, uint32_t* l1, uint32_t* l2,
                             uint32_t* l3) {
@@ -271,7 +273,7 @@ __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t ma
     uint32_t job_live[kMaxJobs];
     for (uint32_t k = 0; k < kMaxJobs; k++) job_live[k] = 1;
     ItemLayout lay;
-    item_layout(job_live, njobs, unit, max_group, grid_waves, false, lay);
+    item_layout(job_live, njobs, unit, max_group, grid_waves, false, lay, max_wpi);
     for (uint32_t k = 0; k < njobs; k++) {
         ctl->item_begin[k] = lay.begin_a[k];
         ctl->item_begin_b[k] = lay.begin_b[k];
@@ -279,14 +281,15 @@ __global__ void k_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t ma
     }
     ctl->group = lay.g;
     ctl->group_b = lay.g_b;
+    ctl->wpi = lay.wpi;
     ctl->items_a = lay.items_a;
     ctl->total_items = lay.total;
 }
 
-hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t njobs_per_ctx,
-                            uint32_t nctx, uint64_t grid_waves, uint32_t* pos0, uint32_t* live0[kMaxDims],
-                            hipStream_t stream) {
-    hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, stream, ctl, d, unit, max_group, njobs_per_ctx, nctx,
+hipError_t launch_loop_init(LoopCtl* ctl, uint32_t d, uint32_t unit, uint32_t max_group, uint32_t max_wpi,
+                            uint32_t njobs_per_ctx, uint32_t nctx, uint64_t grid_waves, uint32_t* pos0,
+                            uint32_t* live0[kMaxDims], hipStream_t stream) {
+    hipLaunchKernelGGL(k_loop_init, dim3(1), dim3(64), 0, stream, ctl, d, unit, max_group, max_wpi, njobs_per_ctx, nctx,
                        grid_waves, pos0,
                        live0[0], live0[1], live0[2], live0[3]);
     return hipGetLastError();

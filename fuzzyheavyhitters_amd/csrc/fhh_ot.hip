@@ -13,9 +13,9 @@
 // fixed-key AES + feed-forward of k_expand (aes0_mmo_tab, round keys as immediates). The 128 base OTs are
 // ideal (the host hands the sender k_i^{s_i}).
 //
-//   k_ot_recv_expand / k_ot_send_expand  one lane per (row, 128-OT block): 2 / 1 AES
-//   k_ot_transpose                        one block per 2048 OTs: LDS-staged 32x32 transposes
-//   k_ot_send_hash / k_ot_recv_hash       one lane per OT: 2 / 1 cr_hash (2 / 1 AES)
+//   k_ot_recv_expand / k_ot_send_expand        one lane per (row, 128-OT block): 2 / 1 AES
+//   k_ot_send_hash_rows / k_ot_recv_hash_rows  one wave per 512 OTs, the 128 x 512 bit tile of T / Q
+//                                              transposed in registers + LDS: 2 / 1 cr_hash per OT
 #include "fhh_internal.h"
 #include "aes_keyed.h"
 #include "bitslice.h"
@@ -127,107 +127,123 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     }
 }
 
-// rows [128][mp / 32] u32 -> cols [mp] uint4, one 256-thread block per tile of 64 words
-// (2048 OTs): the tile's 128 x 64 words are staged in LDS by coalesced row loads, thread
-// (g, w) transposes rows 32 g .. 32 g + 31 of word w in registers, writes the 32 results back
-// with pitch 129 words per word-column (conflict-free), and the block stores the 32 KB of
-// output rows contiguously. 33 KB LDS and 160 VGPRs: 3 waves/SIMD, full-line stores. (Holding
-// all 128 rows of a word in one lane took 256 VGPRs, 1 wave/SIMD, and 16-B stores 512 B apart.)
-// mp is a multiple of 8192 (nblk = mp / 128 is a multiple of 64), so W = mp / 32 is a multiple of
-// 64 and every tile lies inside the row matrix.
-constexpr int kTrPitch = 129;
-__global__ __launch_bounds__(256) void k_ot_transpose(const uint32_t* rows, uint4* cols, OtArgs a) {
-    __shared__ uint32_t tile[64 * kTrPitch];
-    const uint64_t W = a.mp / 32;
-    const uint64_t W_act = (ot_active(a) + 31) / 32;
-    const uint64_t ntiles = (W_act + 63) / 64;
-    const uint64_t j_act = 32 * W_act;
-    const uint32_t t = threadIdx.x, w = t & 63, g = t >> 6;
-    for (uint64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
-        const uint64_t w0 = ti * 64;
+// ---- transpose-fused hashes (r02) ------------------------------------------------------------
+// The hashes read the 128 x m bit matrices (T, Q) in their row form and transpose on the fly, so
+// the separate transpose pass of r01 (k_ot_transpose: an HBM round trip of 32 B per OT, 7 % of the
+// GC + OT crawl) is gone.
+// One wave = one tile of 16 words x 128 rows = 512 OTs. Lane l = 4 q + g loads rows 32 g .. 32 g + 31
+// of word w = 16 tile + q (4 rows x 64 B per load instruction) and transposes them in registers:
+// x[k] = word g of OT 32 w + k. The OTs then reach their lanes through 2 KB of LDS per wave, in
+// four rounds of 8 k's: round r writes x[8 r + kk] to word kk * 64 + l (lane-linear ds_write_b32)
+// and lane l reads OTs kk = (l >> 4) + 4 u, q = l & 15 (u < 2) as ds_read_b128 at kk * 64 + 4 q —
+// 16 distinct q per b128 lane group, banks 4 q .. 4 q + 3 of 64: conflict-free. The staging rides
+// beside the 128 KiB of T-tables (160 KiB per workgroup, one workgroup per CU). LDS accesses of one
+// wave retire in order, so the exchange needs no barrier. The exchange rounds run as a rolled loop
+// (x moves down by 8 words per round): unrolled, the scheduler interleaved the rounds and spilled
+// ~90 VGPRs. The receiver hashes 4 OTs (two rounds) per AES pass, the sender one OT (2 blocks) per
+// pass: its 4-block form still spilled 9 VGPRs beside the tile's 32 words.
+constexpr int kOtTileWords = 16;
+constexpr int kOtRowsThreads = 1024;
+constexpr int kOtWaves = kOtRowsThreads / 64;
+
+__device__ __forceinline__ uint64_t ot_tile_ot(uint64_t tile, uint32_t lane, int r, int u) {
+    return 32 * (tile * kOtTileWords + (lane & 15)) + 8 * r + (lane >> 4) + 4 * u;
+}
+
+__device__ __forceinline__ void ot_tile_load(const uint32_t* rows, uint64_t W, uint64_t tile, uint32_t lane,
+                                             uint32_t (&x)[32]) {
+    const uint32_t q = lane >> 2, g = lane & 3;
+    const uint32_t* p = rows + (uint64_t)(32 * g) * W + tile * kOtTileWords + q;
 #pragma unroll
-        for (int i = 0; i < 32; i++) {
-            const uint32_t r = 4 * i + g;
-            tile[r * 64 + w] = __builtin_nontemporal_load(rows + (uint64_t)r * W + w0 + w);
-        }
-        __syncthreads();
+    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + (uint64_t)i * W);
+    transpose32(x);   // x[k] bit i = row 32 g + i of OT 32 w + k
+}
+
+// one round of the exchange: this lane's OTs ot_tile_ot(tile, lane, r, 0 / 1) as uint4 {word 0..3}
+// from x[0..7] = x[8 r .. 8 r + 7] of the tile, then x moves down by 8 (a rolled round loop keeps
+// the 32 words in registers; indexing x by the round would put them in scratch)
+__device__ __forceinline__ void ot_tile_round(uint32_t* st, uint32_t (&x)[32], uint32_t lane, uint4 (&o)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) st[kk * 64 + lane] = x[kk];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < 2; u++) o[u] = *reinterpret_cast<const uint4*>(st + ((lane >> 4) + 4 * u) * 64 + 4 * (lane & 15));
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 24; i++) x[i] = x[i + 8];
+}
+
+__global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) {
+    __shared__ uint32_t tbl_ot[OtTab::kWords];
+    __shared__ uint32_t stage[kOtWaves][512];
+    ot_fill(tbl_ot);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
+    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtWaves;
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
+    for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
+        ot_tile_load(rows, W, t, lane, x);
+#pragma unroll 1
+        for (int r = 0; r < 4; r++) {
+            uint4 q[2];
+            ot_tile_round(stage[wv], x, lane, q);
 #pragma unroll
-        for (int r = 0; r < 32; r++) x[r] = tile[(32 * g + r) * 64 + w];
-        __syncthreads();
-        transpose32(x);   // x[k] bit r = row 32 g + r of OT 32 (w0 + w) + k
-#pragma unroll
-        for (int k = 0; k < 32; k++) tile[w * kTrPitch + 4 * k + g] = x[k];
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t j = t + 256 * i, base = (j >> 5) * kTrPitch + 4 * (j & 31);
-            if (32 * w0 + j < j_act)
-                cols[32 * w0 + j] = make_uint4(tile[base], tile[base + 1], tile[base + 2], tile[base + 3]);
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kOtThreads) void k_ot_send_hash(OtArgs a) {
-    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
-    OtTab::bases(threadIdx.x & 63, b0, b1);
-    const uint64_t m = ot_active(a);
-    const uint64_t G = (uint64_t)gridDim.x * kOtThreads;
-    // two OTs per lane per pass (OTs j and j + G: coalesced either way), 4 blocks in lockstep
-    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += 2 * G) {
-        uint32_t h[4][4];
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const uint64_t jj = j + u * G;
-            const uint4 q = jj < m ? a.Qt[jj] : make_uint4(0, 0, 0, 0);
-            h[2 * u][0] = q.x; h[2 * u][1] = q.y; h[2 * u][2] = q.z; h[2 * u][3] = q.w;
-            h[2 * u + 1][0] = q.x ^ a.s[0]; h[2 * u + 1][1] = q.y ^ a.s[1];
-            h[2 * u + 1][2] = q.z ^ a.s[2]; h[2 * u + 1][3] = q.w ^ a.s[3];
-        }
-        aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const uint64_t jj = j + u * G;
-            if (jj >= m) break;
-            const uint4 x0 = a.x0[jj];
-            const uint4 x1 = a.x1 ? a.x1[jj]
-                                  : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
-            const uint32_t* h0 = h[2 * u];
-            const uint32_t* h1 = h[2 * u + 1];
-            a.Y0[jj] = make_uint4(x0.x ^ h0[0], x0.y ^ h0[1], x0.z ^ h0[2], x0.w ^ h0[3]);
-            a.Y1[jj] = make_uint4(x1.x ^ h1[0], x1.y ^ h1[1], x1.z ^ h1[2], x1.w ^ h1[3]);
+            for (int u = 0; u < 2; u++) {
+                uint32_t h[2][4] = {{q[u].x, q[u].y, q[u].z, q[u].w},
+                                    {q[u].x ^ a.s[0], q[u].y ^ a.s[1], q[u].z ^ a.s[2], q[u].w ^ a.s[3]}};
+                aes0_mmo_tab<DevOpsX, OtTab, 2>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
+                const uint64_t j = ot_tile_ot(t, lane, r, u);
+                if (j >= m) continue;
+                const uint4 x0 = a.x0[j];
+                const uint4 x1 = a.x1 ? a.x1[j]
+                                      : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+                a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
+                a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
+            }
         }
     }
 }
 
-__global__ __launch_bounds__(kOtThreads) void k_ot_recv_hash(OtArgs a) {
-    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
+__global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) {
+    __shared__ uint32_t tbl_ot[OtTab::kWords];
+    __shared__ uint32_t stage[kOtWaves][512];
     ot_fill(tbl_ot);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t b0, b1;
-    OtTab::bases(threadIdx.x & 63, b0, b1);
-    const uint64_t m = ot_active(a);
-    const uint64_t G = (uint64_t)gridDim.x * kOtThreads;
-    // four OTs per lane per pass (j + u G), 4 blocks in lockstep (one block per lane starved the
-    // LDS pipe: 70 G blocks/s)
-    for (uint64_t j = (uint64_t)blockIdx.x * kOtThreads + threadIdx.x; j < m; j += 4 * G) {
-        uint32_t h[4][4];
+    OtTab::bases(lane, b0, b1);
+    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtWaves;
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
+    for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
+        uint32_t x[32];
+        ot_tile_load(rows, W, t, lane, x);
+#pragma unroll 1
+        for (int r = 0; r < 4; r += 2) {   // two rounds = 4 OTs = 4 blocks in lockstep
+            uint32_t h[4][4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint64_t jj = j + u * G;
-            const uint4 t = jj < m ? a.Tt[jj] : make_uint4(0, 0, 0, 0);
-            h[u][0] = t.x; h[u][1] = t.y; h[u][2] = t.z; h[u][3] = t.w;
-        }
-        aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+            for (int rr = 0; rr < 2; rr++) {
+                uint4 tv[2];
+                ot_tile_round(stage[wv], x, lane, tv);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint64_t jj = j + u * G;
-            if (jj >= m) break;
-            const uint32_t r = (a.choices[jj >> 5] >> (jj & 31)) & 1u;
-            const uint4 y = r ? a.Y1[jj] : a.Y0[jj];
-            a.out[jj] = make_uint4(y.x ^ h[u][0], y.y ^ h[u][1], y.z ^ h[u][2], y.w ^ h[u][3]);
+                for (int u = 0; u < 2; u++) {
+                    h[2 * rr + u][0] = tv[u].x; h[2 * rr + u][1] = tv[u].y;
+                    h[2 * rr + u][2] = tv[u].z; h[2 * rr + u][3] = tv[u].w;
+                }
+            }
+            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
+                if (j >= m) continue;
+                const uint32_t c = (a.choices[j >> 5] >> (j & 31)) & 1u;
+                const uint4 y = (c ? a.Y1 : a.Y0)[j];
+                a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
+            }
         }
     }
 }
@@ -313,14 +329,6 @@ hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_ot_transpose(const uint4* rows, uint4* cols, const OtArgs& a, hipStream_t stream) {
-    if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // the tile mapping of k_ot_transpose
-    const uint64_t tiles = a.mp / 2048, cap = (uint64_t)device_cus() * 8;
-    hipLaunchKernelGGL(k_ot_transpose, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(256), 0, stream,
-                       reinterpret_cast<const uint32_t*>(rows), cols, a);
-    return hipGetLastError();
-}
-
 __global__ void k_mask_word(uint32_t* word, uint32_t mask) {
     if (threadIdx.x == 0) *word &= mask;
 }
@@ -330,13 +338,22 @@ hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_ot_send_hash(const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_send_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), 0, stream, a);
+// fused forms: one 1024-thread workgroup per CU (160 KiB of LDS), waves stride over the tiles
+static int ot_rows_grid(const OtArgs& a) {
+    const uint64_t tiles = (a.m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t need = (tiles + kOtWaves - 1) / kOtWaves, cap = (uint64_t)device_cus();
+    return (int)(need < cap ? (need ? need : 1) : cap);
+}
+
+hipError_t launch_ot_send_hash_rows(const OtArgs& a, hipStream_t stream) {
+    if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // tiles of 16 words stay inside a row
+    hipLaunchKernelGGL(k_ot_send_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_ot_recv_hash(const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_recv_hash, dim3(ot_grid(a.m, kOtThreads)), dim3(kOtThreads), 0, stream, a);
+hipError_t launch_ot_recv_hash_rows(const OtArgs& a, hipStream_t stream) {
+    if (a.mp % 8192 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ot_recv_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
     return hipGetLastError();
 }
 

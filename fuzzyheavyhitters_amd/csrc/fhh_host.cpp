@@ -35,7 +35,7 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kDefaultVariant = 51;  // 4 tables, 128 KiB, 1024 thr, dynamic items (first one static, multi-word on narrow levels), <= 16 entries per item, nontemporal seed stores, sibling-pair AES (r02 A/B vs 34)
+constexpr int kDefaultVariant = 52;  // 4 tables, 128 KiB, 1024 thr, dynamic items (first one static, multi-word on narrow levels), <= 16 entries per item, nontemporal parent-seed loads and child-seed stores, sibling-pair AES (r02b A/Bs vs 34, 51)
 
 constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
 

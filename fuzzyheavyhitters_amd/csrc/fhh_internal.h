@@ -466,12 +466,13 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // ordinary (write-back) child-seed stores instead of nontemporal ones (the power-bound A/B)
 inline uint32_t expand_max_group(int variant) {
     if (variant_is_bs(variant)) return 1u;
-    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 51))
+    return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 52))
                ? 16u : variant == 31 ? 32u : 8u;
 }
 // 51 is 34 with multi-word items on narrow levels and each wave's first item taken statically
-// (k_expand FLAGS bit 12): the only variant whose item_layout may set wpi > 1
-inline uint32_t expand_max_wpi(int variant) { return variant == 51 ? 16u : 1u; }
+// (k_expand FLAGS bit 12), the only variants whose item_layout may set wpi > 1 are 51 and 52 (51 with
+// nontemporal parent-seed loads, FLAGS bit 13)
+inline uint32_t expand_max_wpi(int variant) { return variant == 51 || variant == 52 ? 16u : 1u; }
 inline bool expand_tail_split(int variant) { return variant == 37 || variant == 38; }
 
 }  // namespace fhh

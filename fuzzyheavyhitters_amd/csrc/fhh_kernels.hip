@@ -46,8 +46,10 @@ typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
 // STORE (diagnostic A/B only, never a product variant): 0 = every child seed, 1 = none (a store
 // guarded by an output value that never occurs, so the AES stays live), 2 = dir-0 children only
 // (about the half that survives a prune) — the HBM-write share of k_expand's time and power
-// (entry group g, word w): clients 64 w .. 64 w + 63 of entries [e_base + g group, + group)
-template <class Tab, int NB, bool NT = false, bool PAIR = false, int STORE = 0>
+// (entry group g, word w): clients 64 w .. 64 w + 63 of entries [e_base + g group, + group).
+// NTL: parent seeds read with the nontemporal hint (each is read once per level; the CWs are
+// re-read by every entry group of the level and should keep the L2)
+template <class Tab, int NB, bool NT = false, bool PAIR = false, int STORE = 0, bool NTL = false>
 __device__ __forceinline__ void expand_item_wg(const ExpandJob& J, uint32_t w, uint32_t g, const uint32_t* tbl,
                                                uint32_t lane, uint32_t b0, uint32_t b1, uint32_t* ahead = nullptr,
                                                uint32_t* next = nullptr) {
@@ -77,7 +79,14 @@ __device__ __forceinline__ void expand_item_wg(const ExpandJob& J, uint32_t w, u
 #pragma unroll
             for (int q = 0; q < NB / 2; q++) {
                 const int s = s0 + q;
-                const uint4 sd = J.src_seed[((size_t)src * 2 + s) * npad + c];
+                uint4 sd;
+                if constexpr (NTL) {
+                    const v4u32_t v = __builtin_nontemporal_load(
+                        reinterpret_cast<const v4u32_t*>(J.src_seed + ((size_t)src * 2 + s) * npad + c));
+                    sd = make_uint4(v[0], v[1], v[2], v[3]);
+                } else {
+                    sd = J.src_seed[((size_t)src * 2 + s) * npad + c];
+                }
                 tw[q] = J.src_t[((size_t)src * 2 + s) * nw + w];
                 yw[q] = J.src_y[((size_t)src * 2 + s) * nw + w];
                 const uint32_t sw[4] = {sd.x, sd.y, sd.z, sd.w};
@@ -248,6 +257,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     constexpr int STORE = (FLAGS >> 5) & 3;   // diagnostic variants 43 / 44 only
     constexpr int NBS = (FLAGS >> 7) & 31;
     constexpr bool MW = (FLAGS & 4096) != 0;
+    constexpr bool NTL = (FLAGS & 8192) != 0;   // bit 13: nontemporal parent-seed loads (MW path)
     static_assert(!(MW && (AHEAD || TAIL || NBS > 0 || PF)), "MW: plain dynamic items only");
     static_assert(NBS <= THR / 64, "hybrid: NBS VALU waves out of THR / 64");
     __shared__ uint32_t tbl[Tab::kWords];
@@ -317,7 +327,8 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             const uint32_t local = (uint32_t)(item - J.item_begin);   // < 2^32: groups x nw
             const uint32_t nwi = (J.nw + wpi - 1) / wpi;
             const uint32_t grp = local / nwi, w0 = (local % nwi) * wpi, w1 = min(J.nw, w0 + wpi);
-            for (uint32_t w = w0; w < w1; w++) expand_item_wg<Tab, NB, NT, PAIR, STORE>(J, w, grp, tbl, lane, b0, b1);
+            for (uint32_t w = w0; w < w1; w++)
+                expand_item_wg<Tab, NB, NT, PAIR, STORE, NTL>(J, w, grp, tbl, lane, b0, b1);
         } else if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
         else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
@@ -430,7 +441,8 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(48, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (8 << 7)) \
     X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7)) \
     X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)      \
-    X(51, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096)
+    X(51, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096) \
+    X(52, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096 | 8192)
 
 struct VariantInfo {
     const void* fn;
@@ -461,7 +473,7 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 25; }
+int expand_variant_count() { return kBsVariant + kBsCount + 26; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 

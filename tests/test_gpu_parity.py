@@ -71,7 +71,7 @@ BS_VARIANT = 14   # bitsliced k_expand (csrc/fhh_expand_bs.hip): seeds stored bi
 
 DIAGNOSTIC_VARIANTS = (43, 44)   # store no / half of the child seeds (HBM A/B only, fhh_internal.h)
 
-GENERIC_AES_VARIANT = 33   # T-table k_expand with the generic AES (the default, 51, shares rounds 1-2 of sibling pairs)
+GENERIC_AES_VARIANT = 33   # T-table k_expand with the generic AES (the default, 52, shares rounds 1-2 of sibling pairs)
 HYBRID_VARIANT = 46        # T-table waves + 4 pair-sliced VALU waves per workgroup (expand_ps.h)
 VALU_ONLY_VARIANT = 49     # every wave a pair-sliced VALU wave: pins expand_item_ps deterministically
 

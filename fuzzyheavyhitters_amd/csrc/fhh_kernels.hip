@@ -324,9 +324,9 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             // bulk item = (entry group, chunk of wpi words): local = group * ceil(nw / wpi) + chunk
             // (wpi = 1 is the one-word item of the other variants: grp = local / nw, w = local % nw)
             const uint32_t wpi = __builtin_amdgcn_readfirstlane(ctl ? ctl->wpi : a.wpi);
-            const uint32_t local = (uint32_t)(item - J.item_begin);   // < 2^32: groups x nw
+            const uint64_t local = item - J.item_begin;
             const uint32_t nwi = (J.nw + wpi - 1) / wpi;
-            const uint32_t grp = local / nwi, w0 = (local % nwi) * wpi, w1 = min(J.nw, w0 + wpi);
+            const uint32_t grp = (uint32_t)(local / nwi), w0 = (uint32_t)(local % nwi) * wpi, w1 = min(J.nw, w0 + wpi);
             for (uint32_t w = w0; w < w1; w++)
                 expand_item_wg<Tab, NB, NT, PAIR, STORE, NTL>(J, w, grp, tbl, lane, b0, b1);
         } else if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);

@@ -26,7 +26,7 @@ int main() {
         std::vector<std::vector<uint8_t>> seen(njobs);
         for (uint32_t k = 0; k < njobs; k++) seen[k].assign((size_t)n_live[k] * unit, 0);
         if (L.items_a > L.total) fails++;
-        if (L.wpi < 1 || L.wpi > (max_wpi < 1 ? 1 : max_wpi) || (tail && L.wpi != 1)) fails++;
+        if (L.wpi < 1 || L.wpi > max_wpi || (tail && L.wpi != 1)) fails++;
         if (L.wpi > 1 && L.total < 2 * waves) fails++;
         const uint32_t nwi = (unit + L.wpi - 1) / L.wpi;   // bulk items per entry group
         for (uint64_t item = 0; item < L.total; item++) {
@@ -52,6 +52,17 @@ int main() {
             for (uint8_t v : seen[k])
                 if (v != 1) { fails++; break; }
         if (L.split[0] > n_live[0]) fails++;
+    }
+    // the narrow / wide cases of DESIGN.md §5 at 1M clients (nw 15 625, 4 096 waves)
+    {
+        const uint32_t narrow[4] = {1, 1, 1, 1};   // configs[3]: ~1 entry per (server, dim)
+        fhh::ItemLayout L;
+        fhh::item_layout(narrow, 4, 15625, 16, 4096, false, L, 16);
+        if (L.wpi != 7 || L.total != 4 * 2233) fails++;   // lowered until 2 items per wave
+        const uint32_t wide[2] = {200, 200};                // a deep d = 1 level
+        fhh::item_layout(wide, 2, 15625, 16, 4096, false, L, 16);
+        if (L.g != 16) fails++;
+        if (L.wpi != 1) fails++;
     }
     if (fails) { std::printf("FAIL %d\n", fails); return 1; }
     std::printf("OK\n");

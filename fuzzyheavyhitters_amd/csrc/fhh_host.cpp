@@ -1881,7 +1881,7 @@ int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len) {
     rc = alloc_keys(ctx, n);
     if (rc) return rc;
     DevBuf buf, err;
-    HIP_TRY(ctx, buf.ensure(len));
+    HIP_TRY(ctx, buf.ensure(len + 4));   // k_bincode_cw_tiles reads whole dwords: up to 3 B past len
     HIP_TRY(ctx, err.ensure(4));
     HIP_TRY(ctx, hipMemsetAsync(err.p, 0, 4, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(buf.p, req, len, hipMemcpyHostToDevice, ctx->stream));

@@ -1108,9 +1108,11 @@ __device__ __forceinline__ uint4 load_seed(const uint8_t* p) {
     return make_uint4(x[0], x[1], x[2], x[3]);
 }
 
+// (one lane per client: the CW levels [l_first, L) byte by byte, then level L = roots / key_idx;
+// the CW levels go through k_bincode_cw_tiles below, so the launch starts at l_first = L)
 __global__ void k_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L, uint32_t npad,
                                     uint32_t nw, uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root,
-                                    uint64_t* d_key_idx, uint32_t* err) {
+                                    uint64_t* d_key_idx, uint32_t* err, uint32_t l_first) {
     const uint32_t K = 2 * d;
     const uint64_t KB = 25 + 20ull * L;      // one serialized ibDCFKey
     const uint64_t R = 8 + (uint64_t)K * KB;  // one client: u64 d + d (left, right) pairs
@@ -1118,7 +1120,8 @@ __global__ void k_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, 
     const uint64_t wpb = blockDim.x >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     const uint64_t items = (uint64_t)(L + 1) * K * nw;   // level L = roots / key_idx
-    for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items; item += nwaves) {
+    for (uint64_t item = (uint64_t)l_first * K * nw + (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items;
+         item += nwaves) {
         const uint32_t w = (uint32_t)(item % nw);
         const uint32_t kk = (uint32_t)((item / nw) % K);
         const uint32_t l = (uint32_t)(item / ((uint64_t)nw * K));
@@ -1163,15 +1166,106 @@ __global__ void k_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, 
     }
 }
 
+// The correction words as tiles of 64 clients x kBcLevels levels of one key: a client's window of
+// the payload (20 B per level, at an arbitrary byte offset) is staged into LDS by contiguous aligned
+// dword loads (644 B per client, one wave per client at a time), then each lane (= client) extracts
+// its levels with v_alignbit and the tile leaves as 1 KiB rows of [level][key][client] seeds plus
+// the bit-plane ballots. The byte-per-load form (one lane per client and level, 20 global_load_ubyte
+// 20 KiB apart) reached 0.58 TB/s on 2 GB; row f4, rpc.rs:12-15.
+constexpr int kBcLevels = 32;
+constexpr int kBcRow = 5 * kBcLevels + 1;   // dwords staged per client (odd: conflict-free rows)
+__global__ __launch_bounds__(256) void k_bincode_cw_tiles(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L,
+                                                          uint32_t npad, uint32_t nw, uint4* d_cw_seed,
+                                                          uint64_t* d_cw_bits, uint32_t* err) {
+    __shared__ uint32_t st[64 * kBcRow];
+    const uint32_t K = 2 * d;
+    const uint64_t KB = 25 + 20ull * L, R = 8 + (uint64_t)K * KB;
+    const uint32_t nlb = (L + kBcLevels - 1) / kBcLevels;
+    const uint64_t tiles = (uint64_t)nw * K * nlb;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const uint32_t w = (uint32_t)(tile % nw);
+        const uint32_t kk = (uint32_t)((tile / nw) % K);
+        const uint32_t l0 = (uint32_t)(tile / ((uint64_t)nw * K)) * kBcLevels;
+        const uint32_t nl = min((uint32_t)kBcLevels, L - l0);
+        // stage: wave wv takes clients wv + 4 i (i < 16); all 48 loads of a lane are issued before
+        // the first LDS write (a load -> write pair per client serialised 16 HBM latencies per tile)
+        uint32_t v[16][3];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint64_t c = (uint64_t)w * 64 + wv + 4 * i;
+            const uint64_t s0 = 8 + c * R + 8 + kk * KB + 25 + 20ull * l0;   // level l0's CorWord
+            const uint64_t a0 = s0 & ~3ull;
+            const uint32_t ndw = c < n ? (uint32_t)((s0 + 20ull * nl + 3 - a0) / 4) : 0u;   // <= kBcRow
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(buf + a0);
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const uint32_t j = lane + 64 * r;
+                v[i][r] = j < ndw ? src[j] : 0u;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const uint32_t j = lane + 64 * r;
+                if (j < (uint32_t)kBcRow) st[(wv + 4 * i) * kBcRow + j] = v[i][r];
+            }
+        __syncthreads();
+        const uint64_t c = (uint64_t)w * 64 + lane;
+        const bool valid = c < n;
+        const uint32_t sh = (uint32_t)((8 + c * R + 8 + kk * KB + 25 + 20ull * l0) & 3) * 8;
+        uint32_t bad = 0;
+        for (uint32_t li = wv; li < nl; li += 4) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            uint32_t nib = 0;
+            if (valid) {
+                const uint32_t* row = st + lane * kBcRow + 5 * li;   // 5 li + 5 < kBcRow
+                uint32_t u[5];
+#pragma unroll
+                for (int k = 0; k < 5; k++) u[k] = __builtin_amdgcn_alignbit(row[k + 1], row[k], sh);
+                v = make_uint4(u[0], u[1], u[2], u[3]);
+#pragma unroll
+                for (int b = 0; b < 4; b++) {   // bits.0, bits.1, y_bits.0, y_bits.1 as bincode bools
+                    const uint32_t x = (u[4] >> (8 * b)) & 0xFFu;
+                    bad |= x > 1 ? 1u : 0u;
+                    nib |= (x & 1u) << b;
+                }
+            }
+            const size_t rowi = (size_t)(l0 + li) * K + kk;
+            d_cw_seed[rowi * npad + c] = v;
+            uint64_t q[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) q[b] = __ballot((nib >> b) & 1);
+            if (lane == 0)
+#pragma unroll
+                for (int b = 0; b < 4; b++) d_cw_bits[(rowi * 4 + b) * nw + w] = q[b];
+        }
+        if (bad) atomicOr(err, bad);
+        __syncthreads();
+    }
+}
+
 hipError_t launch_keys_from_bincode(const uint8_t* buf, uint64_t n, uint32_t d, uint32_t L, uint32_t npad, uint32_t nw,
                                     uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
                                     uint32_t* err, hipStream_t stream) {
-    const uint64_t items = (uint64_t)(L + 1) * 2 * d * nw;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const uint64_t tiles = (uint64_t)nw * 2 * d * ((L + kBcLevels - 1) / kBcLevels);
+    if (tiles) {
+        const uint64_t cap = (uint64_t)cus * 8;
+        hipLaunchKernelGGL(k_bincode_cw_tiles, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(256), 0, stream, buf,
+                           n, d, L, npad, nw, d_cw_seed, d_cw_bits, err);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const uint64_t items = (uint64_t)2 * d * nw;   // level L: roots / key_idx / headers
     uint64_t blocks = (items + 3) / 4;
     if (blocks > 8192) blocks = 8192;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_keys_from_bincode, dim3((unsigned)blocks), dim3(256), 0, stream, buf, n, d, L, npad, nw,
-                       d_cw_seed, d_cw_bits, d_root, d_key_idx, err);
+                       d_cw_seed, d_cw_bits, d_root, d_key_idx, err, L);
     return hipGetLastError();
 }
 

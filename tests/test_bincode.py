@@ -43,6 +43,22 @@ def test_bincode_keys_equal_oracle_and_crawl(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,L,d", [(1000, 104, 2), (129, 40, 1), (64, 32, 1)])
+def test_bincode_tiles_equal_oracle(oracle, n, L, d):
+    """The tiled decode (64 clients x 32 levels per tile, clients at every byte alignment of the
+    20-B CorWords): partial level blocks, a partial last client word, d = 2."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(n, L, d, num_sites=7, seed=n + L)
+    k0, _ = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
+    c = fhh.KeyCollection(L, d)
+    c.add_keys_bincode(workload.add_keys_request_bincode(k0.key_idx, k0.root_seed, k0.cw_seed, k0.cw_bits))
+    ki, rs, cw, cb = c.export_keys()
+    assert np.array_equal(ki, k0.key_idx) and np.array_equal(rs, k0.root_seed)
+    assert np.array_equal(cw, k0.cw_seed) and np.array_equal(cb, k0.cw_bits)
+
+
+@pytest.mark.gpu
 def test_bincode_malformed_rejected(oracle):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload

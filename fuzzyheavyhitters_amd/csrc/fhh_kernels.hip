@@ -1038,37 +1038,48 @@ hipError_t launch_init_tables(const uint4* root, const uint64_t* key_idx, uint32
 // --------------------------------------------------------------------------------------
 // add_key wire layout (AoS, client-major) -> SoA. One wave = 64 clients of one (level, key).
 // --------------------------------------------------------------------------------------
+// fhh_add_keys (collect.rs:62 add_key, host AoS -> device SoA): an item is 8 consecutive levels of
+// one key for 64 clients, so a lane reads its client's 128 contiguous bytes of CorWord seeds (one
+// cache line, 16-B aligned: the AoS stride is L x 16 B) and 8 bits bytes, and the wave writes 8
+// coalesced 1 KiB rows (one level per item read a 16-B sliver of 64 lines and came back to the same
+// lines for the next 7 levels); the item past the last level block holds the roots / key_idx
 __global__ void k_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed, const uint8_t* cw_seed,
                                 const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
                                 uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wpb = blockDim.x >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
-    const uint64_t items = (uint64_t)(L + 1) * K * nw;   // level L = roots / key_idx
+    const uint32_t nlb = (L + 7) / 8;
+    const uint64_t items = (uint64_t)(nlb + 1) * K * nw;
     for (uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform(); item < items; item += nwaves) {
         const uint32_t w = (uint32_t)(item % nw);
         const uint32_t kk = (uint32_t)((item / nw) % K);
-        const uint32_t l = (uint32_t)(item / ((uint64_t)nw * K));
+        const uint32_t lb = (uint32_t)(item / ((uint64_t)nw * K));
         const uint64_t c = (uint64_t)w * 64 + lane;
         const bool valid = c < n;
-        if (l < L) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            uint32_t nib = 0;
-            if (valid) {
-                const uint8_t* p = cw_seed + ((c * K + kk) * L + l) * 16;
-                uint32_t x[4];
-                for (int k = 0; k < 4; k++)
-                    x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
-                           ((uint32_t)p[4 * k + 3] << 24);
-                v = make_uint4(x[0], x[1], x[2], x[3]);
-                nib = cw_bits[(c * K + kk) * L + l];
+        if (lb < nlb) {
+            const uint32_t l0 = lb * 8, nl = min(8u, L - l0);
+            const uint4* p = reinterpret_cast<const uint4*>(cw_seed) + (c * K + kk) * L + l0;
+            const uint8_t* pb = cw_bits + (c * K + kk) * L + l0;
+            uint4 v[8];
+            uint32_t nib[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                v[k] = (valid && (uint32_t)k < nl) ? p[k] : make_uint4(0, 0, 0, 0);
+                nib[k] = (valid && (uint32_t)k < nl) ? pb[k] : 0u;
             }
-            const size_t row = (size_t)l * K + kk;
-            d_cw_seed[row * npad + c] = v;
-            uint64_t q[4];
-            for (int b = 0; b < 4; b++) q[b] = __ballot((nib >> b) & 1);
-            if (lane == 0)
-                for (int b = 0; b < 4; b++) d_cw_bits[(row * 4 + b) * nw + w] = q[b];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if ((uint32_t)k >= nl) break;   // wave-uniform
+                const size_t row = (size_t)(l0 + k) * K + kk;
+                d_cw_seed[row * npad + c] = v[k];
+                uint64_t q[4];
+#pragma unroll
+                for (int b = 0; b < 4; b++) q[b] = __ballot((nib[k] >> b) & 1);
+                if (lane == 0)
+#pragma unroll
+                    for (int b = 0; b < 4; b++) d_cw_bits[(row * 4 + b) * nw + w] = q[b];
+            }
         } else {
             uint4 v = make_uint4(0, 0, 0, 0);
             uint32_t ki = 0;
@@ -1273,7 +1284,7 @@ hipError_t launch_keys_from_aos(const uint8_t* key_idx, const uint8_t* root_seed
                                 const uint8_t* cw_bits, uint64_t n, uint32_t K, uint32_t L, uint32_t npad, uint32_t nw,
                                 uint4* d_cw_seed, uint64_t* d_cw_bits, uint4* d_root, uint64_t* d_key_idx,
                                 hipStream_t stream) {
-    const uint64_t items = (uint64_t)(L + 1) * K * nw;
+    const uint64_t items = (uint64_t)((L + 7) / 8 + 1) * K * nw;
     uint64_t blocks = (items + 3) / 4;
     if (blocks > 8192) blocks = 8192;
     if (blocks == 0) return hipSuccess;

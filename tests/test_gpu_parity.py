@@ -195,6 +195,29 @@ def test_crawl_three_and_four_dims(kc, oracle, d, ball, thr, mode):
     assert [int(r.value) for r in res.final] == [int(v) for v in ref.final_values]
 
 
+@pytest.mark.parametrize("L", [1, 7, 37])
+@pytest.mark.parametrize("n", [65, 1000])
+def test_add_keys_upload_bit_exact(kc, oracle, L, n):
+    """fhh_add_keys (host AoS keys -> device SoA, 8 levels per item): partial level blocks and a
+    partial last client word; the uploaded keys export back to the oracle's, and a crawl from them
+    equals the oracle's."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(n, 40, 2, num_sites=4, seed=n + L, ball_size=2)
+    left = np.ascontiguousarray(wl.left[:, :, :L])
+    right = np.ascontiguousarray(wl.right[:, :, :L])
+    k0, k1 = oracle.gen_keys(left, right, wl.root_seeds)
+    c0, c1 = add_pair(kc, k0, k1)
+    c0.tree_init()
+    c1.tree_init()
+    for c, k in ((c0, k0), (c1, k1)):
+        ki, rs, cs, cb = c.export_keys()
+        assert np.array_equal(ki, k.key_idx) and np.array_equal(rs, k.root_seed)
+        assert np.array_equal(cs, k.cw_seed) and np.array_equal(cb, k.cw_bits)
+    ref = oracle.crawl(k0, k1, 0.03, mode="count")
+    res = sim_crawl(c0, c1, 0.03, mode="count")
+    assert list(res.level_children) == list(ref.n_children)
+
+
 @pytest.mark.parametrize("L", [1, 2, 7, 37])
 @pytest.mark.parametrize("d", [1, 2])
 @pytest.mark.parametrize("mode", ["count", "fe"])

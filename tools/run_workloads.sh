@@ -1,5 +1,5 @@
 set -e
-O=gpurun_out/wl; mkdir -p $O
+O=${1:-gpurun_out/wl}; mkdir -p $O
 B="timeout -k 10 300 python bench.py --no-cpu-baseline"
 $B --workload coords --clients 1000000 --dims 2 --data-len 16 --threshold 0.075 --steps 5 > $O/coords.json 2> $O/coords.err
 $B --clients 125000 --steps 10 > $O/zipf_125k.json 2> $O/zipf_125k.err

@@ -378,13 +378,17 @@ def test_sim_crawl_matches_oracle_crawl(kc, oracle, d, n, L, sites, thr):
 def test_every_expand_variant_bit_exact(kc, oracle):
     """All compiled k_expand variants (LDS layout / blocks per lane / workgroup size /
     static or dynamic items) give the oracle's crawl, twice in a row (the dynamic-item
-    counter re-arms itself between launches)."""
+    counter re-arms itself between launches), and the oracle's final-level EvalStates."""
     import ctypes
     from fuzzyheavyhitters_amd import lib, sim_crawl, workload
     wl = workload.zipf_workload(700, 64, 1, num_sites=9, seed=5)
     k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
-    ores = oracle.crawl(k0, k1, 0.01, mode="count")
+    ores = oracle.crawl(k0, k1, 0.01, mode="count", keep_levels=[62])
     exp_counts = np.concatenate(ores.counts)
+    # tree_crawl_last keeps the frontier (collect.rs:775-796): after the crawl the engines hold the
+    # children kept at level L - 2, the parents of the last level
+    last0, last1 = ores.level_states[62]
+    kept = np.nonzero(ores.keeps[62])[0]
     c0, c1 = make_pair(kc, wl.left, wl.right, wl.root_seeds)
     v = 0
     buf = ctypes.create_string_buffer(64)
@@ -398,9 +402,14 @@ def test_every_expand_variant_bit_exact(kc, oracle):
         for _ in range(2):
             res = sim_crawl(c0, c1, 0.01, mode="count")
             assert np.array_equal(np.concatenate(res.counts), exp_counts), f"variant {v} ({buf.value})"
-        # the counts do not depend on the AES (the control bits are constant):
-        # the final frontier's seeds must agree across variants too
+        # the counts do not depend on the AES (the control bits are constant): the
+        # final frontier's seeds must equal the oracle's
         st = [c.export_states() for c in (c0, c1)]
+        for (gs, gt, gy), o in zip(st, (last0, last1)):
+            assert gs.shape[0] == kept.size, f"variant {v} ({buf.value}) frontier size"
+            assert np.array_equal(gs, o.seed[kept]) and np.array_equal(gt, o.t[kept]) and \
+                np.array_equal(gy, o.y[kept]), f"variant {v} ({buf.value}) states vs oracle"
+
         if first is None:
             first = st
         for (sa, ta, ya), (sb, tb, yb) in zip(first, st):

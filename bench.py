@@ -46,6 +46,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def host_threads():
+    """Threads the CPU baselines use, and why: the CPUs this process may run on
+    (os.sched_getaffinity), capped by OMP_NUM_THREADS when the environment sets it — the GPU box
+    exports 16, one GPU's share of its host, and the box's other CPUs belong to the other GPUs'
+    jobs."""
+    avail = len(os.sched_getaffinity(0))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        n = min(env, avail)
+        return n, (f"OMP_NUM_THREADS={env} (one GPU's share of the host's {os.cpu_count()} CPUs), "
+                   f"{avail} CPUs in this process's affinity mask")
+    return avail, f"every CPU in this process's affinity mask ({avail} of {os.cpu_count()})"
+
+
 def shard(n_total: int, world: int, rank: int):
     """Contiguous client range of `rank` (strong scaling: the population is fixed)."""
     base = n_total * rank // world
@@ -64,7 +78,7 @@ def cpu_baseline(args):
     n_cpu, L = 1000, 512
     wl = workload.zipf_workload(n_cpu, L, 1, num_sites=10_000, zipf_s=1.03, ball_size=1, seed=args.seed)
     k0, k1 = O.gen_keys(wl.left, wl.right, wl.root_seeds)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    threads, why = host_threads()
     t0 = time.perf_counter()
     res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds)
     dt = time.perf_counter() - t0
@@ -73,6 +87,9 @@ def cpu_baseline(args):
         "value": res.aes_blocks / dt,
         "unit": "AES blocks/s",
         "cores": threads,
+        "cores_why": why,
+        "host_cpus": os.cpu_count(),
+        "host_cpus_in_affinity": len(os.sched_getaffinity(0)),
         "kind": "port",
         "cpu_model": cpu_model(),
         "full_crawl_wall_s": dt if done == L else None,
@@ -281,7 +298,7 @@ def gc_bench(args, world, rank, local_rank, dist):
             O.gc_eval_eq(tb, gl, el, dc)
             reps += 1
         cpu_t = time.perf_counter() - t1
-        cpu = {"value": m * reps / cpu_t, "unit": "equality tests/s", "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
+        cpu = {"value": m * reps / cpu_t, "unit": "equality tests/s", "cores": host_threads()[0],
                "kind": "port", "sample": f"{m} tests x {reps} reps, oracle garble+eval (byte AES, OpenMP)"}
     if rank == 0:
         lds_bytes = tests * aes_per_test * LDS_BYTES_PER_BLOCK

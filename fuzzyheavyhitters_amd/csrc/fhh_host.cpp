@@ -2188,7 +2188,10 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     if (c0->d != c1->d || c0->L != c1->L) return c0->fail(FHH_E_ARG, "sim_crawl: ctx shapes differ");
     // leader.rs:193-194 and 245-246
     const uint64_t thr = std::max<uint64_t>(1, (uint64_t)(cfg->threshold * (double)cfg->nclients_total));
-    const uint32_t thr_last = std::max<uint32_t>(1, (uint32_t)(uint64_t)(cfg->threshold * (double)cfg->nclients_total));
+    // `as u32` in Rust saturates (leader.rs:245): clamp before narrowing
+    const double thr_last_f = cfg->threshold * (double)cfg->nclients_total;
+    const uint32_t thr_last =
+        std::max<uint32_t>(1, thr_last_f >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)(uint64_t)thr_last_f);
     if (!cfg->host_loop) {
         PhaseClock total;
         rc = sim_crawl_device_loop(c0, c1, cfg, levels, thr, thr_last);   // incl. buffer teardown
@@ -2275,6 +2278,11 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
 int fhh_set_variant(fhh_ctx* ctx, int variant) {
     CTX_CHECK(ctx);
     if (variant < 0 || variant >= expand_variant_count()) return ctx->fail(FHH_E_ARG, "set_variant: no such variant");
+    // 43 / 44 store no / only the dir-0 child seeds (HBM-write A/B): their states are incomplete,
+    // so they are refused unless the caller asks for diagnostics explicitly
+    if ((variant == 43 || variant == 44) && !std::getenv("FHH_DIAGNOSTIC_VARIANTS"))
+        return ctx->fail(FHH_E_ARG, "set_variant: variants 43/44 are diagnostic (incomplete child states); "
+                                    "set FHH_DIAGNOSTIC_VARIANTS=1 to select them");
     ctx->variant = variant;
     ctx->grid = expand_grid(ctx->device, variant);
     return FHH_OK;
@@ -2456,6 +2464,10 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
             return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: NULL buffer");
     const uint32_t nl = b->n_levels ? b->n_levels : 1;
     const uint32_t tl = b->triples_levels ? b->triples_levels : 1;
+    // every level takes fresh triples (MulState::new, mpc.rs:94-98): a batch without per-level
+    // triples verifies one level only (reusing a Beaver triple across openings leaks x - x')
+    if (!b->triples_levels && nl > 1)
+        return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: n_levels > 1 needs triples_levels (fresh triples per level)");
     if (b->triples_levels && b->level + nl > tl)
         return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: levels past the triples held");
     for (uint32_t k = 0; k < nl; k++) {

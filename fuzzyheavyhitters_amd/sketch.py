@@ -16,7 +16,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import FhhSketchBatch, FhhSketchBatch255, check, lib, ptr, u32p, u64p
+from ._lib import FhhError, FhhSketchBatch, FhhSketchBatch255, check, lib, ptr, u32p, u64p
 from .fields import FE255_P, FE_P
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -226,6 +226,9 @@ def sim_sketch_verify(kc, batch: DeviceSketchBatch, force_sequential: bool = Fal
     """Both servers' sketch_at + MulState cor/out shares + verify, on the GPU (main.rs:14-70), for
     levels [level, level + n_levels): level l's stream seed is the key's seed with bytes 12..15
     ^= l, its triples are triples[l] (batch.triples_levels > 0); ok / out_shares per level."""
+    if n_levels < 1 or n_levels > batch.ok.shape[0]:
+        raise FhhError(f"sim_sketch_verify: n_levels {n_levels} outside [1, {batch.ok.shape[0]}] "
+                       "(levels beyond the first need per-level triples: deal_triples)")
     b = batch.struct(force_sequential, level, n_levels)
     check(lib().fhh_sim_sketch_verify_fe(kc.handle, ctypes.byref(b)), kc.handle)
 

@@ -248,9 +248,10 @@ typedef struct fhh_sim_config {
     uint8_t* probe_ty;
     uint64_t* probe_children;
     /* gc = 2: 0 = ideal base OTs (seed pairs derived on the device per level); 1 = real base OTs:
-     * Chou–Orlandi (fhh_base_ot_co15), a fresh instance for each of the 4 OT extensions of every
-     * level, produced by a pool of host threads (OMP_NUM_THREADS) one level ahead of the GPU
-     * (busy time in fhh_stats.base_ot_ms) and uploaded as key schedules before the level's OT. */
+     * Chou–Orlandi (fhh_base_ot_co15), a fresh instance for each of the 2 OT extensions of every
+     * level (the evaluator's labels, then the FE / FieldElm share conversion), produced by a pool of
+     * host threads (OMP_NUM_THREADS) one level ahead of the GPU (busy time in
+     * fhh_stats.base_ot_ms) and uploaded as key schedules before the level's OT. */
     uint32_t base_ot;
 } fhh_sim_config;
 

@@ -11,6 +11,8 @@ expand_dir, prg.rs:92-122) evaluated for just those clients along the same survi
 configs[0] (the reference's own CPU configuration, leader.rs:299-443: 1000 Zipf clients,
 num_sites 10000, s = 1.03, data_len 512, threshold 0.001) is run exactly, on both sides.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -48,6 +50,44 @@ def assert_probe_equal(res, ref, clients_sel=None):
             assert np.array_equal(y[s], oy), f"level {lv} server {s}: y bits differ"
 
 
+GOLDEN_1M = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "zipf_1m_L512.npz")
+
+
+def load_golden_1m():
+    g = np.load(GOLDEN_1M, allow_pickle=False)
+    return {k: g[k] for k in g.files}
+
+
+def assert_equals_golden_1m(wl, res):
+    """The north star's literal target (BASELINE.json): the heavy-hitter output for 1M Zipf
+    clients at data_len 512 — every level's child count and counts (leader.rs:417-440), the
+    kept set per level, and the final paths with their counts (collect.rs:945-1029) — equal the
+    plaintext recount committed as tests/golden/zipf_1m_L512.npz."""
+    g = load_golden_1m()
+    assert str(g["left_sha256"]) == golden_digest(wl.left), "workload generator changed: regenerate the fixture"
+    assert str(g["right_sha256"]) == golden_digest(wl.right), "workload generator changed: regenerate the fixture"
+    L = int(g["data_len"])
+    lc = g["level_children"].astype(np.int64)
+    assert [int(x) for x in res.level_children] == lc.tolist()
+    off = np.concatenate([[0], np.cumsum(lc)])
+    thr = int(g["thr"])
+    for lv in range(L):
+        exp = g["counts"][off[lv]:off[lv + 1]].astype(np.uint64)
+        got = np.asarray(res.counts[lv], np.uint64)
+        assert np.array_equal(got, exp), f"level {lv}: {int(np.sum(got != exp))} of {exp.size} counts differ"
+        assert int(res.level_kept[lv]) == int(np.sum(exp >= thr)), f"level {lv}: kept set differs"
+    paths = np.unpackbits(g["paths"], axis=1, bitorder="big")[:, :L]
+    exp_final = sorted((tuple(int(b) for b in p), int(v)) for p, v in zip(paths, g["values"]))
+    got_final = sorted((tuple(int(b) for b in r.path[0]), int(r.value)) for r in res.final)
+    assert len(got_final) == len(exp_final) == 206
+    assert got_final == exp_final
+
+
+def golden_digest(a) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint8).tobytes()).hexdigest()
+
+
 def crawl_with_probe(n, L, levels, clients, cap, seed=0x5EED, num_sites=10_000, threshold=0.001):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
@@ -78,7 +118,10 @@ def test_sampled_states_bit_exact_full_size(oracle, n, word_step):
         assert res.probe[lv][0].shape[1] == res.level_children[lv] > 0
     assert_probe_equal(res, ref)
     if n > 100_000:
-        return   # 1M: the plaintext recount takes minutes in numpy (tools/verify_full.py runs it)
+        # 1M: the plaintext recount takes ~2 min in numpy, so its result is the committed golden
+        # fixture (tests/golden/make_zipf_1m.py); every level's counts and the heavy hitters
+        assert_equals_golden_1m(wl, res)
+        return
     # the crawl itself (AES-independent) still matches the plaintext recount
     from fuzzyheavyhitters_amd import workload
     cnt, paths, _ = workload.plaintext_crawl(wl.left, wl.right, thr, thr)
@@ -86,6 +129,20 @@ def test_sampled_states_bit_exact_full_size(oracle, n, word_step):
     assert all(np.array_equal(a, np.asarray(b)) for a, b in zip(cnt, res.counts))
     got = sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in res.final)
     assert got == sorted(paths)
+
+
+def test_north_star_1m_fe_shares_equal_golden():
+    """The same 1M crawl with the servers' outputs as FE shares (simulated OT: v0 = r1, v1 = eq ?
+    r0 : r1, collect.rs:439-472) and the last level over FieldElm: the leader's v0 - v1 per child
+    at every level and its final_values (collect.rs:1007-1029) equal the golden counts."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 1_000_000, 512
+    wl = workload.zipf_workload(n, L, 1, num_sites=10_000, zipf_s=1.03, ball_size=1, seed=0x5EED)
+    c0, c1 = fhh.KeyCollection(L, 1), fhh.KeyCollection(L, 1)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    res = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=0x1234)
+    assert_equals_golden_1m(wl, res)
 
 
 def test_configs0_gpu_equals_oracle(oracle):

@@ -8,7 +8,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+CASES = sorted(glob.glob(os.path.join(HERE, "golden", "zipf_d*_n*_L*.npz")))   # make_golden.py fixtures
 
 
 def _pair(left, right, roots):

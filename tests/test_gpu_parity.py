@@ -9,7 +9,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+CASES = sorted(glob.glob(os.path.join(HERE, "golden", "zipf_d*_n*_L*.npz")))   # make_golden.py fixtures
 
 
 def load(path):
@@ -417,6 +417,21 @@ def test_every_expand_variant_bit_exact(kc, oracle):
                 f"variant {v} ({buf.value}) states"
         v += 1
     assert v >= 8
+
+
+def test_diagnostic_variants_refused(monkeypatch):
+    """Variants 43 / 44 store no / half of the child seeds (HBM-write A/B): selecting one without
+    FHH_DIAGNOSTIC_VARIANTS fails loudly instead of crawling with incomplete states."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd._lib import FhhError
+    monkeypatch.delenv("FHH_DIAGNOSTIC_VARIANTS", raising=False)
+    c = fhh.KeyCollection(8, 1)
+    for v in DIAGNOSTIC_VARIANTS:
+        with pytest.raises(FhhError, match="diagnostic"):
+            c.set_variant(v)
+    c.set_variant(52)
+    monkeypatch.setenv("FHH_DIAGNOSTIC_VARIANTS", "1")
+    c.set_variant(43)
 
 
 def test_pair_sliced_aes_data_path(oracle):

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CASES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+CASES = sorted(glob.glob(os.path.join(HERE, "golden", "zipf_d*_n*_L*.npz")))   # make_golden.py (the 1M fixture: test_golden_1m.py)
 
 
 def load(path):

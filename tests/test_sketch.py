@@ -167,6 +167,26 @@ def test_gpu_sim_sketch_verify(oracle, force_sequential, sketch_impl):
     assert np.array_equal(ok_exp, wl.honest)
 
 
+@pytest.mark.gpu
+def test_gpu_sim_sketch_verify_rejects_reused_triples():
+    """A batch without per-level triples verifies one level only: MulState::new takes fresh
+    triples per level (mpc.rs:94-98), and reusing one across openings leaks input differences.
+    Both the Python mirror and the C ABI refuse n_levels > 1 there (nothing is written past the
+    one-level ok / out_shares rows)."""
+    import ctypes
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import sketch as S
+    from fuzzyheavyhitters_amd._lib import FhhError, lib
+    wl = S.sketch_workload(200, 9, seed=5, bad_fraction=0.1)
+    kc = fhh.KeyCollection(8, 1)
+    b = S.DeviceSketchBatch(wl)
+    with pytest.raises(FhhError, match="n_levels"):
+        S.sim_sketch_verify(kc, b, n_levels=3)
+    st = b.struct(level=0, n_levels=3)
+    assert lib().fhh_sim_sketch_verify_fe(kc.handle, ctypes.byref(st)) == -1   # FHH_E_ARG
+    assert b"fresh triples" in lib().fhh_last_error(kc.handle)
+
+
 # ---- U = FieldElm: the last level (sketch_at_last, sketch.rs:202-245; MulState<FieldElm>) ------
 P255 = (1 << 255) - 19
 

@@ -26,6 +26,11 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, u64p, ctypes.c_uint64, ctypes.c_vo
 
 FHH_MAX_DIMS = 4
 
+# value formats of fhh_node_sums_*_device (include/fhh.h)
+FHH_VALS_FE_U64, FHH_VALS_FE_BLOCK, FHH_VALS_FE255_LIMBS, FHH_VALS_FE255_BLOCKPAIR = 0, 1, 2, 3
+# reductions of a multi-device collection (fhh_shard_info)
+FHH_REDUCE_NAMES = {0: "none", 1: "host", 2: "rccl"}
+
 # every symbol include/fhh.h declares
 EXPORTS = [
     "fhh_create", "fhh_destroy", "fhh_last_error", "fhh_reset", "fhh_set_client_base",
@@ -45,6 +50,10 @@ EXPORTS = [
     "fhh_co15_sender_start", "fhh_co15_receiver", "fhh_co15_sender_finish", "fhh_base_ot_co15",
     "fhh_base_ot_last_error",
     "fhh_gc_equality_device", "fhh_gc_equality_host", "fhh_ot_extend_device", "fhh_ot_extend_host",
+    "fhh_create_multi", "fhh_shard_info", "fhh_shard_ctx", "fhh_node_sums_fe_device", "fhh_node_sums_fe255_device",
+    "fhh_gb_garble", "fhh_gb_ot_labels", "fhh_gb_ot_shares", "fhh_ev_ot_labels", "fhh_ev_evaluate", "fhh_ev_ot_shares",
+    "fhh_party_node_sums", "fhh_party_bytes_sent", "fhh_gc_party_level_cfg", "fhh_memcpy_device",
+    "fhh_shard_plan",
 ]
 
 
@@ -94,7 +103,7 @@ class FhhSimConfig(ctypes.Structure):
 
 
 SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_ot.hip", "fhh_loop.hip",
-           "fhh_microbench.hip", "fhh_host.cpp", "fhh_comm.cpp", "fhh_base_ot.cpp")
+           "fhh_microbench.hip", "fhh_host.cpp", "fhh_gcot.cpp", "fhh_group.cpp", "fhh_comm.cpp", "fhh_base_ot.cpp")
 
 
 class FhhSketchBatch(ctypes.Structure):
@@ -173,6 +182,19 @@ class FhhOtBatch(ctypes.Structure):
     ]
 
 
+class FhhGcPartyCfg(ctypes.Structure):
+    _fields_ = [
+        ("label_key", ctypes.c_uint8 * 16),
+        ("delta", ctypes.c_uint8 * 16),
+        ("mask", ctypes.c_uint32),
+        ("pad_", ctypes.c_uint32),
+        ("share_seed", ctypes.c_uint64),
+        ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
+        ("base_chosen", ctypes.c_uint8 * (2 * 128 * 16)),
+        ("base_choice", ctypes.c_uint8 * (2 * 16)),
+    ]
+
+
 def build(verbose: bool = False) -> str:
     """Compile libfhh.so for gfx950 with hipcc (in-tree, travels to the GPU box): one object per
     source, compiled in parallel, then one link."""
@@ -226,6 +248,22 @@ def lib():
     P = ctypes.POINTER
     sig = {
         "fhh_create": (i, [P(vp), u32, u32, i]),
+        "fhh_create_multi": (i, [P(vp), u32, u32, P(i), i]),
+        "fhh_shard_info": (i, [vp, i, P(i), P(i), u64p, u64p, P(i)]),
+        "fhh_shard_ctx": (i, [vp, i, P(vp)]),
+        "fhh_node_sums_fe_device": (i, [vp, P(vp), u64, u32, u64p]),
+        "fhh_node_sums_fe255_device": (i, [vp, P(vp), u64, u32, u32p, u32p]),
+        "fhh_gb_garble": (i, [vp, P(FhhGcPartyCfg), P(vp), u64p]),
+        "fhh_gb_ot_labels": (i, [vp, vp, u64, P(vp), u64p]),
+        "fhh_gb_ot_shares": (i, [vp, vp, u64, P(vp), u64p]),
+        "fhh_ev_ot_labels": (i, [vp, P(FhhGcPartyCfg), P(vp), u64p]),
+        "fhh_ev_evaluate": (i, [vp, vp, u64, vp, u64, P(vp), u64p]),
+        "fhh_ev_ot_shares": (i, [vp, vp, u64]),
+        "fhh_party_node_sums": (i, [vp, vp, vp]),
+        "fhh_party_bytes_sent": (i, [vp, u64p]),
+        "fhh_gc_party_level_cfg": (i, [u64, u32, P(FhhGcPartyCfg)]),
+        "fhh_memcpy_device": (i, [i, vp, vp, u64]),
+        "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),
         "fhh_last_error": (ctypes.c_char_p, [vp]),
         "fhh_reset": (i, [vp]),

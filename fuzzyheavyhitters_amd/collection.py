@@ -21,22 +21,67 @@ class Result:
 
 
 class KeyCollection:
-    """One server's key collection on one GPU (collect.rs:45-1030)."""
+    """One server's key collection (collect.rs:45-1030) on one GPU, or — with `devices` — one
+    collection whose clients are sharded over several GPUs (fhh_create_multi: contiguous ranges
+    of 64-client words, per-child partials reduced over an in-process RCCL communicator, or on
+    the host when a device repeats). The methods are the same either way."""
 
-    def __init__(self, depth: int, n_dims: int, device: int = 0):
+    def __init__(self, depth: int, n_dims: int, device: int = 0, devices=None):
         # KeyCollection::new(seed, depth) (collect.rs:51-60)
         self.depth = depth
         self.n_dims = n_dims
-        self.device = device
+        self.device = device if devices is None else int(devices[0])
+        self.devices = None if devices is None else [int(x) for x in devices]
+        self._owner = None
         h = ctypes.c_void_p()
-        check(lib().fhh_create(ctypes.byref(h), depth, n_dims, device))
+        if devices is None:
+            check(lib().fhh_create(ctypes.byref(h), depth, n_dims, device))
+        else:
+            arr = (ctypes.c_int * len(self.devices))(*self.devices)
+            check(lib().fhh_create_multi(ctypes.byref(h), depth, n_dims, arr, len(self.devices)))
         self._h = h
+
+    @classmethod
+    def _borrowed(cls, owner: "KeyCollection", handle, device: int):
+        """A shard's ctx, owned by `owner` (never destroyed through this object)."""
+        kc = cls.__new__(cls)
+        kc.depth, kc.n_dims, kc.device, kc.devices = owner.depth, owner.n_dims, device, None
+        kc._owner = owner
+        kc._h = handle
+        return kc
+
+    def shard_info(self):
+        """[(device, client_base, n_clients)] per shard and the reduction ("none" / "host" / "rccl")."""
+        from ._lib import FHH_REDUCE_NAMES
+        out = []
+        ns, dev, red = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        base, cnt = ctypes.c_uint64(), ctypes.c_uint64()
+        k = 0
+        while True:
+            self._chk(lib().fhh_shard_info(self._h, k, ctypes.byref(ns), ctypes.byref(dev), ctypes.byref(base),
+                                           ctypes.byref(cnt), ctypes.byref(red)))
+            out.append((dev.value, base.value, cnt.value))
+            k += 1
+            if k >= ns.value:
+                break
+        return out, FHH_REDUCE_NAMES[red.value]
+
+    def shard(self, k: int) -> "KeyCollection":
+        """Shard k's one-GPU collection (per-shard calls: the two-party GC + OT, fhh_gb_* / fhh_ev_*)."""
+        h = ctypes.c_void_p()
+        self._chk(lib().fhh_shard_ctx(self._h, k, ctypes.byref(h)))
+        if h.value == (self._h.value if isinstance(self._h, ctypes.c_void_p) else self._h):
+            return self
+        return KeyCollection._borrowed(self, h, self.shard_info()[0][k][0])
 
     @property
     def handle(self):
         return self._h
 
     def close(self):
+        if getattr(self, "_owner", None) is not None:   # a borrowed shard ctx
+            self._h = None
+            return
         if getattr(self, "_h", None):
             lib().fhh_destroy(self._h)
             self._h = None
@@ -120,6 +165,24 @@ class KeyCollection:
         out = np.zeros(v.shape[0], np.uint64)
         self._chk(lib().fhh_node_sums_fe(self._h, ptr(v, u64p), ptr(out, u64p)))
         return out
+
+    def node_sums_fe_device(self, vals_dev, ld: int, C: int, fmt: int = 0) -> np.ndarray:
+        """collect.rs:487-501 on OT outputs already in device memory (no host round trip):
+        vals_dev = one device pointer (int) per shard, rows [C][ld] (C = the pending crawl's
+        children); fmt FHH_VALS_FE_U64 / FHH_VALS_FE_BLOCK. Returns canonical FE sums [C]."""
+        ptrs = (ctypes.c_void_p * len(vals_dev))(*[int(p) for p in vals_dev])
+        out = np.zeros(max(C, 1), np.uint64)
+        self._chk(lib().fhh_node_sums_fe_device(self._h, ptrs, ld, fmt, ptr(out, u64p)))
+        return out[:C]
+
+    def node_sums_fe255_device(self, vals_dev, ld: int, C: int, fmt: int = 3):
+        """collect.rs:891-905 on device-resident FieldElm OT outputs (FHH_VALS_FE255_LIMBS /
+        FHH_VALS_FE255_BLOCKPAIR) -> (unreduced ints, canonical ints)."""
+        ptrs = (ctypes.c_void_p * len(vals_dev))(*[int(p) for p in vals_dev])
+        unr = np.zeros((max(C, 1), 10), np.uint32)
+        can = np.zeros((max(C, 1), 8), np.uint32)
+        self._chk(lib().fhh_node_sums_fe255_device(self._h, ptrs, ld, fmt, ptr(unr, u32p), ptr(can, u32p)))
+        return [limbs10_to_int(r) for r in unr[:C]], [limbs10_to_int(r) for r in can[:C]]
 
     def node_sums_fe255(self, vals: np.ndarray):
         """collect.rs:891-905: vals [C][n][8] u32 LE limbs -> (unreduced ints, canonical ints)."""

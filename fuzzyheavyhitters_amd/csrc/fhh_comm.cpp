@@ -42,6 +42,11 @@ struct Rccl {
     decltype(&ncclGetErrorString) error_string = nullptr;
     decltype(&ncclCommCount) comm_count = nullptr;
     decltype(&ncclCommUserRank) comm_user_rank = nullptr;
+    // in-process communicators (one KeyCollection over several GPUs, fhh_group.cpp)
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
 };
 
 Rccl g_rccl;
@@ -84,8 +89,12 @@ int load_locked(const char* path) {
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
     r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
     r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(h, "ncclCommUserRank"));
+    r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+    r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(dlsym(h, "ncclCommAbort"));
     if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string ||
-        !r.comm_count || !r.comm_user_rank)
+        !r.comm_count || !r.comm_user_rank || !r.comm_init_all || !r.group_start || !r.group_end || !r.comm_abort)
         return fail(FHH_E_COMM, "librccl lacks an expected symbol");
     g_rccl = r;
     return FHH_OK;
@@ -127,6 +136,71 @@ int comm_allreduce(fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t c
         return FHH_E_COMM;
     }
     return FHH_OK;
+}
+
+// One process driving several GPUs (fhh_create_multi): ncclCommInitAll over the shards' devices,
+// which must be distinct (RCCL refuses two ranks on one GPU: "Duplicate GPU detected").
+int comm_init_all(int n, const int* devices, std::vector<::fhh_comm*>& out, std::string* err) {
+    out.clear();
+    if (ensure_loaded()) {
+        if (err) *err = g_comm_err;
+        return FHH_E_COMM;
+    }
+    std::vector<ncclComm_t> comms((size_t)n, nullptr);
+    const ncclResult_t r = g_rccl.comm_init_all(comms.data(), n, devices);
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclCommInitAll: ") + g_rccl.error_string(r);
+        return FHH_E_COMM;
+    }
+    for (int k = 0; k < n; k++) {
+        auto* c = new ::fhh_comm();
+        c->comm = comms[(size_t)k];
+        c->nranks = n;
+        c->rank = k;
+        c->device = devices[k];
+        out.push_back(c);
+    }
+    return FHH_OK;
+}
+
+// The same all-reduce on every in-process communicator (each on its shard's stream), fused in
+// one ncclGroupStart / ncclGroupEnd: one host thread issues all ranks' halves.
+int comm_group_allreduce(const std::vector<::fhh_comm*>& comms, const std::vector<uint64_t*>& bufs, uint64_t count,
+                         const std::vector<hipStream_t>& streams, std::string* err) {
+    ncclResult_t r = g_rccl.group_start();
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclGroupStart: ") + g_rccl.error_string(r);
+        return FHH_E_COMM;
+    }
+    for (size_t k = 0; k < comms.size(); k++) {
+        if (hipSetDevice(comms[k]->device) != hipSuccess) {
+            (void)g_rccl.group_end();
+            if (err) *err = "hipSetDevice failed";
+            return FHH_E_HIP;
+        }
+        r = g_rccl.all_reduce(bufs[k], bufs[k], count, ncclUint64, ncclSum, comms[k]->comm, streams[k]);
+        if (r != ncclSuccess) {
+            (void)g_rccl.group_end();
+            if (err) *err = std::string("ncclAllReduce: ") + g_rccl.error_string(r);
+            return FHH_E_COMM;
+        }
+    }
+    r = g_rccl.group_end();
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclGroupEnd: ") + g_rccl.error_string(r);
+        return FHH_E_COMM;
+    }
+    return FHH_OK;
+}
+
+// Unblock peers stuck in a collective after one shard failed (RCCL comms: ncclCommAbort; hosted
+// comms: the thread reducer's abort flag, see ThreadReducer).
+void comm_abort(::fhh_comm* c) {
+    if (c && c->comm && g_rccl.comm_abort) {
+        (void)hipSetDevice(c->device);
+        (void)g_rccl.comm_abort(c->comm);
+        c->comm = nullptr;
+    }
 }
 
 }  // namespace fhh

@@ -1,0 +1,799 @@
+// Host side of row f1: the garbled-circuit equality test and the OT extension of tree_crawl
+// (src/equalitytest.rs:25-219, src/collect.rs:419-482) — key schedules and per-level material,
+// the OT-extension runner the device level loop and the C ABI share, the one-process C ABI
+// (fhh_gc_equality_*, fhh_ot_extend_*), and the two-party split (fhh_gb_* / fhh_ev_*: each server
+// runs its half on its own ctx, only the protocol messages cross).
+#include "fhh_engine.h"
+#include "aes_tables.h"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace fhh {
+namespace eng {
+
+// ---- garbled-circuit equality test helpers (row f1) ------------------------------------------
+// FIPS-197 key expansion on little-endian column words (RotWord = rotr 8, rcon in byte 0), the
+// convention of the device T-table rounds (aes_keyed.h)
+void host_key_schedule(const uint8_t key[16], uint32_t (&rk)[11][4]) {
+    uint32_t w[44];
+    for (int i = 0; i < 4; i++)
+        w[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+               ((uint32_t)key[4 * i + 3] << 24);
+    uint32_t rcon = 1;
+    for (int i = 4; i < 44; i++) {
+        uint32_t t = w[i - 1];
+        if (i % 4 == 0) {
+            t = (t >> 8) | (t << 24);
+            t = (uint32_t)SBOX.v[t & 0xFF] | ((uint32_t)SBOX.v[(t >> 8) & 0xFF] << 8) |
+                ((uint32_t)SBOX.v[(t >> 16) & 0xFF] << 16) | ((uint32_t)SBOX.v[t >> 24] << 24);
+            t ^= rcon;
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+        }
+        w[i] = w[i - 4] ^ t;
+    }
+    for (int r = 0; r < 11; r++)
+        for (int c = 0; c < 4; c++) rk[r][c] = w[4 * r + c];
+}
+
+void words_from_bytes(const uint8_t b[16], uint32_t (&w)[4]) {
+    for (int c = 0; c < 4; c++)
+        w[c] = (uint32_t)b[4 * c] | ((uint32_t)b[4 * c + 1] << 8) | ((uint32_t)b[4 * c + 2] << 16) |
+               ((uint32_t)b[4 * c + 3] << 24);
+}
+
+uint64_t host_mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// the level loop's per-level garbler secrets (a fresh key, Delta and mask per tree_crawl call)
+void gc_level_material(uint64_t prf_seed, uint32_t level, uint8_t key[16], uint8_t delta[16], uint32_t* mask) {
+    uint64_t z = host_mix64(prf_seed ^ 0x67635f6c6576656cull ^ ((uint64_t)level << 20));
+    for (int h = 0; h < 2; h++) {
+        z = host_mix64(z);
+        std::memcpy(key + 8 * h, &z, 8);
+    }
+    for (int h = 0; h < 2; h++) {
+        z = host_mix64(z);
+        std::memcpy(delta + 8 * h, &z, 8);
+    }
+    *mask = (uint32_t)(host_mix64(z) & 1);
+}
+
+// validated GcArgs from a batch (device pointers)
+int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
+    if (!b) return ctx->fail(FHH_E_ARG, "gc: NULL batch");
+    if (b->bits < 1 || b->bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
+    if ((uint64_t)b->words * 64 < b->clients) return ctx->fail(FHH_E_ARG, "gc: words < ceil(clients / 64)");
+    const uint64_t n = b->groups * b->clients;
+    if (n && (!b->gb_planes_dev || !b->ev_planes_dev || !b->gb_labels_dev || !b->ev_labels_dev || !b->decode_dev ||
+              !b->out_dev || (b->bits > 1 && !b->tables_dev)))
+        return ctx->fail(FHH_E_ARG, "gc: NULL device buffer");
+    a = GcArgs{};
+    a.gb_planes = b->gb_planes_dev;
+    a.ev_planes = b->ev_planes_dev;
+    a.G = b->groups;
+    a.N = b->clients;
+    a.nw = b->words;
+    a.bits = b->bits;
+    a.mask = b->mask & 1u;
+    host_key_schedule(b->label_key, a.rk_label);
+    words_from_bytes(b->delta, a.delta);
+    a.delta[0] |= 1u;   // colour bit of Delta = 1 (point-and-permute)
+    a.label_nonce = b->label_nonce;
+    a.gate_base = b->gate_base;
+    a.tables = reinterpret_cast<uint4*>(b->tables_dev);
+    a.gb_labels = reinterpret_cast<uint4*>(b->gb_labels_dev);
+    a.ev_labels = reinterpret_cast<uint4*>(b->ev_labels_dev);
+    a.decode = b->decode_dev;
+    a.out = b->out_dev;
+    a.ctl = nullptr;
+    return FHH_OK;
+}
+
+// ---- OT extension runner (row f1's OT) --------------------------------------------------------
+uint64_t ot_padded(uint64_t m) { return (m + 8191) / 8192 * 8192; }
+
+// the sender's base-OT choice bits of a level-loop OT (ideal base OTs; k_ot_level_keys derives
+// the seeds from the same material on the device)
+void ot_level_choice(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s[4]) {
+    const uint64_t z0 = host_mix64(prf ^ 0x6f745f63686f6963ull ^ ((uint64_t)level << 24) ^ ((uint64_t)salt << 20));
+    const uint64_t z1 = host_mix64(z0);
+    s[0] = (uint32_t)z0;
+    s[1] = (uint32_t)(z0 >> 32);
+    s[2] = (uint32_t)z1;
+    s[3] = (uint32_t)(z1 >> 32);
+}
+
+// padded choice-bit buffer of the ctx's OT scratch (mp / 32 words, zero past m)
+hipError_t ot_choices_buffer(fhh_ctx* ctx, uint64_t m, uint32_t** out) {
+    const uint64_t mp = ot_padded(m);
+    hipError_t e = ctx->ot_buf[7].ensure(mp / 8);
+    if (e != hipSuccess) return e;
+    *out = ctx->ot_buf[7].as<uint32_t>();
+    return hipSuccess;
+}
+
+// the 3 x 128 base-OT key schedules from host seeds (receiver k_i^0, k_i^1; sender k_i^{s_i}),
+// uploaded and synchronised (the staging vector is reused by the next call)
+int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev) {
+    ctx->ot_rk_host.assign((size_t)3 * 128 * 44, 0);
+    for (int i = 0; i < 128; i++) {
+        const int si = (s[i / 8] >> (i % 8)) & 1;
+        uint32_t rk[11][4];
+        for (int b = 0; b < 3; b++) {
+            host_key_schedule(seeds + (size_t)(i * 2 + (b < 2 ? b : si)) * 16, rk);
+            std::memcpy(ctx->ot_rk_host.data() + ((size_t)b * 128 + i) * 44, rk, 44 * 4);
+        }
+    }
+    HIP_TRY(ctx, ctx->ot_rk.ensure(ctx->ot_rk_host.size() * 4));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->ot_rk.p, ctx->ot_rk_host.data(), ctx->ot_rk_host.size() * 4,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *rk_dev = ctx->ot_rk.as<uint32_t>();
+    return FHH_OK;
+}
+
+// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer; rk_dev: the base-OT
+// key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
+int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
+           const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr) {
+    if (m == 0) return FHH_OK;
+    const uint64_t mp = ot_padded(m);
+    const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
+    for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
+    for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
+    OtArgs a{};
+    a.m = m;
+    a.mp = mp;
+    a.rk = rk_dev;
+    for (int c = 0; c < 4; c++) a.s[c] = s_words[c];
+    a.choices = choices;
+    a.T = ctx->ot_buf[0].as<uint4>();
+    a.U = ctx->ot_buf[1].as<uint4>();
+    a.Q = ctx->ot_buf[2].as<uint4>();
+    a.x0 = x0;
+    a.x1 = x1;
+    if (delta_words)
+        for (int c = 0; c < 4; c++) a.delta[c] = delta_words[c];
+    a.Y0 = ctx->ot_buf[5].as<uint4>();
+    a.Y1 = ctx->ot_buf[6].as<uint4>();
+    a.out = out;
+    a.tweak_base = tweak_base;
+    a.ctl = ctl;
+    a.per_group = per_group;
+    HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
+    HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
+    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1
+    HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
+    if (tr) {
+        tr->U = a.U;
+        tr->Y0 = a.Y0;
+        tr->Y1 = a.Y1;
+        tr->nblk = mp / 128;
+    }
+    return FHH_OK;
+}
+
+}  // namespace eng
+}  // namespace fhh
+
+extern "C" {
+
+// ---- garbled-circuit equality test (row f1) ------------------------------------------------
+int fhh_gc_equality_device(fhh_ctx* ctx, const fhh_gc_batch* b) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    GcArgs a;
+    rc = gc_args(ctx, b, a);
+    if (rc) return rc;
+    HIP_TRY(ctx, launch_gc_garble(a, ctx->stream));
+    HIP_TRY(ctx, launch_gc_eval(a, ctx->stream));
+    return ctx_sync(ctx);
+}
+
+int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                         uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
+                         uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
+                         uint8_t* decode, uint8_t* out) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
+    if (n == 0) return FHH_OK;
+    if (!gb_bits || !ev_bits || !label_key || !delta || !out) return ctx->fail(FHH_E_ARG, "gc: NULL argument");
+    if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc: n must fit 32 bits");
+    const uint64_t nw = (n + 63) / 64;
+    std::vector<uint64_t> planes[2];
+    const uint8_t* src[2] = {gb_bits, ev_bits};
+    for (int s = 0; s < 2; s++) {
+        planes[s].assign((size_t)bits * nw, 0);
+        for (uint64_t t = 0; t < n; t++)
+            for (uint32_t j = 0; j < bits; j++)
+                if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
+    }
+    DevBuf dp[2], dt, dg, de, dd, dout;
+    for (int s = 0; s < 2; s++) {
+        HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
+        HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, dt.ensure((size_t)std::max(bits - 1, 1u) * 2 * n * 16));
+    HIP_TRY(ctx, dg.ensure((size_t)(bits + 1) * n * 16));
+    HIP_TRY(ctx, de.ensure((size_t)bits * n * 16));
+    HIP_TRY(ctx, dd.ensure(n));
+    HIP_TRY(ctx, dout.ensure(n));
+    fhh_gc_batch b{};
+    b.groups = 1;
+    b.clients = (uint32_t)n;
+    b.words = (uint32_t)nw;
+    b.bits = bits;
+    b.mask = mask;
+    std::memcpy(b.label_key, label_key, 16);
+    std::memcpy(b.delta, delta, 16);
+    b.label_nonce = label_nonce;
+    b.gate_base = gate_base;
+    b.gb_planes_dev = dp[0].as<uint64_t>();
+    b.ev_planes_dev = dp[1].as<uint64_t>();
+    b.tables_dev = dt.as<uint8_t>();
+    b.gb_labels_dev = dg.as<uint8_t>();
+    b.ev_labels_dev = de.as<uint8_t>();
+    b.decode_dev = dd.as<uint8_t>();
+    b.out_dev = dout.as<uint8_t>();
+    rc = fhh_gc_equality_device(ctx, &b);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    if (decode) HIP_TRY(ctx, hipMemcpy(decode, dd.p, n, hipMemcpyDeviceToHost));
+    // SoA [row][t][16] -> AoS [t][row][16]
+    auto soa_to_aos = [&](const DevBuf& d, uint32_t rows, uint8_t* dst) -> int {
+        if (!dst || rows == 0) return FHH_OK;
+        std::vector<uint8_t> h((size_t)rows * n * 16);
+        HIP_TRY(ctx, hipMemcpy(h.data(), d.p, h.size(), hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < rows; r++)
+            for (uint64_t t = 0; t < n; t++)
+                std::memcpy(dst + (t * rows + r) * 16, h.data() + ((size_t)r * n + t) * 16, 16);
+        return FHH_OK;
+    };
+    rc = soa_to_aos(dt, 2 * (bits - 1), tables);
+    if (rc) return rc;
+    rc = soa_to_aos(dg, bits + 1, gb_labels);
+    if (rc) return rc;
+    return soa_to_aos(de, bits, ev_labels);
+}
+
+// ---- OT extension (row f1's OT) ---------------------------------------------------------------
+int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (!b) return ctx->fail(FHH_E_ARG, "ot_extend: NULL batch");
+    if (b->m == 0) return FHH_OK;
+    if (!b->choices_dev || !b->x0_dev || !b->out_dev) return ctx->fail(FHH_E_ARG, "ot_extend: NULL device buffer");
+    uint32_t* ch = nullptr;
+    HIP_TRY(ctx, ot_choices_buffer(ctx, b->m, &ch));
+    const uint64_t mp = ot_padded(b->m), words = (b->m + 31) / 32;
+    HIP_TRY(ctx, hipMemsetAsync(ch, 0, mp / 8, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ch, b->choices_dev, words * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    // clear the bits past m in the last word, in stream order on the device
+    if (b->m % 32) HIP_TRY(ctx, launch_mask_word(ch + words - 1, (1u << (b->m % 32)) - 1, ctx->stream));
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, &b->base_seeds[0][0][0], b->base_choice, &rk);
+    if (rc) return rc;
+    uint32_t sw[4], dw[4];
+    words_from_bytes(b->base_choice, sw);
+    words_from_bytes(b->delta, dw);
+    rc = ot_run(ctx, b->m, ch, reinterpret_cast<const uint4*>(b->x0_dev), reinterpret_cast<const uint4*>(b->x1_dev),
+                b->x1_dev ? nullptr : dw, reinterpret_cast<uint4*>(b->out_dev), rk, sw, b->tweak_base, nullptr, 0,
+                nullptr);
+    if (rc) return rc;
+    return ctx_sync(ctx);
+}
+
+int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1,
+                       const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                       uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (m == 0) return FHH_OK;
+    if (!choices || !x0 || !out || !base_seeds || !base_choice || (!x1 && !delta))
+        return ctx->fail(FHH_E_ARG, "ot_extend: NULL argument");
+    const uint64_t mp = ot_padded(m);
+    std::vector<uint32_t> bits(mp / 32, 0);
+    for (uint64_t j = 0; j < m; j++)
+        if (choices[j] & 1) bits[j / 32] |= 1u << (j % 32);
+    uint32_t* ch = nullptr;
+    HIP_TRY(ctx, ot_choices_buffer(ctx, m, &ch));
+    HIP_TRY(ctx, hipMemcpyAsync(ch, bits.data(), mp / 8, hipMemcpyHostToDevice, ctx->stream));
+    DevBuf d0, d1, dout;
+    HIP_TRY(ctx, d0.ensure(m * 16));
+    HIP_TRY(ctx, dout.ensure(m * 16));
+    HIP_TRY(ctx, hipMemcpyAsync(d0.p, x0, m * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (x1) {
+        HIP_TRY(ctx, d1.ensure(m * 16));
+        HIP_TRY(ctx, hipMemcpyAsync(d1.p, x1, m * 16, hipMemcpyHostToDevice, ctx->stream));
+    }
+    OtOut tr;
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
+    if (rc) return rc;
+    uint32_t sw[4], dw[4] = {0, 0, 0, 0};
+    words_from_bytes(base_choice, sw);
+    if (!x1) words_from_bytes(delta, dw);
+    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : dw, dout.as<uint4>(), rk, sw,
+                tweak_base, nullptr, 0, &tr);
+    if (rc) return rc;
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, m * 16, hipMemcpyDeviceToHost));
+    if (y0_out) HIP_TRY(ctx, hipMemcpy(y0_out, tr.Y0, m * 16, hipMemcpyDeviceToHost));
+    if (y1_out) HIP_TRY(ctx, hipMemcpy(y1_out, tr.Y1, m * 16, hipMemcpyDeviceToHost));
+    if (u_out) {   // rows [128][ceil(m / 128)] of the padded [128][mp / 128] matrix
+        const uint64_t nb = (m + 127) / 128;
+        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
+    }
+    return FHH_OK;
+}
+
+}  // extern "C"
+
+// ================================================================================================
+// Two-party split of a level's GC equality test + OT (collect.rs:419-482 with gc_sender = true on
+// server 0 and false on server 1; equalitytest.rs:25-106). Each server's ctx runs only its own
+// half and keeps its own secrets; what crosses is five byte buffers per level, in protocol order:
+//   G -> E  gc      the garbled tables, the garbler's active labels (+ mask wire), decode bits
+//   E -> G  u1      OT 1 (the evaluator's input labels, equalitytest.rs:67-82, 108-119): U
+//   G -> E  y1      OT 1: Y0 | Y1
+//   E -> G  u2      OT 2 (the share conversion, collect.rs:437-471 / 846-876): U
+//   G -> E  y2      OT 2: Y0 | Y1
+// Buffers are device memory owned by the producing ctx (valid until its next party call); the
+// caller moves them (a network in a deployment, a device copy in the in-process tests).
+// ================================================================================================
+namespace fhh {
+namespace eng {
+
+struct PartyState {
+    int role = -1;              // 0 garbler / OT sender (server 0), 1 evaluator / OT receiver (server 1)
+    int step = 0;               // protocol position (calls must come in order)
+    bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
+    uint64_t C = 0, n = 0, npad = 0, nw = 0, tests = 0, m1 = 0, m2 = 0;
+    uint32_t bits = 0, mask = 0, per2 = 1;
+    uint32_t delta[4] = {0, 0, 0, 0};
+    uint32_t s[2][4] = {};      // sender's base choice words per OT
+    GcArgs g{};                 // garbler: the level's garbling arguments
+    DevBuf planes;              // own share planes [C][bits][nw] (evaluator: OT 1's choice bits)
+    DevBuf gc;                  // garbler: the gc message; evaluator: unused
+    DevBuf labels;              // garbler: OT 1 inputs (evaluator zero labels); evaluator: OT 1 outputs
+    DevBuf x0, x1;              // garbler: OT 2 messages (r0 / r1 ordered by the mask)
+    DevBuf rk;                  // base-OT key schedules [3][128][44] of the current OT, own rows only
+    DevBuf T, U, Q, Y;          // OT matrices (T / Q private) and messages (U or Y0 | Y1)
+    DevBuf choices2;            // evaluator: the GC outputs packed as OT 2's choice words
+    DevBuf out;                 // evaluator: GC output bytes (eq ^ mask)
+    DevBuf recv;                // evaluator: OT 2 outputs = its node values
+    std::vector<uint32_t> rk_host;
+    uint64_t bytes_sent = 0;    // this ctx's outgoing message bytes for the level
+};
+
+void party_destroy(fhh_ctx* ctx) {
+    delete ctx->party;
+    ctx->party = nullptr;
+}
+
+namespace {
+
+PartyState& party_of(fhh_ctx* ctx) {
+    if (!ctx->party) ctx->party = new PartyState();
+    return *ctx->party;
+}
+
+int party_begin(fhh_ctx* ctx, int role) {
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (ctx->group) return ctx->fail(FHH_E_ARG, "party: run the GC + OT per shard (fhh_shard_ctx)");
+    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
+        return ctx->fail(FHH_E_STATE, "party: needs a pending tree_crawl / tree_crawl_last");
+    if (2 * ctx->d > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "party: d <= 4");
+    PartyState& P = party_of(ctx);
+    P.role = role;
+    P.step = 0;
+    P.last = ctx->phase == Phase::kPendingLast;
+    P.C = ctx->pending_C;
+    P.n = ctx->n;
+    P.npad = ctx->npad;
+    P.nw = ctx->nw;
+    P.bits = 2 * ctx->d;
+    P.tests = P.C * P.n;
+    P.per2 = P.last ? 2 : 1;
+    P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
+    P.m2 = P.tests * P.per2;
+    P.bytes_sent = 0;
+    // this server's share planes [C][bits][nw] (collect.rs:393-418)
+    HIP_TRY(ctx, P.planes.ensure(std::max<uint64_t>(P.C * P.bits * P.nw, 1) * 8));
+    if (P.C) {
+        ChildArgs a = ctx_child_args(ctx);
+        HIP_TRY(ctx, launch_share_planes(a, P.planes.as<uint64_t>(), ctx->stream));
+    }
+    return FHH_OK;
+}
+
+// key schedules of one OT's base OTs into P.rk: receiver rows 0 / 1 from both seeds of each base
+// OT, sender row 2 from its chosen seeds (the other party's rows stay zero: never read)
+int party_keys(fhh_ctx* ctx, PartyState& P, const uint8_t* pairs /*[128][2][16] or null*/,
+               const uint8_t* chosen /*[128][16] or null*/) {
+    P.rk_host.assign((size_t)3 * 128 * 44, 0);
+    for (int i = 0; i < 128; i++) {
+        uint32_t w[11][4];
+        for (int b = 0; b < 2 && pairs; b++) {
+            host_key_schedule(pairs + ((size_t)i * 2 + b) * 16, w);
+            std::memcpy(P.rk_host.data() + ((size_t)b * 128 + i) * 44, w, 44 * 4);
+        }
+        if (chosen) {
+            host_key_schedule(chosen + (size_t)i * 16, w);
+            std::memcpy(P.rk_host.data() + ((size_t)2 * 128 + i) * 44, w, 44 * 4);
+        }
+    }
+    HIP_TRY(ctx, P.rk.ensure(P.rk_host.size() * 4));
+    HIP_TRY(ctx, hipMemcpyAsync(P.rk.p, P.rk_host.data(), P.rk_host.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    // the staging vector is rewritten by the next call: finish the copy now
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return FHH_OK;
+}
+
+OtArgs party_ot(PartyState& P, uint64_t m) {
+    OtArgs a{};
+    a.m = m;
+    a.mp = ot_padded(m);
+    a.rk = P.rk.as<uint32_t>();
+    a.T = P.T.as<uint4>();
+    a.U = P.U.as<uint4>();
+    a.Q = P.Q.as<uint4>();
+    return a;
+}
+
+int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver) {
+    const uint64_t rows = 16 * ot_padded(m);   // [128][mp / 128] blocks
+    HIP_TRY(ctx, (receiver ? P.T : P.Q).ensure(rows));
+    if (receiver) HIP_TRY(ctx, P.U.ensure(rows));
+    else HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 32));
+    return FHH_OK;
+}
+
+// message sizes
+uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
+uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)(2 * (P.bits - 1) + P.bits + 1) * 16 + 1); }
+
+int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const char* what) {
+    if (want && !p) return ctx->fail(FHH_E_ARG, std::string("party: NULL ") + what);
+    if (got != want)
+        return ctx->fail(FHH_E_ARG, std::string("party: ") + what + " is " + std::to_string(got) + " bytes, expected " +
+                                        std::to_string(want));
+    return FHH_OK;
+}
+
+// carve the gc message [tables | garbler labels | decode]
+void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
+    const uint64_t t = P.tests;
+    g.tables = reinterpret_cast<uint4*>(base);
+    g.gb_labels = reinterpret_cast<uint4*>(base + (uint64_t)2 * (P.bits - 1) * t * 16);
+    g.decode = base + (uint64_t)(2 * (P.bits - 1) + P.bits + 1) * t * 16;
+}
+
+}  // namespace
+}  // namespace eng
+}  // namespace fhh
+
+extern "C" {
+
+int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes) {
+    CTX_CHECK(ctx);
+    if (!cfg || !gc_msg_dev || !gc_msg_bytes) return ctx->fail(FHH_E_ARG, "gb_garble: NULL argument");
+    int rc = party_begin(ctx, 0);
+    if (rc) return rc;
+    PartyState& P = *ctx->party;
+    P.mask = cfg->mask & 1u;
+    words_from_bytes(cfg->base_choice[0], P.s[0]);
+    words_from_bytes(cfg->base_choice[1], P.s[1]);
+    // garbling (multiple_gb_equality_test, equalitytest.rs:25-65): the evaluator's zero labels are
+    // stored as OT 1's sender inputs at the OT index of the evaluator's choice bits
+    HIP_TRY(ctx, P.gc.ensure(std::max<uint64_t>(gc_bytes(P), 1)));
+    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
+    fhh_gc_batch gb{};
+    gb.groups = P.C;
+    gb.clients = (uint32_t)P.n;
+    gb.words = (uint32_t)P.nw;
+    gb.bits = P.bits;
+    gb.mask = P.mask;
+    std::memcpy(gb.label_key, cfg->label_key, 16);
+    std::memcpy(gb.delta, cfg->delta, 16);
+    gb.gb_planes_dev = P.planes.as<uint64_t>();
+    gb.ev_planes_dev = P.planes.as<uint64_t>();   // not read: the evaluator's labels go by OT
+    gb.tables_dev = P.gc.as<uint8_t>();
+    gb.gb_labels_dev = P.gc.as<uint8_t>();
+    gb.ev_labels_dev = P.labels.as<uint8_t>();
+    gb.decode_dev = P.gc.as<uint8_t>();
+    gb.out_dev = P.gc.as<uint8_t>();
+    rc = gc_args(ctx, &gb, P.g);
+    if (rc) return rc;
+    gc_layout(P, P.gc.as<uint8_t>(), P.g);
+    P.g.ev_ot = 1;
+    P.g.out = nullptr;
+    for (int c = 0; c < 4; c++) P.delta[c] = P.g.delta[c];
+    if (P.tests) HIP_TRY(ctx, launch_gc_garble(P.g, ctx->stream));
+    // OT 2's messages: (r0, r1) if the mask is set, else (r1, r0) (collect.rs:439-452, 846-866); the
+    // garbler's node value is r1
+    HIP_TRY(ctx, P.x0.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+    HIP_TRY(ctx, P.x1.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+    if (P.tests) {
+        ChildArgs a = ctx_child_args(ctx);
+        a.prf_seed = cfg->share_seed;
+        a.gc_N = (uint32_t)P.n;
+        if (P.last) HIP_TRY(ctx, launch_ot_fe255_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
+        else HIP_TRY(ctx, launch_ot_fe_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
+    }
+    // both OTs' sender schedules now (OtSender::init per OT, collect.rs:454-471)
+    rc = party_keys(ctx, P, nullptr, &cfg->base_chosen[0][0][0]);
+    if (rc) return rc;
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 1;
+    *gc_msg_dev = P.gc.as<uint8_t>();
+    *gc_msg_bytes = gc_bytes(P);
+    P.bytes_sent += *gc_msg_bytes;
+    // keep OT 2's chosen seeds for fhh_gb_ot_shares
+    P.rk_host.resize((size_t)3 * 128 * 44 + 128 * 16);
+    std::memcpy(reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), &cfg->base_chosen[1][0][0],
+                128 * 16);
+    return FHH_OK;
+}
+
+static int gb_ot_send(fhh_ctx* ctx, int which, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev,
+                      uint64_t* y_bytes) {
+    CTX_CHECK(ctx);
+    if (!y_dev || !y_bytes) return ctx->fail(FHH_E_ARG, "gb_ot: NULL output");
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    PartyState* Pp = ctx->party;
+    if (!Pp || Pp->role != 0 || Pp->step != 1 + which)
+        return ctx->fail(FHH_E_STATE, which ? "gb_ot_shares: call after fhh_gb_ot_labels" : "gb_ot_labels: call after fhh_gb_garble");
+    PartyState& P = *Pp;
+    const uint64_t m = which ? P.m2 : P.m1;
+    rc = check_in(ctx, u_dev, u_len, m ? u_bytes(m) : 0, "U");
+    if (rc) return rc;
+    if (which) {   // OT 2's schedules from the chosen seeds kept by fhh_gb_garble
+        std::vector<uint8_t> chosen(128 * 16);
+        std::memcpy(chosen.data(), reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), 128 * 16);
+        rc = party_keys(ctx, P, nullptr, chosen.data());
+        if (rc) return rc;
+    }
+    rc = party_ot_buffers(ctx, P, m, false);
+    if (rc) return rc;
+    if (m) {
+        OtArgs a = party_ot(P, m);
+        a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
+        for (int c = 0; c < 4; c++) a.s[c] = P.s[which][c];
+        a.Y0 = P.Y.as<uint4>();
+        a.Y1 = P.Y.as<uint4>() + m;
+        if (which) {
+            a.x0 = P.x0.as<uint4>();
+            a.x1 = P.x1.as<uint4>();
+        } else {   // correlated: x1 = x0 ^ Delta (the evaluator's one labels)
+            a.x0 = P.labels.as<uint4>();
+            a.x1 = nullptr;
+            for (int c = 0; c < 4; c++) a.delta[c] = P.delta[c];
+        }
+        HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
+        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // Y0, Y1
+    }
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 2 + which;
+    *y_dev = P.Y.as<uint8_t>();
+    *y_bytes = m * 32;
+    P.bytes_sent += *y_bytes;
+    return FHH_OK;
+}
+
+int fhh_gb_ot_labels(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev, uint64_t* y_bytes) {
+    return gb_ot_send(ctx, 0, u_dev, u_len, y_dev, y_bytes);
+}
+
+int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev, uint64_t* y_bytes) {
+    return gb_ot_send(ctx, 1, u_dev, u_len, y_dev, y_bytes);
+}
+
+int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** u_dev, uint64_t* u_len) {
+    CTX_CHECK(ctx);
+    if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
+    int rc = party_begin(ctx, 1);
+    if (rc) return rc;
+    PartyState& P = *ctx->party;
+    // OT 1's receiver: choice bits = this server's share planes as they stand (m1 = C bits npad)
+    rc = party_keys(ctx, P, &cfg->base_pairs[0][0][0][0], nullptr);
+    if (rc) return rc;
+    // keep OT 2's seed pairs for fhh_ev_evaluate
+    P.rk_host.resize((size_t)3 * 128 * 44 + 128 * 32);
+    std::memcpy(reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), &cfg->base_pairs[1][0][0][0],
+                128 * 32);
+    rc = party_ot_buffers(ctx, P, P.m1, true);
+    if (rc) return rc;
+    if (P.m1) {
+        OtArgs a = party_ot(P, P.m1);
+        a.choices = P.planes.as<uint32_t>();
+        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));   // T, U
+    }
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 1;
+    *u_dev = P.U.as<uint8_t>();
+    *u_len = P.m1 ? u_bytes(P.m1) : 0;
+    P.bytes_sent += *u_len;
+    return FHH_OK;
+}
+
+int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, const uint8_t* y_dev, uint64_t y_len,
+                    const uint8_t** u_dev, uint64_t* u_len) {
+    CTX_CHECK(ctx);
+    if (!u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_evaluate: NULL output");
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    PartyState* Pp = ctx->party;
+    if (!Pp || Pp->role != 1 || Pp->step != 1) return ctx->fail(FHH_E_STATE, "ev_evaluate: call after fhh_ev_ot_labels");
+    PartyState& P = *Pp;
+    rc = check_in(ctx, gc_msg_dev, gc_len, gc_bytes(P), "gc message");
+    if (rc) return rc;
+    rc = check_in(ctx, y_dev, y_len, P.m1 * 32, "Y (labels OT)");
+    if (rc) return rc;
+    // 1. OT 1 output: the evaluator's active input labels (ev_set_fancy_inputs, equalitytest.rs:108-119)
+    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
+    if (P.m1) {
+        OtArgs a = party_ot(P, P.m1);
+        a.choices = P.planes.as<uint32_t>();
+        a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
+        a.Y1 = a.Y0 + P.m1;
+        a.out = P.labels.as<uint4>();
+        HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
+    }
+    // 2. evaluate (multiple_ev_equality_test); the outputs are packed as OT 2's choice words
+    const uint64_t mp2 = ot_padded(std::max<uint64_t>(P.m2, 1));
+    HIP_TRY(ctx, P.choices2.ensure(mp2 / 8 + 64));
+    HIP_TRY(ctx, hipMemsetAsync(P.choices2.p, 0, mp2 / 8 + 64, ctx->stream));
+    HIP_TRY(ctx, P.out.ensure(std::max<uint64_t>(P.tests, 1)));
+    GcArgs g{};
+    g.G = P.C;
+    g.N = (uint32_t)P.n;
+    g.nw = (uint32_t)P.nw;
+    g.bits = P.bits;
+    gc_layout(P, const_cast<uint8_t*>(gc_msg_dev), g);
+    g.ev_labels = P.labels.as<uint4>();
+    g.ev_ot = 1;
+    g.out = P.out.as<uint8_t>();
+    g.out_packed = P.choices2.as<uint32_t>();
+    g.out_dup = P.per2;
+    if (P.tests) HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
+    // 3. OT 2's receiver: choice = the GC output (collect.rs:461-471); T and U reused
+    std::vector<uint8_t> pairs(128 * 32);
+    std::memcpy(pairs.data(), reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), 128 * 32);
+    rc = ctx_sync(ctx);   // the evaluation read the previous schedules' neighbours only; drain before re-keying
+    if (rc) return rc;
+    rc = party_keys(ctx, P, pairs.data(), nullptr);
+    if (rc) return rc;
+    rc = party_ot_buffers(ctx, P, P.m2, true);
+    if (rc) return rc;
+    if (P.m2) {
+        OtArgs a = party_ot(P, P.m2);
+        a.choices = P.choices2.as<uint32_t>();
+        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));
+    }
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 2;
+    *u_dev = P.U.as<uint8_t>();
+    *u_len = P.m2 ? u_bytes(P.m2) : 0;
+    P.bytes_sent += *u_len;
+    return FHH_OK;
+}
+
+int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_len) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    PartyState* Pp = ctx->party;
+    if (!Pp || Pp->role != 1 || Pp->step != 2) return ctx->fail(FHH_E_STATE, "ev_ot_shares: call after fhh_ev_evaluate");
+    PartyState& P = *Pp;
+    rc = check_in(ctx, y_dev, y_len, P.m2 * 32, "Y (shares OT)");
+    if (rc) return rc;
+    HIP_TRY(ctx, P.recv.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+    if (P.m2) {
+        OtArgs a = party_ot(P, P.m2);
+        a.choices = P.choices2.as<uint32_t>();
+        a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
+        a.Y1 = a.Y0 + P.m2;
+        a.out = P.recv.as<uint4>();
+        HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
+    }
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 3;
+    return FHH_OK;
+}
+
+int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
+    CTX_CHECK(ctx);
+    if (ctx->group) {
+        // every shard ran its own channel (fhh_shard_ctx); sum the shards' device values
+        int S = 0;
+        int rc = fhh_shard_info(ctx, 0, &S, nullptr, nullptr, nullptr, nullptr);
+        if (rc) return rc;
+        std::vector<const void*> v((size_t)S, nullptr);
+        int last = -1;
+        for (int k = 0; k < S; k++) {
+            fhh_ctx* sh = nullptr;
+            uint64_t nk = 0;
+            rc = fhh_shard_ctx(ctx, k, &sh);
+            if (!rc) rc = fhh_shard_info(ctx, k, nullptr, nullptr, nullptr, &nk, nullptr);
+            if (rc) return rc;
+            if (!nk) continue;
+            PartyState* P = sh->party;
+            if (!P || P->step != 3) return ctx->fail(FHH_E_STATE, "party_node_sums: shard " + std::to_string(k) +
+                                                                  "'s OTs are not finished");
+            if (last >= 0 && last != (int)P->last) return ctx->fail(FHH_E_STATE, "party_node_sums: shards disagree");
+            last = P->last;
+            v[(size_t)k] = P->role == 0 ? (P->mask ? P->x1.p : P->x0.p) : P->recv.p;
+        }
+        if (last < 0) return ctx->fail(FHH_E_STATE, "party_node_sums: no shard holds clients");
+        const uint32_t fmt = last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
+        return group_node_sums(ctx, v.data(), false, 0, fmt, sums_a, sums_b);   // ld 0: each shard's n
+    }
+    PartyState* Pp = ctx->party;
+    if (!Pp || Pp->step != 3) return ctx->fail(FHH_E_STATE, "party_node_sums: the level's OTs are not finished");
+    PartyState& P = *Pp;
+    // the garbler's value is r1 = its message for the mask's other side, the evaluator's its OT output;
+    // rows of n values, FE in a block's low 8 bytes, FieldElm as a BlockPair (2 blocks)
+    const void* v = P.role == 0 ? (P.mask ? P.x1.p : P.x0.p) : P.recv.p;
+    const uint32_t fmt = P.last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
+    const void* vv[1] = {v};
+    if (P.last) return fhh_node_sums_fe255_device(ctx, vv, P.n, fmt, static_cast<uint32_t*>(sums_a), static_cast<uint32_t*>(sums_b));
+    return fhh_node_sums_fe_device(ctx, vv, P.n, fmt, static_cast<uint64_t*>(sums_a));
+}
+
+int fhh_party_bytes_sent(const fhh_ctx* ctx, uint64_t* bytes) {
+    CTX_CHECK(ctx);
+    if (bytes) *bytes = ctx->party ? ctx->party->bytes_sent : 0;
+    return FHH_OK;
+}
+
+int fhh_gc_party_level_cfg(uint64_t prf_seed, uint32_t level, fhh_gc_party_cfg* out) {
+    if (!out) {
+        g_err = "gc_party_level_cfg: NULL output";
+        return FHH_E_ARG;
+    }
+    std::memset(out, 0, sizeof(*out));
+    gc_level_material(prf_seed, level, out->label_key, out->delta, &out->mask);
+    out->share_seed = prf_seed;
+    for (uint32_t salt = 0; salt < 2; salt++) {
+        uint32_t sw[4];
+        ot_level_choice(prf_seed, level, salt, sw);
+        std::memcpy(out->base_choice[salt], sw, 16);
+        for (uint32_t i = 0; i < 128; i++) {
+            const uint32_t si = (sw[i >> 5] >> (i & 31)) & 1u;
+            for (uint32_t b = 0; b < 2; b++) {
+                // k_ot_level_keys' seeds (fhh_ot.hip ot_seed_word): the level loop's ideal base OTs
+                const uint64_t z = host_mix64(prf_seed ^ 0x6f745f62617365ull ^ ((uint64_t)level << 24) ^
+                                              ((uint64_t)salt << 20) ^ ((uint64_t)i << 2) ^ b);
+                const uint64_t lo = z, hi = host_mix64(z);
+                std::memcpy(out->base_pairs[salt][i][b], &lo, 8);
+                std::memcpy(out->base_pairs[salt][i][b] + 8, &hi, 8);
+            }
+            std::memcpy(out->base_chosen[salt][i], out->base_pairs[salt][i][si], 16);
+        }
+    }
+    return FHH_OK;
+}
+
+}  // extern "C"

@@ -7,10 +7,8 @@
 // per-dim prefix tables that live on the GPU (fhh_internal.h); pruning edits index lists
 // on the host and never moves state (the reference does O(F) Vec::remove of whole nodes,
 // collect.rs:918-929).
-#include "fhh_internal.h"
-#include "field_arith.h"
+#include "fhh_engine.h"
 #include "aes_tables.h"
-#include "../../include/fhh.h"
 
 #include <hip/hip_runtime.h>
 
@@ -29,163 +27,12 @@
 #include <unordered_map>
 #include <vector>
 
-using namespace fhh;
+thread_local std::string fhh::eng::g_err;
 
 namespace {
-
-thread_local std::string g_err;
 
 constexpr int kDefaultVariant = 52;  // 4 tables, 128 KiB, 1024 thr, dynamic items (first one static, multi-word on narrow levels), <= 16 entries per item, nontemporal parent-seed loads and child-seed stores, sibling-pair AES (r02b A/Bs vs 34, 51)
 
-constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;   // fastfield.rs:24-28
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { release(); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    // grow-only; contents are NOT preserved
-    hipError_t ensure(size_t nbytes) {
-        if (nbytes <= bytes && p) return hipSuccess;
-        release();
-        if (nbytes == 0) nbytes = 256;
-        hipError_t e = hipMalloc(&p, nbytes);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return e;
-        }
-        bytes = nbytes;
-        return hipSuccess;
-    }
-    template <class T> T* as() const { return static_cast<T*>(p); }
-};
-
-struct PinnedBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    ~PinnedBuf() {
-        if (p) (void)hipHostFree(p);
-    }
-    hipError_t ensure(size_t nbytes) {
-        if (nbytes <= bytes && p) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-        if (nbytes == 0) nbytes = 256;
-        hipError_t e = hipHostMalloc(&p, nbytes, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return e;
-        }
-        bytes = nbytes;
-        return hipSuccess;
-    }
-    template <class T> T* as() const { return static_cast<T*>(p); }
-};
-
-struct DimTable {
-    DevBuf seed[2], t[2], y[2];
-    size_t cap[2] = {0, 0};       // entries
-    int cur = 0;                  // buffer that holds the frontier's entries
-    std::vector<uint32_t> live;   // frontier entries (indices into buffer `cur`), ordered
-};
-
-struct Node {
-    uint32_t pos[kMaxDims];       // position of the node's dim-j entry in tab[j].live
-};
-
-enum class Phase { kNoInit, kFrontier, kPending, kPendingLast };
-
-// 320-bit little-endian u32 helpers for FE255 (field.rs)
-using Limbs10 = std::array<uint32_t, 10>;
-
-}  // namespace
-
-struct fhh_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;       // execution stream (own_stream, or the peer's in pair mode)
-    hipStream_t own_stream = nullptr;
-    fhh_ctx* peer = nullptr;            // pair mode: ctx whose staging/timing this ctx's syncs also retire
-    uint32_t L = 0, d = 0, K = 0;
-    uint64_t n = 0, npad = 0, nw = 0;
-    uint64_t client_base = 0;
-    int variant = 0;              // k_expand variant (fhh_set_variant)
-    int grid = 0;
-    uint32_t loop_cap_hint = 0;   // device loop: capacity the previous crawl grew to
-    DevBuf work_counter;          // dynamic item distribution
-
-    // host-staged keys (add_key); uploaded at tree_init
-    std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;
-    uint64_t h_n = 0;
-    bool dev_keys = false;        // keys resident on the device (uploaded or generated)
-    bool keys_bs = false;         // cw_seed / root_seed rows in the bitsliced layout
-    bool tab_bs = false;          // prefix tables (since the last tree_init) in the bitsliced layout
-
-    DevBuf cw_seed, cw_bits, root_seed, key_idx, valid;
-    DimTable tab[kMaxDims];
-
-    Phase phase = Phase::kNoInit;
-    uint32_t level = 0;           // depth of the frontier (= CorWord index of next crawl)
-    std::vector<Node> frontier;
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hist;   // per depth: (parent, i)
-    uint64_t pending_C = 0;
-    int child_buf[kMaxDims] = {0};
-    DevBuf lists;                 // per crawl: live lists of every dim + parent_pos, one upload
-    const uint32_t* live_ptr[kMaxDims] = {nullptr};
-    const uint32_t* parent_pos_ptr = nullptr;   // [F][d] u32 for pending children
-
-    // frontier_last (collect.rs:33, 909-914): surviving (parent, i) + values
-    std::vector<std::pair<uint32_t, uint32_t>> last_nodes;
-    std::vector<Limbs10> last_values;
-    uint32_t last_depth = 0;
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> last_hist;
-
-    DevBuf scratch, scratch2;
-    DevBuf ot_buf[8], ot_rk;                     // OT extension scratch (T U Q - - Y0 Y1 choices)
-    std::vector<uint32_t> ot_rk_host;            // key schedules staged for ot_rk
-    std::vector<PinnedBuf*> stage;   // pinned staging for async H2D, recycled at every sync
-    size_t stage_used = 0;
-
-    fhh_stats stats{};
-    bool timing = true;
-    uint32_t timing_every = 1;   // device level loop: time every K-th k_expand launch
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
-    std::vector<std::pair<size_t, uint64_t>> ev_pending;   // (pool index, blocks)
-    size_t ev_next = 0;
-
-    std::string err;
-
-    int fail(int code, const std::string& msg) {
-        err = msg;
-        g_err = msg;
-        return code;
-    }
-};
-
-#define CTX_CHECK(ctx)                                              \
-    do {                                                            \
-        if (!(ctx)) {                                               \
-            g_err = "null fhh_ctx";                                 \
-            return FHH_E_ARG;                                       \
-        }                                                           \
-    } while (0)
-
-#define HIP_TRY(ctx, expr)                                                                   \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess)                                                                \
-            return (ctx)->fail(e_ == hipErrorOutOfMemory ? FHH_E_NOMEM : FHH_E_HIP,          \
-                               std::string(#expr) + ": " + hipGetErrorString(e_));          \
-    } while (0)
-
-namespace {
 
 // ---- timing -------------------------------------------------------------------------------
 hipError_t timing_begin(fhh_ctx* ctx, size_t* slot) {
@@ -598,16 +445,6 @@ ChildArgs child_args(fhh_ctx* c0, fhh_ctx* c1) {
     return a;
 }
 
-int share_planes_out(fhh_ctx* ctx, uint64_t* host_out) {
-    if (!host_out || ctx->pending_C == 0) return FHH_OK;
-    const size_t words = ctx->pending_C * 2 * ctx->d * ctx->nw;
-    HIP_TRY(ctx, ctx->scratch.ensure(words * 8));
-    ChildArgs a = child_args(ctx, nullptr);
-    HIP_TRY(ctx, launch_share_planes(a, ctx->scratch.as<uint64_t>(), ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(host_out, ctx->scratch.p, words * 8, hipMemcpyDeviceToHost, ctx->stream));
-    return sync(ctx);
-}
-
 int prune_impl(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
     if (ctx->phase != Phase::kPending) return ctx->fail(FHH_E_STATE, "tree_prune without a pending tree_crawl");
     if (n != ctx->pending_C)
@@ -748,183 +585,118 @@ int set_device(fhh_ctx* ctx) {
 
 }  // namespace
 
-// ---- garbled-circuit equality test helpers (row f1) ------------------------------------------
-namespace {
-// FIPS-197 key expansion on little-endian column words (RotWord = rotr 8, rcon in byte 0), the
-// convention of the device T-table rounds (aes_keyed.h)
-void host_key_schedule(const uint8_t key[16], uint32_t (&rk)[11][4]) {
-    uint32_t w[44];
-    for (int i = 0; i < 4; i++)
-        w[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
-               ((uint32_t)key[4 * i + 3] << 24);
-    uint32_t rcon = 1;
-    for (int i = 4; i < 44; i++) {
-        uint32_t t = w[i - 1];
-        if (i % 4 == 0) {
-            t = (t >> 8) | (t << 24);
-            t = (uint32_t)SBOX.v[t & 0xFF] | ((uint32_t)SBOX.v[(t >> 8) & 0xFF] << 8) |
-                ((uint32_t)SBOX.v[(t >> 16) & 0xFF] << 16) | ((uint32_t)SBOX.v[t >> 24] << 24);
-            t ^= rcon;
-            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0)) & 0xFF;
+namespace fhh {
+namespace eng {
+int ctx_sync(fhh_ctx* ctx) { return sync(ctx); }
+int ctx_set_device(fhh_ctx* ctx) { return set_device(ctx); }
+ChildArgs ctx_child_args(fhh_ctx* ctx) { return child_args(ctx, nullptr); }
+
+int crawl_level(fhh_ctx* ctx, bool last, uint64_t* n_children, uint64_t* planes, uint64_t pitch_words,
+                uint64_t word_off) {
+    int rc = crawl_one(ctx, last);
+    if (rc) return rc;
+    if (n_children) *n_children = ctx->pending_C;
+    if (planes && ctx->pending_C) {
+        // k_share_planes writes [C][2d][nw] on the device; one strided copy lands this ctx's words
+        // in the caller's rows (the gather of a multi-device ctx costs no host pass)
+        const size_t rows = ctx->pending_C * 2 * ctx->d;
+        HIP_TRY(ctx, ctx->scratch.ensure(rows * ctx->nw * 8));
+        ChildArgs a = child_args(ctx, nullptr);
+        HIP_TRY(ctx, launch_share_planes(a, ctx->scratch.as<uint64_t>(), ctx->stream));
+        HIP_TRY(ctx, hipMemcpy2DAsync(planes + word_off, pitch_words * 8, ctx->scratch.p, ctx->nw * 8, ctx->nw * 8, rows,
+                                      hipMemcpyDeviceToHost, ctx->stream));
+    }
+    return sync(ctx);
+}
+
+bool fmt_is_fe255(uint32_t fmt) { return fmt == FHH_VALS_FE255_LIMBS || fmt == FHH_VALS_FE255_BLOCKPAIR; }
+
+static size_t fmt_bytes(uint32_t fmt) {
+    return fmt == FHH_VALS_FE_U64 ? 8 : fmt == FHH_VALS_FE_BLOCK ? 16 : 32;
+}
+
+int node_partials(fhh_ctx* ctx, const void* vals, uint32_t fmt, uint64_t ld, uint64_t col0, bool host,
+                  uint64_t** partials_dev) {
+    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
+        return ctx->fail(FHH_E_STATE, "node_sums without a pending crawl");
+    if (fmt > FHH_VALS_FE255_BLOCKPAIR) return ctx->fail(FHH_E_ARG, "node_sums: unknown value format");
+    const uint64_t C = ctx->pending_C, n = ctx->n;
+    const size_t eb = fmt_bytes(fmt), per = fmt_is_fe255(fmt) ? 8 : 2;
+    HIP_TRY(ctx, ctx->scratch2.ensure(std::max<uint64_t>(C, 1) * per * 8));
+    *partials_dev = ctx->scratch2.as<uint64_t>();
+    if (C == 0) return FHH_OK;
+    if (!vals) return ctx->fail(FHH_E_ARG, "node_sums: NULL values");
+    if (ld < col0 + n) return ctx->fail(FHH_E_ARG, "node_sums: row pitch shorter than the client count");
+    const void* src = vals;
+    uint64_t pitch = ld;
+    if (host) {
+        // this ctx's column block of the caller's [C][ld] rows, one strided host-to-device copy
+        HIP_TRY(ctx, ctx->scratch.ensure(C * n * eb));
+        HIP_TRY(ctx, hipMemcpy2DAsync(ctx->scratch.p, n * eb, static_cast<const uint8_t*>(vals) + col0 * eb, ld * eb,
+                                      n * eb, C, hipMemcpyHostToDevice, ctx->stream));
+        src = ctx->scratch.p;
+        pitch = n;
+    }
+    HIP_TRY(ctx, launch_sum_vals(src, fmt, C, n, pitch, *partials_dev, ctx->stream));
+    return FHH_OK;
+}
+
+int node_sums_finish(fhh_ctx* ctx, const uint64_t* h, uint32_t fmt, void* out_a, void* out_b) {
+    const uint64_t C = ctx->pending_C;
+    if (!fmt_is_fe255(fmt)) {
+        if (C && !out_a) return ctx->fail(FHH_E_ARG, "node_sums_fe: NULL sums");
+        uint64_t* sums = static_cast<uint64_t*>(out_a);
+        for (uint64_t c = 0; c < C; c++) sums[c] = fe_canon_from_limbs(h[2 * c], h[2 * c + 1]);
+        return FHH_OK;
+    }
+    uint32_t* unr = static_cast<uint32_t*>(out_a);
+    uint32_t* can = static_cast<uint32_t*>(out_b);
+    for (uint64_t c = 0; c < C; c++) {
+        Limbs10 v = limbs_from_partials(&h[c * 8]);
+        if (unr) std::memcpy(unr + c * 10, v.data(), 40);
+        if (can) {
+            auto r = ::fe255_reduce(v);
+            std::memcpy(can + c * 8, r.data(), 32);
         }
-        w[i] = w[i - 4] ^ t;
-    }
-    for (int r = 0; r < 11; r++)
-        for (int c = 0; c < 4; c++) rk[r][c] = w[4 * r + c];
-}
-
-void words_from_bytes(const uint8_t b[16], uint32_t (&w)[4]) {
-    for (int c = 0; c < 4; c++)
-        w[c] = (uint32_t)b[4 * c] | ((uint32_t)b[4 * c + 1] << 8) | ((uint32_t)b[4 * c + 2] << 16) |
-               ((uint32_t)b[4 * c + 3] << 24);
-}
-
-uint64_t host_mix64(uint64_t z) {
-    z += 0x9e3779b97f4a7c15ull;
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
-
-// the level loop's per-level garbler secrets (a fresh key, Delta and mask per tree_crawl call)
-void gc_level_material(uint64_t prf_seed, uint32_t level, uint8_t key[16], uint8_t delta[16], uint32_t* mask) {
-    uint64_t z = host_mix64(prf_seed ^ 0x67635f6c6576656cull ^ ((uint64_t)level << 20));
-    for (int h = 0; h < 2; h++) {
-        z = host_mix64(z);
-        std::memcpy(key + 8 * h, &z, 8);
-    }
-    for (int h = 0; h < 2; h++) {
-        z = host_mix64(z);
-        std::memcpy(delta + 8 * h, &z, 8);
-    }
-    *mask = (uint32_t)(host_mix64(z) & 1);
-}
-
-// validated GcArgs from a batch (device pointers)
-int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
-    if (!b) return ctx->fail(FHH_E_ARG, "gc: NULL batch");
-    if (b->bits < 1 || b->bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
-    if ((uint64_t)b->words * 64 < b->clients) return ctx->fail(FHH_E_ARG, "gc: words < ceil(clients / 64)");
-    const uint64_t n = b->groups * b->clients;
-    if (n && (!b->gb_planes_dev || !b->ev_planes_dev || !b->gb_labels_dev || !b->ev_labels_dev || !b->decode_dev ||
-              !b->out_dev || (b->bits > 1 && !b->tables_dev)))
-        return ctx->fail(FHH_E_ARG, "gc: NULL device buffer");
-    a = GcArgs{};
-    a.gb_planes = b->gb_planes_dev;
-    a.ev_planes = b->ev_planes_dev;
-    a.G = b->groups;
-    a.N = b->clients;
-    a.nw = b->words;
-    a.bits = b->bits;
-    a.mask = b->mask & 1u;
-    host_key_schedule(b->label_key, a.rk_label);
-    words_from_bytes(b->delta, a.delta);
-    a.delta[0] |= 1u;   // colour bit of Delta = 1 (point-and-permute)
-    a.label_nonce = b->label_nonce;
-    a.gate_base = b->gate_base;
-    a.tables = reinterpret_cast<uint4*>(b->tables_dev);
-    a.gb_labels = reinterpret_cast<uint4*>(b->gb_labels_dev);
-    a.ev_labels = reinterpret_cast<uint4*>(b->ev_labels_dev);
-    a.decode = b->decode_dev;
-    a.out = b->out_dev;
-    a.ctl = nullptr;
-    return FHH_OK;
-}
-}  // namespace
-
-// ---- OT extension runner (row f1's OT) --------------------------------------------------------
-namespace {
-uint64_t ot_padded(uint64_t m) { return (m + 8191) / 8192 * 8192; }
-
-// the sender's base-OT choice bits of a level-loop OT (ideal base OTs; k_ot_level_keys derives
-// the seeds from the same material on the device)
-void ot_level_choice(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s[4]) {
-    const uint64_t z0 = host_mix64(prf ^ 0x6f745f63686f6963ull ^ ((uint64_t)level << 24) ^ ((uint64_t)salt << 20));
-    const uint64_t z1 = host_mix64(z0);
-    s[0] = (uint32_t)z0;
-    s[1] = (uint32_t)(z0 >> 32);
-    s[2] = (uint32_t)z1;
-    s[3] = (uint32_t)(z1 >> 32);
-}
-
-// padded choice-bit buffer of the ctx's OT scratch (mp / 32 words, zero past m)
-hipError_t ot_choices_buffer(fhh_ctx* ctx, uint64_t m, uint32_t** out) {
-    const uint64_t mp = ot_padded(m);
-    hipError_t e = ctx->ot_buf[7].ensure(mp / 8);
-    if (e != hipSuccess) return e;
-    *out = ctx->ot_buf[7].as<uint32_t>();
-    return hipSuccess;
-}
-
-struct OtOut {            // optional transcript (device pointers into the scratch)
-    const uint4* U = nullptr;
-    const uint4* Y0 = nullptr;
-    const uint4* Y1 = nullptr;
-    uint64_t nblk = 0;
-};
-
-// the 3 x 128 base-OT key schedules from host seeds (receiver k_i^0, k_i^1; sender k_i^{s_i}),
-// uploaded and synchronised (the staging vector is reused by the next call)
-int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev) {
-    ctx->ot_rk_host.assign((size_t)3 * 128 * 44, 0);
-    for (int i = 0; i < 128; i++) {
-        const int si = (s[i / 8] >> (i % 8)) & 1;
-        uint32_t rk[11][4];
-        for (int b = 0; b < 3; b++) {
-            host_key_schedule(seeds + (size_t)(i * 2 + (b < 2 ? b : si)) * 16, rk);
-            std::memcpy(ctx->ot_rk_host.data() + ((size_t)b * 128 + i) * 44, rk, 44 * 4);
-        }
-    }
-    HIP_TRY(ctx, ctx->ot_rk.ensure(ctx->ot_rk_host.size() * 4));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->ot_rk.p, ctx->ot_rk_host.data(), ctx->ot_rk_host.size() * 4,
-                                hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    *rk_dev = ctx->ot_rk.as<uint32_t>();
-    return FHH_OK;
-}
-
-// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer; rk_dev: the base-OT
-// key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
-int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
-           const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr) {
-    if (m == 0) return FHH_OK;
-    const uint64_t mp = ot_padded(m);
-    const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
-    for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
-    for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
-    OtArgs a{};
-    a.m = m;
-    a.mp = mp;
-    a.rk = rk_dev;
-    for (int c = 0; c < 4; c++) a.s[c] = s_words[c];
-    a.choices = choices;
-    a.T = ctx->ot_buf[0].as<uint4>();
-    a.U = ctx->ot_buf[1].as<uint4>();
-    a.Q = ctx->ot_buf[2].as<uint4>();
-    a.x0 = x0;
-    a.x1 = x1;
-    if (delta_words)
-        for (int c = 0; c < 4; c++) a.delta[c] = delta_words[c];
-    a.Y0 = ctx->ot_buf[5].as<uint4>();
-    a.Y1 = ctx->ot_buf[6].as<uint4>();
-    a.out = out;
-    a.tweak_base = tweak_base;
-    a.ctl = ctl;
-    a.per_group = per_group;
-    HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
-    HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
-    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1
-    HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
-    if (tr) {
-        tr->U = a.U;
-        tr->Y0 = a.Y0;
-        tr->Y1 = a.Y1;
-        tr->nblk = mp / 128;
+        if (ctx->phase == Phase::kPendingLast) ctx->last_values[c] = v;
     }
     return FHH_OK;
 }
-}  // namespace
+
+int add_keys_bincode_records(fhh_ctx* ctx, uint64_t n, const uint8_t* recs) {
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    if (ctx->dev_keys || ctx->h_n) return ctx->fail(FHH_E_STATE, "add_keys_bincode: ctx already holds keys");
+    const uint64_t KB = 25 + 20ull * ctx->L, R = 8 + (uint64_t)ctx->K * KB, len = 8 + n * R;
+    rc = alloc_keys(ctx, n);
+    if (rc) return rc;
+    DevBuf buf, err;
+    HIP_TRY(ctx, buf.ensure(len + 4));   // k_bincode_cw_tiles reads whole dwords: up to 3 B past len
+    HIP_TRY(ctx, err.ensure(4));
+    HIP_TRY(ctx, hipMemsetAsync(err.p, 0, 4, ctx->stream));
+    // the u64 client count, then the records (a shard of a multi-device ctx uploads its slice)
+    HIP_TRY(ctx, hipMemcpyAsync(buf.p, &n, 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(buf.as<uint8_t>() + 8, recs, n * R, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_keys_from_bincode(buf.as<uint8_t>(), n, ctx->d, ctx->L, (uint32_t)ctx->npad, (uint32_t)ctx->nw,
+                                          ctx->cw_seed.as<uint4>(), ctx->cw_bits.as<uint64_t>(),
+                                          ctx->root_seed.as<uint4>(), ctx->key_idx.as<uint64_t>(), err.as<uint32_t>(),
+                                          ctx->stream));
+    uint32_t herr = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    if (herr) {
+        ctx->n = 0;
+        return ctx->fail(FHH_E_ARG, std::string("add_keys_bincode: malformed request (") +
+                                        ((herr & 1) ? "bool byte > 1 " : "") + ((herr & 2) ? "cor_words length " : "") +
+                                        ((herr & 4) ? "dims per client" : "") + ")");
+    }
+    ctx->dev_keys = true;
+    ctx->keys_bs = false;
+    return FHH_OK;
+}
+}  // namespace eng
+}  // namespace fhh
 
 // ---- device-resident level loop (fhh_sim_crawl, host_loop = 0) ---------------------------------
 // FHH_DEBUG_PHASES=1 prints host wall-clock per crawl phase to stderr (setup / loop / readback)
@@ -1700,6 +1472,8 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
 
 void fhh_destroy(fhh_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->group) return group_destroy(ctx);
+    if (ctx->party) party_destroy(ctx);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& pr : ctx->ev_pool) {
@@ -1713,6 +1487,7 @@ void fhh_destroy(fhh_ctx* ctx) {
 
 int fhh_reset(fhh_ctx* ctx) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_reset(ctx);
     int rc = set_device(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1738,6 +1513,7 @@ int fhh_reset(fhh_ctx* ctx) {
 
 int fhh_set_client_base(fhh_ctx* ctx, uint64_t client_base) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_set_client_base(ctx, client_base);
     ctx->client_base = client_base;
     return FHH_OK;
 }
@@ -1763,6 +1539,7 @@ int fhh_gen_keys_pair(fhh_ctx* c0, fhh_ctx* c1, uint64_t n, const uint8_t* left_
         g_err = "null fhh_ctx";
         return FHH_E_ARG;
     }
+    if (c0->group || c1->group) return group_gen_keys_pair(c0, c1, n, left_bits, right_bits, root_seeds);
     if (c0->device != c1->device || c0->d != c1->d || c0->L != c1->L)
         return c0->fail(FHH_E_ARG, "gen_keys_pair: ctxs differ in device/d/L");
     if (c0->dev_keys || c1->dev_keys || c0->h_n || c1->h_n)
@@ -1819,12 +1596,14 @@ int fhh_gen_keys_pair(fhh_ctx* c0, fhh_ctx* c1, uint64_t n, const uint8_t* left_
 
 int fhh_num_clients(const fhh_ctx* ctx, uint64_t* n) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_num_clients(ctx, n);
     if (n) *n = ctx->dev_keys ? ctx->n : ctx->h_n;
     return FHH_OK;
 }
 
 int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t* cw_seed, uint8_t* cw_bits) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_export_keys(ctx, key_idx, root_seed, cw_seed, cw_bits);
     int rc = set_device(ctx);
     if (rc) return rc;
     if (!ctx->dev_keys) {
@@ -1868,6 +1647,7 @@ int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t*
 
 int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_add_keys_bincode(ctx, req, len);
     int rc = set_device(ctx);
     if (rc) return rc;
     if (!req || len < 8) return ctx->fail(FHH_E_ARG, "add_keys_bincode: buffer shorter than the u64 length");
@@ -1878,34 +1658,12 @@ int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len) {
     if (n == 0) return ctx->fail(FHH_E_ARG, "add_keys_bincode: no clients");
     if (n > (len - 8) / R || 8 + n * R != len)
         return ctx->fail(FHH_E_ARG, "add_keys_bincode: length does not match n clients x n_dims x data_len");
-    rc = alloc_keys(ctx, n);
-    if (rc) return rc;
-    DevBuf buf, err;
-    HIP_TRY(ctx, buf.ensure(len + 4));   // k_bincode_cw_tiles reads whole dwords: up to 3 B past len
-    HIP_TRY(ctx, err.ensure(4));
-    HIP_TRY(ctx, hipMemsetAsync(err.p, 0, 4, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(buf.p, req, len, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, launch_keys_from_bincode(buf.as<uint8_t>(), n, ctx->d, ctx->L, (uint32_t)ctx->npad, (uint32_t)ctx->nw,
-                                          ctx->cw_seed.as<uint4>(), ctx->cw_bits.as<uint64_t>(),
-                                          ctx->root_seed.as<uint4>(), ctx->key_idx.as<uint64_t>(), err.as<uint32_t>(),
-                                          ctx->stream));
-    uint32_t herr = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, ctx->stream));
-    rc = sync(ctx);
-    if (rc) return rc;
-    if (herr) {
-        ctx->n = 0;
-        return ctx->fail(FHH_E_ARG, std::string("add_keys_bincode: malformed request (") +
-                                        ((herr & 1) ? "bool byte > 1 " : "") + ((herr & 2) ? "cor_words length " : "") +
-                                        ((herr & 4) ? "dims per client" : "") + ")");
-    }
-    ctx->dev_keys = true;
-    ctx->keys_bs = false;
-    return FHH_OK;
+    return add_keys_bincode_records(ctx, n, req + 8);
 }
 
 int fhh_tree_init(fhh_ctx* ctx) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_tree_init(ctx);
     int rc = set_device(ctx);
     if (rc) return rc;
     rc = upload_staged_keys(ctx);
@@ -1937,87 +1695,84 @@ int fhh_tree_init(fhh_ctx* ctx) {
 
 int fhh_tree_crawl(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_tree_crawl(ctx, false, n_children, share_planes);
     int rc = set_device(ctx);
     if (rc) return rc;
-    rc = crawl_one(ctx, false);
-    if (rc) return rc;
-    if (n_children) *n_children = ctx->pending_C;
-    rc = share_planes_out(ctx, share_planes);
-    if (rc) return rc;
-    return sync(ctx);
+    return crawl_level(ctx, false, n_children, share_planes, ctx->nw, 0);
 }
 
 int fhh_tree_crawl_last(fhh_ctx* ctx, uint64_t* n_children, uint64_t* share_planes) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_tree_crawl(ctx, true, n_children, share_planes);
     int rc = set_device(ctx);
     if (rc) return rc;
-    rc = crawl_one(ctx, true);
+    return crawl_level(ctx, true, n_children, share_planes, ctx->nw, 0);
+}
+
+// node sums of one ctx (single GPU): partials on the device, one copy back, host finish
+static int node_sums_single(fhh_ctx* ctx, const void* vals, bool host, uint64_t ld, uint32_t fmt, void* out_a,
+                            void* out_b) {
+    int rc = set_device(ctx);
     if (rc) return rc;
-    if (n_children) *n_children = ctx->pending_C;
-    rc = share_planes_out(ctx, share_planes);
+    uint64_t* part = nullptr;
+    rc = node_partials(ctx, vals, fmt, ld, 0, host, &part);
     if (rc) return rc;
-    return sync(ctx);
+    const uint64_t per = fmt_is_fe255(fmt) ? 8 : 2;
+    std::vector<uint64_t> h(ctx->pending_C * per);
+    if (!h.empty()) HIP_TRY(ctx, hipMemcpyAsync(h.data(), part, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    rc = sync(ctx);
+    if (rc) return rc;
+    return node_sums_finish(ctx, h.data(), fmt, out_a, out_b);
 }
 
 int fhh_node_sums_fe(fhh_ctx* ctx, const uint64_t* vals, uint64_t* sums) {
     CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
-        return ctx->fail(FHH_E_STATE, "node_sums without a pending crawl");
-    const uint64_t C = ctx->pending_C, n = ctx->n;
-    if (C == 0) return FHH_OK;
-    if (!vals || !sums) return ctx->fail(FHH_E_ARG, "node_sums_fe: NULL buffer");
-    HIP_TRY(ctx, ctx->scratch.ensure(C * n * 8));
-    HIP_TRY(ctx, ctx->scratch2.ensure(C * 2 * 8));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, vals, C * n * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, launch_sum_fe(ctx->scratch.as<uint64_t>(), C, n, ctx->scratch2.as<uint64_t>(), ctx->stream));
-    std::vector<uint64_t> h(C * 2);
-    HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->scratch2.p, C * 16, hipMemcpyDeviceToHost, ctx->stream));
-    rc = sync(ctx);
-    if (rc) return rc;
-    for (uint64_t c = 0; c < C; c++) sums[c] = fe_canon_from_limbs(h[2 * c], h[2 * c + 1]);
-    return FHH_OK;
+    if (ctx->group) {
+        const void* v[1] = {vals};
+        return group_node_sums(ctx, v, true, 0, FHH_VALS_FE_U64, sums, nullptr);
+    }
+    return node_sums_single(ctx, vals, true, ctx->n, FHH_VALS_FE_U64, sums, nullptr);
 }
 
 int fhh_node_sums_fe255(fhh_ctx* ctx, const uint32_t* vals, uint32_t* sums_unreduced, uint32_t* sums_canonical) {
     CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    if (ctx->phase != Phase::kPending && ctx->phase != Phase::kPendingLast)
-        return ctx->fail(FHH_E_STATE, "node_sums without a pending crawl");
-    const uint64_t C = ctx->pending_C, n = ctx->n;
-    if (C == 0) return FHH_OK;
-    if (!vals) return ctx->fail(FHH_E_ARG, "node_sums_fe255: NULL vals");
-    HIP_TRY(ctx, ctx->scratch.ensure(C * n * 32));
-    HIP_TRY(ctx, ctx->scratch2.ensure(C * 8 * 8));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->scratch.p, vals, C * n * 32, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, launch_sum_fe255(ctx->scratch.as<uint32_t>(), C, n, ctx->scratch2.as<uint64_t>(), ctx->stream));
-    std::vector<uint64_t> h(C * 8);
-    HIP_TRY(ctx, hipMemcpyAsync(h.data(), ctx->scratch2.p, C * 64, hipMemcpyDeviceToHost, ctx->stream));
-    rc = sync(ctx);
-    if (rc) return rc;
-    for (uint64_t c = 0; c < C; c++) {
-        Limbs10 v = limbs_from_partials(&h[c * 8]);
-        if (sums_unreduced) std::memcpy(sums_unreduced + c * 10, v.data(), 40);
-        if (sums_canonical) {
-            auto r = fe255_reduce(v);
-            std::memcpy(sums_canonical + c * 8, r.data(), 32);
-        }
-        if (ctx->phase == Phase::kPendingLast) ctx->last_values[c] = v;
+    if (ctx->group) {
+        const void* v[1] = {vals};
+        return group_node_sums(ctx, v, true, 0, FHH_VALS_FE255_LIMBS, sums_unreduced, sums_canonical);
     }
-    return FHH_OK;
+    return node_sums_single(ctx, vals, true, ctx->n, FHH_VALS_FE255_LIMBS, sums_unreduced, sums_canonical);
+}
+
+int fhh_node_sums_fe_device(fhh_ctx* ctx, const void* const* vals_dev, uint64_t ld, uint32_t format, uint64_t* sums) {
+    CTX_CHECK(ctx);
+    if (format != FHH_VALS_FE_U64 && format != FHH_VALS_FE_BLOCK)
+        return ctx->fail(FHH_E_ARG, "node_sums_fe_device: format must be FHH_VALS_FE_U64 or FHH_VALS_FE_BLOCK");
+    if (!vals_dev) return ctx->fail(FHH_E_ARG, "node_sums_fe_device: NULL vals_dev");
+    if (ctx->group) return group_node_sums(ctx, vals_dev, false, ld, format, sums, nullptr);
+    return node_sums_single(ctx, vals_dev[0], false, ld ? ld : ctx->n, format, sums, nullptr);
+}
+
+int fhh_node_sums_fe255_device(fhh_ctx* ctx, const void* const* vals_dev, uint64_t ld, uint32_t format,
+                               uint32_t* sums_unreduced, uint32_t* sums_canonical) {
+    CTX_CHECK(ctx);
+    if (format != FHH_VALS_FE255_LIMBS && format != FHH_VALS_FE255_BLOCKPAIR)
+        return ctx->fail(FHH_E_ARG, "node_sums_fe255_device: format must be FHH_VALS_FE255_LIMBS or _BLOCKPAIR");
+    if (!vals_dev) return ctx->fail(FHH_E_ARG, "node_sums_fe255_device: NULL vals_dev");
+    if (ctx->group) return group_node_sums(ctx, vals_dev, false, ld, format, sums_unreduced, sums_canonical);
+    return node_sums_single(ctx, vals_dev[0], false, ld ? ld : ctx->n, format, sums_unreduced, sums_canonical);
 }
 
 int fhh_tree_prune(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
     CTX_CHECK(ctx);
     if (n && !keep) return ctx->fail(FHH_E_ARG, "tree_prune: NULL keep");
+    if (ctx->group) return group_tree_prune(ctx, keep, n, false);
     return prune_impl(ctx, keep, n);
 }
 
 int fhh_tree_prune_last(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
     CTX_CHECK(ctx);
     if (n && !keep) return ctx->fail(FHH_E_ARG, "tree_prune_last: NULL keep");
+    if (ctx->group) return group_tree_prune(ctx, keep, n, true);
     if (ctx->phase != Phase::kPendingLast && ctx->last_nodes.empty() && n != 0)
         return ctx->fail(FHH_E_STATE, "tree_prune_last without tree_crawl_last");
     if (n != ctx->last_nodes.size())
@@ -2038,6 +1793,14 @@ int fhh_tree_prune_last(fhh_ctx* ctx, const uint8_t* keep, uint64_t n) {
 
 int fhh_frontier_size(const fhh_ctx* ctx, uint64_t* n_frontier, uint64_t* n_frontier_last) {
     CTX_CHECK(ctx);
+    if (ctx->group) {
+        if (!group_lead(ctx)) {
+            if (n_frontier) *n_frontier = 0;
+            if (n_frontier_last) *n_frontier_last = 0;
+            return FHH_OK;
+        }
+        return fhh_frontier_size(group_lead(ctx), n_frontier, n_frontier_last);
+    }
     if (n_frontier) *n_frontier = ctx->phase == Phase::kPending ? ctx->pending_C : ctx->frontier.size();
     if (n_frontier_last) *n_frontier_last = ctx->last_nodes.size();
     return FHH_OK;
@@ -2045,6 +1808,13 @@ int fhh_frontier_size(const fhh_ctx* ctx, uint64_t* n_frontier, uint64_t* n_fron
 
 int fhh_final_shares(fhh_ctx* ctx, uint64_t* n_final, uint32_t* levels, uint8_t* paths, uint32_t* values) {
     CTX_CHECK(ctx);
+    if (ctx->group) {
+        fhh_ctx* lead = group_lead(ctx);
+        if (!lead) return ctx->fail(FHH_E_STATE, "final_shares: no keys placed on the shards");
+        const int rc = fhh_final_shares(lead, n_final, levels, paths, values);
+        if (rc) ctx->fail(rc, lead->err);
+        return rc;
+    }
     const uint64_t F = ctx->last_nodes.size();
     if (n_final) *n_final = F;
     if (levels) *levels = ctx->last_depth;
@@ -2060,6 +1830,7 @@ int fhh_final_shares(fhh_ctx* ctx, uint64_t* n_final, uint32_t* levels, uint8_t*
 
 int fhh_export_states(fhh_ctx* ctx, uint64_t* n_nodes, uint8_t* seeds, uint8_t* t, uint8_t* y) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_export_states(ctx, n_nodes, seeds, t, y);
     int rc = set_device(ctx);
     if (rc) return rc;
     if (ctx->phase == Phase::kNoInit) return ctx->fail(FHH_E_STATE, "export_states before tree_init");
@@ -2151,6 +1922,7 @@ int fhh_sim_eq_count(fhh_ctx* c0, fhh_ctx* c1, uint64_t* counts) {
         g_err = "null fhh_ctx";
         return FHH_E_ARG;
     }
+    if (c0->group || c1->group) return c0->fail(FHH_E_ARG, "sim_eq_count: per-shard harness entry (use fhh_sim_crawl on a multi-device ctx)");
     int rc = set_device(c0);
     if (rc) return rc;
     if (!counts) return c0->fail(FHH_E_ARG, "sim_eq_count: NULL counts");
@@ -2162,6 +1934,7 @@ int fhh_sim_ot_sums(fhh_ctx* c0, fhh_ctx* c1, uint64_t prf_seed, void* sums0, vo
         g_err = "null fhh_ctx";
         return FHH_E_ARG;
     }
+    if (c0->group || c1->group) return c0->fail(FHH_E_ARG, "sim_ot_sums: per-shard harness entry (use fhh_sim_crawl on a multi-device ctx)");
     int rc = set_device(c0);
     if (rc) return rc;
     if (!sums0 || !sums1) return c0->fail(FHH_E_ARG, "sim_ot_sums: NULL buffer");
@@ -2173,6 +1946,7 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
         g_err = "sim_crawl: NULL argument";
         return FHH_E_ARG;
     }
+    if (c0->group || c1->group) return group_sim_crawl(c0, c1, cfg);
     int rc = set_device(c0);
     if (rc) return rc;
     const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
@@ -2277,6 +2051,7 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
 
 int fhh_set_variant(fhh_ctx* ctx, int variant) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_each(ctx, fhh_set_variant, variant);
     if (variant < 0 || variant >= expand_variant_count()) return ctx->fail(FHH_E_ARG, "set_variant: no such variant");
     // 43 / 44 store no / only the dir-0 child seeds (HBM-write A/B): their states are incomplete,
     // so they are refused unless the caller asks for diagnostics explicitly
@@ -2305,21 +2080,34 @@ int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* gri
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_get_stats(ctx, out);
     if (out) *out = ctx->stats;
     return FHH_OK;
 }
 
 int fhh_reset_stats(fhh_ctx* ctx) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_each(ctx, [](fhh_ctx* c, int) { return fhh_reset_stats(c); }, 0);
     ctx->stats = fhh_stats{};
     return FHH_OK;
 }
 
 int fhh_set_timing(fhh_ctx* ctx, int enabled) {
     CTX_CHECK(ctx);
+    if (ctx->group) return group_each(ctx, fhh_set_timing, enabled);
     if (enabled < 0) return ctx->fail(FHH_E_ARG, "set_timing: enabled must be >= 0");
     ctx->timing = enabled != 0;
     ctx->timing_every = enabled > 1 ? (uint32_t)enabled : 1;
+    return FHH_OK;
+}
+
+int fhh_memcpy_device(int device, void* dst_dev, const void* src_dev, uint64_t bytes) {
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess && bytes) e = hipMemcpy(dst_dev, src_dev, bytes, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) {
+        g_err = std::string("memcpy_device: ") + hipGetErrorString(e);
+        return FHH_E_HIP;
+    }
     return FHH_OK;
 }
 
@@ -2661,159 +2449,4 @@ int fhh_sim_sketch_verify_fe255(fhh_ctx* ctx, const fhh_sketch_batch255* b) {
     v.n = b->n_keys;
     HIP_TRY(ctx, launch_verify_fe255(v, ctx->stream));
     return sync(ctx);
-}
-
-// ---- garbled-circuit equality test (row f1) ------------------------------------------------
-int fhh_gc_equality_device(fhh_ctx* ctx, const fhh_gc_batch* b) {
-    CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    GcArgs a;
-    rc = gc_args(ctx, b, a);
-    if (rc) return rc;
-    HIP_TRY(ctx, launch_gc_garble(a, ctx->stream));
-    HIP_TRY(ctx, launch_gc_eval(a, ctx->stream));
-    return sync(ctx);
-}
-
-int fhh_gc_equality_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                         uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
-                         uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
-                         uint8_t* decode, uint8_t* out) {
-    CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc: bits must be in [1, 8]");
-    if (n == 0) return FHH_OK;
-    if (!gb_bits || !ev_bits || !label_key || !delta || !out) return ctx->fail(FHH_E_ARG, "gc: NULL argument");
-    if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc: n must fit 32 bits");
-    const uint64_t nw = (n + 63) / 64;
-    std::vector<uint64_t> planes[2];
-    const uint8_t* src[2] = {gb_bits, ev_bits};
-    for (int s = 0; s < 2; s++) {
-        planes[s].assign((size_t)bits * nw, 0);
-        for (uint64_t t = 0; t < n; t++)
-            for (uint32_t j = 0; j < bits; j++)
-                if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
-    }
-    DevBuf dp[2], dt, dg, de, dd, dout;
-    for (int s = 0; s < 2; s++) {
-        HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
-        HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    }
-    HIP_TRY(ctx, dt.ensure((size_t)std::max(bits - 1, 1u) * 2 * n * 16));
-    HIP_TRY(ctx, dg.ensure((size_t)(bits + 1) * n * 16));
-    HIP_TRY(ctx, de.ensure((size_t)bits * n * 16));
-    HIP_TRY(ctx, dd.ensure(n));
-    HIP_TRY(ctx, dout.ensure(n));
-    fhh_gc_batch b{};
-    b.groups = 1;
-    b.clients = (uint32_t)n;
-    b.words = (uint32_t)nw;
-    b.bits = bits;
-    b.mask = mask;
-    std::memcpy(b.label_key, label_key, 16);
-    std::memcpy(b.delta, delta, 16);
-    b.label_nonce = label_nonce;
-    b.gate_base = gate_base;
-    b.gb_planes_dev = dp[0].as<uint64_t>();
-    b.ev_planes_dev = dp[1].as<uint64_t>();
-    b.tables_dev = dt.as<uint8_t>();
-    b.gb_labels_dev = dg.as<uint8_t>();
-    b.ev_labels_dev = de.as<uint8_t>();
-    b.decode_dev = dd.as<uint8_t>();
-    b.out_dev = dout.as<uint8_t>();
-    rc = fhh_gc_equality_device(ctx, &b);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
-    if (decode) HIP_TRY(ctx, hipMemcpy(decode, dd.p, n, hipMemcpyDeviceToHost));
-    // SoA [row][t][16] -> AoS [t][row][16]
-    auto soa_to_aos = [&](const DevBuf& d, uint32_t rows, uint8_t* dst) -> int {
-        if (!dst || rows == 0) return FHH_OK;
-        std::vector<uint8_t> h((size_t)rows * n * 16);
-        HIP_TRY(ctx, hipMemcpy(h.data(), d.p, h.size(), hipMemcpyDeviceToHost));
-        for (uint32_t r = 0; r < rows; r++)
-            for (uint64_t t = 0; t < n; t++)
-                std::memcpy(dst + (t * rows + r) * 16, h.data() + ((size_t)r * n + t) * 16, 16);
-        return FHH_OK;
-    };
-    rc = soa_to_aos(dt, 2 * (bits - 1), tables);
-    if (rc) return rc;
-    rc = soa_to_aos(dg, bits + 1, gb_labels);
-    if (rc) return rc;
-    return soa_to_aos(de, bits, ev_labels);
-}
-
-// ---- OT extension (row f1's OT) ---------------------------------------------------------------
-int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
-    CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    if (!b) return ctx->fail(FHH_E_ARG, "ot_extend: NULL batch");
-    if (b->m == 0) return FHH_OK;
-    if (!b->choices_dev || !b->x0_dev || !b->out_dev) return ctx->fail(FHH_E_ARG, "ot_extend: NULL device buffer");
-    uint32_t* ch = nullptr;
-    HIP_TRY(ctx, ot_choices_buffer(ctx, b->m, &ch));
-    const uint64_t mp = ot_padded(b->m), words = (b->m + 31) / 32;
-    HIP_TRY(ctx, hipMemsetAsync(ch, 0, mp / 8, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ch, b->choices_dev, words * 4, hipMemcpyDeviceToDevice, ctx->stream));
-    // clear the bits past m in the last word, in stream order on the device
-    if (b->m % 32) HIP_TRY(ctx, launch_mask_word(ch + words - 1, (1u << (b->m % 32)) - 1, ctx->stream));
-    const uint32_t* rk = nullptr;
-    rc = ot_host_keys(ctx, &b->base_seeds[0][0][0], b->base_choice, &rk);
-    if (rc) return rc;
-    uint32_t sw[4], dw[4];
-    words_from_bytes(b->base_choice, sw);
-    words_from_bytes(b->delta, dw);
-    rc = ot_run(ctx, b->m, ch, reinterpret_cast<const uint4*>(b->x0_dev), reinterpret_cast<const uint4*>(b->x1_dev),
-                b->x1_dev ? nullptr : dw, reinterpret_cast<uint4*>(b->out_dev), rk, sw, b->tweak_base, nullptr, 0,
-                nullptr);
-    if (rc) return rc;
-    return sync(ctx);
-}
-
-int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1,
-                       const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
-                       uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out) {
-    CTX_CHECK(ctx);
-    int rc = set_device(ctx);
-    if (rc) return rc;
-    if (m == 0) return FHH_OK;
-    if (!choices || !x0 || !out || !base_seeds || !base_choice || (!x1 && !delta))
-        return ctx->fail(FHH_E_ARG, "ot_extend: NULL argument");
-    const uint64_t mp = ot_padded(m);
-    std::vector<uint32_t> bits(mp / 32, 0);
-    for (uint64_t j = 0; j < m; j++)
-        if (choices[j] & 1) bits[j / 32] |= 1u << (j % 32);
-    uint32_t* ch = nullptr;
-    HIP_TRY(ctx, ot_choices_buffer(ctx, m, &ch));
-    HIP_TRY(ctx, hipMemcpyAsync(ch, bits.data(), mp / 8, hipMemcpyHostToDevice, ctx->stream));
-    DevBuf d0, d1, dout;
-    HIP_TRY(ctx, d0.ensure(m * 16));
-    HIP_TRY(ctx, dout.ensure(m * 16));
-    HIP_TRY(ctx, hipMemcpyAsync(d0.p, x0, m * 16, hipMemcpyHostToDevice, ctx->stream));
-    if (x1) {
-        HIP_TRY(ctx, d1.ensure(m * 16));
-        HIP_TRY(ctx, hipMemcpyAsync(d1.p, x1, m * 16, hipMemcpyHostToDevice, ctx->stream));
-    }
-    OtOut tr;
-    const uint32_t* rk = nullptr;
-    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
-    if (rc) return rc;
-    uint32_t sw[4], dw[4] = {0, 0, 0, 0};
-    words_from_bytes(base_choice, sw);
-    if (!x1) words_from_bytes(delta, dw);
-    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : dw, dout.as<uint4>(), rk, sw,
-                tweak_base, nullptr, 0, &tr);
-    if (rc) return rc;
-    rc = sync(ctx);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy(out, dout.p, m * 16, hipMemcpyDeviceToHost));
-    if (y0_out) HIP_TRY(ctx, hipMemcpy(y0_out, tr.Y0, m * 16, hipMemcpyDeviceToHost));
-    if (y1_out) HIP_TRY(ctx, hipMemcpy(y1_out, tr.Y1, m * 16, hipMemcpyDeviceToHost));
-    if (u_out) {   // rows [128][ceil(m / 128)] of the padded [128][mp / 128] matrix
-        const uint64_t nb = (m + 127) / 128;
-        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
-    }
-    return FHH_OK;
 }

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 struct fhh_comm;   // include/fhh.h (fhh_comm.cpp)
 
@@ -269,8 +270,10 @@ hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t st
 // zero: clear partials first (host-driven launches); the device loop's k_prune clears them instead
 hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream, bool zero);
 hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials /*[C][16]*/, hipStream_t stream);
-hipError_t launch_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][2]*/, hipStream_t stream);
-hipError_t launch_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n, uint64_t* partials /*[C][8]*/, hipStream_t stream);
+// per-child limb partials of values [C][ld] (n per row) in format fmt (FHH_VALS_*): FE -> [C][2],
+// FE255 -> [C][8]
+hipError_t launch_sum_vals(const void* vals, uint32_t fmt, uint64_t C, uint64_t n, uint64_t ld, uint64_t* partials,
+                           hipStream_t stream);
 hipError_t launch_keygen(const KeygenArgs& a, hipStream_t stream);
 hipError_t launch_init_tables(const uint4* root, const uint64_t* key_idx, uint32_t dim, uint32_t K, uint32_t npad,
                               uint32_t nw, uint4* seed, uint64_t* t, uint64_t* y, hipStream_t stream);
@@ -286,6 +289,12 @@ int expand_grid(int device, int variant);
 // RCCL all-reduce (sum, u64) on `stream` (fhh_comm.cpp); asynchronous
 int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t count, hipStream_t stream,
                    std::string* err);
+// in-process communicators over distinct devices (ncclCommInitAll), a grouped in-place all-reduce
+// (ncclGroupStart/End, one stream per communicator) and abort (fhh_comm.cpp)
+int comm_init_all(int n, const int* devices, std::vector<::fhh_comm*>& out, std::string* err);
+int comm_group_allreduce(const std::vector<::fhh_comm*>& comms, const std::vector<uint64_t*>& bufs, uint64_t count,
+                         const std::vector<hipStream_t>& streams, std::string* err);
+void comm_abort(::fhh_comm* c);
 // device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
 // entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);

@@ -852,14 +852,19 @@ hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials, hipStream
     return hipGetLastError();
 }
 
-// ---- sums of host-provided OT outputs -------------------------------------------------
-__global__ __launch_bounds__(kReduceThreads) void k_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n,
-                                                          uint64_t* partials) {
+// ---- per-child sums of the OT outputs (collect.rs:487-501, 891-905) ----------------------------
+// Values [C][ld] in one of the FHH_VALS_* formats (include/fhh.h): host-provided u64 / u32 limbs
+// (staged by the engine) or OT outputs left on the device (16-B blocks: an FE little-endian in
+// bytes 0..7, fastfield.rs:414-431; a FieldElm as a BlockPair of 32 big-endian bytes,
+// field.rs:465-492). Sums are 32-bit-limb partials in u64 (2^32 clients of headroom), reduced once
+// on the host: [C][2] for FE, [C][8] for FE255 (the exact unreduced BigUint add_lazy sum).
+__global__ __launch_bounds__(kReduceThreads) void k_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t ld,
+                                                          uint32_t stride, uint64_t* partials) {
     __shared__ uint64_t red[2 * (kReduceThreads / 64)];
     for (uint64_t c = blockIdx.x; c < C; c += gridDim.x) {
         uint64_t v[2] = {0, 0};
         for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint64_t x = vals[c * n + i];
+            const uint64_t x = vals[(c * ld + i) * stride];
             v[0] += x & 0xFFFFFFFFull;
             v[1] += x >> 32;
         }
@@ -871,22 +876,27 @@ __global__ __launch_bounds__(kReduceThreads) void k_sum_fe(const uint64_t* vals,
     }
 }
 
-hipError_t launch_sum_fe(const uint64_t* vals, uint64_t C, uint64_t n, uint64_t* partials, hipStream_t stream) {
-    if (C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sum_fe, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream, vals, C, n, partials);
-    return hipGetLastError();
-}
-
+template <bool BLOCKPAIR>
 __global__ __launch_bounds__(kReduceThreads) void k_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n,
-                                                             uint64_t* partials) {
+                                                             uint64_t ld, uint64_t* partials) {
     __shared__ uint64_t red[8 * (kReduceThreads / 64)];
     for (uint64_t c = blockIdx.x; c < C; c += gridDim.x) {
         uint64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint4* p = reinterpret_cast<const uint4*>(vals + (c * n + i) * 8);
+            const uint4* p = reinterpret_cast<const uint4*>(vals + (c * ld + i) * 8);
             const uint4 lo = p[0], hi = p[1];
-            v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
-            v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+            if (BLOCKPAIR) {
+                uint64_t r[4];
+                blockpair_to_limbs(lo, hi, r);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    v[2 * k] += r[k] & 0xFFFFFFFFull;
+                    v[2 * k + 1] += r[k] >> 32;
+                }
+            } else {
+                v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
+                v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+            }
         }
         block_sum_u64<8>(v, red);
         if (threadIdx.x == 0)
@@ -894,9 +904,27 @@ __global__ __launch_bounds__(kReduceThreads) void k_sum_fe255(const uint32_t* va
     }
 }
 
-hipError_t launch_sum_fe255(const uint32_t* vals, uint64_t C, uint64_t n, uint64_t* partials, hipStream_t stream) {
+hipError_t launch_sum_vals(const void* vals, uint32_t fmt, uint64_t C, uint64_t n, uint64_t ld, uint64_t* partials,
+                           hipStream_t stream) {
     if (C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sum_fe255, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream, vals, C, n, partials);
+    switch (fmt) {
+        case FHH_VALS_FE_U64:
+        case FHH_VALS_FE_BLOCK:
+            hipLaunchKernelGGL(k_sum_fe, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream,
+                               static_cast<const uint64_t*>(vals), C, n, ld, fmt == FHH_VALS_FE_BLOCK ? 2u : 1u,
+                               partials);
+            break;
+        case FHH_VALS_FE255_LIMBS:
+            hipLaunchKernelGGL(k_sum_fe255<false>, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream,
+                               static_cast<const uint32_t*>(vals), C, n, ld, partials);
+            break;
+        case FHH_VALS_FE255_BLOCKPAIR:
+            hipLaunchKernelGGL(k_sum_fe255<true>, dim3(child_grid(C)), dim3(kReduceThreads), 0, stream,
+                               static_cast<const uint32_t*>(vals), C, n, ld, partials);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -4,7 +4,8 @@
  *
  * Drop-in boundary: `impl KeyCollection<T = FE, U = FieldElm>` (src/collect.rs:45-1030),
  * called by the tarpc `Collector` handlers (src/bin/server.rs:64-171). One fhh_ctx is one
- * server's KeyCollection bound to one GPU. Every entry point below names the reference
+ * server's KeyCollection bound to one GPU (fhh_create) or sharded over several
+ * (fhh_create_multi). Every entry point below names the reference
  * item it replaces. A reference-side binding (Rust `extern "C"` + build.rs) is shown in
  * INTEGRATION.md.
  *
@@ -97,6 +98,36 @@ int fhh_add_keys_bincode(fhh_ctx* ctx, const uint8_t* req, uint64_t len);
 int fhh_gen_keys_pair(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t n, const uint8_t* left_bits,
                       const uint8_t* right_bits, const uint8_t* root_seeds);
 
+/* ---- one KeyCollection over several GPUs (north_star) -----------------------
+ * KeyCollection::new on n_devices GPUs: one collection whose clients are sharded over the devices
+ * (devices[k] may repeat — two shards on one GPU run the same code on a one-GPU box). At
+ * tree_init (or add_keys_bincode / gen_keys_pair) the clients are cut into contiguous ranges of
+ * whole 64-client words, one per shard, and every KeyCollection entry point of this header fans
+ * out over the shards (one host thread per shard, each on its own device and stream) with the
+ * results of a one-GPU collection: share planes are gathered in client order, node sums are summed
+ * over the shards as u64 32-bit-limb partials — an in-process RCCL all-reduce (ncclCommInitAll,
+ * one grouped ncclAllReduce over the shards' streams) when the devices are distinct, on the host
+ * otherwise (or with FHH_GROUP_REDUCE=host) — and reduced mod p once; prune applies the keep mask
+ * to every shard; fhh_sim_crawl runs the device level loop per shard pair with the per-level
+ * all-reduce over the same communicators. The reference server holds one such collection behind
+ * its Mutex (src/bin/server.rs:44-52, 332-335). */
+int fhh_create_multi(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, const int* devices, int n_devices);
+#define FHH_REDUCE_NONE 0   /* one shard                        */
+#define FHH_REDUCE_HOST 1   /* partials summed on the host      */
+#define FHH_REDUCE_RCCL 2   /* in-process RCCL all-reduce       */
+/* Shard k of a collection (a one-GPU ctx is one shard): shard count, device, first client and
+ * client count (0 before the keys are placed), and the reduction the collection uses. */
+int fhh_shard_info(const fhh_ctx* ctx, int shard, int* n_shards, int* device, uint64_t* client_base,
+                   uint64_t* n_clients, int* reduction);
+/* The placement fhh_create_multi uses (host arithmetic, no device call): shard k of n_shards gets
+ * clients [client_base[k], client_base[k] + n_clients[k]) = the 64-client words
+ * [nw k / n_shards, nw (k + 1) / n_shards), nw = ceil(n / 64). */
+int fhh_shard_plan(uint64_t n_clients, int n_shards, uint64_t* client_base, uint64_t* n_clients_out);
+/* The one-GPU ctx of shard k (the ctx itself for a one-GPU ctx): per-shard calls such as the
+ * two-party GC + OT below run on it — one channel per shard, as the reference splits a level's
+ * tests over its channels (collect.rs:423-430). Owned by the collection. */
+int fhh_shard_ctx(fhh_ctx* ctx, int shard, fhh_ctx** out);
+
 /* Number of clients (len of `keys`). */
 int fhh_num_clients(const fhh_ctx* ctx, uint64_t* n);
 
@@ -125,6 +156,20 @@ int fhh_node_sums_fe(fhh_ctx* ctx, const uint64_t* vals, uint64_t* sums);
  * (field.rs:337-339); sums_canonical [C][8] = mod 2^255-19. Either may be NULL. The sums
  * become the frontier_last values (collect.rs:909-914). */
 int fhh_node_sums_fe255(fhh_ctx* ctx, const uint32_t* vals, uint32_t* sums_unreduced, uint32_t* sums_canonical);
+
+/* Node sums of OT outputs that are already in device memory (no host round trip), e.g. the
+ * outputs of the GPU OT extension. vals_dev[k] = shard k's values [C][ld] (ld >= the shard's
+ * client count; 0 = each shard's client count) on shard k's GPU; a one-GPU ctx passes one
+ * pointer. Formats: */
+#define FHH_VALS_FE_U64 0           /* u64, any FE representation (FE::new)                       */
+#define FHH_VALS_FE_BLOCK 1         /* 16-B OT blocks, the FE little-endian in bytes 0..7
+                                       (FE <-> Block, fastfield.rs:414-431)                       */
+#define FHH_VALS_FE255_LIMBS 2      /* 8 x u32 little-endian limbs (< 2^256)                      */
+#define FHH_VALS_FE255_BLOCKPAIR 3  /* 2 x 16-B OT blocks: the value's 32 big-endian bytes
+                                       (FieldElm <-> BlockPair, field.rs:465-492)                 */
+int fhh_node_sums_fe_device(fhh_ctx* ctx, const void* const* vals_dev, uint64_t ld, uint32_t format, uint64_t* sums);
+int fhh_node_sums_fe255_device(fhh_ctx* ctx, const void* const* vals_dev, uint64_t ld, uint32_t format,
+                               uint32_t* sums_unreduced, uint32_t* sums_canonical);
 
 /* tree_prune (collect.rs:918-929) / tree_prune_last (collect.rs:931-942). */
 int fhh_tree_prune(fhh_ctx* ctx, const uint8_t* keep, uint64_t n);
@@ -443,6 +488,60 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
                        const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                        uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out);
 
+/* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
+ * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;
+ * equalitytest.rs:25-106): each server runs only its own half on its own ctx, right after its
+ * fhh_tree_crawl / fhh_tree_crawl_last, and keeps its secrets; what crosses is five byte buffers,
+ * in this order:
+ *   server 0 (garbler, OT sender)                         server 1 (evaluator, OT receiver)
+ *   fhh_gb_garble        -> gc  ---------------------->   fhh_ev_ot_labels -> u1
+ *   fhh_gb_ot_labels(u1) -> y1  ---------------------->   fhh_ev_evaluate(gc, y1) -> u2
+ *   fhh_gb_ot_shares(u2) -> y2  ---------------------->   fhh_ev_ot_shares(y2)
+ *   fhh_party_node_sums                                   fhh_party_node_sums
+ * (the evaluator may call fhh_ev_ot_labels before receiving gc). Outputs are device buffers owned
+ * by the producing ctx, valid until its next party call; inputs are device pointers on the
+ * receiving ctx's GPU (the caller moves the bytes: a network in a deployment, a device copy in the
+ * in-process tests). The circuit, labels and OTs are those of fhh_gc_batch / fhh_ot_batch;
+ * gc = [tables (bits-1) x 2 | garbler labels bits + 1 | decode 1 B] per test, tests = C x n in
+ * child-major order; u = the OT receiver's [128][m padded to 8192 / 128] blocks; y = Y0 | Y1
+ * ([m] blocks each). OT 1 moves the evaluator's input labels (m = C x 2d x npad: its share planes
+ * are the choice bits), OT 2 the FE share (m = C x n; a FieldElm at tree_crawl_last = a
+ * BlockPair, 2 OTs per test, collect.rs:846-876). The garbler's node value is r1 = r0 + 1, the
+ * evaluator's the OT output (collect.rs:439-472); fhh_party_node_sums sums them on the device:
+ * non-last level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm
+ * (the frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own
+ * channel, as the reference runs a level's tests over several channels (collect.rs:423-430). */
+typedef struct fhh_gc_party_cfg {
+    /* garbler only (fresh per level: AesRng::new(), collect.rs:432) */
+    uint8_t label_key[16];               /* label PRG key                                          */
+    uint8_t delta[16];                   /* free-XOR offset (bit 0 forced to 1)                    */
+    uint32_t mask;                       /* the level's mask bit (equalitytest.rs:38-43)           */
+    uint32_t pad_;
+    uint64_t share_seed;                 /* PRF key of the r0 values (T::random(), collect.rs:441) */
+    /* the base OTs of OT 1 (index 0) and OT 2 (index 1) (OtSender/OtReceiver::init,
+     * collect.rs:454-471): the OT-extension receiver holds both seeds of every base OT, the sender
+     * one seed per base OT and its choice bits (e.g. from fhh_co15_*) */
+    uint8_t base_pairs[2][128][2][16];   /* evaluator                                              */
+    uint8_t base_chosen[2][128][16];     /* garbler: base_pairs[t][i][s_i]                         */
+    uint8_t base_choice[2][16];          /* garbler: s (bit i % 8 of byte i / 8)                   */
+} fhh_gc_party_cfg;
+int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes);
+int fhh_gb_ot_labels(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);
+int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);
+int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** u_dev, uint64_t* u_bytes);
+int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_msg_bytes, const uint8_t* y_dev,
+                    uint64_t y_bytes, const uint8_t** u_dev, uint64_t* u_bytes);
+int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_bytes);
+/* sums_a = uint64_t[C] (non-last level) or uint32_t[C][10] unreduced (last); sums_b = NULL or
+ * uint32_t[C][8] canonical (last level) */
+int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b);
+/* bytes this ctx sent in the level so far (its outgoing messages) */
+int fhh_party_bytes_sent(const fhh_ctx* ctx, uint64_t* bytes);
+/* The in-process level loop's per-level material (fhh_sim_config.gc = 2, ideal base OTs) for
+ * prf_seed and level, so a two-ctx run can reproduce fhh_sim_crawl's transcripts; a deployment
+ * draws fresh randomness instead. */
+int fhh_gc_party_level_cfg(uint64_t prf_seed, uint32_t level, fhh_gc_party_cfg* out);
+
 /* ---- base OTs (the OT extension's init, collect.rs:454-471) -------------------------------
  * Chou–Orlandi "simplest OT" over NIST P-256 (ocelot runs it over Ristretto; not vendored, so the
  * group and the wire format differ: functionality only). Points are 65-byte uncompressed SEC1;
@@ -509,6 +608,10 @@ int fhh_debug_launch_gaps(int device, int which, int reps, double* us_per_kernel
  * 100 MHz s_memrealtime ticks; buf NULL disarms); launches = launches recorded so far. */
 int fhh_wave_profile_arm(int device, uint64_t* buf, uint32_t cap);
 int fhh_wave_profile_launches(int device, uint32_t* launches);
+
+/* Device-to-device copy (synchronous): the channel stand-in of the in-process two-party runs,
+ * which move each party's messages into buffers the other party owns. */
+int fhh_memcpy_device(int device, void* dst_dev, const void* src_dev, uint64_t bytes);
 
 /* Device properties the library targets (gfx950). */
 int fhh_device_info(int device, char* arch_name, size_t cap, int* num_cus);

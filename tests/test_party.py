@@ -1,0 +1,125 @@
+"""The two servers' halves of the GC equality test + OT, each on its own ctx (fhh_gb_* / fhh_ev_*;
+src/collect.rs:419-482 with gc_sender = true on server 0 and false on server 1,
+src/equalitytest.rs:25-106). Only the protocol's five messages per level cross (party.Channel
+copies them into memory the receiving server owns). With fhh_sim_crawl's per-level material the
+split run reproduces the in-process GC + OT crawl (fhh_sim_config.gc = 2) level by level, and its
+heavy hitters equal the plaintext recount."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(wl, L, d, devices=None):
+    import fuzzyheavyhitters_amd as fhh
+    c0 = fhh.KeyCollection(L, d, devices=devices)
+    c1 = fhh.KeyCollection(L, d, devices=devices)
+    fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+    return c0, c1
+
+
+def _assert_same_crawl(a, b):
+    assert list(a.level_children) == list(b.level_children)
+    for lv, (x, y) in enumerate(zip(a.counts, b.counts)):
+        assert np.array_equal(np.asarray(x, np.uint64), np.asarray(y, np.uint64)), f"level {lv}"
+    assert [(r.path, r.value) for r in a.final] == [(r.path, r.value) for r in b.final]
+
+
+@pytest.mark.parametrize("d,n,L,thr", [(1, 300, 24, 0.02), (2, 200, 12, 0.05), (1, 64 * 3, 20, 0.03)],
+                         ids=["d1", "d2", "whole-words"])
+def test_two_party_equals_in_process_gc_ot(d, n, L, thr):
+    """Level by level: the leader's v0 - v1 per child and the final heavy hitters of the split run
+    equal fhh_sim_crawl(gc = "ot") (both parties in one device loop) on the same material."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(n, max(L, 32), d, num_sites=5, seed=3 + d)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    c0, c1 = _keys(wl, L, d)
+    ref = fhh.sim_crawl(c0, c1, thr, mode="fe", prf_seed=77, gc="ot")
+    p0, p1 = _keys(wl, L, d)
+    got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77)
+    _assert_same_crawl(ref, got)
+    assert len(got.final) > 0
+    t = max(1, int(thr * n))
+    cnt, paths, vals = workload.plaintext_crawl(wl.left, wl.right, t, t)
+    assert sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in got.final) == sorted(paths)
+    # message sizes (the bytes that would cross the servers' channel)
+    lb = got.level_bytes[0]
+    C0, bits = int(got.level_children[0]), 2 * d
+    npad = (n + 63) // 64 * 64
+    assert lb["gc"] == C0 * n * ((2 * (bits - 1) + bits + 1) * 16 + 1)
+    assert lb["y1"] == C0 * bits * npad * 32 and lb["y2"] == C0 * n * 32
+
+
+def test_two_party_fresh_randomness_same_output():
+    """Independent per-level material (another label key, Delta, mask, r0 and base OTs per level)
+    changes every transcript but not the leader's output."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import party, workload
+    n, L = 250, 20
+    wl = workload.zipf_workload(n, 32, 1, num_sites=4, seed=12)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    a0, a1 = _keys(wl, L, 1)
+    b0, b1 = _keys(wl, L, 1)
+    ra = fhh.two_party_crawl(a0, a1, 0.02, prf_seed=1)
+    rb = fhh.two_party_crawl(b0, b1, 0.02, cfg_fn=lambda lv, k=0: party.level_cfg(0xABCDEF ^ (lv * 7919), lv + 1000))
+    _assert_same_crawl(ra, rb)
+
+
+def test_two_party_multi_device_shards():
+    """A multi-device collection runs one protocol instance per shard over its own channel (the
+    reference spreads a level's tests over several channels, collect.rs:423-430) and reduces the
+    parties' device-resident sums over its shards: same output as the one-GPU in-process crawl."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 64 * 7 + 11, 24
+    wl = workload.zipf_workload(n, 32, 1, num_sites=6, seed=31)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    c0, c1 = _keys(wl, L, 1)
+    ref = fhh.sim_crawl(c0, c1, 0.02, mode="fe", prf_seed=5, gc="ot")
+    g0, g1 = _keys(wl, L, 1, devices=[0, 0, 0])
+    got = fhh.two_party_crawl(g0, g1, 0.02, prf_seed=5)
+    _assert_same_crawl(ref, got)
+
+
+def test_party_calls_out_of_order_refused():
+    """Each half checks the protocol order and the message sizes (FHH_E_STATE / FHH_E_ARG)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import party, workload
+    from fuzzyheavyhitters_amd._lib import lib
+    wl = workload.zipf_workload(100, 32, 1, num_sites=3, seed=1)
+    c0, c1 = _keys(wl, 32, 1)
+    out, nb = ctypes.c_void_p(), ctypes.c_uint64()
+    cfg = party.level_cfg(1, 0)
+    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == -2   # no crawl
+    c0.tree_init()
+    c1.tree_init()
+    c0.tree_crawl()
+    c1.tree_crawl()
+    assert lib().fhh_gb_ot_labels(c0.handle, None, 0, ctypes.byref(out), ctypes.byref(nb)) == -2        # before garble
+    assert lib().fhh_ev_evaluate(c1.handle, None, 0, None, 0, ctypes.byref(out), ctypes.byref(nb)) == -2
+    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == 0
+    assert lib().fhh_gb_ot_labels(c0.handle, out, 12345, ctypes.byref(out), ctypes.byref(nb)) == -1     # wrong size
+    assert b"expected" in lib().fhh_last_error(c0.handle)
+
+
+def test_two_party_configs1_full_size():
+    """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): the split
+    GC + OT crawl equals the in-process GC + OT crawl level by level, and both equal the plaintext
+    recount (222 heavy hitters). Prints the bytes that would cross the channel."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 100_000, 512
+    wl = workload.zipf_workload(n, L, 1, num_sites=10_000, zipf_s=1.03, seed=0x5EED)
+    c0, c1 = _keys(wl, L, 1)
+    ref = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=7, gc="ot")
+    del c0, c1
+    p0, p1 = _keys(wl, L, 1)
+    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7)
+    _assert_same_crawl(ref, got)
+    assert len(got.final) == 222
+    tot = {k: sum(lb[k] for lb in got.level_bytes) for k in got.level_bytes[0]}
+    print("configs[1] two-party channel bytes per crawl:", tot, "max per level:",
+          max(sum(lb.values()) for lb in got.level_bytes))

@@ -521,7 +521,8 @@ def main():
                        f"servers in-process" + (" (= configs[2] sharded over 8 GPUs)" if n_total == 1_000_000 else "")
                        + (" (= configs[1])" if n_total == 100_000 else ""))
         else:
-            wl_name = "configs[3]: lat/lon l-inf balls (synthetic county-centroid-shaped points), d=2, data_len 16"
+            wl_name = ("configs[3]: lat/lon l-inf balls around the reference's county centroids "
+                       "(data/county_centroids.csv, Zipf-weighted, 8 km uniform_in_square jitter), d=2, data_len 16")
         metric = ("client×prefix key evals/sec (AES blocks/s) + full-crawl wall time, 1M clients"
                   if n_total == 1_000_000 and args.workload == "zipf" else
                   f"client×prefix key evals/sec (AES blocks/s) + full-crawl wall time, {n_total} clients")
@@ -540,8 +541,9 @@ def main():
             "data": ("synthetic: seeded Zipf workload shaped like leader.rs (num_sites strings + 8-bit augmentation), "
                      "keys by GPU keygen, resident in HBM before the timed region"
                      if args.workload == "zipf" else
-                     "synthetic: Zipf-weighted synthetic county-centroid-shaped points (data/county_centroids.csv "
-                     "not used), keys by GPU keygen"),
+                     "synthetic clients over the reference's real county centroids (data/county_centroids.csv via "
+                     "tests/golden/county_centroids.npz): Zipf-weighted county draw, uniform_in_square jitter of "
+                     "side 8 km, i16 centidegrees; keys by GPU keygen"),
             "config": {
                 "workload": wl_name,
                 "clients_total": n_total, "clients_per_gpu": n_local, "data_len": args.data_len,

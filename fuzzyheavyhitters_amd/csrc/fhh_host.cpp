@@ -644,8 +644,8 @@ int node_partials(fhh_ctx* ctx, const void* vals, uint32_t fmt, uint64_t ld, uin
 int node_sums_finish(fhh_ctx* ctx, const uint64_t* h, uint32_t fmt, void* out_a, void* out_b) {
     const uint64_t C = ctx->pending_C;
     if (!fmt_is_fe255(fmt)) {
-        if (C && !out_a) return ctx->fail(FHH_E_ARG, "node_sums_fe: NULL sums");
-        uint64_t* sums = static_cast<uint64_t*>(out_a);
+        uint64_t* sums = static_cast<uint64_t*>(out_a);   // NULL: a shard that only takes part
+        if (!sums) return FHH_OK;
         for (uint64_t c = 0; c < C; c++) sums[c] = fe_canon_from_limbs(h[2 * c], h[2 * c + 1]);
         return FHH_OK;
     }
@@ -862,8 +862,12 @@ int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uin
         DevBuf np;
         HIP_TRY(c0, np.ensure((size_t)F_cap * d * 4));
         const int keep_par = level & 1;
-        if (preserve && b == keep_par && keep_nodes)
-            HIP_TRY(c0, hipMemcpy(np.p, B.pos[b].p, (size_t)keep_nodes * d * 4, hipMemcpyDeviceToDevice));
+        if (preserve && b == keep_par && keep_nodes) {
+            // stream-ordered (the engine streams do not wait for the null stream), and finished
+            // before the old buffer is released
+            HIP_TRY(c0, hipMemcpyAsync(np.p, B.pos[b].p, (size_t)keep_nodes * d * 4, hipMemcpyDeviceToDevice, c0->stream));
+            HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+        }
         std::swap(B.pos[b].p, np.p);
         std::swap(B.pos[b].bytes, np.bytes);
     }
@@ -873,15 +877,16 @@ int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uin
         DevBuf npart, nred;
         HIP_TRY(c0, npart.ensure(C_new * 16 * 8));
         // FE levels add into the partials (k_sim_ot_fe client chunks); k_prune re-zeroes them
-        HIP_TRY(c0, hipMemset(npart.p, 0, C_new * 16 * 8));
+        HIP_TRY(c0, hipMemsetAsync(npart.p, 0, C_new * 16 * 8, c0->stream));
         if (B.distributed) HIP_TRY(c0, nred.ensure(C_new * 16 * 8));
         // ... and, multi-rank, the local partials too: the all-reduces of the no-op levels
         // after an abort re-reduce them, which must reproduce the same sums
         if (preserve && keep_children) {
-            HIP_TRY(c0, hipMemcpy(npart.p, B.partials.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice));
+            HIP_TRY(c0, hipMemcpyAsync(npart.p, B.partials.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice, c0->stream));
             if (B.distributed)
-                HIP_TRY(c0, hipMemcpy(nred.p, B.reduced.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice));
+                HIP_TRY(c0, hipMemcpyAsync(nred.p, B.reduced.p, (size_t)keep_children * per * 8, hipMemcpyDeviceToDevice, c0->stream));
         }
+        HIP_TRY(c0, hipStreamSynchronize(c0->stream));
         std::swap(B.partials.p, npart.p);
         std::swap(B.partials.bytes, npart.bytes);
         if (B.distributed) {
@@ -1727,6 +1732,7 @@ static int node_sums_single(fhh_ctx* ctx, const void* vals, bool host, uint64_t 
 
 int fhh_node_sums_fe(fhh_ctx* ctx, const uint64_t* vals, uint64_t* sums) {
     CTX_CHECK(ctx);
+    if (!sums) return ctx->fail(FHH_E_ARG, "node_sums_fe: NULL sums");
     if (ctx->group) {
         const void* v[1] = {vals};
         return group_node_sums(ctx, v, true, 0, FHH_VALS_FE_U64, sums, nullptr);
@@ -1747,7 +1753,7 @@ int fhh_node_sums_fe_device(fhh_ctx* ctx, const void* const* vals_dev, uint64_t 
     CTX_CHECK(ctx);
     if (format != FHH_VALS_FE_U64 && format != FHH_VALS_FE_BLOCK)
         return ctx->fail(FHH_E_ARG, "node_sums_fe_device: format must be FHH_VALS_FE_U64 or FHH_VALS_FE_BLOCK");
-    if (!vals_dev) return ctx->fail(FHH_E_ARG, "node_sums_fe_device: NULL vals_dev");
+    if (!vals_dev || !sums) return ctx->fail(FHH_E_ARG, "node_sums_fe_device: NULL vals_dev / sums");
     if (ctx->group) return group_node_sums(ctx, vals_dev, false, ld, format, sums, nullptr);
     return node_sums_single(ctx, vals_dev[0], false, ld ? ld : ctx->n, format, sums, nullptr);
 }
@@ -2103,7 +2109,10 @@ int fhh_set_timing(fhh_ctx* ctx, int enabled) {
 
 int fhh_memcpy_device(int device, void* dst_dev, const void* src_dev, uint64_t bytes) {
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess && bytes) e = hipMemcpy(dst_dev, src_dev, bytes, hipMemcpyDeviceToDevice);
+    // a device-to-device hipMemcpy may return before the copy lands; the engine's non-blocking
+    // streams do not wait for the null stream, so finish it here
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst_dev, src_dev, bytes, hipMemcpyDeviceToDevice, nullptr);
+    if (e == hipSuccess && bytes) e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess) {
         g_err = std::string("memcpy_device: ") + hipGetErrorString(e);
         return FHH_E_HIP;

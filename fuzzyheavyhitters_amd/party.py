@@ -103,13 +103,15 @@ class TwoPartyResult:
 
 
 def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
-                    prf_seed: int = 0, levels: int = 0, cfg_fn=None) -> TwoPartyResult:
+                    prf_seed: int = 0, levels: int = 0, cfg_fn=None, expect_counts=None) -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between
     the two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both,
     run the level's protocol through the channel, take each server's node sums from its own
     device (fhh_party_node_sums), keep_values on the leader, prune both. `cfg_fn(level)` gives the
     level's fhh_gc_party_cfg (default: level_cfg(prf_seed, level), fhh_sim_crawl's material); for a
-    multi-device collection `cfg_fn(level, shard)`, one protocol instance per shard."""
+    multi-device collection `cfg_fn(level, shard)`, one protocol instance per shard.
+    `expect_counts` (tests): per-level v0 - v1 to compare against as the crawl goes (raises at the
+    first level that differs instead of crawling on a wrong frontier)."""
     L = levels or c0.depth
     n_total = nclients_total if nclients_total is not None else c0.num_clients()
     thr = max(1, int(threshold * n_total))
@@ -151,6 +153,10 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
             res.counts.append(np.array([((a % FE255_P) - (b % FE255_P)) % FE255_P for a, b in zip(s0, s1)], np.uint64))
             c0.tree_prune_last(keep)
             c1.tree_prune_last(keep)
+        if expect_counts is not None and not np.array_equal(res.counts[-1], np.asarray(expect_counts[lv], np.uint64)):
+            bad = np.nonzero(res.counts[-1] != np.asarray(expect_counts[lv], np.uint64))[0]
+            raise ValueError(f"two-party crawl: level {lv}: {bad.size} of {C0} children differ (first {bad[:5]}: "
+                             f"{res.counts[-1][bad[:5]]} vs {np.asarray(expect_counts[lv])[bad[:5]]})")
     res.final = KeyCollection.final_values(c0.final_shares(), c1.final_shares())
     return res
 

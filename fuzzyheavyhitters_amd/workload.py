@@ -135,14 +135,34 @@ def geo_to_int(lat: np.ndarray, lon: np.ndarray):
     return np.round(lat * 100.0).astype(np.int16), np.round(lon * 100.0).astype(np.int16)
 
 
+def reference_centroids() -> np.ndarray:
+    """The reference's county centroids (data/county_centroids.csv, 3 233 rows, file order) as
+    [num][lat, lon] degrees, from the committed data fixture tests/golden/county_centroids.npz
+    (made by tests/golden/make_county_centroids.py; load_centroids, sample_covid_data.rs:17-30)."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                        "county_centroids.npz")
+    z = np.load(path, allow_pickle=False)
+    return np.stack([z["lat"], z["lon"]], 1)
+
+
 def coords_workload(n: int, ball_size: int = 1, num_centroids: int = 3233, zipf_s: float = 1.03,
-                    side_km: float = 10.0, seed: int = 0x5EED, client_offset: int = 0) -> Workload:
-    """Config D: d = 2 (lat, lon), data_len = 16. Points = Zipf-weighted county-like centroids
-    jittered uniformly in a side_km square (`uniform_in_square`, sample_covid_data.rs:45-62),
-    converted to i16 centidegrees; keys per `gen_l_inf_ball_from_coords` (ibDCF.rs:189-205):
-    bounds (c -/+ ball) clamped to +-9000 (lat) / +-18000 (lon), i16 -> 16 bits MSB first
-    (two's complement, sample_driving_data.rs:25-28)."""
-    cents = synthetic_centroids(num_centroids)
+                    side_km: float = 8.0, seed: int = 0x5EED, client_offset: int = 0,
+                    centroids: str = "reference") -> Workload:
+    """Config D: d = 2 (lat, lon), data_len = 16. Points = the reference's county
+    centroids (`centroids="reference"`, data/county_centroids.csv; "synthetic" = the r01/r02
+    stand-in of the same shape) drawn Zipf-weighted over counties, jittered uniformly in a square
+    of side aug_len = 8 km (`uniform_in_square`, sample_covid_data.rs:45-62, called with
+    Some(aug_len) by leader.rs:67-75, aug_len = 8 at leader.rs:331), converted to i16 centidegrees
+    (sample_driving_data.rs:11-15); keys per `gen_l_inf_ball_from_coords` (ibDCF.rs:189-205):
+    bounds (c -/+ ball) clamped to +-9000 (lat) / +-18000 (lon), i16 -> 16 bits MSB first (two's
+    complement, sample_driving_data.rs:25-28). The reference weighs counties by COVID case records
+    (a CSV it does not ship); the Zipf weight over the file order stands in for it."""
+    if centroids == "reference":   # num_centroids < 3233: the file's first rows (small tests)
+        cents = reference_centroids()[:num_centroids]
+        num_centroids = cents.shape[0]
+    else:
+        cents = synthetic_centroids(num_centroids)
     idx = zipf_indices(np.random.default_rng([seed, 11]), client_offset + n, num_centroids, zipf_s)[client_offset:]
     jr = np.random.default_rng([seed, 12])
     u = jr.random((client_offset + n, 2))[client_offset:]

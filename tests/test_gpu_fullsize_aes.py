@@ -170,15 +170,18 @@ def test_configs0_gpu_equals_oracle(oracle):
     assert st["aes_blocks"] * 2 == ores.aes_blocks
 
 
-@pytest.mark.parametrize("thr_frac,levels", [(0.075, [0, 5, 9, 13]), (0.01, [0, 7, 14, 15])],
-                         ids=["config-threshold", "deep"])
-def test_configs3_sampled_states_bit_exact(oracle, thr_frac, levels):
+@pytest.mark.parametrize("thr_frac,levels,heavy", [(0.075, [0, 5, 9, 13], 0), (0.01, [0, 7, 14, 15], 54),
+                                                   (0.001, [0, 9, 15], 1046)],
+                         ids=["config-threshold", "deep", "dense"])
+def test_configs3_sampled_states_bit_exact(oracle, thr_frac, levels, heavy):
     """configs[3] at its full size (src/bin/config.json: 1M clients, d = 2 lat/lon, data_len 16,
-    ball 1, threshold 0.075 — the synthetic centroids keep no node past level 13 there, so a
-    0.01 run crawls to the leaves too): the d = 2 path (dim-prefix dedup, per-dim entry tables, a
-    node = a pair of entries) at 1M clients. The probe reads every child's per-dim states for a
-    client in every 8th word at four non-empty levels and the oracle replays them; the counts of
-    every level equal the plaintext recount."""
+    ball 1, threshold 0.075) on the reference's own county centroids (data/county_centroids.csv,
+    Zipf-weighted, 8 km uniform_in_square jitter): the d = 2 path (dim-prefix dedup, per-dim
+    entry tables, a node = a pair of entries) at 1M clients. At the config's 0.075 no node
+    survives past level 13 (0 heavy hitters: one centidegree cell never holds 7.5 % of the
+    clients), so 0.01 (54) and 0.001 (1 046 heavy hitters) crawl to the leaves too. The probe
+    reads every child's per-dim states for a client in every 8th word at non-empty levels and the
+    oracle replays them; the counts of every level equal the plaintext recount."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
     n, L = 1_000_000, 16
@@ -201,4 +204,5 @@ def test_configs3_sampled_states_bit_exact(oracle, thr_frac, levels):
     assert all(np.array_equal(a, np.asarray(b)) for a, b in zip(cnt, res.counts))
     got = sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in res.final)
     assert got == sorted(paths)
+    assert len(got) == heavy
     print("configs[3] children per level:", [int(x) for x in res.level_children], "heavy hitters:", len(got))

@@ -117,7 +117,7 @@ def test_two_party_configs1_full_size():
     ref = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=7, gc="ot")
     del c0, c1
     p0, p1 = _keys(wl, L, 1)
-    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7)
+    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7, expect_counts=ref.counts)
     _assert_same_crawl(ref, got)
     assert len(got.final) == 222
     tot = {k: sum(lb[k] for lb in got.level_bytes) for k in got.level_bytes[0]}

@@ -235,6 +235,132 @@ def bincode_bench(args, world, rank, local_rank, dist):
     return 0
 
 
+def dropin_bench(args, world, rank, local_rank, dist):
+    """The KeyCollection ABI path a Rust server calls (collect.rs:370-505 through include/fhh.h,
+    INTEGRATION.md §3) against the fused device-resident loop, both servers in this process on one
+    GPU, --clients clients (configs[1] = 100000), data_len 512. One step = one full crawl:
+      fused      the bench's own step: fhh_sim_crawl count mode (k_expand, equality count, keep and
+                 prune on the device, no host round trip per level)
+      dropin     per level: fhh_tree_crawl on both servers with the share planes copied to the host
+                 (the GC input), the leader's equality count from the planes on the host (standing
+                 in for the GC + OT), fhh_node_sums_fe on both servers with host OT outputs
+                 [C][n] u64 (copied to the device), keep, fhh_tree_prune on both
+      gcot       fhh_sim_crawl with the GPU GC + OT in every level (both parties in one device loop)
+      two-party  the same GC + OT split between the two servers' ctxs (fhh_gb_* / fhh_ev_*), the
+                 five messages per level copied device to device, node sums of the device-resident
+                 OT outputs (fhh_party_node_sums)
+    Every leg's heavy hitters are checked against the fused crawl's."""
+    import numpy as np
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L, d = args.clients, args.data_len, args.dims
+    wl = workload.zipf_workload(n, L, d, num_sites=args.num_sites, zipf_s=args.zipf, ball_size=args.ball,
+                                seed=args.seed)
+
+    def pair():
+        c0, c1 = fhh.KeyCollection(L, d, device=local_rank), fhh.KeyCollection(L, d, device=local_rank)
+        fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
+        return c0, c1
+
+    c0, c1 = pair()
+    thr = max(1, int(args.threshold * n))
+    nw = (n + 63) // 64
+    valid = np.full(nw, np.uint64(0xFFFFFFFFFFFFFFFF))
+    if n % 64:
+        valid[-1] = np.uint64((1 << (n % 64)) - 1)
+    vals = np.random.default_rng(1).integers(0, 1 << 62, (512, n), dtype=np.uint64)   # host OT outputs
+
+    def dropin_crawl():
+        c0.tree_init()
+        c1.tree_init()
+        final = []
+        per = {"crawl_planes": 0.0, "leader": 0.0, "node_sums": 0.0, "prune": 0.0}
+        for lv in range(L):
+            last = lv == L - 1
+            t0 = time.perf_counter()
+            C, p0 = (c0.tree_crawl_last if last else c0.tree_crawl)(share_planes=True)
+            _, p1 = (c1.tree_crawl_last if last else c1.tree_crawl)(share_planes=True)
+            t1 = time.perf_counter()
+            diff = np.zeros((C, nw), np.uint64)
+            for j in range(2 * d):
+                diff |= p0[:, j] ^ p1[:, j]
+            cnt = np.bitwise_count(~diff & valid).sum(axis=1)
+            keep = cnt >= thr
+            t2 = time.perf_counter()
+            if C > vals.shape[0]:
+                raise SystemExit(f"dropin: {C} children > the {vals.shape[0]} rows of host values")
+            v = vals[:C]
+            if not last:
+                c0.node_sums_fe(v)
+                c1.node_sums_fe(v)
+            t3 = time.perf_counter()
+            if last:
+                c0.tree_prune_last(keep)
+                c1.tree_prune_last(keep)
+                final = int(keep.sum())
+            else:
+                c0.tree_prune(keep)
+                c1.tree_prune(keep)
+            t4 = time.perf_counter()
+            per["crawl_planes"] += t1 - t0
+            per["leader"] += t2 - t1
+            per["node_sums"] += t3 - t2
+            per["prune"] += t4 - t3
+        return final, per
+
+    def timed(fn, reps):
+        best, out = None, None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return best, out
+
+    reps = max(1, args.steps)
+    for _ in range(args.warmup):
+        fhh.sim_crawl(c0, c1, args.threshold, mode="count", record=False)
+    t_fused, res = timed(lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="count", record=False), reps)
+    hh = len(res.final)
+    dropin_crawl()   # warm-up (buffer growth)
+    t_dropin, (hh_d, per) = timed(dropin_crawl, reps)
+    assert hh_d == hh, f"drop-in path found {hh_d} heavy hitters, fused {hh}"
+    out = {
+        "metric": "drop-in KeyCollection ABI path vs the fused device loop: full-crawl wall time",
+        "value": t_dropin, "unit": "s per crawl", "n_gpus": 1, "steps": reps, "warmup": args.warmup,
+        "ms_per_step": t_dropin * 1e3, "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic Zipf workload (leader.rs shape), GPU keygen; host OT outputs are random u64",
+        "config": {"workload": f"{n} Zipf clients, data_len {L}, d {d}, threshold {args.threshold}, both servers",
+                   "parallelism": "single GPU"},
+        "fused_crawl_s": t_fused, "dropin_crawl_s": t_dropin, "dropin_over_fused": t_dropin / t_fused,
+        "dropin_ms_per_level": {k: v / L * 1e3 for k, v in per.items()},   # the last timed crawl
+        "dropin_overhead_ms_per_level": (t_dropin - t_fused) / L * 1e3,
+        "heavy_hitters": hh,
+    }
+    if not args.no_party:
+        del c0, c1
+        g0, g1 = pair()
+        t_gc, res_gc = timed(lambda: fhh.sim_crawl(g0, g1, args.threshold, mode="fe", prf_seed=7, gc="ot",
+                                                   record=False), 1)
+        del g0, g1
+        p0, p1 = pair()
+        t_2p, res_2p = timed(lambda: fhh.two_party_crawl(p0, p1, args.threshold, prf_seed=7), 1)
+        assert len(res_2p.final) == len(res_gc.final) == hh
+        tot = {k: sum(lb.get(k, 0) for lb in res_2p.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
+        out.update({
+            "gcot_in_process_crawl_s": t_gc, "gcot_two_party_crawl_s": t_2p,
+            "two_party_over_in_process": t_2p / t_gc,
+            "two_party_channel_bytes_per_crawl": tot,
+            "two_party_channel_bytes_total": sum(tot.values()),
+            "two_party_max_bytes_per_level": max(sum(lb.values()) for lb in res_2p.level_bytes),
+        })
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def gc_bench(args, world, rank, local_rank, dist):
     """Row f1: one step = the garbled-circuit equality tests of one crawl level at configs[1]
     scale (--gc-groups children x --clients clients per GPU, 2d-bit share strings):
@@ -348,11 +474,14 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
-    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc", "bincode"],
+    ap.add_argument("--no-party", action="store_true", help="--workload dropin: skip the GC + OT legs")
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc", "bincode", "dropin"],
                     help="zipf = the metric's Zipf crawl (default 1M clients; --clients 100000 = configs[1]); "
                          "coords = configs[3] (d=2 lat/lon, data_len 16); sketch = configs[4] (sketch + Beaver "
                          "verification); gc = row f1 (garbled-circuit equality tests of one level); "
-                         "bincode = row f4 (add_keys payload decoded on the GPU, --clients per GPU)")
+                         "bincode = row f4 (add_keys payload decoded on the GPU, --clients per GPU); "
+                         "dropin = the KeyCollection ABI path per level and the two-party GC + OT split vs the "
+                         "fused loops (--clients 100000 = configs[1])")
     ap.add_argument("--gc-groups", type=int, default=256, help="--workload gc: children per level")
     ap.add_argument("--gc-clients", type=int, default=100_000, help="--workload gc: clients per GPU")
     ap.add_argument("--gc", default="none", choices=["none", "ot", "ideal"],
@@ -410,6 +539,8 @@ def main():
         return gc_bench(args, world, rank, local_rank, dist)
     if args.workload == "bincode":
         return bincode_bench(args, world, rank, local_rank, dist)
+    if args.workload == "dropin":
+        return dropin_bench(args, world, rank, local_rank, dist)
     if args.gc != "none" and args.mode != "fe":
         args.mode = "fe"   # the GC equality test feeds the OT share conversion (collect.rs:419-482)
 

@@ -239,6 +239,8 @@ void host_key_schedule(const uint8_t key[16], uint32_t (&rk)[11][4]);
 void words_from_bytes(const uint8_t b[16], uint32_t (&w)[4]);
 uint64_t host_mix64(uint64_t z);
 void gc_level_material(uint64_t prf_seed, uint32_t level, uint8_t key[16], uint8_t delta[16], uint32_t* mask);
+void gc_chunk_material(uint64_t prf_seed, uint32_t level, uint64_t chunk, uint8_t key[16], uint8_t delta[16],
+                       uint32_t* mask);
 int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a);
 uint64_t ot_padded(uint64_t m);
 void ot_level_choice(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s[4]);
@@ -252,7 +254,7 @@ struct OtOut {            // optional transcript (device pointers into the scrat
 int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev);
 int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
            const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr);
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off = 0);
 
 }  // namespace eng
 }  // namespace fhh

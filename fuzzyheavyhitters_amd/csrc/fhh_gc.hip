@@ -67,12 +67,15 @@ __device__ __forceinline__ uint32_t plane_bit(const uint64_t* planes, uint64_t g
     return (uint32_t)(planes[((size_t)g * bits + j) * nw + (i >> 6)] >> (i & 63)) & 1u;
 }
 
-// tests to run: G * N, or, inside the level loop, the children the previous prune left
+// tests to run: G * N, or, inside the level loop, those of the chunk's groups [g_off, g_off + G)
+// that the previous prune left (C children)
 __device__ __forceinline__ uint64_t gc_active(const GcArgs& a) {
     if (!a.ctl) return a.G * a.N;
     if (a.ctl->abort) return 0;
     const uint64_t C = a.ctl->C;
-    return (C < a.G ? C : a.G) * a.N;
+    if (C <= a.g_off) return 0;
+    const uint64_t g = C - a.g_off;
+    return (g < a.G ? g : a.G) * a.N;
 }
 
 __device__ __forceinline__ void st_blk(uint4* base, uint64_t row, uint64_t n, uint64_t t, const uint32_t (&v)[4]) {
@@ -105,11 +108,12 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     constexpr int W = 2 * B + 1;
     const uint64_t n_act = gc_active(a);
     for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
-        const uint64_t g = t / a.N;
+        const uint64_t g = t / a.N;                  // group within the chunk
         const uint32_t i = (uint32_t)(t - g * a.N);
+        const uint64_t tg = a.g_off * a.N + t;       // the test's index in the whole level
         // zero labels, generated per wire pair as the gates consume them (registers do not
         // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B
-        const uint64_t ctr0 = a.label_nonce + t * W;
+        const uint64_t ctr0 = a.label_nonce + tg * W;
         uint32_t acc[4];
 #pragma unroll
         for (int k = 0; k < B; k++) {
@@ -117,8 +121,8 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
                                 {(uint32_t)(ctr0 + B + 1 + k), (uint32_t)((ctr0 + B + 1 + k) >> 32), 0u, 0u}};
             aes_rk<GcTab, 2>(s, tbl_gc, b0, b1, lrk);
             // active labels: the garbler's bit (sent in the clear), the evaluator's (via OT)
-            const uint32_t gb = plane_bit(a.gb_planes, g, B, k, a.nw, i);
-            const uint32_t eb = a.ev_ot ? 0u : plane_bit(a.ev_planes, g, B, k, a.nw, i);
+            const uint32_t gb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
+            const uint32_t eb = a.ev_ot ? 0u : plane_bit(a.ev_planes, a.g_off + g, B, k, a.nw, i);
             uint32_t x[4], y[4], bz[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
                 h[3][c] = bz[c] ^ D[c];
             }
             const uint32_t pa = acc[0] & 1u, pb = bz[0] & 1u;
-            const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
+            const uint64_t j = 2 * (a.gate_base + tg * (B - 1) + (k - 1));
             const uint64_t tw[4] = {j, j, j + 1, j + 1};
             tccr<4>(h, tw, tbl_gc, b0, b1, zrk);
             uint32_t TG[4], TE[4];
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
                     h[1][c] = x[c] ^ y[c];
                 }
                 const uint32_t sa = acc[0] & 1u, sb = h[1][0] & 1u;
-                const uint64_t j = 2 * (a.gate_base + t * (B - 1) + (k - 1));
+                const uint64_t j = 2 * (a.gate_base + (a.g_off * a.N + t) * (B - 1) + (k - 1));
                 const uint64_t tw[2] = {j, j + 1};
                 tccr<2>(h, tw, tbl_gc, b0, b1, zrk);
 #pragma unroll

@@ -65,6 +65,15 @@ void gc_level_material(uint64_t prf_seed, uint32_t level, uint8_t key[16], uint8
     *mask = (uint32_t)(host_mix64(z) & 1);
 }
 
+// chunk k of a level's GC (the in-process loop splits a level's tests in chunks of children, each a
+// fresh protocol instance, as the reference's channels are, collect.rs:423-430); chunk 0 = the
+// level's material
+void gc_chunk_material(uint64_t prf_seed, uint32_t level, uint64_t chunk, uint8_t key[16], uint8_t delta[16],
+                       uint32_t* mask) {
+    gc_level_material(chunk ? host_mix64(prf_seed ^ (0x6368756e6b000000ull + chunk)) : prf_seed, level, key, delta,
+                      mask);
+}
+
 // validated GcArgs from a batch (device pointers)
 int gc_args(fhh_ctx* ctx, const fhh_gc_batch* b, GcArgs& a) {
     if (!b) return ctx->fail(FHH_E_ARG, "gc: NULL batch");
@@ -143,7 +152,7 @@ int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t 
 // key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
 int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
            const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr) {
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off) {
     if (m == 0) return FHH_OK;
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
@@ -168,6 +177,7 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     a.tweak_base = tweak_base;
     a.ctl = ctl;
     a.per_group = per_group;
+    a.g_off = g_off;
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
     HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1

@@ -915,6 +915,16 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     const int variant = c0->variant;
     const uint64_t grid_waves = (uint64_t)c0->grid * (expand_threads(variant) / 64);
     const uint32_t per_level_per = cfg->mode == 0 ? 1 : 4;   // partial u64 per child (non-last)
+    // GC + OT chunk: children per protocol instance, so the level's GC and OT buffers (~400 B per
+    // test at d = 1) stay within FHH_GC_CHUNK_BYTES (default 64 GiB): one chunk per level at
+    // configs[1], ~160 children per chunk at 1M clients
+    uint64_t gc_groups = ~0ull;
+    if (cfg->gc) {
+        uint64_t budget = 64ull << 30;
+        if (const char* e = std::getenv("FHH_GC_CHUNK_BYTES")) budget = std::strtoull(e, nullptr, 10);
+        const uint64_t per_test = 200ull * 2 * d + 2;
+        gc_groups = std::max<uint64_t>(1, budget / (per_test * std::max<uint64_t>(c0->npad, 1)));
+    }
     PhaseClock pc;
     LoopBuffers B;
     B.distributed = cfg->comm || cfg->allreduce;
@@ -1070,115 +1080,136 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             a.ctl = B.ctl.as<LoopCtl>();
             uint64_t* part = B.partials.as<uint64_t>();
             if (cfg->gc && pmode != 0) {
-                // garbled-circuit equality (tree_crawl with gc_sender, collect.rs:419-482):
-                // both servers' share planes, server 0 garbles, server 1 evaluates
+                // garbled-circuit equality (tree_crawl with gc_sender, collect.rs:419-482): both
+                // servers' share planes, server 0 garbles, server 1 evaluates. The level's tests
+                // run in chunks of gc_groups children (bounded memory at 1M clients; the reference
+                // splits a level's tests over its channels the same way, collect.rs:423-430), each
+                // chunk a fresh protocol instance: its own garbler key / Delta / mask and base OTs
                 const uint32_t bits = 2 * d;
-                const uint64_t tests = C_cap * c0->n;
                 const size_t plane_bytes = (size_t)C_cap * bits * c0->nw * 8;
                 for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
-                HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
-                HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
-                // OT mode: the evaluator's zero labels at OT index (g bits + j) npad + i
-                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * C_cap * c0->npad * 16));
-                HIP_TRY(c0, B.gc_decode.ensure(tests));
-                HIP_TRY(c0, B.gc_out.ensure(tests));
                 ChildArgs pa = a;
                 HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[0].as<uint64_t>(), c0->stream));
                 pa.s0 = a.s1;
                 HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[1].as<uint64_t>(), c0->stream));
-                fhh_gc_batch gb{};
-                gb.groups = C_cap;
-                gb.clients = (uint32_t)c0->n;
-                gb.words = (uint32_t)c0->nw;
-                gb.bits = bits;
-                gc_level_material(cfg->prf_seed, lv, gb.label_key, gb.delta, &gb.mask);
-                gb.gb_planes_dev = B.gc_planes[0].as<uint64_t>();
-                gb.ev_planes_dev = B.gc_planes[1].as<uint64_t>();
-                gb.tables_dev = B.gc_tables.as<uint8_t>();
-                gb.gb_labels_dev = B.gc_gbl.as<uint8_t>();
-                gb.ev_labels_dev = B.gc_evl.as<uint8_t>();
-                gb.decode_dev = B.gc_decode.as<uint8_t>();
-                gb.out_dev = B.gc_out.as<uint8_t>();
-                GcArgs g{};
-                rc = gc_args(c0, &gb, g);
-                if (rc) return rc;
-                g.ctl = B.ctl.as<LoopCtl>();
+                const uint64_t Gc = std::min<uint64_t>(C_cap, gc_groups);
+                const uint64_t chunks = (C_cap + Gc - 1) / Gc;
                 const bool real_ot = cfg->gc >= 2;
-                g.ev_ot = real_ot ? 1u : 0u;
-                HIP_TRY(c0, launch_gc_garble(g, c0->stream));
-                HIP_TRY(c0, c0->ot_rk.ensure((size_t)3 * 128 * 44 * 4));
-                if (real_ot) {
-                    // the evaluator's input labels by OT extension (gb_set_fancy_inputs /
-                    // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1 receives the
-                    // labels of its share bits, server 0 sends (zero label, zero label ^ Delta)
-                    // OT index (g bits + j) npad + i: the choice bits are server 1's share planes
-                    // [C][bits][nw] as they stand (m1 is a multiple of 128: npad of 64, bits even)
-                    const uint64_t m1 = (uint64_t)C_cap * bits * c0->npad;
-                    const uint32_t* ch = B.gc_planes[1].as<uint32_t>();
-                    uint32_t sw[4];
-                    ot_level_choice(cfg->prf_seed, lv, 0, sw);
-                    const uint32_t* rk1 = c0->ot_rk.as<uint32_t>();
-                    if (B.base_ot) {
-                        rc = upload_base_ot(c0, B, 2 * lv);
-                        if (rc) return rc;
-                        rk1 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 0) * 3 * 128 * 44;
-                    } else {
-                        HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 0, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
-                    }
-                    HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
-                    rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(), rk1, sw, 0,
-                                B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits, nullptr);
-                    if (rc) return rc;
-                    g.ev_labels = B.gc_evact.as<uint4>();
-                }
+                if (B.base_ot && chunks > 1)
+                    return c0->fail(FHH_E_ARG, "sim_crawl: real base OTs need the level's GC in one chunk "
+                                               "(raise FHH_GC_CHUNK_BYTES)");
+                const uint64_t tests = Gc * c0->n;
                 const uint32_t per2 = pmode == 1 ? 1 : 2;   // OTs per test of the share conversion
-                if (real_ot) {
-                    // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
-                    uint32_t* ch = nullptr;
-                    HIP_TRY(c0, ot_choices_buffer(c0, tests * per2, &ch));
-                    g.out_packed = ch;
-                    g.out_dup = per2;
-                }
-                HIP_TRY(c0, launch_gc_eval(g, c0->stream));
-                a.gc_out = g.out;
-                a.gc_N = g.N;
-                a.gc_mask = g.mask;
-                if (real_ot) {
-                    // the share conversion by OT extension (collect.rs:437-471; 846-876 at the last
-                    // level, where a FieldElm travels as a BlockPair = 2 OTs): server 0 sends
-                    // (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
-                    const uint32_t per = per2;
-                    const uint64_t m2 = tests * per;
-                    HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
-                    HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
-                    HIP_TRY(c0, B.gc_recv.ensure(m2 * 16));
-                    if (pmode == 1)
-                        HIP_TRY(c0, launch_ot_fe_messages(a, g.mask, B.gc_msg[0].as<uint4>(),
-                                                          B.gc_msg[1].as<uint4>(), c0->stream));
-                    else
-                        HIP_TRY(c0, launch_ot_fe255_messages(a, g.mask, B.gc_msg[0].as<uint4>(),
-                                                             B.gc_msg[1].as<uint4>(), c0->stream));
-                    const uint32_t* ch = g.out_packed;
-                    uint32_t sw[4];
-                    ot_level_choice(cfg->prf_seed, lv, 1, sw);
-                    const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
-                    if (B.base_ot) {
-                        rc = upload_base_ot(c0, B, 2 * lv + 1);
-                        if (rc) return rc;
-                        rk2 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 1) * 3 * 128 * 44;
-                    } else {
-                        HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, 1, sw, c0->ot_rk.as<uint32_t>(), c0->stream));
-                    }
-                    rc = ot_run(c0, m2, ch, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
-                                B.gc_recv.as<uint4>(), rk2, sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * per,
-                                nullptr);
+                HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
+                HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
+                // OT mode: the evaluator's zero labels at OT index (g bits + j) npad + i
+                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * Gc * c0->npad * 16));
+                HIP_TRY(c0, B.gc_decode.ensure(tests));
+                HIP_TRY(c0, B.gc_out.ensure(tests));
+                HIP_TRY(c0, c0->ot_rk.ensure((size_t)3 * 128 * 44 * 4));
+                for (uint64_t k = 0; k < chunks; k++) {
+                    const uint64_t g_off = k * Gc;
+                    fhh_gc_batch gb{};
+                    gb.groups = Gc;
+                    gb.clients = (uint32_t)c0->n;
+                    gb.words = (uint32_t)c0->nw;
+                    gb.bits = bits;
+                    gc_chunk_material(cfg->prf_seed, lv, k, gb.label_key, gb.delta, &gb.mask);
+                    gb.gb_planes_dev = B.gc_planes[0].as<uint64_t>();
+                    gb.ev_planes_dev = B.gc_planes[1].as<uint64_t>();
+                    gb.tables_dev = B.gc_tables.as<uint8_t>();
+                    gb.gb_labels_dev = B.gc_gbl.as<uint8_t>();
+                    gb.ev_labels_dev = B.gc_evl.as<uint8_t>();
+                    gb.decode_dev = B.gc_decode.as<uint8_t>();
+                    gb.out_dev = B.gc_out.as<uint8_t>();
+                    GcArgs g{};
+                    rc = gc_args(c0, &gb, g);
                     if (rc) return rc;
-                    a.ot_recv = B.gc_recv.as<uint4>();
+                    g.ctl = B.ctl.as<LoopCtl>();
+                    g.g_off = g_off;
+                    g.ev_ot = real_ot ? 1u : 0u;
+                    HIP_TRY(c0, launch_gc_garble(g, c0->stream));
+                    if (real_ot) {
+                        // the evaluator's input labels by OT extension (gb_set_fancy_inputs /
+                        // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1 receives the
+                        // labels of its share bits, server 0 sends (zero label, zero label ^ Delta);
+                        // OT index (g bits + j) npad + i: the choice bits are server 1's share planes
+                        // [C][bits][nw] from the chunk's first group on, as they stand (m1 is a
+                        // multiple of 128: npad of 64, bits even)
+                        const uint64_t m1 = Gc * bits * c0->npad;
+                        const uint32_t* ch = B.gc_planes[1].as<uint32_t>() + g_off * bits * c0->nw * 2;
+                        uint32_t sw[4];
+                        ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k), sw);
+                        const uint32_t* rk1 = c0->ot_rk.as<uint32_t>();
+                        if (B.base_ot) {
+                            rc = upload_base_ot(c0, B, 2 * lv);
+                            if (rc) return rc;
+                            rk1 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 0) * 3 * 128 * 44;
+                        } else {
+                            HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k), sw,
+                                                             c0->ot_rk.as<uint32_t>(), c0->stream));
+                        }
+                        HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
+                        rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(), rk1, sw, 0,
+                                    B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits, nullptr, g_off);
+                        if (rc) return rc;
+                        g.ev_labels = B.gc_evact.as<uint4>();
+                        // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
+                        uint32_t* och = nullptr;
+                        HIP_TRY(c0, ot_choices_buffer(c0, tests * per2, &och));
+                        g.out_packed = och;
+                        g.out_dup = per2;
+                    }
+                    HIP_TRY(c0, launch_gc_eval(g, c0->stream));
+                    ChildArgs ca = a;   // this chunk's children
+                    ca.c_off = g_off;
+                    ca.c_cnt = Gc;
+                    ca.gc_out = g.out;
+                    ca.gc_N = g.N;
+                    ca.gc_mask = g.mask;
+                    if (real_ot) {
+                        // the share conversion by OT extension (collect.rs:437-471; 846-876 at the
+                        // last level, where a FieldElm travels as a BlockPair = 2 OTs): server 0
+                        // sends (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
+                        const uint64_t m2 = tests * per2;
+                        HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
+                        HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
+                        HIP_TRY(c0, B.gc_recv.ensure(m2 * 16));
+                        if (pmode == 1)
+                            HIP_TRY(c0, launch_ot_fe_messages(ca, g.mask, B.gc_msg[0].as<uint4>(),
+                                                              B.gc_msg[1].as<uint4>(), c0->stream));
+                        else
+                            HIP_TRY(c0, launch_ot_fe255_messages(ca, g.mask, B.gc_msg[0].as<uint4>(),
+                                                                 B.gc_msg[1].as<uint4>(), c0->stream));
+                        uint32_t sw[4];
+                        ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw);
+                        const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
+                        if (B.base_ot) {
+                            rc = upload_base_ot(c0, B, 2 * lv + 1);
+                            if (rc) return rc;
+                            rk2 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 1) * 3 * 128 * 44;
+                        } else {
+                            HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw,
+                                                             c0->ot_rk.as<uint32_t>(), c0->stream));
+                        }
+                        rc = ot_run(c0, m2, g.out_packed, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
+                                    B.gc_recv.as<uint4>(), rk2, sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * per2,
+                                    nullptr, g_off);
+                        if (rc) return rc;
+                        ca.ot_recv = B.gc_recv.as<uint4>();
+                    }
+                    // the chunk's children's sums (FE: atomics into the partials k_prune zeroed;
+                    // FE255: one store per child)
+                    if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(ca, part, c0->stream, false));
+                    else HIP_TRY(c0, launch_sim_ot_fe255(ca, part, c0->stream));
                 }
+            } else if (pmode == 0) {
+                HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
+            } else if (pmode == 1) {
+                HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream, false));
+            } else {
+                HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
             }
-            if (pmode == 0) HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
-            else if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream, false));
-            else HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
             // -- cross-rank sum (client-sharded multi-GPU)
             // (the count is the capacity bound: entries past C are never read)
             if (cfg->comm) {

@@ -184,6 +184,11 @@ struct ChildArgs {
     uint32_t gc_mask;
     // OT mode: the receiver's FE share of (c, i) is the OT output ot_recv[c * gc_N + i] (low 8 B)
     const uint4* ot_recv;
+    // child window of the GC + OT kernels (a chunk of the level's children, as the reference splits
+    // a level's tests over its channels, collect.rs:423-430): children [c_off, c_off + c_cnt) only,
+    // gc_out / ot_recv / OT messages indexed (c - c_off) * gc_N + i; c_cnt = 0: every child
+    uint64_t c_off;
+    uint64_t c_cnt;
 };
 
 // Garbled-circuit equality tests (row f1, equalitytest.rs:25-219): tests t = g * N + i for
@@ -214,6 +219,8 @@ struct GcArgs {
     uint32_t out_dup;            // out_packed: each output bit repeated out_dup (1 or 2) times
     uint32_t* out_packed;        // non-null: k_gc_eval also writes the outputs as bit words
                                  // (tests t0.. of a 64-aligned wave slice; the FE-share OT choices)
+    uint64_t g_off;              // chunk: groups [g_off, g_off + G) of the planes; tests, labels and
+                                 // gate tweaks keep their whole-level index (g_off N + t)
 };
 
 struct PruneArgs {
@@ -315,6 +322,7 @@ struct OtArgs {
     uint64_t tweak_base;
     const LoopCtl* ctl;
     uint64_t per_group;
+    uint64_t g_off;              // level loop chunk: OTs of groups [g_off, ctl->C) only
 };
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);

@@ -545,6 +545,14 @@ __device__ __forceinline__ uint64_t child_count(const ChildArgs& a) {
     return a.ctl ? (a.ctl->abort ? 0 : a.ctl->C) : a.C;
 }
 
+// the children a windowed kernel (GC + OT glue) visits: [c_off, min(C, c_off + c_cnt))
+__device__ __forceinline__ uint64_t child_end(const ChildArgs& a) {
+    const uint64_t C = child_count(a);
+    if (!a.c_cnt) return C;
+    const uint64_t e = a.c_off + a.c_cnt;
+    return e < C ? e : C;
+}
+
 __device__ __forceinline__ void child_entries(const ChildArgs& a, uint64_t c, uint32_t (&e)[kMaxDims]) {
     const uint64_t p = c >> a.d;
     const uint32_t i = (uint32_t)(c & ((1u << a.d) - 1));
@@ -594,6 +602,7 @@ __global__ __launch_bounds__(kEqThreads) void k_eq_count(ChildArgs a, uint64_t* 
 }
 
 static int child_grid(uint64_t C) { return (int)(C < 65535 ? (C ? C : 1) : 65535); }
+static uint64_t window_cap(const ChildArgs& a) { return a.c_cnt && a.c_cnt < a.C ? a.c_cnt : a.C; }
 
 hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
@@ -642,7 +651,7 @@ constexpr uint64_t kFeP = (1ull << 62) - (1ull << 30) - 1;
 // evaluator's garbled-circuit output XOR the garbler's mask (the OT receiver's choice bit and
 // the sender's message order, collect.rs:437-471: the received value is r0 iff eq)
 __device__ __forceinline__ bool sim_eq_bit(const ChildArgs& a, const uint32_t (&e)[kMaxDims], uint64_t c, uint32_t i) {
-    if (a.gc_out) return ((a.gc_out[c * a.gc_N + i] ^ a.gc_mask) & 1u) != 0;
+    if (a.gc_out) return ((a.gc_out[(c - a.c_off) * a.gc_N + i] ^ a.gc_mask) & 1u) != 0;
     return (eq_word(a, e, i >> 6) >> (i & 63)) & 1;
 }
 
@@ -653,10 +662,10 @@ constexpr uint32_t kSimOtChunk = 16 * kReduceThreads;
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[4 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_count(a);
+    const uint64_t C_ = child_end(a);
     const uint32_t i_begin = blockIdx.y * kSimOtChunk;
     const uint32_t i_end = min(i_begin + kSimOtChunk, a.n);
-    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         const uint64_t bc = mix64(base ^ c);
@@ -667,7 +676,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
             uint64_t v1;                                         // receiver gets pair[o] (A.5)
             if (a.ot_recv) {                                     // ... through the OT extension
-                const uint4 b = a.ot_recv[c * a.gc_N + i];
+                const uint4 b = a.ot_recv[(c - a.c_off) * a.gc_N + i];
                 v1 = (uint64_t)b.x | ((uint64_t)b.y << 32);      // FE::try_from(Block), fastfield.rs:414-421
             } else {
                 v1 = sim_eq_bit(a, e, c, i) ? r0 : r1;
@@ -688,23 +697,24 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
 // the value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430)
 __global__ __launch_bounds__(kReduceThreads) void k_ot_fe_messages(ChildArgs a, uint32_t mask, uint4* x0, uint4* x1) {
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_count(a);
-    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+    const uint64_t C_ = child_end(a);
+    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         const uint64_t bc = mix64(base ^ c);
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
             uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
             if (r0 >= kFeP) r0 -= kFeP;
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;
             const uint64_t m0 = mask ? r0 : r1, m1 = mask ? r1 : r0;
-            x0[c * a.gc_N + i] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
-            x1[c * a.gc_N + i] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
+            x0[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
+            x1[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
         }
     }
 }
 
 hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ot_fe_messages, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, mask, x0, x1);
+    hipLaunchKernelGGL(k_ot_fe_messages, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, mask, x0,
+                       x1);
     return hipGetLastError();
 }
 
@@ -715,7 +725,8 @@ hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t 
         if (e != hipSuccess) return e;
     }
     const uint32_t chunks = a.n ? (a.n + kSimOtChunk - 1) / kSimOtChunk : 1;
-    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(a.C), chunks), dim3(kReduceThreads), 0, stream, a, partials);
+    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(window_cap(a)), chunks), dim3(kReduceThreads), 0, stream, a,
+                       partials);
     return hipGetLastError();
 }
 
@@ -759,8 +770,8 @@ __device__ __forceinline__ void blockpair_to_limbs(uint4 b0, uint4 b1, uint64_t 
 __global__ __launch_bounds__(kReduceThreads) void k_ot_fe255_messages(ChildArgs a, uint32_t mask, uint4* x0,
                                                                       uint4* x1) {
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_count(a);
-    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+    const uint64_t C_ = child_end(a);
+    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         const uint64_t bc = mix64(base ^ c);
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
             const uint64_t bi = mix64(bc ^ (a.client_base + i));
@@ -779,7 +790,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_ot_fe255_messages(ChildArgs 
             fe255_canon(r1);
             const uint64_t* m0 = mask ? r0 : r1;
             const uint64_t* m1 = mask ? r1 : r0;
-            const size_t t = c * a.gc_N + i;
+            const size_t t = (c - a.c_off) * a.gc_N + i;
             x0[2 * t] = limbs_to_block(m0[3], m0[2]);
             x0[2 * t + 1] = limbs_to_block(m0[1], m0[0]);
             x1[2 * t] = limbs_to_block(m1[3], m1[2]);
@@ -790,15 +801,16 @@ __global__ __launch_bounds__(kReduceThreads) void k_ot_fe255_messages(ChildArgs 
 
 hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ot_fe255_messages, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, mask, x0, x1);
+    hipLaunchKernelGGL(k_ot_fe255_messages, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, mask,
+                       x0, x1);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[16 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_count(a);
-    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+    const uint64_t C_ = child_end(a);
+    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         const uint64_t bc = mix64(base ^ c);
@@ -825,7 +837,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
             fe255_canon(r1);
             uint64_t got[4];
             if (a.ot_recv) {   // FieldElm::try_from(BlockPair): big-endian 32 bytes (field.rs:466-476)
-                const size_t t = c * a.gc_N + i;
+                const size_t t = (c - a.c_off) * a.gc_N + i;
                 blockpair_to_limbs(a.ot_recv[2 * t], a.ot_recv[2 * t + 1], got);
             } else {
 #pragma unroll
@@ -848,7 +860,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
 
 hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sim_ot_fe255, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, partials);
+    hipLaunchKernelGGL(k_sim_ot_fe255, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, partials);
     return hipGetLastError();
 }
 

@@ -32,11 +32,13 @@ __device__ __forceinline__ void ot_fill(uint32_t* tbl) {
     __syncthreads();
 }
 
-// OTs to run: m, or inside the level loop per_group * min(groups, ctl->C)
+// OTs to run: m, or inside the level loop per_group * min(groups, ctl->C - g_off)
 __device__ __forceinline__ uint64_t ot_active(const OtArgs& a) {
     if (!a.ctl) return a.m;
     if (a.ctl->abort) return 0;
-    const uint64_t v = a.per_group * a.ctl->C;
+    const uint64_t C = a.ctl->C;
+    if (C <= a.g_off) return 0;
+    const uint64_t v = a.per_group * (C - a.g_off);   // the chunk's groups from g_off on
     return v < a.m ? v : a.m;
 }
 

@@ -169,6 +169,25 @@ def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot"])
+def test_gpu_crawl_with_gc_in_chunks(monkeypatch, gc_mode):
+    """A level's GC + OT split into chunks of children, each a fresh protocol instance (the
+    reference spreads a level's tests over its channels, collect.rs:423-430; the device loop
+    chunks so the GC and OT buffers of 1M clients stay bounded): FHH_GC_CHUNK_BYTES small enough
+    for 3 children per chunk -> the same sums, keep decisions and heavy hitters as the plaintext
+    harness (the last chunk of a level partial, chunks past C no-ops)."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(1000, 48, 1, num_sites=30, seed=17)
+    c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    plain = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=3)
+    npad = (1000 + 63) // 64 * 64
+    monkeypatch.setenv("FHH_GC_CHUNK_BYTES", str(3 * 402 * npad))   # 3 children x ~402 B per test (d = 1)
+    with_gc = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=3, gc=gc_mode)
+    assert _sig(with_gc) == _sig(plain)
+    assert max(plain.level_children) > 6 and len(with_gc.final) > 0
+
+
+@pytest.mark.gpu
 def test_gpu_crawl_gc_rejects_count_mode():
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sim_crawl, workload

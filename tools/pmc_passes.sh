@@ -1,20 +1,20 @@
 #!/bin/bash
-# Run one rocprofv3 --pmc pass per argument group over `python3 bench.py $BENCH_ARGS`
-# (each pass its own run, --kernel-trace only, killed after 120 s), into gpurun_out/pmc_<tag>/.
-# Usage: BENCH_ARGS="--steps 1 --warmup 1 --no-cpu-baseline" tools/pmc_passes.sh <tag> "C1 C2 .." "C3 .." ...
+# PMC passes of one bench.py command (run from the repo root on the GPU box), one rocprofv3 run
+# per counter group (the hardware cannot collect them together; --kernel-trace only beside --pmc):
+#   tools/pmc_passes.sh <tag> <bench args...>   -> gpurun_out/pmc_<tag>/p<k>/...
+# Summaries: python tools/pmc_means.py gpurun_out/pmc_<tag> [kernel] --json out.json
 set -u
 TAG=$1; shift
-ARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}
 export TMPDIR=/tmp
-OUT=$PWD/gpurun_out/pmc_$TAG
+OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
-i=0
-for pass in "$@"; do
-  i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $pass -T --output-format csv -d $OUT/p$i -o p$i -- \
-      python3 bench.py $ARGS > $OUT/p$i.log 2>&1
+k=0
+for group in "SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE GRBM_COUNT" \
+             "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES"; do
+  k=$((k + 1))
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc $group --output-format csv -d $OUT/p$k -o p$k -- \
+      python3 bench.py "$@" > $OUT/p$k.log 2>&1
   rc=$?
-  echo "pass $i ($pass) rc=$rc"
-  case $rc in 0) ;; *) echo "stopping after rc=$rc"; exit $rc;; esac
+  echo "pass $k ($group) rc=$rc"
+  case $rc in 0) ;; *) exit $rc;; esac
 done
-echo done

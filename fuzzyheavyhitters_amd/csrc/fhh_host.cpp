@@ -187,7 +187,12 @@ int table_ensure(fhh_ctx* ctx, DimTable& T, int buf, size_t entries) {
     size_t cap = std::max<size_t>(entries, T.cap[buf] * 2);
     cap = std::max<size_t>(cap, 4);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    HIP_TRY(ctx, T.seed[buf].ensure(cap * 2 * ctx->npad * 16));
+    if (T.seed[buf].ensure(cap * 2 * ctx->npad * 16) != hipSuccess) {
+        // the doubling does not fit (32 MB per entry at 1M clients): exactly what is needed
+        (void)hipGetLastError();
+        cap = std::max<size_t>(entries, 4);
+        HIP_TRY(ctx, T.seed[buf].ensure(cap * 2 * ctx->npad * 16));
+    }
     HIP_TRY(ctx, T.t[buf].ensure(cap * 2 * ctx->nw * 8));
     HIP_TRY(ctx, T.y[buf].ensure(cap * 2 * ctx->nw * 8));
     T.cap[buf] = cap;
@@ -848,6 +853,51 @@ int table_grow(fhh_ctx* ctx, DimTable& T, int buf, size_t cap, size_t keep) {
     return FHH_OK;
 }
 
+void table_release(DimTable& T, int buf) {
+    T.seed[buf].release();
+    T.t[buf].release();
+    T.y[buf].release();
+    T.cap[buf] = 0;
+}
+
+size_t table_entry_bytes(const fhh_ctx* c) { return 2 * c->npad * 16 + 2 * 2 * c->nw * 8; }
+
+// Entry capacity of every dim table after a device-loop abort that needs `need` entries. 2x the
+// next power of two (few resumes) when the tables of the servers on this device fit beside what
+// else is allocated; else 1.25x the need in 64-entry steps; else the need itself. At 1M clients an
+// entry is 32 MB (both sides' seeds), so the doubling alone overshot 288 GB at configs[3]'s dense
+// thresholds (2 servers x d dims x 2 parities of tables on one GPU).
+int loop_entry_cap(fhh_ctx* const (&cs)[2], uint32_t d, uint32_t E_cap, uint32_t need, uint32_t la, uint32_t& out) {
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(cs[0], hipMemGetInfo(&free_b, &total_b));
+    size_t held = 0, old_pres = 0, n_tab = 0;   // bytes the tables hold now; largest preserved one
+    for (fhh_ctx* c : cs) {
+        if (c->device != cs[0]->device) continue;
+        const size_t bpe = table_entry_bytes(c);
+        for (uint32_t j = 0; j < d; j++) {
+            held += (c->tab[j].cap[0] + c->tab[j].cap[1]) * bpe;
+            old_pres = std::max(old_pres, c->tab[j].cap[1 - (la & 1)] * bpe);
+            n_tab += 2;
+        }
+    }
+    const size_t bpe = table_entry_bytes(cs[0]);
+    const size_t margin = (size_t)2 << 30;
+    const size_t avail = free_b + held > margin ? free_b + held - margin : 0;
+    const uint64_t cand[3] = {(uint64_t)next_pow2(need) * 2, ((uint64_t)need * 5 / 4 + 63) / 64 * 64, need};
+    out = std::max<uint32_t>(E_cap, need);
+    for (uint64_t e : cand) {
+        e = std::max<uint64_t>(e, E_cap);
+        if (e * bpe * n_tab + old_pres <= avail) {
+            out = (uint32_t)e;
+            break;
+        }
+    }
+    if (std::getenv("FHH_DEBUG_LOOP"))
+        std::fprintf(stderr, "[fhh loop] entry cap: need %u -> %u (%.1f GB of tables, %.1f GB available)\n", need,
+                     out, (double)out * bpe * n_tab / 1e9, (double)avail / 1e9);
+    return FHH_OK;
+}
+
 // (re)size the loop buffers; preserve what a resumed prune of `level` still reads
 int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uint32_t levels, uint32_t level,
                 bool preserve, uint32_t keep_nodes, uint32_t keep_children, uint32_t per) {
@@ -1290,18 +1340,27 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 // grow, keep what the prune of abort_level reads, resume there
                 const uint32_t la = h->abort_level;
                 const bool la_last = la + 1 == levels;
-                const uint32_t nE = std::max(B.E_cap, next_pow2(std::max<uint32_t>(h->need_entries, 1)) * 2);
+                uint32_t nE = 0;
+                rc = loop_entry_cap(cs, d, B.E_cap, std::max<uint32_t>(h->need_entries, 1), la, nE);
+                if (rc) return rc;
                 const uint32_t nF = std::max(B.F_cap, next_pow2(std::max<uint32_t>(h->need_nodes, 1)) * 2);
                 const uint32_t la_per = cfg->mode == 0 ? 1 : (la_last ? 16 : 4);
                 if (std::getenv("FHH_DEBUG_LOOP"))
                     std::fprintf(stderr, "[fhh loop] abort at level %u (batch end %u): need_entries %u need_nodes %u "
                                  "F %u C %u -> E_cap %u F_cap %u\n", la, lv, h->need_entries, h->need_nodes, h->F,
                                  h->C, nE, nF);
+                // the tables of parity la & 1 are rewritten by level la + 1: released first, so the
+                // peak while the preserved ones are copied is one old table, not all of them
+                for (fhh_ctx* c : cs)
+                    for (uint32_t j = 0; j < d; j++) table_release(c->tab[j], la & 1);
                 for (fhh_ctx* c : cs)
                     for (uint32_t j = 0; j < d; j++) {
                         // child tables of level la (parity 1 - la&1) hold 2 * n_live(la) entries
                         rc = table_grow(c, c->tab[j], 1 - (la & 1), nE, 2 * (size_t)h->n_live[j]);
                         if (rc) return rc;
+                    }
+                for (fhh_ctx* c : cs)
+                    for (uint32_t j = 0; j < d; j++) {
                         rc = table_grow(c, c->tab[j], la & 1, nE, 0);
                         if (rc) return rc;
                     }

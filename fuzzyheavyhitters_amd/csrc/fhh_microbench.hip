@@ -3,6 +3,8 @@
 //   which = 0: v_xor_b32 lane-ops/s, every CU, 8 waves/SIMD, independent chains
 //   which = 1: ds_read_b32 bytes/s with the k_expand access pattern (per-lane replica,
 //              bank-conflict free, data-dependent byte index)
+//   which = 5: v_mad_u64_u32 lane-ops/s (the 32 x 32 + 64 -> 64 multiply-add of the FE products of
+//              k_sketch_fe), 8 waves/SIMD, independent chains; 6: the same at 4 waves/SIMD
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/fhh.h"
@@ -43,6 +45,25 @@ __global__ __launch_bounds__(256) void k_bitop3_peak(uint32_t* out, uint32_t ite
 #pragma unroll
     for (int k = 0; k < 16; k++) acc ^= x[k];
     if (acc == 0x12345678u) out[0] = acc;   // keep live
+}
+
+// v_mad_u64_u32: 16 independent 64-bit accumulators, each step one 32 x 32 + 64 multiply-add
+__global__ __launch_bounds__(256) void k_mad64_peak(uint32_t* out, uint32_t iters, uint32_t seed) {
+    uint64_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = (uint64_t)(seed * (threadIdx.x + 1) + k * 0x9e3779b9u + blockIdx.x) << 7;
+    const uint32_t m = seed | 0x10001u;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) x[k] = (uint64_t)(uint32_t)x[(k + 1 + r) & 15] * (m + r) + x[k];
+        }
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc ^= x[k];
+    if (acc == 0x12345678u) out[0] = (uint32_t)acc;   // keep live
 }
 
 __global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters) {
@@ -270,12 +291,14 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
         if (which == 0 || which >= 2) {
             // 0: v_xor_b32, 8 waves/SIMD; 2: v_bitop3_b32, 8 waves/SIMD;
             // 3: v_bitop3_b32, 2 waves/SIMD; 4: v_xor_b32, 2 waves/SIMD
-            const int wps = (which == 3 || which == 4) ? 2 : 8;
+            const int wps = (which == 3 || which == 4) ? 2 : (which == 6 ? 4 : 8);
             const int blocks = cus * wps;   // 256-thread blocks = 4 waves = one per SIMD
             const uint32_t iters = 4096;
             (void)hipEventRecord(a, 0);
             if (which == 0 || which == 4)
                 hipLaunchKernelGGL(fhh::k_valu_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else if (which == 5 || which == 6)
+                hipLaunchKernelGGL(fhh::k_mad64_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             else
                 hipLaunchKernelGGL(fhh::k_bitop3_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             (void)hipEventRecord(b, 0);

@@ -224,6 +224,10 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
     for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
         ot_tile_load(rows, W, t, lane, x);
+        // the lane's 8 OTs of the tile share one choice word (ot_tile_ot: j >> 5 = 16 t + (lane & 15));
+        // read once per tile, and only if the word holds an active OT (the buffer may end at m bits)
+        const uint64_t cwi = t * kOtTileWords + (lane & 15);
+        const uint32_t cw = 32 * cwi < m ? a.choices[cwi] : 0u;
 #pragma unroll 1
         for (int r = 0; r < 4; r += 2) {   // two rounds = 4 OTs = 4 blocks in lockstep
             uint32_t h[4][4];
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
             for (int b = 0; b < 4; b++) {
                 const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
                 if (j >= m) continue;
-                const uint32_t c = (a.choices[j >> 5] >> (j & 31)) & 1u;
+                const uint32_t c = (cw >> (j & 31)) & 1u;
                 const uint4 y = (c ? a.Y1 : a.Y0)[j];
                 a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
             }

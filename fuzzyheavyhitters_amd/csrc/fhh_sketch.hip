@@ -379,6 +379,191 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
     }
 }
 
+// ---- producer / consumer form (r03) --------------------------------------------------------
+// PMC put the fused kernel at 0.33 of VALU and 0.35 of LDS issue: every wave runs a pass's AES
+// (LDS-bound) and then its FE products (VALU-bound, ~63 % of the VALU instructions), and the waves
+// of a workgroup stay in step, so the two phases add instead of overlapping. Here the roles are
+// split: waves 0..7 of the 1024-thread workgroup only run the keystream AES and waves 8..15 only the
+// draws' products; wave w and wave w + 8 form a pair that hands over a phase's blocks (PCB per lane)
+// through LDS. A phase: the producers run the AES of pass g into registers while the consumers
+// multiply out pass g - 1 from the buffer; barrier; the producers store pass g; barrier. Waves are
+// dealt to SIMDs round-robin, so every SIMD holds two producers and two consumers, and the consumers'
+// VALU work fills the slots the producers leave while they wait on the LDS.
+// A pair task = KPW keys at LPK = 64 / KPW lanes per key; lane l of a key's segment takes keystream
+// blocks (PCB p + q) LPK + l, q < PCB, in pass p, so a task is ceil(nb / (PCB LPK)) phases, and the
+// pairs of the grid run the tasks in rounds (uniform across the grid, so every wave meets every
+// barrier). The consumer issues its next pass's (x, kx) loads one phase ahead. LDS: 128 KiB tables +
+// 11 KiB round keys (the producers' 8 x KPW schedules) + 16 KiB buffer (PCB = 2).
+constexpr int kPcPairs = 8;
+constexpr int kPcThreads = 1024;
+constexpr int kPcBlocks = 2;   // keystream blocks per producer lane per phase
+
+template <int KPW>
+__global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
+    constexpr int LPK = 64 / KPW;
+    constexpr int PCB = kPcBlocks;
+    using Tab = Tab4T32<DevOpsX>;
+    __shared__ uint32_t tbl[Tab::kWords];
+    __shared__ uint4 rks[kPcPairs][KPW][11];
+    __shared__ uint4 buf[kPcPairs][PCB][64];
+    for (int i = threadIdx.x; i < Tab::kWords; i += kPcThreads) tbl[i] = Tab::word(c_T0_sk.v, i);
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const bool prod = wv < kPcPairs;
+    const uint32_t pair = prod ? wv : wv - kPcPairs;
+    const uint32_t seg = lane / LPK, sl = lane % LPK;
+    uint32_t b0, b1;
+    Tab::bases(lane, b0, b1);
+    const uint64_t mask = (1ull << 62) - 1;
+    const uint64_t F = a.n_nodes;
+    const uint64_t nb = (F + 3 + 1) / 2;   // keystream blocks per key: draws 0..F+2
+    const uint64_t passes = (nb + PCB * LPK - 1) / (PCB * LPK);
+    const uint64_t ntasks = (a.n_keys + KPW - 1) / KPW;
+    const uint64_t pairs_total = (uint64_t)gridDim.x * kPcPairs;
+    const uint64_t rounds = (ntasks + pairs_total - 1) / pairs_total;
+    const uint64_t steps = rounds * passes;   // producer phases; the consumer trails by one
+    auto task_of = [&](uint64_t step, uint64_t& p) -> uint64_t {   // step -> (task, pass p)
+        const uint64_t round = step / passes;
+        p = step - round * passes;
+        return round * pairs_total + (uint64_t)blockIdx.x * kPcPairs + pair;
+    };
+    // the two roles run separate loops (so neither's loop-carried registers weigh on the other)
+    // with the same two barriers per phase
+    if (prod) {
+        for (uint64_t g = 0; g <= steps; g++) {
+            uint32_t st[PCB][4];
+            uint64_t p;
+            const uint64_t task = g < steps ? task_of(g, p) : ntasks;
+            const bool produced = task < ntasks;   // wave-uniform
+            if (produced) {
+                const uint64_t k = task * KPW + seg;
+                const uint64_t kk = k < a.n_keys ? k : task * KPW;
+                if (p == 0) {
+                    // the task's key schedules, once per key (every lane of the segment computes it
+                    // through the tables, lane 0 stores it)
+                    uint32_t seed[4];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
+                    seed[3] ^= a.level;   // the level's stream (bytes 12..15)
+                    uint32_t full[11][4];
+                    key_schedule_tab<Tab>(seed, full, tbl, b0, b1);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    if (sl == 0) {
+#pragma unroll
+                        for (int r = 0; r < 11; r++) rks[pair][seg][r] = make_uint4(full[r][0], full[r][1], full[r][2], full[r][3]);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+#pragma unroll
+                for (int q = 0; q < PCB; q++) {
+                    const uint64_t b = (PCB * p + q) * LPK + sl;
+                    st[q][0] = 0u;
+                    st[q][1] = 0u;
+                    st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
+                    st[q][3] = __builtin_bswap32((uint32_t)b);
+                }
+                aes_lds_rk<Tab, PCB>(st, tbl, b0, b1, rks[pair][seg]);
+            }
+            __syncthreads();   // the consumers are done with the buffer
+            if (produced) {
+#pragma unroll
+                for (int q = 0; q < PCB; q++) buf[pair][q][lane] = make_uint4(st[q][0], st[q][1], st[q][2], st[q][3]);
+            }
+            __syncthreads();   // pass g is in the buffer
+        }
+        return;
+    }
+    unsigned __int128 ax = 0, a2x = 0, akx = 0;
+    uint64_t rnd0 = 0, rnd1 = 0, xv_n[2 * PCB] = {}, kxv_n[2 * PCB] = {};
+    bool rej = false;
+    auto load_xkx = [&](uint64_t step) {   // the (x, kx) of the lane's 2 PCB draws of `step`
+        uint64_t p;
+        const uint64_t task = task_of(step, p);
+#pragma unroll
+        for (int i = 0; i < 2 * PCB; i++) xv_n[i] = kxv_n[i] = 0;
+        if (task >= ntasks) return;
+        const uint64_t k = task * KPW + seg;
+        if (k >= a.n_keys) return;
+#pragma unroll
+        for (int q = 0; q < PCB; q++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint64_t pos = 2 * ((PCB * p + q) * LPK + sl) + h;
+                if (pos >= 3 && pos < F + 3) {
+                    xv_n[2 * q + h] = a.x[k * F + pos - 3];
+                    kxv_n[2 * q + h] = a.kx[k * F + pos - 3];
+                }
+            }
+    };
+    if (steps > 0) load_xkx(0);
+    for (uint64_t g = 0; g <= steps; g++) {
+        if (g > 0) {
+            const uint64_t step = g - 1;
+            uint64_t p;
+            const uint64_t task = task_of(step, p);
+            uint64_t xv[2 * PCB], kxv[2 * PCB];
+#pragma unroll
+            for (int i = 0; i < 2 * PCB; i++) {
+                xv[i] = xv_n[i];
+                kxv[i] = kxv_n[i];
+            }
+            if (step + 1 < steps) load_xkx(step + 1);   // one phase ahead
+            if (task < ntasks) {   // wave-uniform
+                const uint64_t k = task * KPW + seg;
+                const bool kact = k < a.n_keys;
+                if (p == 0) {
+                    ax = a2x = akx = 0;
+                    rnd0 = rnd1 = 0;
+                    rej = false;
+                }
+#pragma unroll
+                for (int q = 0; q < PCB; q++) {
+                    const uint4 s = buf[pair][q][lane];
+                    const uint64_t b = (PCB * p + q) * LPK + sl;
+                    const uint64_t dr[2] = {(uint64_t)s.x | ((uint64_t)s.y << 32), (uint64_t)s.z | ((uint64_t)s.w << 32)};
+#pragma unroll
+                    for (int h = 0; h < 2; h++)   // positions past the stream carry x = kx = 0: no-ops
+                        sketch_draw_lazy(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
+                                         ax, a2x, akx);
+                }
+                ax = fe_red128(ax);
+                a2x = fe_red128(a2x);
+                akx = fe_red128(akx);
+                if (p == passes - 1) {
+                    const uint64_t rej_mask = __ballot(rej);
+                    const uint64_t seg_bits = (LPK == 64 ? ~0ull : ((1ull << LPK) - 1)) << (seg * LPK);
+                    const bool key_rej = a.force_sequential || (rej_mask & seg_bits) != 0;
+                    const uint64_t rx = seg_fe_sum<LPK>((uint64_t)ax), r2x = seg_fe_sum<LPK>((uint64_t)a2x),
+                                   rkx = seg_fe_sum<LPK>((uint64_t)akx);
+                    const uint64_t rand1 = __shfl(rnd0, seg * LPK, 64);
+                    const uint64_t rand2 = __shfl(rnd1, seg * LPK, 64);
+                    const uint64_t rand3 = __shfl(rnd0, seg * LPK + 1, 64);
+                    if (kact && sl == 0) {
+                        if (!key_rej) {
+                            uint64_t* o = a.out + 6 * k;
+                            o[0] = rx;
+                            o[1] = r2x;
+                            o[2] = rkx;
+                            o[3] = rand1;
+                            o[4] = rand2;
+                            o[5] = rand3;
+                        } else {
+                            uint32_t seed[4];
+#pragma unroll
+                            for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * k + c];
+                            seed[3] ^= a.level;
+                            sketch_sequential_otf<Tab>(tbl, b0, b1, seed, a.x + k * F, a.kx + k * F, F, a.out + 6 * k);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();   // the producers may overwrite the buffer
+        __syncthreads();   // the next pass is in the buffer
+    }
+}
+
 constexpr int kSketchKeysPerWave = 4;
 // default form: 8 keys per wave (8 lanes per key: at 256 nodes 130 blocks fill 9 passes of 16
 // slots, 90 % of the slots), four-table LDS layout, 1024 threads, round keys in LDS
@@ -446,20 +631,27 @@ static uint64_t sketch_resident_waves() {
 
 // cost in passes of one launch of n keys at LPK lanes per key (+ half a pass per round for the key
 // schedule, the reductions and the stores)
-static double sketch_launch_cost(uint64_t n, uint64_t nb, int lpk, uint64_t W) {
+static double sketch_launch_cost(uint64_t n, uint64_t nb, int lpk, uint64_t W, int nbp = kSketchNbpOtf) {
     if (n == 0) return 0.0;
     const uint64_t kpw = 64 / lpk, tasks = (n + kpw - 1) / kpw, rounds = (tasks + W - 1) / W;
-    const uint64_t passes = ((nb + lpk - 1) / lpk + kSketchNbpOtf - 1) / kSketchNbpOtf;
+    const uint64_t passes = ((nb + lpk - 1) / lpk + nbp - 1) / nbp;
     return (double)rounds * ((double)passes + 0.5);
 }
 
+// W = resident waves (fused form, nbp = 2 blocks per lane per pass) or resident producer / consumer
+// pairs (nbp = 1: one block per lane per phase)
+SketchPlan plan_sketch_nbp(uint64_t n_keys, uint32_t n_nodes, uint64_t W, int nbp);
 SketchPlan plan_sketch(uint64_t n_keys, uint32_t n_nodes, uint64_t W) {
+    return plan_sketch_nbp(n_keys, n_nodes, W, kSketchNbpOtf);
+}
+
+SketchPlan plan_sketch_nbp(uint64_t n_keys, uint32_t n_nodes, uint64_t W, int nbp) {
     static const int kLpk[4] = {8, 16, 32, 64};
     const uint64_t nb = ((uint64_t)n_nodes + 4) / 2;
     SketchPlan best{n_keys, 8, 8};
-    double best_cost = sketch_launch_cost(n_keys, nb, 8, W);
+    double best_cost = sketch_launch_cost(n_keys, nb, 8, W, nbp);
     for (int L : kLpk) {   // one launch (ties keep the smaller LPK: less redundant schedule work)
-        const double c = sketch_launch_cost(n_keys, nb, L, W);
+        const double c = sketch_launch_cost(n_keys, nb, L, W, nbp);
         if (c < best_cost) best_cost = c, best = SketchPlan{n_keys, L, L};
     }
     for (int Lm : kLpk) {   // R full rounds at Lm, the rest at Lt (+ half a pass for the second launch)
@@ -468,7 +660,7 @@ SketchPlan plan_sketch(uint64_t n_keys, uint32_t n_nodes, uint64_t W) {
         const uint64_t n_main = R * W * kpw;
         if (n_main >= n_keys) continue;
         for (int Lt : kLpk) {
-            const double c = sketch_launch_cost(n_main, nb, Lm, W) + sketch_launch_cost(n_keys - n_main, nb, Lt, W) + 0.5;
+            const double c = sketch_launch_cost(n_main, nb, Lm, W, nbp) + sketch_launch_cost(n_keys - n_main, nb, Lt, W, nbp) + 0.5;
             if (c < best_cost) best_cost = c, best = SketchPlan{n_main, Lm, Lt};
         }
     }
@@ -490,13 +682,54 @@ extern "C" int fhh_sketch_plan(uint64_t n_keys, uint32_t n_nodes, uint64_t resid
 // default kernel at LPK 8 for every key (the form before plan_sketch)
 static int g_sketch_impl = 0;
 extern "C" int fhh_sketch_set_impl(int impl) {
-    if (impl < 0 || impl > 3) return FHH_E_ARG;
+    if (impl < 0 || impl > 4) return FHH_E_ARG;
     g_sketch_impl = impl;
     return FHH_OK;
 }
 
+// the producer / consumer form: one 1024-thread workgroup per CU (155 KiB of LDS), the same
+// planned split of the keys over lanes-per-key as the fused form, priced at kPcBlocks per phase
+template <int KPW>
+static hipError_t launch_sketch_pc_kpw(const SketchArgs& a, int cus, hipStream_t stream) {
+    const uint64_t tasks = (a.n_keys + KPW - 1) / KPW;
+    uint64_t blocks = (tasks + kPcPairs - 1) / kPcPairs;
+    if (blocks > (uint64_t)cus) blocks = (uint64_t)cus;
+    hipLaunchKernelGGL(k_sketch_fe_pc<KPW>, dim3((unsigned)blocks), dim3(kPcThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+static hipError_t launch_sketch_pc_lpk(int lpk, const SketchArgs& a, int cus, hipStream_t stream) {
+    if (a.n_keys == 0) return hipSuccess;
+    switch (lpk) {
+        case 8: return launch_sketch_pc_kpw<8>(a, cus, stream);
+        case 16: return launch_sketch_pc_kpw<4>(a, cus, stream);
+        case 32: return launch_sketch_pc_kpw<2>(a, cus, stream);
+        default: return launch_sketch_pc_kpw<1>(a, cus, stream);
+    }
+}
+
+static hipError_t launch_sketch_pc(const SketchArgs& a, hipStream_t stream) {
+    int cus = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus < 1) cus = 256;
+    const SketchPlan p = plan_sketch_nbp(a.n_keys, a.n_nodes, (uint64_t)cus * kPcPairs, kPcBlocks);
+    SketchArgs m = a;
+    m.n_keys = p.n_main;
+    hipError_t e = launch_sketch_pc_lpk(p.lpk_main, m, cus, stream);
+    if (e != hipSuccess || p.n_main == a.n_keys) return e;
+    SketchArgs t = a;
+    t.seeds = a.seeds + 16 * p.n_main;
+    t.x = a.x ? a.x + p.n_main * a.n_nodes : nullptr;
+    t.kx = a.kx ? a.kx + p.n_main * a.n_nodes : nullptr;
+    t.out = a.out + 6 * p.n_main;
+    t.n_keys = a.n_keys - p.n_main;
+    return launch_sketch_pc_lpk(p.lpk_tail, t, cus, stream);
+}
+
 hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     if (a.n_keys == 0) return hipSuccess;
+    if (g_sketch_impl == 4) return launch_sketch_pc(a, stream);
     if (g_sketch_impl == 1)
         return launch_sketch_kernel(k_sketch_fe<kSketchKeysPerWave>, kSketchThreads, kSketchKeysPerWave, a, stream);
     if (g_sketch_impl == 2)

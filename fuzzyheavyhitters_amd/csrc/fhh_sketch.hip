@@ -396,15 +396,15 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
 // 11 KiB round keys (the producers' 8 x KPW schedules) + 16 KiB buffer (PCB = 2).
 constexpr int kPcPairs = 8;
 constexpr int kPcThreads = 1024;
-constexpr int kPcBlocks = 2;   // keystream blocks per producer lane per phase
+// keystream blocks per producer lane per phase: 3, with the key's schedule kept in VGPRs (4 with the
+// schedule expanded on the fly spilled in the consumer and ran 287.6 vs 235.6 us per launch, r03)
+constexpr int kPcBlocks = 3;
 
-template <int KPW>
+template <int KPW, int PCB = kPcBlocks>
 __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
     constexpr int LPK = 64 / KPW;
-    constexpr int PCB = kPcBlocks;
     using Tab = Tab4T32<DevOpsX>;
     __shared__ uint32_t tbl[Tab::kWords];
-    __shared__ uint4 rks[kPcPairs][KPW][11];
     __shared__ uint4 buf[kPcPairs][PCB][64];
     for (int i = threadIdx.x; i < Tab::kWords; i += kPcThreads) tbl[i] = Tab::word(c_T0_sk.v, i);
     __syncthreads();
@@ -430,6 +430,7 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
     // the two roles run separate loops (so neither's loop-carried registers weigh on the other)
     // with the same two barriers per phase
     if (prod) {
+        uint32_t rk[11][4];   // the lane's key's schedule (its segment's key), kept for the task
         for (uint64_t g = 0; g <= steps; g++) {
             uint32_t st[PCB][4];
             uint64_t p;
@@ -438,22 +439,12 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
             if (produced) {
                 const uint64_t k = task * KPW + seg;
                 const uint64_t kk = k < a.n_keys ? k : task * KPW;
-                if (p == 0) {
-                    // the task's key schedules, once per key (every lane of the segment computes it
-                    // through the tables, lane 0 stores it)
+                if (p == 0) {   // the task's key schedules, once per key, through the tables
                     uint32_t seed[4];
 #pragma unroll
                     for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
                     seed[3] ^= a.level;   // the level's stream (bytes 12..15)
-                    uint32_t full[11][4];
-                    key_schedule_tab<Tab>(seed, full, tbl, b0, b1);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    if (sl == 0) {
-#pragma unroll
-                        for (int r = 0; r < 11; r++) rks[pair][seg][r] = make_uint4(full[r][0], full[r][1], full[r][2], full[r][3]);
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
+                    key_schedule_tab<Tab>(seed, rk, tbl, b0, b1);
                 }
 #pragma unroll
                 for (int q = 0; q < PCB; q++) {
@@ -463,7 +454,7 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
                     st[q][3] = __builtin_bswap32((uint32_t)b);
                 }
-                aes_lds_rk<Tab, PCB>(st, tbl, b0, b1, rks[pair][seg]);
+                aes_rk<Tab, PCB>(st, tbl, b0, b1, rk);
             }
             __syncthreads();   // the consumers are done with the buffer
             if (produced) {
@@ -502,13 +493,8 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
             const uint64_t step = g - 1;
             uint64_t p;
             const uint64_t task = task_of(step, p);
-            uint64_t xv[2 * PCB], kxv[2 * PCB];
-#pragma unroll
-            for (int i = 0; i < 2 * PCB; i++) {
-                xv[i] = xv_n[i];
-                kxv[i] = kxv_n[i];
-            }
-            if (step + 1 < steps) load_xkx(step + 1);   // one phase ahead
+            const uint64_t* xv = xv_n;
+            const uint64_t* kxv = kxv_n;
             if (task < ntasks) {   // wave-uniform
                 const uint64_t k = task * KPW + seg;
                 const bool kact = k < a.n_keys;
@@ -530,6 +516,7 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
                 ax = fe_red128(ax);
                 a2x = fe_red128(a2x);
                 akx = fe_red128(akx);
+                if (step + 1 < steps) load_xkx(step + 1);   // a phase ahead: they land during the barriers
                 if (p == passes - 1) {
                     const uint64_t rej_mask = __ballot(rej);
                     const uint64_t seg_bits = (LPK == 64 ? ~0ull : ((1ull << LPK) - 1)) << (seg * LPK);
@@ -741,13 +728,18 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     m.n_keys = p.n_main;
     hipError_t e = launch_sketch_lpk(p.lpk_main, m, stream);
     if (e != hipSuccess || p.n_main == a.n_keys) return e;
-    SketchArgs t = a;   // the tail: the same launch on the keys past n_main
+    SketchArgs t = a;   // the tail: the keys past n_main, in one round of the producer / consumer form
     t.seeds = a.seeds + 16 * p.n_main;
     t.x = a.x ? a.x + p.n_main * a.n_nodes : nullptr;
     t.kx = a.kx ? a.kx + p.n_main * a.n_nodes : nullptr;
     t.out = a.out + 6 * p.n_main;
     t.n_keys = a.n_keys - p.n_main;
-    return launch_sketch_lpk(p.lpk_tail, t, stream);
+    // (r03, configs[4]: its 3 blocks per lane cover a 130-block key at LPK 64 in one pass where the
+    // fused form takes two: 16.2 vs 28.8 us; the main launch stays fused, 227 vs 236 us)
+    int cus = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return launch_sketch_pc_lpk(p.lpk_tail, t, cus > 0 ? cus : 256, stream);
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

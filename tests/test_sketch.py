@@ -112,8 +112,9 @@ def test_split_steps_equal_fused(oracle):
 @pytest.fixture(params=[0, 1, 2, 3, 4], ids=["lds-sched", "r01-256", "otf-1024", "lds-sched-lpk8", "prod-cons"])
 def sketch_impl(request):
     """every k_sketch_fe form (fhh_sketch_set_impl): round keys in LDS with the planned lanes per key
-    (default), r01's, on the fly, round keys in LDS at 8 lanes per key throughout, and the
-    producer / consumer form (AES waves and product waves paired through LDS, r03)"""
+    (default: the planned tail launch in the producer / consumer form), r01's, on the fly, round keys
+    in LDS at 8 lanes per key throughout, and the producer / consumer form for every key (AES waves and
+    product waves paired through LDS, r03)"""
     from fuzzyheavyhitters_amd import lib
     assert lib().fhh_sketch_set_impl(request.param) == 0
     yield request.param

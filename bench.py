@@ -508,6 +508,10 @@ def main():
                          "device count) and the per-level all-reduce runs through the hosted communicator "
                          "(the same cfg.comm path, partials summed by gloo) instead of RCCL, which cannot "
                          "place two ranks on one GPU. Never a measurement.")
+    ap.add_argument("--rehearse-rccl", action="store_true",
+                    help="as --rehearse (ranks share devices), but the ranks first try the RCCL communicator: "
+                         "its socket bootstrap completes and RCCL then refuses two ranks on one GPU, which "
+                         "exercises the init-failure fallback to the hosted communicator. Never a measurement.")
     ap.add_argument("--timing-every", type=int, default=1,
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
     args = ap.parse_args()
@@ -519,6 +523,8 @@ def main():
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
     import torch
+    if args.rehearse_rccl:
+        args.rehearse = True
     if args.rehearse:
         local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -571,7 +577,7 @@ def main():
         f"(GPU keygen {c0.stats()['keygen_ms']:.1f} ms)")
 
     comm, collective = None, {"kind": "none"}
-    if world > 1 and args.rehearse:
+    if world > 1 and args.rehearse and not args.rehearse_rccl:
         comm = fhh.HostedComm(local_rank)
         collective = {"kind": "REHEARSAL: hosted communicator (gloo all-reduce of the partials), not RCCL",
                       "comm_ranks": world, "comm_rank": rank}
@@ -581,11 +587,27 @@ def main():
         # sockets stay on loopback unless the environment says otherwise (the data path is xGMI)
         if int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world:
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        comm = fhh.RcclComm(local_rank)
-        nr, rk = comm.info()
-        collective = {"kind": "rccl ncclAllReduce(sum, u64) of per-child partials on the engine stream",
-                      "comm_ranks": nr, "comm_rank": rk}
-        log(f"[rank {rank}] RCCL communicator: {nr} ranks, rank {rk}")
+        err = None
+        try:
+            comm = fhh.RcclComm(local_rank)
+        except fhh.FhhError as e:   # an RCCL init error (not a hang) on any rank
+            err = str(e)
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        if any(errs):
+            # every rank falls back together: the same level loop with the per-level sum of the
+            # partials through the hosted communicator (gloo), labelled as such in the line
+            if comm is not None:
+                comm.close()
+            comm = fhh.HostedComm(local_rank)
+            collective = {"kind": "hosted communicator (gloo all-reduce of the partials): RCCL init failed",
+                          "rccl_error": next(e for e in errs if e), "comm_ranks": world, "comm_rank": rank}
+            log(f"[rank {rank}] RCCL init failed ({collective['rccl_error']}); hosted all-reduce instead")
+        else:
+            nr, rk = comm.info()
+            collective = {"kind": "rccl ncclAllReduce(sum, u64) of per-child partials on the engine stream",
+                          "comm_ranks": nr, "comm_rank": rk}
+            log(f"[rank {rank}] RCCL communicator: {nr} ranks, rank {rk}")
 
     def step():
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,

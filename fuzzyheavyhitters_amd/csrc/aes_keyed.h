@@ -46,6 +46,134 @@ __device__ __forceinline__ void aes_rk(uint32_t (&s)[NB][4], const uint32_t* tbl
         }
 }
 
+// T_k lookup with k known only after unrolling (folds to one term<k>)
+template <class Tab>
+__device__ __forceinline__ uint32_t term_k(int k, const uint32_t* tbl, uint32_t b0, uint32_t b1, uint32_t x) {
+    switch (k & 3) {
+        case 0: return Tab::template term<0>(tbl, b0, b1, x);
+        case 1: return Tab::template term<1>(tbl, b0, b1, x);
+        case 2: return Tab::template term<2>(tbl, b0, b1, x);
+        default: return Tab::template term<3>(tbl, b0, b1, x);
+    }
+}
+
+// s <- AES_rk(s) for NB blocks that differ from block 0 only in the byte at row R of column C
+// (one lane's AES-CTR blocks whose counters share every other byte, e.g. the OT expand's blocks
+// c0 + 64 q + lane with c0 a multiple of 256). The key addition keeps the difference in that byte;
+// round 1 sends it through T_R into output column D = (C - R) & 3 alone (MixColumns stays in its
+// column), and in round 2 each output column takes exactly one byte of column D (ShiftRows). So
+// blocks 1.. cost 1 + 4 lookups in rounds 1-2 instead of 32 (k_expand's sibling pairs, variant 34,
+// use the same structure for the zero key): 133 instead of 160 per block. Exact for any inputs
+// that meet the precondition; the caller guarantees it.
+// Round keys come from a source: RkRegs (registers / SGPRs) or RkLds (one ds_read_b128 per round).
+struct RkRegs {
+    const uint32_t (&rk)[11][4];
+    __device__ __forceinline__ void get(int r, uint32_t (&w)[4]) const {
+#pragma unroll
+        for (int c = 0; c < 4; c++) w[c] = rk[r][c];
+    }
+};
+struct RkLds {
+    const uint4* rkl;
+    __device__ __forceinline__ void get(int r, uint32_t (&w)[4]) const {
+        const uint4 k = rkl[r];
+        w[0] = k.x;
+        w[1] = k.y;
+        w[2] = k.z;
+        w[3] = k.w;
+    }
+};
+
+template <class Tab, int NB, int R, int C, class Rk>
+__device__ __forceinline__ void aes_ctr_shared(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                               const Rk& src) {
+    constexpr int D = (C - R + 4) & 3;
+    uint32_t rk[4];
+    src.get(0, rk);
+    uint32_t a[4], d[NB];
+#pragma unroll
+    for (int c = 0; c < 4; c++) a[c] = s[0][c] ^ rk[c];
+#pragma unroll
+    for (int q = 0; q < NB; q++) d[q] = s[q][C] ^ rk[C];
+    src.get(1, rk);
+    // round 1 (block 0 in full; the others differ only in column D's term R)
+    uint32_t y[4], pd = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k] = term_k<Tab>(k, tbl, b0, b1, a[(c + k) & 3]);
+        if (c == D) {
+            pd = DevOpsX::xor3(t[(R + 1) & 3], t[(R + 2) & 3], t[(R + 3) & 3]);
+            y[c] = DevOpsX::xor3(pd, t[R], rk[c]);
+        } else {
+            y[c] = DevOpsX::xor3(DevOpsX::xor3(t[0], t[1], t[2]), t[3], rk[c]);
+        }
+    }
+    uint32_t yd[NB];
+    yd[0] = y[D];
+#pragma unroll
+    for (int q = 1; q < NB; q++) yd[q] = DevOpsX::xor3(pd, term_k<Tab>(R, tbl, b0, b1, d[q]), rk[D]);
+    src.get(2, rk);
+    // round 2: output column c takes row k = (D - c) & 3 of column D
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k] = term_k<Tab>(k, tbl, b0, b1, y[(c + k) & 3]);
+        const int k = (D - c + 4) & 3;
+        const uint32_t pex = DevOpsX::xor3(t[(k + 1) & 3], t[(k + 2) & 3], t[(k + 3) & 3]);
+        x[0][c] = DevOpsX::xor3(pex, t[k], rk[c]);
+#pragma unroll
+        for (int q = 1; q < NB; q++) x[q][c] = DevOpsX::xor3(pex, term_k<Tab>(k, tbl, b0, b1, yd[q]), rk[c]);
+    }
+#pragma unroll
+    for (int r = 3; r < 10; r++) {
+        src.get(r, rk);
+        uint32_t z[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                z[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, rk[c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = z[q][c];
+    }
+    src.get(10, rk);
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi), rk[c]);
+        }
+}
+
+template <class Tab, int NB, int R, int C>
+__device__ __forceinline__ void aes_rk_ctr(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                           const uint32_t (&rk)[11][4]) {
+    aes_ctr_shared<Tab, NB, R, C>(s, tbl, b0, b1, RkRegs{rk});
+}
+
+template <class Tab, int NB, int R, int C>
+__device__ __forceinline__ void aes_lds_rk_ctr(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                               const uint4* rkl) {
+    aes_ctr_shared<Tab, NB, R, C>(s, tbl, b0, b1, RkLds{rkl});
+}
+
 // s <- AES_rk0(s) for blocks [0, Q) and AES_rk1(s) for blocks [Q, 2Q): two uniform key
 // schedules (the OT receiver's row keys k_i^0, k_i^1) with all 2Q blocks in lockstep
 template <class Tab, int Q>

@@ -59,6 +59,9 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     // 44-word schedule is live in SGPRs at a time (both at once spilled it into VGPRs: 128 VGPRs
     // plus scratch)
     constexpr int kOtSlices = 4;
+    // a lane's blocks c0 + 64 q + lane (c0 a multiple of 256) differ only in byte 0: aes_rk_ctr
+    // shares rounds 1-2 of blocks 1..3 with block 0 (559 instead of 640 lookups per lane and key)
+    static_assert(64 * kOtSlices <= 256, "the slices' counters must differ in byte 0 alone");
     __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
     ot_fill(tbl_ot);
     uint32_t b0, b1;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
         {
             uint32_t rk[11][4];
             ld_rk(a.rk + (size_t)(RECV ? i : 256 + i) * 44, rk);
-            aes_rk<OtTab, kOtSlices>(g, tbl_ot, b0, b1, rk);   // G(k_i^0) (receiver) / G(k_i^{s_i})
+            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g, tbl_ot, b0, b1, rk);   // G(k_i^0) (receiver) / G(k_i^{s_i})
         }
         if (RECV) {
             uint32_t g1[kOtSlices][4];
@@ -106,7 +109,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
             }
             uint32_t rk[11][4];
             ld_rk(a.rk + (size_t)(128 + i) * 44, rk);
-            aes_rk<OtTab, kOtSlices>(g1, tbl_ot, b0, b1, rk);   // G(k_i^1)
+            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g1, tbl_ot, b0, b1, rk);   // G(k_i^1)
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
                 const uint64_t c = c0 + 64 * q + lane;

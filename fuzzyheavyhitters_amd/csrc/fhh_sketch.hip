@@ -295,8 +295,14 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
                     st[q][3] = __builtin_bswap32((uint32_t)b);
                 }
-                if constexpr (SCHED == 2) aes_lds_rk<Tab, NBP>(st, tbl, b0, b1, rkl);
-                else if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
+                if constexpr (SCHED == 2) {
+                    // the pass's counters differ only in byte 15 (the low byte of the big-endian
+                    // block index) unless a lane's blocks straddle a multiple of 256: then rounds 1-2
+                    // of the second block reuse the first's terms (aes_ctr_shared, 293 vs 320 lookups)
+                    const bool same_hi = (bb >> 8) == ((bb + LPK * (NBP - 1)) >> 8);
+                    if (__ballot(!same_hi) == 0) aes_lds_rk_ctr<Tab, NBP, 3, 3>(st, tbl, b0, b1, rkl);
+                    else aes_lds_rk<Tab, NBP>(st, tbl, b0, b1, rkl);
+                } else if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
                 else aes_rk<Tab, NBP>(st, tbl, b0, b1, rk);
                 if constexpr (NBP > 2) load_xkx();
                 unsigned __int128 ax = rx, a2x = r2x, akx = rkx;
@@ -454,7 +460,11 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
                     st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
                     st[q][3] = __builtin_bswap32((uint32_t)b);
                 }
-                aes_rk<Tab, PCB>(st, tbl, b0, b1, rk);
+                {   // counters differing only in byte 15 (see k_sketch_fe): shared rounds 1-2
+                    const uint64_t bf = PCB * p * LPK + sl, bl = (PCB * p + PCB - 1) * LPK + sl;
+                    if (__ballot((bf >> 8) != (bl >> 8)) == 0) aes_rk_ctr<Tab, PCB, 3, 3>(st, tbl, b0, b1, rk);
+                    else aes_rk<Tab, PCB>(st, tbl, b0, b1, rk);
+                }
             }
             __syncthreads();   // the consumers are done with the buffer
             if (produced) {

@@ -99,3 +99,26 @@ def test_bench_two_rank_rehearsal_equals_one_rank():
     for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
         assert two[k] == one[k], k
     assert two["config"]["clients_total"] == one["config"]["clients_total"] == 20000
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rccl_bootstrap_and_fallback():
+    """The RCCL leg of bench.py's N > 1 path on one GPU (--rehearse-rccl): two torchrun ranks build
+    the RCCL communicator over the loopback bootstrap bench.py configures; RCCL then refuses two ranks
+    on one device (its duplicate-GPU check runs after the bootstrap's all-gather, so reaching it means
+    the unique id, the sockets and the rank exchange worked), both ranks see the error and fall back
+    together to the hosted communicator, and the crawl still equals the single-rank run."""
+    import random
+    import sys as _sys
+    common = ["--clients", "20000", "--data-len", "128", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"]
+    one = _bench_line([_sys.executable, "-u", "bench.py", *common])
+    port = str(29300 + random.randrange(300))
+    two = _bench_line([_sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                       "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2",
+                       "--rehearse-rccl", *common])
+    col = two["config"]["collective"]
+    assert "RCCL init failed" in col["kind"], col
+    assert "ncclCommInitRank" in col["rccl_error"], col
+    assert col["comm_ranks"] == 2
+    for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
+        assert two[k] == one[k], k

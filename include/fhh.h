@@ -367,9 +367,11 @@ int fhh_deal_triples_fe(fhh_ctx* ctx, uint64_t n, uint32_t levels, uint64_t seed
                         uint64_t* triples1_dev);
 /* k_sketch_fe implementation for A/B (process-wide): 0 = default (four-table LDS layout, 1024
  * threads, each key's round keys computed once into LDS, lanes per key chosen per launch by
- * fhh_sketch_plan), 1 = the r01 kernel (schedule in registers, 256 threads), 2 = 8 lanes per key
- * with the round keys expanded on the fly per pass, 3 = 0 at 8 lanes per key for every key. All
- * are bit-identical; FHH_E_ARG for any other value. */
+ * fhh_sketch_plan; the plan's tail launch in the producer / consumer form), 1 = the r01 kernel
+ * (schedule in registers, 256 threads), 2 = 8 lanes per key with the round keys expanded on the fly
+ * per pass, 3 = 0 at 8 lanes per key for every key, 4 = the producer / consumer form for every key
+ * (AES waves and product waves paired through LDS). All are bit-identical; FHH_E_ARG for any other
+ * value. */
 int fhh_sketch_set_impl(int impl);
 /* The default form's launch plan for n_keys keys of n_nodes nodes on `resident_waves` waves (CUs x
  * 16 on MI355X): keys [0, *n_main) run at *lpk_main lanes per key, the rest in a second launch at

@@ -52,12 +52,12 @@ def test_create_fails_cleanly_without_gpu(fhh):
 
 
 def test_sketch_impl_switch_validates(fhh):
-    """fhh_sketch_set_impl (the k_sketch_fe A/B switch) accepts 0..3 and rejects the rest; no GPU
+    """fhh_sketch_set_impl (the k_sketch_fe A/B switch) accepts 0..4 and rejects the rest; no GPU
     call is made."""
     lib = fhh.lib()
-    assert lib.fhh_sketch_set_impl(4) != 0
+    assert lib.fhh_sketch_set_impl(5) != 0
     assert lib.fhh_sketch_set_impl(-1) != 0
-    for impl in (1, 2, 3, 0):
+    for impl in (1, 2, 3, 4, 0):
         assert lib.fhh_sketch_set_impl(impl) == 0
 
 

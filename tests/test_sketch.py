@@ -123,8 +123,11 @@ def sketch_impl(request):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_keys,n_nodes", [(1, 0), (3, 1), (5, 2), (70, 63), (64, 64), (130, 125), (257, 300),
-                                            (2000, 40), (1001, 256), (40000, 256)])
+                                            (2000, 40), (1001, 256), (40000, 256), (300, 700)])
 def test_gpu_sketch_at_bit_exact(oracle, n_keys, n_nodes, sketch_impl):
+    """(300, 700): 352 keystream blocks per key, so some passes' blocks straddle block 256 and take
+    the generic AES instead of the shared-rounds form (aes_ctr_shared needs the counters to differ in
+    byte 15 alone)"""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import sketch as S
     wl = S.sketch_workload(n_keys, n_nodes, seed=n_keys * 7 + n_nodes, bad_fraction=0.1)

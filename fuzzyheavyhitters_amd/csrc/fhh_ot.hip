@@ -244,15 +244,28 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
                     h[2 * rr + u][2] = tv[u].z; h[2 * rr + u][3] = tv[u].w;
                 }
             }
+            // OTs 0, 1 of the pass have their chosen Y in flight while the AES runs (r03: without the
+            // Y loads the kernel was 18 % faster, `profiles/r03/ot_diag/`): straight into the exchange
+            // stage, idle until the next pass (global_load_lds, 1 KiB per wave and OT, lane-linear);
+            // OTs 2, 3 load after it (16 more VGPRs, or 8 for just these two, spill beside the tile)
+            auto ysrc = [&](int b) -> const uint4* {   // the OT's chosen Y (inactive OTs: a valid block)
+                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
+                return j < m ? (((cw >> (j & 31)) & 1u) ? a.Y1 : a.Y0) + j : a.Y0;
+            };
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the exchange's stage reads are done
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ysrc(b)), &stage[wv][256 * b], 16, 0, 0);
             aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stage's Y blocks have landed
 #pragma unroll
             for (int b = 0; b < 4; b++) {
+                const uint4 y = b < 2 ? *reinterpret_cast<const uint4*>(&stage[wv][256 * b + 4 * lane]) : *ysrc(b);
                 const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
                 if (j >= m) continue;
-                const uint32_t c = (cw >> (j & 31)) & 1u;
-                const uint4 y = (c ? a.Y1 : a.Y0)[j];
                 a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
             }
+            __builtin_amdgcn_wave_barrier();   // the Y reads precede the next pass's stage writes
         }
     }
 }

@@ -546,6 +546,9 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
                             o[4] = rand2;
                             o[5] = rand3;
                         } else {
+                            // a from_rng redraw (P ~ 2^-32 per draw) or force_sequential: this lane
+                            // replays the key's sequential stream; the workgroup's other waves wait
+                            // for it at the phase barrier (correct, and rare outside the tests)
                             uint32_t seed[4];
 #pragma unroll
                             for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * k + c];

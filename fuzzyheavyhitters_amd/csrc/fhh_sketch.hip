@@ -708,11 +708,21 @@ static hipError_t launch_sketch_pc_lpk(int lpk, const SketchArgs& a, int cus, hi
     }
 }
 
+// CU count of the current device, queried once per device (the sketch launches run per level)
+static int sketch_cus() {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
 static hipError_t launch_sketch_pc(const SketchArgs& a, hipStream_t stream) {
-    int cus = 256, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus < 1) cus = 256;
+    const int cus = sketch_cus();
     const SketchPlan p = plan_sketch_nbp(a.n_keys, a.n_nodes, (uint64_t)cus * kPcPairs, kPcBlocks);
     SketchArgs m = a;
     m.n_keys = p.n_main;
@@ -749,10 +759,7 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     t.n_keys = a.n_keys - p.n_main;
     // (r03, configs[4]: its 3 blocks per lane cover a 130-block key at LPK 64 in one pass where the
     // fused form takes two: 16.2 vs 28.8 us; the main launch stays fused, 227 vs 236 us)
-    int cus = 256, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return launch_sketch_pc_lpk(p.lpk_tail, t, cus > 0 ? cus : 256, stream);
+    return launch_sketch_pc_lpk(p.lpk_tail, t, sketch_cus(), stream);
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

@@ -77,7 +77,8 @@ def test_oracle_garbling_is_input_independent(oracle):
 
 # ---- HIP path -------------------------------------------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,bits", [(1, 1), (3, 4), (63, 2), (64, 2), (65, 3), (1000, 2), (4097, 8), (20000, 4)])
+@pytest.mark.parametrize("n,bits", [(1, 1), (3, 4), (63, 2), (64, 2), (65, 3), (1000, 2), (4097, 8), (20000, 4),
+                                    (500, 5), (300, 6), (130, 7)])
 def test_gpu_gc_bit_exact(oracle, n, bits):
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import gc

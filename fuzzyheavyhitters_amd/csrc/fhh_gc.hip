@@ -93,6 +93,10 @@ __device__ __forceinline__ void ld_blk(const uint4* base, uint64_t row, uint64_t
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
+    // a workgroup without tests leaves before filling 128 KiB of tables (the level loop enqueues a
+    // level's chunks up to its capacity, and chunks past the level's children run empty: r03 measured
+    // 31 us per empty launch with the fill); the test is uniform over the workgroup
+    if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;
     gc_fill(tbl_gc);
     uint32_t b0, b1;
     GcTab::bases(threadIdx.x & 63, b0, b1);
@@ -192,6 +196,7 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x) {
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
+    if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;   // no tests: skip the table fill
     gc_fill(tbl_gc);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;

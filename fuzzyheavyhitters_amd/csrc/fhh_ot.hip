@@ -63,10 +63,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     // shares rounds 1-2 of blocks 1..3 with block 0 (559 instead of 640 lookups per lane and key)
     static_assert(64 * kOtSlices <= 256, "the slices' counters must differ in byte 0 alone");
     __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
     const uint32_t lane = threadIdx.x & 63;
-    OtTab::bases(lane, b0, b1);
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
     // the active tiles (rows x 64 kOtSlices blocks) in contiguous runs per wave: consecutive tiles
@@ -77,6 +74,11 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
     const uint64_t wave = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6);
     const uint64_t run = (tiles + nwaves - 1) / nwaves;
+    // a workgroup whose waves have no tiles (an empty chunk of the level loop) skips the table fill
+    if ((uint64_t)blockIdx.x * (kOtThreads / 64) * run >= tiles) return;
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
     const uint64_t t_end = min(tiles, (wave + 1) * run);
     for (uint64_t t = wave * run; t < t_end; t++) {
         const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_row));
@@ -181,12 +183,13 @@ __device__ __forceinline__ void ot_tile_round(uint32_t* st, uint32_t (&x)[32], u
 __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
-    ot_fill(tbl_ot);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
     const uint64_t m = ot_active(a), W = a.mp / 32;
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    if ((uint64_t)blockIdx.x * kOtWaves >= tiles) return;   // no tiles for this workgroup: skip the fill
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kOtWaves;
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
     for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
@@ -216,12 +219,13 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) 
 __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
-    ot_fill(tbl_ot);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
     const uint64_t m = ot_active(a), W = a.mp / 32;
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    if ((uint64_t)blockIdx.x * kOtWaves >= tiles) return;   // no tiles for this workgroup: skip the fill
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kOtWaves;
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
     for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {

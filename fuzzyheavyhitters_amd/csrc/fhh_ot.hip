@@ -339,7 +339,9 @@ static int device_cus() {
 
 static int ot_grid(uint64_t items, int threads) {
     const uint64_t need = (items + threads - 1) / threads;
-    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 4 : 16);
+    // 1024-thread workgroups: one per CU (the 128 KiB tables are filled once per CU; 4 per CU before
+    // r03: receiver expand -3.1 %)
+    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 1 : 16);
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 

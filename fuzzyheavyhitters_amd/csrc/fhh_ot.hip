@@ -339,9 +339,9 @@ static int device_cus() {
 
 static int ot_grid(uint64_t items, int threads) {
     const uint64_t need = (items + threads - 1) / threads;
-    // 1024-thread workgroups: one per CU (the 128 KiB tables are filled once per CU; 4 per CU before
-    // r03: receiver expand -3.1 %)
-    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 1 : 16);
+    // 1024-thread workgroups: 4 per CU (one per CU measured -3.1 % for the receiver expand at
+    // configs[1] but +6 % at 1M clients, where the longer per-wave tile runs balance worse; r03)
+    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 4 : 16);
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 

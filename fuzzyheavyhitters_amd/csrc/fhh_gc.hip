@@ -268,9 +268,10 @@ static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     if (e != hipSuccess) return e;
     const uint64_t n = a.G * a.N;
     const uint64_t need = (n + kGcThreads - 1) / kGcThreads;
-    // one resident 1024-thread workgroup per CU, striding over the tests: every workgroup fills its
-    // 128 KiB of tables once (8 per CU before r03: evaluate -5.6 %, garble neutral)
-    const int grid = (int)(need < (uint64_t)cus ? (need ? need : 1) : (uint64_t)cus);
+    // 8 workgroups per CU (one resident per CU, each filling its tables once, measured -5.6 % for
+    // evaluate at configs[1] but +3.2 % for evaluate and +0.7 % for the whole GC + OT crawl at 1M
+    // clients, alternated twice; r03)
+    const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
     if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
     else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
     return hipGetLastError();

@@ -236,19 +236,21 @@ def bincode_bench(args, world, rank, local_rank, dist):
 
 
 def dropin_bench(args, world, rank, local_rank, dist):
-    """The KeyCollection ABI path a Rust server calls (collect.rs:370-505 through include/fhh.h,
-    INTEGRATION.md §3) against the fused device-resident loop, both servers in this process on one
-    GPU, --clients clients (configs[1] = 100000), data_len 512. One step = one full crawl:
-      fused      the bench's own step: fhh_sim_crawl count mode (k_expand, equality count, keep and
-                 prune on the device, no host round trip per level)
-      dropin     per level: fhh_tree_crawl on both servers with the share planes copied to the host
-                 (the GC input), the leader's equality count from the planes on the host (standing
-                 in for the GC + OT), fhh_node_sums_fe on both servers with host OT outputs
-                 [C][n] u64 (copied to the device), keep, fhh_tree_prune on both
-      gcot       fhh_sim_crawl with the GPU GC + OT in every level (both parties in one device loop)
-      two-party  the same GC + OT split between the two servers' ctxs (fhh_gb_* / fhh_ev_*), the
-                 five messages per level copied device to device, node sums of the device-resident
-                 OT outputs (fhh_party_node_sums)
+    """The KeyCollection ABI path a Rust server runs per level (collect.rs:370-507 through
+    include/fhh.h; server.rs:96-118), timed against the fused device loop of the
+    same protocol, --clients clients (configs[1] = 100000), data_len 512, both servers on one GPU.
+    One step = one full crawl with the GPU garbled-circuit equality test and both OT extensions in
+    every level (ideal base-OT material in both, so the legs do the same work):
+      fused     fhh_sim_crawl(gc = 2): both parties inside one device-resident level loop
+      dropin    per level, each server on its own ctx: fhh_tree_crawl (share planes stay on the
+                device), the party halves fhh_gb_* / fhh_ev_* with the five messages read where the
+                sender produced them (the channel's bytes are counted, not moved), fhh_party_node_sums
+                on each server's device-resident OT outputs, fhh_keep_values (C), fhh_tree_prune
+      dropin-2shard   the same on a two-shard fhh_create_multi collection per server (both shards on
+                this GPU, host reduction), each shard its own protocol instance
+      dropin-copy     (--dropin-copy) dropin with every message copied into the receiver's buffer
+      host-values     (--dropin-host-values) r03's leg: share planes to the host, the leader's count
+                standing in for the GC + OT, host OT values summed by fhh_node_sums_fe
     Every leg's heavy hitters are checked against the fused crawl's."""
     import numpy as np
     import torch
@@ -258,58 +260,15 @@ def dropin_bench(args, world, rank, local_rank, dist):
     wl = workload.zipf_workload(n, L, d, num_sites=args.num_sites, zipf_s=args.zipf, ball_size=args.ball,
                                 seed=args.seed)
 
-    def pair():
-        c0, c1 = fhh.KeyCollection(L, d, device=local_rank), fhh.KeyCollection(L, d, device=local_rank)
+    def pair(devices=None):
+        c0 = fhh.KeyCollection(L, d, device=local_rank, devices=devices)
+        c1 = fhh.KeyCollection(L, d, device=local_rank, devices=devices)
         fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
         return c0, c1
 
-    c0, c1 = pair()
-    thr = max(1, int(args.threshold * n))
-    nw = (n + 63) // 64
-    valid = np.full(nw, np.uint64(0xFFFFFFFFFFFFFFFF))
-    if n % 64:
-        valid[-1] = np.uint64((1 << (n % 64)) - 1)
-    vals = np.random.default_rng(1).integers(0, 1 << 62, (512, n), dtype=np.uint64)   # host OT outputs
-
-    def dropin_crawl():
-        c0.tree_init()
-        c1.tree_init()
-        final = []
-        per = {"crawl_planes": 0.0, "leader": 0.0, "node_sums": 0.0, "prune": 0.0}
-        for lv in range(L):
-            last = lv == L - 1
-            t0 = time.perf_counter()
-            C, p0 = (c0.tree_crawl_last if last else c0.tree_crawl)(share_planes=True)
-            _, p1 = (c1.tree_crawl_last if last else c1.tree_crawl)(share_planes=True)
-            t1 = time.perf_counter()
-            diff = np.zeros((C, nw), np.uint64)
-            for j in range(2 * d):
-                diff |= p0[:, j] ^ p1[:, j]
-            cnt = np.bitwise_count(~diff & valid).sum(axis=1)
-            keep = cnt >= thr
-            t2 = time.perf_counter()
-            if C > vals.shape[0]:
-                raise SystemExit(f"dropin: {C} children > the {vals.shape[0]} rows of host values")
-            v = vals[:C]
-            if not last:
-                c0.node_sums_fe(v)
-                c1.node_sums_fe(v)
-            t3 = time.perf_counter()
-            if last:
-                c0.tree_prune_last(keep)
-                c1.tree_prune_last(keep)
-                final = int(keep.sum())
-            else:
-                c0.tree_prune(keep)
-                c1.tree_prune(keep)
-            t4 = time.perf_counter()
-            per["crawl_planes"] += t1 - t0
-            per["leader"] += t2 - t1
-            per["node_sums"] += t3 - t2
-            per["prune"] += t4 - t3
-        return final, per
-
-    def timed(fn, reps):
+    def timed(fn, reps, warm=1):
+        for _ in range(warm):
+            fn()
         best, out = None, None
         for _ in range(reps):
             torch.cuda.synchronize()
@@ -321,42 +280,103 @@ def dropin_bench(args, world, rank, local_rank, dist):
         return best, out
 
     reps = max(1, args.steps)
-    for _ in range(args.warmup):
-        fhh.sim_crawl(c0, c1, args.threshold, mode="count", record=False)
-    t_fused, res = timed(lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="count", record=False), reps)
-    hh = len(res.final)
-    dropin_crawl()   # warm-up (buffer growth)
-    t_dropin, (hh_d, per) = timed(dropin_crawl, reps)
-    assert hh_d == hh, f"drop-in path found {hh_d} heavy hitters, fused {hh}"
+    warm = max(0, args.warmup)
     out = {
-        "metric": "drop-in KeyCollection ABI path vs the fused device loop: full-crawl wall time",
-        "value": t_dropin, "unit": "s per crawl", "n_gpus": 1, "steps": reps, "warmup": args.warmup,
-        "ms_per_step": t_dropin * 1e3, "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32", "data": "synthetic Zipf workload (leader.rs shape), GPU keygen; host OT outputs are random u64",
-        "config": {"workload": f"{n} Zipf clients, data_len {L}, d {d}, threshold {args.threshold}, both servers",
-                   "parallelism": "single GPU"},
-        "fused_crawl_s": t_fused, "dropin_crawl_s": t_dropin, "dropin_over_fused": t_dropin / t_fused,
-        "dropin_ms_per_level": {k: v / L * 1e3 for k, v in per.items()},   # the last timed crawl
-        "dropin_overhead_ms_per_level": (t_dropin - t_fused) / L * 1e3,
-        "heavy_hitters": hh,
+        "metric": "drop-in KeyCollection ABI path (two parties, GC + OT every level) vs the fused device loop: "
+                  "full-crawl wall time",
+        "unit": "s per crawl", "n_gpus": 1, "steps": reps, "warmup": warm, "higher_is_better": False,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic Zipf workload (leader.rs shape), GPU keygen",
+        "config": {"workload": f"{n} Zipf clients, data_len {L}, d {d}, threshold {args.threshold}, both servers, "
+                               "GC + OT (ideal base-OT material) every level", "parallelism": "single GPU"},
     }
+    c0, c1 = pair()
+    t_fused, res = timed(lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False),
+                         reps, warm)
+    hh = len(res.final)
+    del c0, c1
+
+    def dropin_leg(devices=None, channel="inplace"):
+        p0, p1 = pair(devices)
+        tm = {}
+
+        def run():
+            tm.clear()
+            return fhh.two_party_crawl(p0, p1, args.threshold, prf_seed=7, channel=channel, timing=tm, record=False)
+        t, r = timed(run, reps, warm)
+        assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
+        tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
+        return t, {k: v / L * 1e3 for k, v in tm.items()}, tot
+
+    t_d, per_d, bytes_d = dropin_leg()
+    out.update({
+        "value": t_d, "ms_per_step": t_d * 1e3,
+        "fused_protocol_crawl_s": t_fused, "dropin_crawl_s": t_d, "dropin_over_fused": t_d / t_fused,
+        "dropin_ms_per_level": per_d,
+        "dropin_overhead_ms_per_level": (t_d - t_fused) / L * 1e3,
+        "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",
+        "channel_bytes_per_crawl": bytes_d, "channel_bytes_total": sum(bytes_d.values()),
+        "heavy_hitters": hh,
+    })
     if not args.no_party:
-        del c0, c1
-        g0, g1 = pair()
-        t_gc, res_gc = timed(lambda: fhh.sim_crawl(g0, g1, args.threshold, mode="fe", prf_seed=7, gc="ot",
-                                                   record=False), 1)
-        del g0, g1
-        p0, p1 = pair()
-        t_2p, res_2p = timed(lambda: fhh.two_party_crawl(p0, p1, args.threshold, prf_seed=7), 1)
-        assert len(res_2p.final) == len(res_gc.final) == hh
-        tot = {k: sum(lb.get(k, 0) for lb in res_2p.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
-        out.update({
-            "gcot_in_process_crawl_s": t_gc, "gcot_two_party_crawl_s": t_2p,
-            "two_party_over_in_process": t_2p / t_gc,
-            "two_party_channel_bytes_per_crawl": tot,
-            "two_party_channel_bytes_total": sum(tot.values()),
-            "two_party_max_bytes_per_level": max(sum(lb.values()) for lb in res_2p.level_bytes),
-        })
+        t_2, per_2, _ = dropin_leg(devices=[local_rank, local_rank])
+        out.update({"dropin_2shard_crawl_s": t_2, "dropin_2shard_over_fused": t_2 / t_fused,
+                    "dropin_2shard_ms_per_level": per_2,
+                    "dropin_2shard_note": "fhh_create_multi over [this GPU, this GPU]: host reduction of the shards' "
+                                          "device-resident sums, one protocol instance per shard"})
+    if args.dropin_copy:
+        t_c, per_c, _ = dropin_leg(channel="copy")
+        out.update({"dropin_copy_crawl_s": t_c, "dropin_copy_over_fused": t_c / t_fused,
+                    "dropin_copy_ms_per_level": per_c})
+    if args.dropin_host_values:
+        c0, c1 = pair()
+        nw = (n + 63) // 64
+        valid = np.full(nw, np.uint64(0xFFFFFFFFFFFFFFFF))
+        if n % 64:
+            valid[-1] = np.uint64((1 << (n % 64)) - 1)
+        thr = max(1, int(args.threshold * n))
+        vals = np.random.default_rng(1).integers(0, 1 << 62, (512, n), dtype=np.uint64)   # host OT outputs
+        per = {"crawl_planes": 0.0, "leader": 0.0, "node_sums": 0.0, "prune": 0.0}
+
+        def host_values_crawl():
+            for k in per:
+                per[k] = 0.0
+            c0.tree_init()
+            c1.tree_init()
+            final = 0
+            for lv in range(L):
+                last = lv == L - 1
+                t0 = time.perf_counter()
+                C, p0 = (c0.tree_crawl_last if last else c0.tree_crawl)(share_planes=True)
+                _, p1 = (c1.tree_crawl_last if last else c1.tree_crawl)(share_planes=True)
+                t1 = time.perf_counter()
+                diff = np.zeros((C, nw), np.uint64)
+                for j in range(2 * d):
+                    diff |= p0[:, j] ^ p1[:, j]
+                keep = np.bitwise_count(~diff & valid).sum(axis=1) >= thr
+                t2 = time.perf_counter()
+                if C > vals.shape[0]:
+                    raise SystemExit(f"dropin: {C} children > the {vals.shape[0]} rows of host values")
+                if not last:
+                    c0.node_sums_fe(vals[:C])
+                    c1.node_sums_fe(vals[:C])
+                t3 = time.perf_counter()
+                if last:
+                    c0.tree_prune_last(keep)
+                    c1.tree_prune_last(keep)
+                    final = int(keep.sum())
+                else:
+                    c0.tree_prune(keep)
+                    c1.tree_prune(keep)
+                t4 = time.perf_counter()
+                per["crawl_planes"] += t1 - t0
+                per["leader"] += t2 - t1
+                per["node_sums"] += t3 - t2
+                per["prune"] += t4 - t3
+            return final
+        t_h, hh_h = timed(host_values_crawl, reps, warm)
+        assert hh_h == hh, f"host-values leg found {hh_h} heavy hitters, fused {hh}"
+        out.update({"host_values_crawl_s": t_h, "host_values_ms_per_level": {k: v / L * 1e3 for k, v in per.items()}})
     print(json.dumps(out), flush=True)
     return 0
 
@@ -448,6 +468,95 @@ def gc_bench(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def launch_plan(gpus: int, env, device_count: int, rehearse: bool):
+    """How this invocation runs, decided before any GPU call: ("run", None), ("relaunch", None) —
+    `python bench.py --gpus N` with N > 1 and no torchrun environment starts itself under
+    torch.distributed.run as N ranks (a child process; this one exits with its code) — or
+    ("error", message). A torchrun world that differs from --gpus, or more GPUs asked for than the
+    node shows (outside --rehearse), is an error: a line that timed fewer GPUs than it names must
+    not exist."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return "run", None
+        if not rehearse and device_count < gpus:
+            return "error", f"--gpus {gpus}: only {device_count} GPU(s) visible on this node"
+        return "relaunch", None
+    world = int(ws)
+    if world != gpus:
+        return "error", (f"WORLD_SIZE={world} but --gpus={gpus}: the line would time {world} rank(s) while "
+                         f"naming {gpus}")
+    if not rehearse and device_count and world > device_count:
+        return "error", f"{world} ranks but only {device_count} GPU(s) visible (use --rehearse to share devices)"
+    return "run", None
+
+
+def relaunch_cmd(argv, gpus: int, port: int):
+    """The torchrun command `python bench.py --gpus N` re-launches itself with (one node, one rank
+    per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def collective_after_init(errs, rehearse_rccl: bool):
+    """Every rank's RCCL init error (None = ok), gathered. ("rccl", None) when all succeeded;
+    under --rehearse-rccl (ranks share a GPU, RCCL refuses them) ("hosted", error) — the ranks fall
+    back together to the hosted all-reduce; otherwise ("fail", error): a measurement without RCCL's
+    data path is not the measurement asked for, so every rank exits non-zero."""
+    err = next((e for e in errs if e), None)
+    if err is None:
+        return "rccl", None
+    return ("hosted" if rehearse_rccl else "fail"), err
+
+
+def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
+    """The real protocol's crawl on the headline's keys (tree_crawl with gc_sender per level,
+    collect.rs:419-482, with OtSender/OtReceiver::init per channel and level, :454-471; the leader's
+    loop leader.rs:422-440): the GPU garbled-circuit equality test and both OT extensions in every
+    level, each OT extension (and each chunk of a level's children) on its own 128 real Chou–Orlandi
+    base OTs from host threads. One warm-up crawl over the first 32 levels (allocates the GC + OT
+    buffers at this capacity), then one timed full crawl, bracketed like the headline."""
+    import torch
+    import fuzzyheavyhitters_amd as fhh
+
+    def run(levels=None):
+        return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=False,
+                             comm=comm, gc="ot", base_ot=True, levels=levels)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    run(levels=min(32, args.data_len))
+    barrier()
+    c0.reset_stats()
+    c1.reset_stats()
+    t0 = time.perf_counter()
+    res = run()
+    barrier()
+    wall = time.perf_counter() - t0
+    s0 = c0.stats()
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    hh = len(res.final)
+    return {
+        "wall_s": wall,
+        "heavy_hitters": hh,
+        "heavy_hitters_equal_headline": hh == headline_hh,
+        "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per OT extension per level and chunk)",
+        "base_ot_host_ms": s0["base_ot_ms"],
+        "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
+        "expand_gpu_ms": s0["expand_ms"],
+        "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,
+        "timing": "HIP events on the engine stream around every level's GC + OT step and k_expand (rank 0)",
+        "warmup": "one 32-level protocol crawl before the timed one",
+        "workload": "the headline's keys and clients, mode fe (FE shares, FieldElm last level), GC + OT every level",
+    }
+
+
 def load_pmc(config: str):
     """Committed rocprofv3 PMC summary of k_expand for this workload (tools/profile.sh +
     tools/pmc_summary.py -> profiles/pmc_expand.json, keyed by workload)."""
@@ -474,7 +583,11 @@ def main():
     ap.add_argument("--ball", type=int, default=1)
     ap.add_argument("--threshold", type=float, default=0.001)
     ap.add_argument("--mode", default="count", choices=["count", "fe"])
-    ap.add_argument("--no-party", action="store_true", help="--workload dropin: skip the GC + OT legs")
+    ap.add_argument("--no-party", action="store_true", help="--workload dropin: skip the two-shard leg")
+    ap.add_argument("--dropin-copy", action="store_true",
+                    help="--workload dropin: also time the drop-in path with every message copied to the receiver")
+    ap.add_argument("--dropin-host-values", action="store_true",
+                    help="--workload dropin: also time r03's host-values leg (planes to the host, host OT values)")
     ap.add_argument("--workload", default="zipf", choices=["zipf", "coords", "sketch", "gc", "bincode", "dropin"],
                     help="zipf = the metric's Zipf crawl (default 1M clients; --clients 100000 = configs[1]); "
                          "coords = configs[3] (d=2 lat/lon, data_len 16); sketch = configs[4] (sketch + Beaver "
@@ -514,17 +627,32 @@ def main():
                          "exercises the init-failure fallback to the hosted communicator. Never a measurement.")
     ap.add_argument("--timing-every", type=int, default=1,
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
+    ap.add_argument("--no-protocol-crawl", action="store_true",
+                    help="skip the real protocol's crawl (GC + OT + real base OTs every level) that follows the "
+                         "headline's timed region on the zipf workload")
     args = ap.parse_args()
+    if args.rehearse_rccl:
+        args.rehearse = True
+
+    import torch
+    # before any GPU call (torch.cuda.device_count does not initialise the GPU on this image)
+    plan, why = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), args.rehearse)
+    if plan == "error":
+        log(f"bench.py: {why}")
+        return 2
+    if plan == "relaunch":
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = relaunch_cmd(sys.argv[1:], args.gpus, port)
+        log("bench.py: --gpus", args.gpus, "without a torchrun world: relaunching as", " ".join(cmd))
+        return subprocess.run(cmd).returncode
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-
-    import torch
-    if args.rehearse_rccl:
-        args.rehearse = True
     if args.rehearse:
         local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
@@ -594,15 +722,24 @@ def main():
             err = str(e)
         errs = [None] * world
         dist.all_gather_object(errs, err)
-        if any(errs):
-            # every rank falls back together: the same level loop with the per-level sum of the
-            # partials through the hosted communicator (gloo), labelled as such in the line
+        how, rccl_err = collective_after_init(errs, args.rehearse_rccl)
+        if how == "fail":
+            # every rank saw the same gathered errors: all leave together, no line is printed
+            log(f"[rank {rank}] RCCL init failed ({rccl_err}); refusing to measure N>1 without RCCL")
+            if comm is not None:
+                comm.close()
+            dist.barrier()
+            dist.destroy_process_group()
+            return 3
+        if how == "hosted":
+            # --rehearse-rccl: every rank falls back together: the same level loop with the per-level
+            # sum of the partials through the hosted communicator (gloo), labelled as such in the line
             if comm is not None:
                 comm.close()
             comm = fhh.HostedComm(local_rank)
             collective = {"kind": "hosted communicator (gloo all-reduce of the partials): RCCL init failed",
-                          "rccl_error": next(e for e in errs if e), "comm_ranks": world, "comm_rank": rank}
-            log(f"[rank {rank}] RCCL init failed ({collective['rccl_error']}); hosted all-reduce instead")
+                          "rccl_error": rccl_err, "comm_ranks": world, "comm_rank": rank}
+            log(f"[rank {rank}] RCCL init failed ({rccl_err}); hosted all-reduce instead (rehearsal)")
         else:
             nr, rk = comm.info()
             collective = {"kind": "rccl ncclAllReduce(sum, u64) of per-child partials on the engine stream",
@@ -632,6 +769,9 @@ def main():
     s0, s1 = c0.stats(), c1.stats()
     blocks = s0["aes_blocks"] + s1["aes_blocks"]
     ref_evals = s0["ref_evals"] + s1["ref_evals"]
+    # per-level cross-rank all-reduce (HIP events around ncclAllReduce on the engine stream)
+    ar_us = s0["allreduce_ms"] * 1e3 / s0["allreduce_timed"] if s0["allreduce_timed"] else None
+    ar_us_max = ar_us
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -639,6 +779,13 @@ def main():
         b = torch.tensor([blocks, ref_evals], dtype=torch.int64)
         dist.all_reduce(b)
         blocks, ref_evals = int(b[0].item()), int(b[1].item())
+        a = torch.tensor([ar_us or 0.0], dtype=torch.float64)
+        dist.all_reduce(a, op=dist.ReduceOp.MAX)
+        ar_us_max = float(a.item()) if ar_us is not None else None
+    headline_hh = len(res.final)
+    proto = None
+    if args.workload == "zipf" and args.gc == "none" and not args.no_protocol_crawl:
+        proto = protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh)
 
     if rank == 0:
         launches = max(1, s0["expand_launches_timed"])
@@ -712,6 +859,12 @@ def main():
             "ref_equiv_evals_per_s": ref_evals / elapsed,
             "aes_blocks_per_step": blocks / args.steps,
             "base_ot_ms_per_step": s0.get("base_ot_ms", 0.0) / args.steps if args.base_ot else None,
+            "allreduce_us_per_level": ar_us,
+            "allreduce_us_per_level_max_rank": ar_us_max,
+            "allreduce_note": ("HIP events around the per-level cross-rank all-reduce on the engine stream (rank 0; "
+                               "max over ranks beside it); null on one GPU"),
+            "protocol_crawl_wall_s": proto["wall_s"] if proto else None,
+            "protocol_crawl": proto,
             "final_heavy_hitters": len(res.final),
             "levels": int(len(res.level_children)),
             "children_total": int(res.level_children.sum()),
@@ -763,4 +916,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

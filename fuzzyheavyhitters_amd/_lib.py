@@ -68,6 +68,10 @@ class FhhStats(ctypes.Structure):
         ("keygen_ms", ctypes.c_double),
         ("expand_launches_timed", ctypes.c_uint64),
         ("base_ot_ms", ctypes.c_double),
+        ("allreduce_ms", ctypes.c_double),
+        ("allreduce_timed", ctypes.c_uint64),
+        ("gcot_ms", ctypes.c_double),
+        ("gcot_timed", ctypes.c_uint64),
     ]
 
 

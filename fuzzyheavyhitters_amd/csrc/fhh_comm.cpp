@@ -14,6 +14,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -22,6 +23,9 @@
 struct fhh_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    // set once by comm_abort (ncclCommAbort freed the communicator; `comm` itself is left in place
+    // so a peer thread inside comm_allreduce never sees it change)
+    std::atomic<bool> aborted{false};
     // hosted communicator (fhh_comm_create_hosted): the same cfg->comm code path of the level
     // loop, with the sum done by a host callback instead of RCCL (tests without RCCL ranks)
     fhh_allreduce_fn hosted = nullptr;
@@ -130,6 +134,10 @@ int comm_allreduce(fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t c
         }
         return FHH_OK;
     }
+    if (c->aborted.load()) {
+        if (err) *err = "ncclAllReduce: communicator aborted by a failing peer";
+        return FHH_E_COMM;
+    }
     const ncclResult_t r = g_rccl.all_reduce(send, recv, count, ncclUint64, ncclSum, c->comm, stream);
     if (r != ncclSuccess) {
         if (err) *err = std::string("ncclAllReduce: ") + g_rccl.error_string(r);
@@ -196,12 +204,13 @@ int comm_group_allreduce(const std::vector<::fhh_comm*>& comms, const std::vecto
 // Unblock peers stuck in a collective after one shard failed (RCCL comms: ncclCommAbort; hosted
 // comms: the thread reducer's abort flag, see ThreadReducer).
 void comm_abort(::fhh_comm* c) {
-    if (c && c->comm && g_rccl.comm_abort) {
-        (void)hipSetDevice(c->device);
-        (void)g_rccl.comm_abort(c->comm);
-        c->comm = nullptr;
-    }
+    if (!c || !c->comm || !g_rccl.comm_abort) return;
+    if (c->aborted.exchange(true)) return;   // another thread got here first
+    (void)hipSetDevice(c->device);
+    (void)g_rccl.comm_abort(c->comm);
 }
+
+int comm_rank(const ::fhh_comm* c) { return c ? c->rank : 0; }
 
 }  // namespace fhh
 
@@ -259,7 +268,7 @@ int fhh_comm_create_hosted(fhh_comm** out, int nranks, int rank, int device, fhh
 
 void fhh_comm_destroy(fhh_comm* comm) {
     if (!comm) return;
-    if (comm->comm && g_rccl.comm_destroy) {
+    if (comm->comm && !comm->aborted.load() && g_rccl.comm_destroy) {
         (void)hipSetDevice(comm->device);
         (void)g_rccl.comm_destroy(comm->comm);
     }

@@ -479,6 +479,9 @@ int group_sim_crawl(fhh_ctx* g0, fhh_ctx* g1, const fhh_sim_config* cfg) {
     }
     std::vector<int> rcs(G0.shards.size(), 0);
     std::vector<std::thread> th;
+    // the first failing shard releases its peers waiting in a collective, once for the whole call
+    // (two shards failing together must not both abort the same communicators)
+    std::once_flag abort_once;
     for (size_t k : act)
         th.emplace_back([&, k] {
             fhh_sim_config c = *cfg;
@@ -489,12 +492,12 @@ int group_sim_crawl(fhh_ctx* g0, fhh_ctx* g1, const fhh_sim_config* cfg) {
                 c.counts_capacity = 0;
             }
             rcs[k] = fhh_sim_crawl(G0.shards[k], G1.shards[k], &c);
-            if (rcs[k]) {
-                // release the peers waiting in this level's collective
-                tr.abort();
-                if (red == FHH_REDUCE_RCCL)
-                    for (auto* cm : G0.comms) comm_abort(cm);
-            }
+            if (rcs[k])
+                std::call_once(abort_once, [&] {
+                    tr.abort();
+                    if (red == FHH_REDUCE_RCCL)
+                        for (auto* cm : comms) comm_abort(cm);
+                });
         });
     for (auto& t : th) t.join();
     for (auto* c : hosted) fhh_comm_destroy(c);
@@ -522,6 +525,10 @@ int group_get_stats(const fhh_ctx* g, fhh_stats* out) {
         t.keygen_ms += v.keygen_ms;
         t.expand_launches_timed += v.expand_launches_timed;
         t.base_ot_ms += v.base_ot_ms;
+        t.allreduce_ms += v.allreduce_ms;
+        t.allreduce_timed += v.allreduce_timed;
+        t.gcot_ms += v.gcot_ms;
+        t.gcot_timed += v.gcot_timed;
     }
     if (out) *out = t;
     return FHH_OK;

@@ -17,6 +17,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -53,11 +55,24 @@ hipError_t timing_end(fhh_ctx* ctx, size_t slot, uint64_t blocks) {
     return hipEventRecord(ctx->ev_pool[slot].second, ctx->stream);
 }
 
+// `blocks` tags of the event pairs that bracket the level loop's cross-rank all-reduce and its
+// GC + OT step (share planes to the last chunk's sums)
+constexpr uint64_t kAllreduceTag = ~0ull;
+constexpr uint64_t kGcotTag = ~1ull;
+
 // call after the stream is synchronised
 void timing_resolve(fhh_ctx* ctx) {
     for (auto& pr : ctx->ev_pending) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ctx->ev_pool[pr.first].first, ctx->ev_pool[pr.first].second) == hipSuccess) {
+        if (hipEventElapsedTime(&ms, ctx->ev_pool[pr.first].first, ctx->ev_pool[pr.first].second) != hipSuccess)
+            continue;
+        if (pr.second == kAllreduceTag) {
+            ctx->stats.allreduce_ms += ms;
+            ctx->stats.allreduce_timed++;
+        } else if (pr.second == kGcotTag) {
+            ctx->stats.gcot_ms += ms;
+            ctx->stats.gcot_timed++;
+        } else {
             ctx->stats.expand_ms += ms;
             ctx->stats.expand_blocks_timed += pr.second;
             ctx->stats.expand_launches_timed++;
@@ -717,25 +732,33 @@ struct PhaseClock {
     }
 };
 
-// Host producer of the real base OTs (fhh_sim_config.base_ot): worker threads compute instances
-// 0, 1, ... (level l's OT extensions are 2 l and 2 l + 1) with their key schedules
-// [3][128][44] (receiver k_i^0, k_i^1; sender k_i^{s_i}); wait(k) blocks until k is done.
+// Host producer of the real base OTs (fhh_sim_config.base_ot). Every OT extension of the crawl —
+// level lv, chunk k: the evaluator's labels (salt 2 k) and the share conversion (salt 2 k + 1) —
+// starts from its own 128 Chou–Orlandi OTs (AlszSender/AlszReceiver::init per channel and level,
+// collect.rs:454-471). The level loop requests instances (lv, salt) ahead of the level it enqueues
+// (the chunk count of a level follows the loop's capacity, so it is known only then); worker threads
+// compute them in request order with their key schedules [3][128][44] (receiver k_i^0, k_i^1; sender
+// k_i^{s_i}); wait(i) blocks until request i is done.
 struct BaseOtProducer {
-    uint32_t instances;
+    struct Inst {
+        uint32_t lv, salt;
+        std::vector<uint32_t> rk;
+        bool done = false;
+    };
+    uint64_t prf;
     uint8_t seed[32];
-    std::vector<uint8_t> choices;
-    std::vector<uint32_t> rk;                     // [instances][3][128][44]
-    std::vector<uint8_t> done;
-    std::atomic<uint32_t> next{0};
+    std::deque<Inst> insts;                          // stable addresses under push_back
+    std::map<uint64_t, size_t> index;                // (lv << 32 | salt) -> request
+    size_t next_work = 0;
+    bool stop = false;
     std::mutex mu;
-    std::condition_variable cv;
+    std::condition_variable cv_done, cv_work;
     int rc = FHH_OK;
     std::string err;
     std::vector<std::thread> workers;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    double busy_ms = 0;                            // wall time until the last instance finished
-    BaseOtProducer(uint32_t n, const uint8_t s[32], std::vector<uint8_t> ch)
-        : instances(n), choices(std::move(ch)), rk((size_t)n * 3 * 128 * 44), done(n, 0) {
+    double busy_ms = 0;                              // wall time until the last instance finished
+    BaseOtProducer(uint64_t prf_seed, const uint8_t s[32]) : prf(prf_seed) {
         std::memcpy(seed, s, 32);
         unsigned nt = std::thread::hardware_concurrency();
         if (const char* e = std::getenv("OMP_NUM_THREADS")) nt = (unsigned)std::atoi(e);
@@ -743,40 +766,71 @@ struct BaseOtProducer {
         for (unsigned w = 0; w < nt; w++) workers.emplace_back([this] { work(); });
     }
     ~BaseOtProducer() {
-        next = instances;   // stop handing out work
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv_work.notify_all();
         for (auto& t : workers) t.join();
+    }
+    size_t request(uint32_t lv, uint32_t salt) {
+        std::lock_guard<std::mutex> lk(mu);
+        const uint64_t key = (uint64_t)lv << 32 | salt;
+        auto it = index.find(key);
+        if (it != index.end()) return it->second;
+        insts.push_back(Inst{lv, salt, {}, false});
+        index.emplace(key, insts.size() - 1);
+        cv_work.notify_one();
+        return insts.size() - 1;
     }
     void work() {
         std::vector<uint8_t> pairs(128 * 32), chosen(128 * 16);
         for (;;) {
-            const uint32_t k = next.fetch_add(1);
-            if (k >= instances) return;
+            Inst* in = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_work.wait(lk, [&] { return stop || next_work < insts.size(); });
+                if (stop) return;
+                in = &insts[next_work++];
+            }
+            // the OT-extension sender's base choice bits: the words the ideal mode uses (ot_level_choice)
+            uint32_t sw[4];
+            ot_level_choice(prf, in->lv, in->salt, sw);
+            uint8_t ch[16];
+            std::memcpy(ch, sw, 16);
             std::string e;
-            const int r = base_ot_instance(k, seed, &choices[(size_t)k * 16], pairs.data(), chosen.data(), &e);
-            if (!r)
+            const int r = base_ot_instance((uint64_t)in->lv << 32 | in->salt, seed, ch, pairs.data(), chosen.data(), &e);
+            std::vector<uint32_t> rk;
+            if (!r) {
+                rk.resize((size_t)3 * 128 * 44);
                 for (int i = 0; i < 128; i++) {
                     uint32_t w[11][4];
                     for (int b = 0; b < 3; b++) {
                         host_key_schedule(b < 2 ? &pairs[((size_t)i * 2 + b) * 16] : &chosen[(size_t)i * 16], w);
-                        std::memcpy(&rk[(((size_t)k * 3 + b) * 128 + i) * 44], w, 44 * 4);
+                        std::memcpy(&rk[((size_t)b * 128 + i) * 44], w, 44 * 4);
                     }
                 }
+            }
             std::lock_guard<std::mutex> lk(mu);
             if (r && !rc) {
                 rc = r;
                 err = e;
             }
-            done[k] = 1;
+            in->rk.swap(rk);
+            in->done = true;
             busy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            cv.notify_all();
+            cv_done.notify_all();
         }
     }
-    int wait(uint32_t k) {
+    int wait(size_t i) {
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return done[k] != 0 || rc != FHH_OK; });
+        cv_done.wait(lk, [&] { return insts[i].done || rc != FHH_OK; });
         return rc;
     }
-    const uint32_t* schedules(uint32_t k) const { return &rk[(size_t)k * 3 * 128 * 44]; }
+    const uint32_t* schedules(size_t i) {
+        std::lock_guard<std::mutex> lk(mu);
+        return insts[i].rk.data();
+    }
 };
 
 struct LoopBuffers {
@@ -787,6 +841,7 @@ struct LoopBuffers {
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
+    DevBuf agree;                                // multi-rank: the growth decision's flags (loop_entry_cap)
     bool distributed = false;
     uint64_t* red() const { return distributed ? reduced.as<uint64_t>() : partials.as<uint64_t>(); }
     // parity probe (cfg->probe_*): per probed level, the gathered states at stride probe_stride
@@ -794,11 +849,14 @@ struct LoopBuffers {
     DevBuf probe_seed[kMaxProbe], probe_ty[kMaxProbe];
     uint64_t probe_stride[kMaxProbe] = {};
     DevBuf probe_C, probe_clients;
-    // cfg->base_ot: the key schedules [levels][2 OTs][3][128][44] of the real base OTs
+    // cfg->base_ot: the key schedules [3][128][44] of the real base OTs, uploaded into a ring of
+    // kBaseRing slots on the engine stream (stream order: a slot is rewritten only after the OT
+    // kernels enqueued before the copy have read it)
+    static constexpr uint32_t kBaseRing = 8;
     bool base_ot = false;
     DevBuf base_rk;
+    uint32_t base_slot = 0;
     std::unique_ptr<BaseOtProducer> bot;
-    std::vector<uint8_t> bot_uploaded;   // per instance
     std::vector<DevBuf*> hist_epochs;            // hist rows; a new epoch per F_cap growth
     std::vector<uint32_t*> hist_ptr;             // per level
     uint32_t E_cap = 0, F_cap = 0;
@@ -810,17 +868,17 @@ struct LoopBuffers {
     }
 };
 
-// wait for base-OT instance k and copy its key schedules to the device (once; a resumed level
-// reuses them). The copy is from pageable memory, so it has left the host buffer on return.
-int upload_base_ot(fhh_ctx* c0, LoopBuffers& B, uint32_t k) {
-    if (B.bot_uploaded.empty()) B.bot_uploaded.assign(B.bot->instances, 0);
-    if (B.bot_uploaded[k]) return FHH_OK;
-    const int rc = B.bot->wait(k);
+// wait for the base OTs of OT extension (lv, salt) and copy their key schedules to the next ring
+// slot; returns the slot's device address. The copy is from pageable memory, so it has left the host
+// buffer on return.
+int upload_base_ot(fhh_ctx* c0, LoopBuffers& B, uint32_t lv, uint32_t salt, const uint32_t** rk_dev) {
+    const size_t i = B.bot->request(lv, salt);
+    const int rc = B.bot->wait(i);
     if (rc) return c0->fail(rc, "base OTs: " + B.bot->err);
     const size_t words = (size_t)3 * 128 * 44;
-    HIP_TRY(c0, hipMemcpyAsync(B.base_rk.as<uint32_t>() + (size_t)k * words, B.bot->schedules(k), words * 4,
-                               hipMemcpyHostToDevice, c0->stream));
-    B.bot_uploaded[k] = 1;
+    uint32_t* dst = B.base_rk.as<uint32_t>() + (size_t)(B.base_slot++ % LoopBuffers::kBaseRing) * words;
+    HIP_TRY(c0, hipMemcpyAsync(dst, B.bot->schedules(i), words * 4, hipMemcpyHostToDevice, c0->stream));
+    *rk_dev = dst;
     return FHH_OK;
 }
 
@@ -867,7 +925,16 @@ size_t table_entry_bytes(const fhh_ctx* c) { return 2 * c->npad * 16 + 2 * 2 * c
 // else is allocated; else 1.25x the need in 64-entry steps; else the need itself. At 1M clients an
 // entry is 32 MB (both sides' seeds), so the doubling alone overshot 288 GB at configs[3]'s dense
 // thresholds (2 servers x d dims x 2 parities of tables on one GPU).
-int loop_entry_cap(fhh_ctx* const (&cs)[2], uint32_t d, uint32_t E_cap, uint32_t need, uint32_t la, uint32_t& out) {
+//
+// Ranks of a sharded crawl (cfg->comm / cfg->allreduce) must pick the SAME capacity: the abort level
+// of every later batch, the loop's all-reduce sequence and count (C_cap x per) and the next crawl's
+// loop_cap_hint all follow from it, and their free memory differs. So each rank's "does candidate k
+// fit here" flags are summed over the ranks through the loop's own reduction and the first candidate
+// that fits on every rank is taken. FHH_TEST_TABLE_BYTES="a0,a1,..." replaces the available bytes of
+// comm rank r by a_r (the last entry for higher ranks; entry 0 without a communicator): tests force
+// different free memory per rank with it.
+int loop_entry_cap(fhh_ctx* const (&cs)[2], const fhh_sim_config* cfg, LoopBuffers& B, uint32_t d, uint32_t E_cap,
+                   uint32_t need, uint32_t la, uint32_t& out) {
     size_t free_b = 0, total_b = 0;
     HIP_TRY(cs[0], hipMemGetInfo(&free_b, &total_b));
     size_t held = 0, old_pres = 0, n_tab = 0;   // bytes the tables hold now; largest preserved one
@@ -882,16 +949,52 @@ int loop_entry_cap(fhh_ctx* const (&cs)[2], uint32_t d, uint32_t E_cap, uint32_t
     }
     const size_t bpe = table_entry_bytes(cs[0]);
     const size_t margin = (size_t)2 << 30;
-    const size_t avail = free_b + held > margin ? free_b + held - margin : 0;
-    const uint64_t cand[3] = {(uint64_t)next_pow2(need) * 2, ((uint64_t)need * 5 / 4 + 63) / 64 * 64, need};
-    out = std::max<uint32_t>(E_cap, need);
-    for (uint64_t e : cand) {
-        e = std::max<uint64_t>(e, E_cap);
-        if (e * bpe * n_tab + old_pres <= avail) {
-            out = (uint32_t)e;
-            break;
+    size_t avail = free_b + held > margin ? free_b + held - margin : 0;
+    if (const char* e = std::getenv("FHH_TEST_TABLE_BYTES")) {
+        const int r = cfg->comm ? comm_rank(cfg->comm) : 0;
+        std::string s(e);
+        size_t pos = 0;
+        for (int k = 0;; k++) {
+            const size_t comma = s.find(',', pos);
+            avail = (size_t)std::strtoull(s.substr(pos, comma - pos).c_str(), nullptr, 10);
+            if (k == r || comma == std::string::npos) break;
+            pos = comma + 1;
         }
     }
+    const uint64_t cand[3] = {(uint64_t)next_pow2(need) * 2, ((uint64_t)need * 5 / 4 + 63) / 64 * 64, need};
+    uint64_t nofit[3];
+    for (int k = 0; k < 3; k++) {
+        const uint64_t e = std::max<uint64_t>(cand[k], E_cap);
+        nofit[k] = e * bpe * n_tab + old_pres <= avail ? 0 : 1;
+    }
+    if (cfg->comm || cfg->allreduce) {
+        // every rank reaches this abort at the same level (the frontier is replicated and the
+        // capacities agree), so the extra collective pairs up across ranks
+        fhh_ctx* c0 = cs[0];
+        HIP_TRY(c0, B.agree.ensure(2 * 3 * 8));
+        uint64_t* dv = B.agree.as<uint64_t>();
+        HIP_TRY(c0, hipMemcpyAsync(dv, nofit, sizeof nofit, hipMemcpyHostToDevice, c0->stream));
+        if (cfg->comm) {
+            std::string err;
+            if (comm_allreduce(cfg->comm, dv, dv + 3, 3, c0->stream, &err)) return c0->fail(FHH_E_COMM, err);
+        } else {
+            if (!cfg->xchg_dev || cfg->xchg_capacity < 3)
+                return c0->fail(FHH_E_ARG, "sim: all-reduce exchange buffer too small");
+            HIP_TRY(c0, hipMemcpyAsync(cfg->xchg_dev, dv, sizeof nofit, hipMemcpyDeviceToDevice, c0->stream));
+            HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+            if (cfg->allreduce(cfg->xchg_dev, 3, cfg->allreduce_user) != 0)
+                return c0->fail(FHH_E_CALLBACK, "all-reduce callback failed");
+            HIP_TRY(c0, hipMemcpyAsync(dv + 3, cfg->xchg_dev, sizeof nofit, hipMemcpyDeviceToDevice, c0->stream));
+        }
+        HIP_TRY(c0, hipMemcpyAsync(nofit, dv + 3, sizeof nofit, hipMemcpyDeviceToHost, c0->stream));
+        HIP_TRY(c0, hipStreamSynchronize(c0->stream));
+    }
+    out = std::max<uint32_t>(E_cap, need);
+    for (int k = 0; k < 3; k++)
+        if (!nofit[k]) {
+            out = (uint32_t)std::max<uint64_t>(cand[k], E_cap);
+            break;
+        }
     if (std::getenv("FHH_DEBUG_LOOP"))
         std::fprintf(stderr, "[fhh loop] entry cap: need %u -> %u (%.1f GB of tables, %.1f GB available)\n", need,
                      out, (double)out * bpe * n_tab / 1e9, (double)avail / 1e9);
@@ -999,24 +1102,16 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     rc = loop_resize(c0, B, cap0, cap0, levels, 0, false, 0, 0, 1);
     if (rc) return rc;
     if (cfg->gc == 2 && cfg->base_ot) {
-        // the two OT extensions of every level each start with 128 Chou–Orlandi base OTs
-        // (AlszSender/AlszReceiver::init, collect.rs:454-471): host threads produce them in level
-        // order while this thread enqueues the crawl, which waits only for the level it is about
-        // to enqueue; the sender's base choice bits are the per-level words the ideal mode uses
-        std::vector<uint8_t> choices((size_t)2 * levels * 16);
-        for (uint32_t lv = 0; lv < levels; lv++)
-            for (uint32_t salt = 0; salt < 2; salt++) {
-                uint32_t sw[4];
-                ot_level_choice(cfg->prf_seed, lv, salt, sw);
-                std::memcpy(&choices[((size_t)lv * 2 + salt) * 16], sw, 16);
-            }
+        // the OT extensions of every level and chunk each start with 128 Chou–Orlandi base OTs
+        // (AlszSender/AlszReceiver::init, collect.rs:454-471): host threads produce them a few levels
+        // ahead of this thread's enqueueing, which waits only for the chunk it is about to enqueue
         uint8_t seed[32];
         for (int k = 0; k < 4; k++) {
             const uint64_t z = host_mix64(cfg->prf_seed ^ (0x626173655f6f74ull + (uint64_t)k));
             std::memcpy(seed + 8 * k, &z, 8);
         }
-        HIP_TRY(c0, B.base_rk.ensure((size_t)2 * levels * 3 * 128 * 44 * 4));
-        B.bot = std::make_unique<BaseOtProducer>(2 * levels, seed, std::move(choices));
+        HIP_TRY(c0, B.base_rk.ensure((size_t)LoopBuffers::kBaseRing * 3 * 128 * 44 * 4));
+        B.bot = std::make_unique<BaseOtProducer>(cfg->prf_seed, seed);
         B.base_ot = true;
     }
     if (cfg->probe_n_levels) {
@@ -1138,6 +1233,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 const uint32_t bits = 2 * d;
                 const size_t plane_bytes = (size_t)C_cap * bits * c0->nw * 8;
                 for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
+                size_t gc_slot = 0;
+                if (timed) HIP_TRY(c0, timing_begin(c0, &gc_slot));
                 ChildArgs pa = a;
                 HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[0].as<uint64_t>(), c0->stream));
                 pa.s0 = a.s1;
@@ -1145,9 +1242,13 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 const uint64_t Gc = std::min<uint64_t>(C_cap, gc_groups);
                 const uint64_t chunks = (C_cap + Gc - 1) / Gc;
                 const bool real_ot = cfg->gc >= 2;
-                if (B.base_ot && chunks > 1)
-                    return c0->fail(FHH_E_ARG, "sim_crawl: real base OTs need the level's GC in one chunk "
-                                               "(raise FHH_GC_CHUNK_BYTES)");
+                if (B.base_ot) {
+                    // keep the producer a few levels ahead of the enqueueing (at this capacity's chunk
+                    // count; a level enqueued after a growth requests its extra chunks itself)
+                    constexpr uint32_t kAhead = 4;
+                    for (uint32_t l = lv; l < std::min(levels, lv + kAhead); l++)
+                        for (uint64_t salt = 0; salt < 2 * chunks; salt++) (void)B.bot->request(l, (uint32_t)salt);
+                }
                 const uint64_t tests = Gc * c0->n;
                 const uint32_t per2 = pmode == 1 ? 1 : 2;   // OTs per test of the share conversion
                 HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
@@ -1192,9 +1293,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k), sw);
                         const uint32_t* rk1 = c0->ot_rk.as<uint32_t>();
                         if (B.base_ot) {
-                            rc = upload_base_ot(c0, B, 2 * lv);
+                            rc = upload_base_ot(c0, B, lv, (uint32_t)(2 * k), &rk1);
                             if (rc) return rc;
-                            rk1 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 0) * 3 * 128 * 44;
                         } else {
                             HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k), sw,
                                                              c0->ot_rk.as<uint32_t>(), c0->stream));
@@ -1235,9 +1335,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw);
                         const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
                         if (B.base_ot) {
-                            rc = upload_base_ot(c0, B, 2 * lv + 1);
+                            rc = upload_base_ot(c0, B, lv, (uint32_t)(2 * k + 1), &rk2);
                             if (rc) return rc;
-                            rk2 = B.base_rk.as<uint32_t>() + ((size_t)lv * 2 + 1) * 3 * 128 * 44;
                         } else {
                             HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw,
                                                              c0->ot_rk.as<uint32_t>(), c0->stream));
@@ -1253,6 +1352,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(ca, part, c0->stream, false));
                     else HIP_TRY(c0, launch_sim_ot_fe255(ca, part, c0->stream));
                 }
+                if (timed) HIP_TRY(c0, timing_end(c0, gc_slot, kGcotTag));
             } else if (pmode == 0) {
                 HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
             } else if (pmode == 1) {
@@ -1264,8 +1364,11 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             // (the count is the capacity bound: entries past C are never read)
             if (cfg->comm) {
                 std::string err;
+                size_t ar_slot = 0;
+                if (timed) HIP_TRY(c0, timing_begin(c0, &ar_slot));
                 if (comm_allreduce(cfg->comm, part, B.red(), C_cap * per, c0->stream, &err))
                     return c0->fail(FHH_E_COMM, err);
+                if (timed) HIP_TRY(c0, timing_end(c0, ar_slot, kAllreduceTag));
             } else if (cfg->allreduce) {
                 const uint64_t count = C_cap * per;
                 if (!cfg->xchg_dev || cfg->xchg_capacity < count)
@@ -1341,7 +1444,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 const uint32_t la = h->abort_level;
                 const bool la_last = la + 1 == levels;
                 uint32_t nE = 0;
-                rc = loop_entry_cap(cs, d, B.E_cap, std::max<uint32_t>(h->need_entries, 1), la, nE);
+                rc = loop_entry_cap(cs, cfg, B, d, B.E_cap, std::max<uint32_t>(h->need_entries, 1), la, nE);
                 if (rc) return rc;
                 const uint32_t nF = std::max(B.F_cap, next_pow2(std::max<uint32_t>(h->need_nodes, 1)) * 2);
                 const uint32_t la_per = cfg->mode == 0 ? 1 : (la_last ? 16 : 4);
@@ -1375,8 +1478,9 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         }
     }
     if (B.bot) {
-        const int brc = B.bot->wait(B.bot->instances - 1);
-        if (brc) return c0->fail(brc, "base OTs: " + B.bot->err);
+        // every instance the crawl used was waited for at its upload; lookahead ones still running
+        // are abandoned (the destructor stops the workers after their current instance)
+        std::lock_guard<std::mutex> lk(B.bot->mu);
         c0->stats.base_ot_ms += B.bot->busy_ms;
     }
     c0->loop_cap_hint = std::max(B.E_cap, B.F_cap);   // the next crawl starts at this size

@@ -301,7 +301,10 @@ int comm_allreduce(::fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t
 int comm_init_all(int n, const int* devices, std::vector<::fhh_comm*>& out, std::string* err);
 int comm_group_allreduce(const std::vector<::fhh_comm*>& comms, const std::vector<uint64_t*>& bufs, uint64_t count,
                          const std::vector<hipStream_t>& streams, std::string* err);
+// abort once (a second call, or one racing it from another shard thread, is a no-op); the handle
+// stays valid until fhh_comm_destroy, which then skips ncclCommDestroy
 void comm_abort(::fhh_comm* c);
+int comm_rank(const ::fhh_comm* c);   // the rank given at creation
 // device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
 // entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);

@@ -17,6 +17,8 @@
 //   k_ot_send_hash_rows / k_ot_recv_hash_rows  one wave per 512 OTs, the 128 x 512 bit tile of T / Q
 //                                              transposed in registers + LDS: 2 / 1 cr_hash per OT
 #include "fhh_internal.h"
+
+#include <atomic>
 #include "aes_keyed.h"
 #include "bitslice.h"
 
@@ -326,15 +328,15 @@ hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, con
 // CU count of the current device, queried once per device (the level loop launches these
 // kernels thousands of times per crawl)
 static int device_cus() {
-    static int cache[64] = {};
+    static std::atomic<int> cache[64] = {};   // shard threads of a multi-device ctx share it
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int cus = 0;
+    int cus = cache[dev].load(std::memory_order_relaxed);
+    if (!cus) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        cache[dev] = cus;
+        cache[dev].store(cus, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return cus;
 }
 
 static int ot_grid(uint64_t items, int threads) {

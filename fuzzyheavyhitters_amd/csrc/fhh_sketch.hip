@@ -13,6 +13,8 @@
 //   k_sketch_fe255 / k_mul_fe255 / k_verify_fe255: the same for U = FieldElm (GF(2^255 - 19)),
 //                 the last level's sketch_at_last (sketch.rs:202-245).
 #include "fhh_internal.h"
+
+#include <atomic>
 #include "expand_kernel.h"
 #include "aes_tables.h"
 #include "field_arith.h"
@@ -399,7 +401,8 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
 // blocks (PCB p + q) LPK + l, q < PCB, in pass p, so a task is ceil(nb / (PCB LPK)) phases, and the
 // pairs of the grid run the tasks in rounds (uniform across the grid, so every wave meets every
 // barrier). The consumer issues its next pass's (x, kx) loads one phase ahead. LDS: 128 KiB tables +
-// 11 KiB round keys (the producers' 8 x KPW schedules) + 16 KiB buffer (PCB = 2).
+// the hand-over buffer, 8 pairs x PCB x 64 lanes x 16 B = 24 KiB at PCB = 3 (152 KiB; the producers
+// keep their keys' schedules in VGPRs).
 constexpr int kPcPairs = 8;
 constexpr int kPcThreads = 1024;
 // keystream blocks per producer lane per phase: 3, with the key's schedule kept in VGPRs (4 with the
@@ -412,6 +415,7 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
     using Tab = Tab4T32<DevOpsX>;
     __shared__ uint32_t tbl[Tab::kWords];
     __shared__ uint4 buf[kPcPairs][PCB][64];
+    static_assert(sizeof(tbl) + sizeof(buf) <= 160 * 1024, "k_sketch_fe_pc: static LDS above the CU's 160 KiB");
     for (int i = threadIdx.x; i < Tab::kWords; i += kPcThreads) tbl[i] = Tab::word(c_T0_sk.v, i);
     __syncthreads();
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -614,19 +618,21 @@ static hipError_t launch_sketch_lpk(int lpk, const SketchArgs& a, hipStream_t st
 
 // resident waves of the LDS-schedule kernel on the current device (cached per device)
 static uint64_t sketch_resident_waves() {
-    static uint64_t cache[64] = {};
+    static std::atomic<uint64_t> cache[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!cache[dev]) {
+    uint64_t w = cache[dev].load(std::memory_order_relaxed);
+    if (!w) {
         int cus = 256, per_cu = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
                 &per_cu, reinterpret_cast<const void*>(k_sketch_fe<8, SkTab4, kSketchThreadsOtf, 2, kSketchNbpOtf>),
                 kSketchThreadsOtf, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
-        cache[dev] = (uint64_t)(cus > 0 ? cus : 256) * per_cu * (kSketchThreadsOtf / 64);
+        w = (uint64_t)(cus > 0 ? cus : 256) * per_cu * (kSketchThreadsOtf / 64);
+        cache[dev].store(w, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return w;
 }
 
 // cost in passes of one launch of n keys at LPK lanes per key (+ half a pass per round for the key
@@ -639,7 +645,7 @@ static double sketch_launch_cost(uint64_t n, uint64_t nb, int lpk, uint64_t W, i
 }
 
 // W = resident waves (fused form, nbp = 2 blocks per lane per pass) or resident producer / consumer
-// pairs (nbp = 1: one block per lane per phase)
+// pairs (nbp = kPcBlocks = 3 blocks per producer lane per phase)
 SketchPlan plan_sketch_nbp(uint64_t n_keys, uint32_t n_nodes, uint64_t W, int nbp);
 SketchPlan plan_sketch(uint64_t n_keys, uint32_t n_nodes, uint64_t W) {
     return plan_sketch_nbp(n_keys, n_nodes, W, kSketchNbpOtf);
@@ -708,17 +714,18 @@ static hipError_t launch_sketch_pc_lpk(int lpk, const SketchArgs& a, int cus, hi
     }
 }
 
-// CU count of the current device, queried once per device (the sketch launches run per level)
+// CU count of the current device, queried once per device (the sketch launches run per level; the
+// shard threads of a multi-device ctx may fill the cache concurrently, hence the atomics)
 static int sketch_cus() {
-    static int cache[64] = {};
+    static std::atomic<int> cache[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int cus = 0;
+    int cus = cache[dev].load(std::memory_order_relaxed);
+    if (!cus) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        cache[dev] = cus;
+        cache[dev].store(cus, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return cus;
 }
 
 static hipError_t launch_sketch_pc(const SketchArgs& a, hipStream_t stream) {

@@ -10,6 +10,7 @@ receiving party owns (`fhh_memcpy_device`) and counts the bytes.
 from __future__ import annotations
 
 import ctypes
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -29,17 +30,28 @@ def level_cfg(prf_seed: int, level: int) -> FhhGcPartyCfg:
 
 
 class Channel:
-    """One direction of the servers' channel: a message becomes a copy in memory the receiving
-    party owns (a torch buffer on its GPU), reused across levels."""
+    """One direction of the servers' channel. mode "copy": a message becomes a copy in memory the
+    receiving party owns (a torch buffer on its GPU, reused across levels) — the bytes a deployment
+    moves over the network, moved here device to device. mode "inplace" (both parties on one GPU):
+    the receiver reads the message where the sender's ctx produced it. That is safe in this protocol
+    order because each party's messages live in their own buffers (gc, U, Y0 | Y1) and a party
+    rewrites one only after the peer's call that consumed it has returned (every call returns after
+    its device work is complete)."""
 
-    def __init__(self, device: int):
+    def __init__(self, device: int, mode: str = "copy"):
         import torch
+        if mode not in ("copy", "inplace"):
+            raise ValueError(f"Channel mode {mode!r}")
         self.torch = torch
         self.device = device
+        self.mode = mode
         self.bufs: dict = {}
         self.bytes = 0
 
     def send(self, name: str, src_ptr: int, nbytes: int) -> int:
+        if self.mode == "inplace":
+            self.bytes += nbytes
+            return src_ptr
         buf = self.bufs.get(name)
         if buf is None or buf.numel() < nbytes:
             buf = self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=f"cuda:{self.device}")
@@ -103,7 +115,8 @@ class TwoPartyResult:
 
 
 def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
-                    prf_seed: int = 0, levels: int = 0, cfg_fn=None, expect_counts=None) -> TwoPartyResult:
+                    prf_seed: int = 0, levels: int = 0, cfg_fn=None, expect_counts=None,
+                    channel: str = "copy", timing: dict | None = None, record: bool = True) -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between
     the two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both,
     run the level's protocol through the channel, take each server's node sums from its own
@@ -111,7 +124,12 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     level's fhh_gc_party_cfg (default: level_cfg(prf_seed, level), fhh_sim_crawl's material); for a
     multi-device collection `cfg_fn(level, shard)`, one protocol instance per shard.
     `expect_counts` (tests): per-level v0 - v1 to compare against as the crawl goes (raises at the
-    first level that differs instead of crawling on a wrong frontier)."""
+    first level that differs instead of crawling on a wrong frontier). `channel`: "copy" (every
+    message copied into a buffer of the receiver) or "inplace" (the receiver reads the sender's
+    buffer; both shards of a pair must share a GPU). `timing` (a dict) accumulates the host wall
+    seconds of each phase of the level loop: crawl, gcot, node_sums, keep, prune (every call returns
+    after its device work, so these are the phases' elapsed times). record=False skips the per-level
+    v0 - v1 records (res.counts) the timed bench does not need."""
     L = levels or c0.depth
     n_total = nclients_total if nclients_total is not None else c0.num_clients()
     thr = max(1, int(threshold * n_total))
@@ -121,38 +139,60 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     # splits a level's tests over several channels, collect.rs:423-430)
     S = len(c0.shard_info()[0])
     shards = [(c0.shard(k), c1.shard(k)) for k in range(S)] if S > 1 else [(c0, c1)]
-    chans = [(Channel(a.device), Channel(b.device)) for a, b in shards]
+    if channel == "inplace" and any(a.device != b.device for a, b in shards):
+        raise ValueError("two_party_crawl: an in-place channel needs both parties of a pair on one GPU")
+    chans = [(Channel(a.device, channel), Channel(b.device, channel)) for a, b in shards]
     res = TwoPartyResult()
     c0.tree_init()
     c1.tree_init()
-    from .fields import FE_P
+    from .fields import FE255_P, FE_P
+    tm = timing if timing is not None else {}
+    for k in ("crawl", "gcot", "node_sums", "keep", "prune"):
+        tm.setdefault(k, 0.0)
+    clock = time.perf_counter
+    shard_clients = [a.num_clients() for a, _ in shards]
     for lv in range(L):
         last = lv == L - 1
+        t0 = clock()
         C0, _ = (c0.tree_crawl_last if last else c0.tree_crawl)()
         C1, _ = (c1.tree_crawl_last if last else c1.tree_crawl)()
         assert C0 == C1
+        t1 = clock()
         sizes = {}
         for k, ((a, b), (to_gb, to_ev)) in enumerate(zip(shards, chans)):
-            if a.num_clients() == 0:
+            if shard_clients[k] == 0:
                 continue
             cfg = cfg_fn(lv) if S == 1 else cfg_fn(lv, k)
             for name, v in run_level(a, b, cfg, cfg, to_gb, to_ev).items():
                 sizes[name] = sizes.get(name, 0) + v
         res.level_bytes.append(sizes)
+        t2 = clock()
         s0 = party_sums(c0, C0, last)
         s1 = party_sums(c1, C1, last)
+        t3 = clock()
         res.level_children.append(C0)
         if not last:
             keep = KeyCollection.keep_values(n_total, thr, s0, s1)
-            res.counts.append(((s0.astype(object) - s1.astype(object)) % FE_P).astype(np.uint64))
+            t4 = clock()
             c0.tree_prune(keep)
             c1.tree_prune(keep)
         else:
             keep = KeyCollection.keep_values_last(n_total, thr_last, s0, s1)
-            from .fields import FE255_P
-            res.counts.append(np.array([((a % FE255_P) - (b % FE255_P)) % FE255_P for a, b in zip(s0, s1)], np.uint64))
+            t4 = clock()
             c0.tree_prune_last(keep)
             c1.tree_prune_last(keep)
+        t5 = clock()
+        tm["crawl"] += t1 - t0
+        tm["gcot"] += t2 - t1
+        tm["node_sums"] += t3 - t2
+        tm["keep"] += t4 - t3
+        tm["prune"] += t5 - t4
+        if not (record or expect_counts is not None):
+            continue
+        if not last:
+            res.counts.append(((s0.astype(object) - s1.astype(object)) % FE_P).astype(np.uint64))
+        else:
+            res.counts.append(np.array([((a % FE255_P) - (b % FE255_P)) % FE255_P for a, b in zip(s0, s1)], np.uint64))
         if expect_counts is not None and not np.array_equal(res.counts[-1], np.asarray(expect_counts[lv], np.uint64)):
             bad = np.nonzero(res.counts[-1] != np.asarray(expect_counts[lv], np.uint64))[0]
             raise ValueError(f"two-party crawl: level {lv}: {bad.size} of {C0} children differ (first {bad[:5]}: "

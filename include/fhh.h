@@ -571,6 +571,14 @@ typedef struct fhh_stats {
     double keygen_ms;
     uint64_t expand_launches_timed; /* k_expand launches covered by expand_ms             */
     double base_ot_ms;          /* host time of the real base OTs (fhh_sim_config.base_ot) */
+    double allreduce_ms;        /* device loop, cfg->comm / allreduce: summed per-level cross-rank
+                                 * all-reduce time (HIP events around it on the engine stream,
+                                 * on the levels fhh_set_timing times)                      */
+    uint64_t allreduce_timed;   /* all-reduces covered by allreduce_ms                        */
+    double gcot_ms;             /* device loop, cfg->gc: summed per-level GC + OT step time (share
+                                 * planes, garble, OTs, evaluate, share sums; HIP events on the
+                                 * engine stream, on the levels fhh_set_timing times)        */
+    uint64_t gcot_timed;        /* levels covered by gcot_ms                                  */
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);

@@ -122,3 +122,52 @@ def test_bench_two_rank_rccl_bootstrap_and_fallback():
     assert col["comm_ranks"] == 2
     for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
         assert two[k] == one[k], k
+
+
+def test_launch_plan_refuses_a_world_that_differs_from_gpus():
+    """bench.py decides how it runs before any GPU call: a torchrun world that is not --gpus, or more
+    GPUs than the node shows, exits non-zero; --gpus N > 1 without a torchrun world relaunches itself
+    as N ranks (one node, rendezvous on 127.0.0.1)."""
+    import bench
+    assert bench.launch_plan(1, {}, 1, False) == ("run", None)
+    assert bench.launch_plan(1, {}, 0, False) == ("run", None)
+    assert bench.launch_plan(8, {}, 8, False) == ("relaunch", None)
+    assert bench.launch_plan(8, {}, 1, True) == ("relaunch", None)          # rehearsal shares the GPU
+    how, why = bench.launch_plan(8, {}, 1, False)
+    assert how == "error" and "only 1 GPU" in why
+    assert bench.launch_plan(2, {"WORLD_SIZE": "2"}, 8, False) == ("run", None)
+    how, why = bench.launch_plan(8, {"WORLD_SIZE": "1"}, 8, False)
+    assert how == "error" and "WORLD_SIZE=1" in why
+    how, _ = bench.launch_plan(1, {"WORLD_SIZE": "4"}, 8, False)
+    assert how == "error"
+    how, _ = bench.launch_plan(4, {"WORLD_SIZE": "4"}, 1, False)
+    assert how == "error"
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}, 1, True) == ("run", None)
+    cmd = bench.relaunch_cmd(["--gpus", "8", "--steps", "3"], 8, 29555)
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_rccl_init_failure_fails_the_measurement():
+    """An RCCL init error on any rank ends every rank with a non-zero exit unless the run is the
+    one-GPU --rehearse-rccl rehearsal (which falls back to the hosted all-reduce and says so)."""
+    import bench
+    assert bench.collective_after_init([None, None], False) == ("rccl", None)
+    assert bench.collective_after_init([None, "ncclCommInitRank: invalid usage"], False) == \
+        ("fail", "ncclCommInitRank: invalid usage")
+    assert bench.collective_after_init(["x", "x"], True) == ("hosted", "x")
+
+
+@pytest.mark.parametrize("world,gpus", [("3", "2"), ("1", "8")])
+def test_bench_exits_nonzero_on_world_mismatch(world, gpus):
+    """The guard runs before any GPU call: on this GPU-less container the process exits 2 with the
+    reason, no JSON line."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE=world, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", gpus, "--steps", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert f"WORLD_SIZE={world} but --gpus={gpus}" in r.stderr
+    assert r.stdout.strip() == ""

@@ -170,22 +170,28 @@ def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gc_mode", ["ideal", "ot"])
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15"])
 def test_gpu_crawl_with_gc_in_chunks(monkeypatch, gc_mode):
     """A level's GC + OT split into chunks of children, each a fresh protocol instance (the
     reference spreads a level's tests over its channels, collect.rs:423-430; the device loop
     chunks so the GC and OT buffers of 1M clients stay bounded): FHH_GC_CHUNK_BYTES small enough
     for 3 children per chunk -> the same sums, keep decisions and heavy hitters as the plaintext
-    harness (the last chunk of a level partial, chunks past C no-ops)."""
+    harness (the last chunk of a level partial, chunks past C no-ops). "ot+co15": every chunk's two
+    OT extensions start from their own real Chou–Orlandi base OTs (the metric's 1M crawl runs ~7
+    chunks per level), with capacity growth and resumed levels (init_capacity 2)."""
     from fuzzyheavyhitters_amd import sim_crawl, workload
     wl = workload.zipf_workload(1000, 48, 1, num_sites=30, seed=17)
     c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
     plain = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=3)
     npad = (1000 + 63) // 64 * 64
     monkeypatch.setenv("FHH_GC_CHUNK_BYTES", str(3 * 402 * npad))   # 3 children x ~402 B per test (d = 1)
-    with_gc = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=3, gc=gc_mode)
+    co15 = gc_mode.endswith("co15")
+    with_gc = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=3, gc=gc_mode.split("+")[0], base_ot=co15,
+                        init_capacity=2 if co15 else 0)
     assert _sig(with_gc) == _sig(plain)
     assert max(plain.level_children) > 6 and len(with_gc.final) > 0
+    if co15:
+        assert c0.stats()["base_ot_ms"] > 0
 
 
 @pytest.mark.gpu

@@ -122,6 +122,14 @@ def test_sampled_states_bit_exact_full_size(oracle, n, word_step):
         # fixture (tests/golden/make_zipf_1m.py); every level's counts and the heavy hitters
         assert_equals_golden_1m(wl, res)
         return
+    # configs[1]: every level's counts, the 222 heavy hitters with their counts and the AES-block
+    # total equal the ORACLE's own crawl (tests/golden/oracle_zipf_100k_L512.npz,
+    # tests/golden/make_oracle_100k.py)
+    from test_oracle_100k import assert_counts_equal_oracle, load_oracle_100k
+    g = load_oracle_100k()
+    assert_counts_equal_oracle(g, res.level_children, res.counts,
+                               [(tuple(int(b) for b in r.path[0]), int(r.value)) for r in res.final])
+    assert c0.stats()["aes_blocks"] * 2 == int(g["aes_blocks"])
     # the crawl itself (AES-independent) still matches the plaintext recount
     from fuzzyheavyhitters_amd import workload
     cnt, paths, _ = workload.plaintext_crawl(wl.left, wl.right, thr, thr)

@@ -216,3 +216,38 @@ def test_group_node_sums_of_device_values():
     unr2, can2 = g0.node_sums_fe255(np.ascontiguousarray(limbs))
     assert unr == unr2 and can == can2
     assert unr == [sum(row) for row in ints]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["count", "fe"])
+def test_group_sim_crawl_agrees_on_growth_when_free_memory_differs(monkeypatch, capfd, mode):
+    """The device loop grows its tables when a level overflows, choosing the capacity from this GPU's
+    free memory (loop_entry_cap). Shards of one crawl must choose the same capacity — the abort level
+    of every later batch and each rank's all-reduce sequence and count follow from it — so the choice
+    is agreed over the loop's own reduction. FHH_TEST_TABLE_BYTES gives shard 0 ample room and shard 1
+    none: the shards grow alike (the debug log shows one capacity sequence) and the crawl equals the
+    one-GPU one, with several resumes from capacity 2."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 64 * 13 + 5, 40
+    wl = workload.zipf_workload(n, L, 1, num_sites=20, seed=21)
+    s0, s1 = _pair(L, 1)
+    g0, g1 = _pair(L, 1, [0, 0])
+    fhh.gen_keys_pair(s0, s1, wl.left, wl.right, wl.root_seeds)
+    fhh.gen_keys_pair(g0, g1, wl.left, wl.right, wl.root_seeds)
+    a = fhh.sim_crawl(s0, s1, 0.01, mode=mode, prf_seed=9, init_capacity=2)
+    monkeypatch.setenv("FHH_TEST_TABLE_BYTES", f"{1 << 40},0")
+    monkeypatch.setenv("FHH_DEBUG_LOOP", "1")
+    capfd.readouterr()
+    b = fhh.sim_crawl(g0, g1, 0.01, mode=mode, prf_seed=9, init_capacity=2)
+    err = capfd.readouterr().err
+    caps = [ln for ln in err.splitlines() if "[fhh loop] entry cap" in ln]
+    seq = lambda lines: [ln.split("need ")[1].split(" (")[0] for ln in lines]   # "need E -> cap" per growth
+    roomy = seq(ln for ln in caps if not ln.endswith(" 0.0 GB available"))
+    tight = seq(ln for ln in caps if ln.endswith(" 0.0 GB available"))
+    assert len(tight) >= 2 and roomy == tight, err[-2000:]   # >= 2 growths, the same capacities on both
+    assert list(a.level_children) == list(b.level_children)
+    assert list(a.level_kept) == list(b.level_kept)
+    assert all(np.array_equal(x, y) for x, y in zip(a.counts, b.counts))
+    assert [(r.path, r.value) for r in a.final] == [(r.path, r.value) for r in b.final]
+    assert len(a.final) > 0

@@ -27,11 +27,13 @@ def _assert_same_crawl(a, b):
     assert [(r.path, r.value) for r in a.final] == [(r.path, r.value) for r in b.final]
 
 
+@pytest.mark.parametrize("channel", ["copy", "inplace"])
 @pytest.mark.parametrize("d,n,L,thr", [(1, 300, 24, 0.02), (2, 200, 12, 0.05), (1, 64 * 3, 20, 0.03)],
                          ids=["d1", "d2", "whole-words"])
-def test_two_party_equals_in_process_gc_ot(d, n, L, thr):
+def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel):
     """Level by level: the leader's v0 - v1 per child and the final heavy hitters of the split run
-    equal fhh_sim_crawl(gc = "ot") (both parties in one device loop) on the same material."""
+    equal fhh_sim_crawl(gc = "ot") (both parties in one device loop) on the same material, whether
+    each message is copied into the receiver's buffer or read where the sender produced it."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
     wl = workload.zipf_workload(n, max(L, 32), d, num_sites=5, seed=3 + d)
@@ -39,7 +41,7 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr):
     c0, c1 = _keys(wl, L, d)
     ref = fhh.sim_crawl(c0, c1, thr, mode="fe", prf_seed=77, gc="ot")
     p0, p1 = _keys(wl, L, d)
-    got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77)
+    got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77, channel=channel)
     _assert_same_crawl(ref, got)
     assert len(got.final) > 0
     t = max(1, int(thr * n))
@@ -68,7 +70,8 @@ def test_two_party_fresh_randomness_same_output():
     _assert_same_crawl(ra, rb)
 
 
-def test_two_party_multi_device_shards():
+@pytest.mark.parametrize("channel", ["copy", "inplace"])
+def test_two_party_multi_device_shards(channel):
     """A multi-device collection runs one protocol instance per shard over its own channel (the
     reference spreads a level's tests over several channels, collect.rs:423-430) and reduces the
     parties' device-resident sums over its shards: same output as the one-GPU in-process crawl."""
@@ -80,7 +83,7 @@ def test_two_party_multi_device_shards():
     c0, c1 = _keys(wl, L, 1)
     ref = fhh.sim_crawl(c0, c1, 0.02, mode="fe", prf_seed=5, gc="ot")
     g0, g1 = _keys(wl, L, 1, devices=[0, 0, 0])
-    got = fhh.two_party_crawl(g0, g1, 0.02, prf_seed=5)
+    got = fhh.two_party_crawl(g0, g1, 0.02, prf_seed=5, channel=channel)
     _assert_same_crawl(ref, got)
 
 

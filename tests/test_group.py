@@ -243,8 +243,8 @@ def test_group_sim_crawl_agrees_on_growth_when_free_memory_differs(monkeypatch, 
     err = capfd.readouterr().err
     caps = [ln for ln in err.splitlines() if "[fhh loop] entry cap" in ln]
     seq = lambda lines: [ln.split("need ")[1].split(" (")[0] for ln in lines]   # "need E -> cap" per growth
-    roomy = seq(ln for ln in caps if not ln.endswith(" 0.0 GB available"))
-    tight = seq(ln for ln in caps if ln.endswith(" 0.0 GB available"))
+    roomy = seq(ln for ln in caps if not ln.endswith(" 0.0 GB available)"))
+    tight = seq(ln for ln in caps if ln.endswith(" 0.0 GB available)"))
     assert len(tight) >= 2 and roomy == tight, err[-2000:]   # >= 2 growths, the same capacities on both
     assert list(a.level_children) == list(b.level_children)
     assert list(a.level_kept) == list(b.level_kept)

@@ -10,7 +10,7 @@ OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 k=0
 for group in "SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE GRBM_COUNT" \
-             "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES"; do
+             "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES"; do
   k=$((k + 1))
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc $group --output-format csv -d $OUT/p$k -o p$k -- \
       python3 bench.py "$@" > $OUT/p$k.log 2>&1

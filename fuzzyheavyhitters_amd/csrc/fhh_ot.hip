@@ -19,6 +19,8 @@
 #include "fhh_internal.h"
 
 #include <atomic>
+#include <cstdlib>
+
 #include "aes_keyed.h"
 #include "bitslice.h"
 
@@ -276,6 +278,138 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
     }
 }
 
+// ---- prefetching forms (r04): fewer, register-richer waves --------------------------------------
+// PMC of the r03 hashes (profiles/r03/gcot_1m_pmc_means.json): the receive hash's waves issue VALU / LDS
+// in 25 % of their cycles and sit in s_waitcnt for ~57 % (SQ_WAIT_INST_ANY only 18 %): they wait on
+// memory — the tile's 32 row loads at every tile start and the chosen Y blocks after each pass's AES —
+// and with 4 waves per SIMD at 128 VGPRs there is no room to keep a second tile or the Y blocks in
+// flight. Here a workgroup has THREADS / 64 waves (512: 2 per SIMD, 256 VGPRs each; 768: 3 per SIMD,
+// 168 each) and every wave keeps the NEXT tile's 32 row words and the current pass's messages in
+// flight behind the current pass's AES: the next tile's loads are issued right after this tile's
+// transpose, a pass's Y (receiver) / x0, x1 (sender) loads right before its AES.
+__device__ __forceinline__ void ot_tile_issue(const uint32_t* rows, uint64_t W, uint64_t tile, uint32_t lane,
+                                              uint32_t (&x)[32]) {
+    const uint32_t q = lane >> 2, g = lane & 3;
+    const uint32_t* p = rows + (uint64_t)(32 * g) * W + tile * kOtTileWords + q;
+#pragma unroll
+    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + (uint64_t)i * W);
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_ot_recv_hash_pf(OtArgs a) {
+    constexpr int WAVES = THREADS / 64;
+    __shared__ uint32_t tbl_ot[OtTab::kWords];
+    __shared__ uint32_t stage[WAVES][512];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+    uint32_t x[32];
+    if (t < tiles) ot_tile_issue(rows, W, t, lane, x);
+    for (; t < tiles; t += nwaves) {
+        transpose32(x);
+        uint32_t xn[32];
+        const uint64_t tn = t + nwaves;
+        if (tn < tiles) ot_tile_issue(rows, W, tn, lane, xn);   // wave-uniform
+        const uint64_t cwi = t * kOtTileWords + (lane & 15);
+        const uint32_t cw = 32 * cwi < m ? a.choices[cwi] : 0u;
+#pragma unroll 1
+        for (int r = 0; r < 4; r += 2) {
+            uint32_t h[4][4];
+#pragma unroll
+            for (int rr = 0; rr < 2; rr++) {
+                uint4 tv[2];
+                ot_tile_round(stage[wv], x, lane, tv);
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    h[2 * rr + u][0] = tv[u].x; h[2 * rr + u][1] = tv[u].y;
+                    h[2 * rr + u][2] = tv[u].z; h[2 * rr + u][3] = tv[u].w;
+                }
+            }
+            uint4 y[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {   // the chosen Y of the pass's 4 OTs, in flight during its AES
+                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
+                y[b] = j < m ? (((cw >> (j & 31)) & 1u) ? a.Y1 : a.Y0)[j] : make_uint4(0, 0, 0, 0);
+            }
+            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
+                if (j >= m) continue;
+                a.out[j] = make_uint4(y[b].x ^ h[b][0], y[b].y ^ h[b][1], y[b].z ^ h[b][2], y[b].w ^ h[b][3]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) x[i] = xn[i];
+    }
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_ot_send_hash_pf(OtArgs a) {
+    constexpr int WAVES = THREADS / 64;
+    __shared__ uint32_t tbl_ot[OtTab::kWords];
+    __shared__ uint32_t stage[WAVES][512];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+    uint32_t x[32];
+    if (t < tiles) ot_tile_issue(rows, W, t, lane, x);
+    for (; t < tiles; t += nwaves) {
+        transpose32(x);
+        uint32_t xn[32];
+        const uint64_t tn = t + nwaves;
+        if (tn < tiles) ot_tile_issue(rows, W, tn, lane, xn);   // wave-uniform
+#pragma unroll 1
+        for (int r = 0; r < 4; r++) {
+            uint4 q[2];
+            ot_tile_round(stage[wv], x, lane, q);
+            uint4 m0[2], m1[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {   // the pass's messages, in flight during its AES
+                const uint64_t j = ot_tile_ot(t, lane, r, u);
+                const uint64_t jj = j < m ? j : 0;
+                m0[u] = a.x0[jj];
+                m1[u] = a.x1 ? a.x1[jj]
+                             : make_uint4(m0[u].x ^ a.delta[0], m0[u].y ^ a.delta[1], m0[u].z ^ a.delta[2],
+                                          m0[u].w ^ a.delta[3]);
+            }
+            uint32_t h[4][4];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                h[2 * u][0] = q[u].x; h[2 * u][1] = q[u].y; h[2 * u][2] = q[u].z; h[2 * u][3] = q[u].w;
+                h[2 * u + 1][0] = q[u].x ^ a.s[0]; h[2 * u + 1][1] = q[u].y ^ a.s[1];
+                h[2 * u + 1][2] = q[u].z ^ a.s[2]; h[2 * u + 1][3] = q[u].w ^ a.s[3];
+            }
+            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x, 2 OTs x 2 blocks
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint64_t j = ot_tile_ot(t, lane, r, u);
+                if (j >= m) continue;
+                a.Y0[j] = make_uint4(m0[u].x ^ h[2 * u][0], m0[u].y ^ h[2 * u][1], m0[u].z ^ h[2 * u][2],
+                                     m0[u].w ^ h[2 * u][3]);
+                a.Y1[j] = make_uint4(m1[u].x ^ h[2 * u + 1][0], m1[u].y ^ h[2 * u + 1][1], m1[u].z ^ h[2 * u + 1][2],
+                                     m1[u].w ^ h[2 * u + 1][3]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) x[i] = xn[i];
+    }
+}
+
 // Level-loop base OTs (ideal): the 128 seed pairs derived from (prf_seed, level, salt) on the
 // device, so an enqueued level needs no host data; key schedules [3][128][44] (k_i^0, k_i^1,
 // k_i^{s_i}). One thread per key.
@@ -375,15 +509,43 @@ static int ot_rows_grid(const OtArgs& a) {
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 
+// hash forms (A/B, process-wide, read once): FHH_OT_SEND_HASH / FHH_OT_RECV_HASH = 0 (r03: 1024
+// threads, 4 waves per SIMD), 512 or 768 (the prefetching forms)
+static int ot_hash_form(bool send) {
+    static std::atomic<int> form[2] = {-1, -1};
+    int f = form[send].load(std::memory_order_relaxed);
+    if (f < 0) {
+        const char* e = std::getenv(send ? "FHH_OT_SEND_HASH" : "FHH_OT_RECV_HASH");
+        f = e ? std::atoi(e) : 0;
+        if (f != 512 && f != 768) f = 0;
+        form[send].store(f, std::memory_order_relaxed);
+    }
+    return f;
+}
+
+static int ot_rows_grid_waves(const OtArgs& a, int waves) {
+    const uint64_t tiles = (a.m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t need = (tiles + waves - 1) / waves, cap = (uint64_t)device_cus();
+    return (int)(need < cap ? (need ? need : 1) : cap);
+}
+
 hipError_t launch_ot_send_hash_rows(const OtArgs& a, hipStream_t stream) {
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // tiles of 16 words stay inside a row
-    hipLaunchKernelGGL(k_ot_send_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    switch (ot_hash_form(true)) {
+        case 512: hipLaunchKernelGGL(k_ot_send_hash_pf<512>, dim3(ot_rows_grid_waves(a, 8)), dim3(512), 0, stream, a); break;
+        case 768: hipLaunchKernelGGL(k_ot_send_hash_pf<768>, dim3(ot_rows_grid_waves(a, 12)), dim3(768), 0, stream, a); break;
+        default: hipLaunchKernelGGL(k_ot_send_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_ot_recv_hash_rows(const OtArgs& a, hipStream_t stream) {
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ot_recv_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    switch (ot_hash_form(false)) {
+        case 512: hipLaunchKernelGGL(k_ot_recv_hash_pf<512>, dim3(ot_rows_grid_waves(a, 8)), dim3(512), 0, stream, a); break;
+        case 768: hipLaunchKernelGGL(k_ot_recv_hash_pf<768>, dim3(ot_rows_grid_waves(a, 12)), dim3(768), 0, stream, a); break;
+        default: hipLaunchKernelGGL(k_ot_recv_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

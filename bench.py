@@ -295,6 +295,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
                          reps, warm)
     hh = len(res.final)
     del c0, c1
+    print(f"dropin: fused protocol crawl {t_fused:.2f} s, {hh} heavy hitters", file=sys.stderr, flush=True)
 
     def dropin_leg(devices=None, channel="inplace"):
         p0, p1 = pair(devices)
@@ -306,6 +307,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
         t, r = timed(run, reps, warm)
         assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
         tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
+        print(f"dropin: leg devices={devices} channel={channel}: {t:.2f} s", file=sys.stderr, flush=True)
         return t, {k: v / L * 1e3 for k, v in tm.items()}, tot
 
     t_d, per_d, bytes_d = dropin_leg()

@@ -196,6 +196,8 @@ class FhhGcPartyCfg(ctypes.Structure):
         ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
         ("base_chosen", ctypes.c_uint8 * (2 * 128 * 16)),
         ("base_choice", ctypes.c_uint8 * (2 * 16)),
+        ("child_begin", ctypes.c_uint64),
+        ("child_count", ctypes.c_uint64),
     ]
 
 

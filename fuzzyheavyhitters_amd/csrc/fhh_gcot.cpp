@@ -372,6 +372,11 @@ struct PartyState {
     int role = -1;              // 0 garbler / OT sender (server 0), 1 evaluator / OT receiver (server 1)
     int step = 0;               // protocol position (calls must come in order)
     bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
+    // C = this instance's children: the chunk [c_off, c_off + C) of the level's level_C children
+    // (fhh_gc_party_cfg.child_begin / child_count); covered = children whose OTs are finished
+    uint64_t c_off = 0, level_C = 0, covered = 0;
+    uint32_t level_id = 0;
+    bool level_last = false;
     uint64_t C = 0, n = 0, npad = 0, nw = 0, tests = 0, m1 = 0, m2 = 0;
     uint32_t bits = 0, mask = 0, per2 = 1;
     uint32_t delta[4] = {0, 0, 0, 0};
@@ -385,7 +390,8 @@ struct PartyState {
     DevBuf T, U, Q, Y;          // OT matrices (T / Q private) and messages (U or Y0 | Y1)
     DevBuf choices2;            // evaluator: the GC outputs packed as OT 2's choice words
     DevBuf out;                 // evaluator: GC output bytes (eq ^ mask)
-    DevBuf recv;                // evaluator: OT 2 outputs = its node values
+    DevBuf recv;                // evaluator: OT 2 outputs of the chunk
+    DevBuf vals;                // the level's node values [level_C][n] (x per2 blocks), filled per chunk
     std::vector<uint32_t> rk_host;
     uint64_t bytes_sent = 0;    // this ctx's outgoing message bytes for the level
 };
@@ -402,7 +408,7 @@ PartyState& party_of(fhh_ctx* ctx) {
     return *ctx->party;
 }
 
-int party_begin(fhh_ctx* ctx, int role) {
+int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     if (ctx->group) return ctx->fail(FHH_E_ARG, "party: run the GC + OT per shard (fhh_shard_ctx)");
@@ -410,10 +416,25 @@ int party_begin(fhh_ctx* ctx, int role) {
         return ctx->fail(FHH_E_STATE, "party: needs a pending tree_crawl / tree_crawl_last");
     if (2 * ctx->d > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "party: d <= 4");
     PartyState& P = party_of(ctx);
+    const bool last = ctx->phase == Phase::kPendingLast;
+    // the chunk of children (collect.rs:423-430: a level's tests split over channels), in order
+    const uint64_t LC = ctx->pending_C, b = cfg->child_begin;
+    if (cfg->child_count == 0 && b != 0) return ctx->fail(FHH_E_ARG, "party: child_begin without child_count");
+    if (b > LC || (cfg->child_count && b == LC && LC))
+        return ctx->fail(FHH_E_ARG, "party: child_begin " + std::to_string(b) + " past the level's " +
+                                        std::to_string(LC) + " children");
+    if (b != 0 && (P.level_id != ctx->level || P.level_last != last || P.level_C != LC || P.covered != b))
+        return ctx->fail(FHH_E_STATE, "party: chunk at child " + std::to_string(b) + " does not follow the level's " +
+                                          "finished children (" + std::to_string(P.covered) + ")");
     P.role = role;
     P.step = 0;
-    P.last = ctx->phase == Phase::kPendingLast;
-    P.C = ctx->pending_C;
+    P.last = last;
+    P.level_id = ctx->level;
+    P.level_last = last;
+    P.level_C = LC;
+    if (b == 0) P.covered = 0;
+    P.c_off = b;
+    P.C = cfg->child_count ? std::min<uint64_t>(cfg->child_count, LC - b) : LC;
     P.n = ctx->n;
     P.npad = ctx->npad;
     P.nw = ctx->nw;
@@ -422,13 +443,28 @@ int party_begin(fhh_ctx* ctx, int role) {
     P.per2 = P.last ? 2 : 1;
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
     P.m2 = P.tests * P.per2;
-    P.bytes_sent = 0;
-    // this server's share planes [C][bits][nw] (collect.rs:393-418)
+    if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
+    // this server's share planes [C][bits][nw] of the chunk (collect.rs:393-418)
     HIP_TRY(ctx, P.planes.ensure(std::max<uint64_t>(P.C * P.bits * P.nw, 1) * 8));
     if (P.C) {
         ChildArgs a = ctx_child_args(ctx);
+        a.c_off = P.c_off;
+        a.c_cnt = P.C;
         HIP_TRY(ctx, launch_share_planes(a, P.planes.as<uint64_t>(), ctx->stream));
     }
+    // the level's node values, one row of n per child (a block, or a BlockPair at the last level)
+    if (b == 0) HIP_TRY(ctx, P.vals.ensure(std::max<uint64_t>(LC * P.n * P.per2, 1) * 16));
+    return FHH_OK;
+}
+
+// a finished chunk's node values into the level's rows [c_off, c_off + C) (the evaluator's OT 2
+// outputs, or the garbler's r1 = its message for the mask's other side, collect.rs:439-472)
+int party_chunk_done(fhh_ctx* ctx, PartyState& P, const void* chunk_vals) {
+    const uint64_t bytes = P.C * P.n * P.per2 * 16;
+    if (bytes)
+        HIP_TRY(ctx, hipMemcpyAsync(P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * 16, chunk_vals, bytes,
+                                    hipMemcpyDeviceToDevice, ctx->stream));
+    P.covered = P.c_off + P.C;
     return FHH_OK;
 }
 
@@ -503,7 +539,7 @@ extern "C" {
 int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes) {
     CTX_CHECK(ctx);
     if (!cfg || !gc_msg_dev || !gc_msg_bytes) return ctx->fail(FHH_E_ARG, "gb_garble: NULL argument");
-    int rc = party_begin(ctx, 0);
+    int rc = party_begin(ctx, 0, cfg);
     if (rc) return rc;
     PartyState& P = *ctx->party;
     P.mask = cfg->mask & 1u;
@@ -540,7 +576,9 @@ int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_
     HIP_TRY(ctx, P.x0.ensure(std::max<uint64_t>(P.m2, 1) * 16));
     HIP_TRY(ctx, P.x1.ensure(std::max<uint64_t>(P.m2, 1) * 16));
     if (P.tests) {
-        ChildArgs a = ctx_child_args(ctx);
+        ChildArgs a = ctx_child_args(ctx);   // the chunk's children
+        a.c_off = P.c_off;
+        a.c_cnt = P.C;
         a.prf_seed = cfg->share_seed;
         a.gc_N = (uint32_t)P.n;
         if (P.last) HIP_TRY(ctx, launch_ot_fe255_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
@@ -600,6 +638,10 @@ static int gb_ot_send(fhh_ctx* ctx, int which, const uint8_t* u_dev, uint64_t u_
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
         HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // Y0, Y1
     }
+    if (which) {   // the chunk is done on this side: its node values r1 into the level's rows
+        rc = party_chunk_done(ctx, P, P.mask ? P.x1.p : P.x0.p);
+        if (rc) return rc;
+    }
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 2 + which;
@@ -620,7 +662,7 @@ int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const u
 int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** u_dev, uint64_t* u_len) {
     CTX_CHECK(ctx);
     if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
-    int rc = party_begin(ctx, 1);
+    int rc = party_begin(ctx, 1, cfg);
     if (rc) return rc;
     PartyState& P = *ctx->party;
     // OT 1's receiver: choice bits = this server's share planes as they stand (m1 = C bits npad)
@@ -727,6 +769,8 @@ int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_len) {
         a.out = P.recv.as<uint4>();
         HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     }
+    rc = party_chunk_done(ctx, P, P.recv.p);   // the OT outputs are this server's node values
+    if (rc) return rc;
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 3;
@@ -750,22 +794,25 @@ int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
             if (rc) return rc;
             if (!nk) continue;
             PartyState* P = sh->party;
-            if (!P || P->step != 3) return ctx->fail(FHH_E_STATE, "party_node_sums: shard " + std::to_string(k) +
-                                                                  "'s OTs are not finished");
+            if (!P || P->step != 3 || P->covered != P->level_C)
+                return ctx->fail(FHH_E_STATE, "party_node_sums: shard " + std::to_string(k) +
+                                                  "'s OTs are not finished for every child of the level");
             if (last >= 0 && last != (int)P->last) return ctx->fail(FHH_E_STATE, "party_node_sums: shards disagree");
             last = P->last;
-            v[(size_t)k] = P->role == 0 ? (P->mask ? P->x1.p : P->x0.p) : P->recv.p;
+            v[(size_t)k] = P->vals.p;
         }
         if (last < 0) return ctx->fail(FHH_E_STATE, "party_node_sums: no shard holds clients");
         const uint32_t fmt = last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
         return group_node_sums(ctx, v.data(), false, 0, fmt, sums_a, sums_b);   // ld 0: each shard's n
     }
     PartyState* Pp = ctx->party;
-    if (!Pp || Pp->step != 3) return ctx->fail(FHH_E_STATE, "party_node_sums: the level's OTs are not finished");
+    if (!Pp || Pp->step != 3 || Pp->covered != Pp->level_C)
+        return ctx->fail(FHH_E_STATE, "party_node_sums: the level's OTs are not finished for every child");
     PartyState& P = *Pp;
-    // the garbler's value is r1 = its message for the mask's other side, the evaluator's its OT output;
-    // rows of n values, FE in a block's low 8 bytes, FieldElm as a BlockPair (2 blocks)
-    const void* v = P.role == 0 ? (P.mask ? P.x1.p : P.x0.p) : P.recv.p;
+    // the garbler's value is r1 = its message for the mask's other side, the evaluator's its OT output
+    // (gathered per chunk into P.vals); rows of n values, FE in a block's low 8 bytes, FieldElm as a
+    // BlockPair (2 blocks)
+    const void* v = P.vals.p;
     const uint32_t fmt = P.last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
     const void* vv[1] = {v};
     if (P.last) return fhh_node_sums_fe255_device(ctx, vv, P.n, fmt, static_cast<uint32_t*>(sums_a), static_cast<uint32_t*>(sums_b));

@@ -610,10 +610,11 @@ hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t str
     return hipGetLastError();
 }
 
-// out [C][2d][nw]: left dims then right dims, E = y ^ t (collect.rs:399-405)
+// out [C][2d][nw]: left dims then right dims, E = y ^ t (collect.rs:399-405); with a child window
+// (c_cnt > 0) only children [c_off, c_off + c_cnt), at rows c - c_off
 __global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, uint64_t* out) {
-    const uint64_t C_ = child_count(a);
-    for (uint64_t c = blockIdx.x; c < C_; c += gridDim.x) {
+    const uint64_t C_ = child_end(a);
+    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
         for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) {
@@ -623,7 +624,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, ui
                 for (int j = 0; j < kMaxDims; j++)
                     if (j < (int)a.d) {
                         const size_t idx = ((size_t)e[j] * 2 + s) * a.nw + w;
-                        out[((size_t)c * 2 * a.d + (size_t)s * a.d + j) * a.nw + w] =
+                        out[((size_t)(c - a.c_off) * 2 * a.d + (size_t)s * a.d + j) * a.nw + w] =
                             (a.s0.t[j][idx] ^ a.s0.y[j][idx]) & a.valid[w];
                     }
         }
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, ui
 
 hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_share_planes, dim3(child_grid(a.C)), dim3(kReduceThreads), 0, stream, a, out);
+    hipLaunchKernelGGL(k_share_planes, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, out);
     return hipGetLastError();
 }
 

@@ -143,9 +143,26 @@ __device__ __forceinline__ uint64_t fe_red128(unsigned __int128 v) {
     return r;
 }
 
-// sketch_draw with the three inner-product terms accumulated unreduced: a pass adds at most 4
-// products (< 2^124 each, canonical x and a 62-bit draw) to an accumulator that starts below
-// 2^62, so one fe_red128 per accumulator per pass replaces a reduction per product
+// v^2 mod p for v < 2^62 (a masked draw): after the two folds r < 1.5 * 2^62 + 2^31, so one
+// conditional subtraction makes it canonical (fe_mulc's second one is for operands up to 2^63)
+__device__ __forceinline__ uint64_t fe_sqr62(uint64_t v) {
+    const unsigned __int128 w = (unsigned __int128)v * v;
+    const uint64_t mask = (1ull << 62) - 1;
+    const unsigned __int128 h = w >> 62;
+    const unsigned __int128 t = (w & mask) + h + (h << 30);
+    const uint64_t h2 = (uint64_t)(t >> 62);
+    const uint64_t r = ((uint64_t)t & mask) + h2 + (h2 << 30);
+    return r >= kFeP_ ? r - kFeP_ : r;
+}
+
+// sketch_draw with the three inner-product terms accumulated unreduced, one fe_red128 per
+// accumulator per pass instead of a reduction per product. CANON = false (the fused kernel, at
+// most 4 products per accumulator per pass) multiplies the stored x / kx words as they are: x = x'
+// (mod p) gives the same sum mod p, and 4 products of a u64 word and a value below 2^62 (the draw,
+// or its canonical square) plus an accumulator below 2^62 stay below 2^128:
+// 4 (2^64 - 1)(2^62 - 1) + 2^62 = 2^128 - 2^66 - 2^64 + 2^62 + 4. CANON = true reduces x and kx
+// first (products below 2^124: room for the producer / consumer form's 6 per phase).
+template <bool CANON = true>
 __device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint64_t xv, uint64_t kxv, uint64_t F,
                                                  int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1,
                                                  unsigned __int128& ax, unsigned __int128& a2x,
@@ -157,11 +174,14 @@ __device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint6
     rej |= live && v >= kFeP_;
     rnd0 = (is_rand && h == 0) ? v : rnd0;
     rnd1 = (is_rand && h == 1) ? v : rnd1;
-    const uint64_t r2 = fe_mulc(v, v);
-    xv = fe_canon_dev(xv);
+    const uint64_t r2 = fe_sqr62(v);
+    if constexpr (CANON) {
+        xv = fe_canon_dev(xv);
+        kxv = fe_canon_dev(kxv);
+    }
     ax += (unsigned __int128)xv * v;
     a2x += (unsigned __int128)xv * r2;
-    akx += (unsigned __int128)fe_canon_dev(kxv) * v;
+    akx += (unsigned __int128)kxv * v;
 }
 
 __device__ __forceinline__ uint64_t wave_fe_sum(uint64_t v) {
@@ -317,8 +337,8 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         if constexpr (OTF)
-                            sketch_draw_lazy(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0,
-                                             rnd1, ax, a2x, akx);
+                            sketch_draw_lazy<(2 * NBP > 4)>(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F,
+                                                            h, rej, rnd0, rnd1, ax, a2x, akx);
                         else
                             sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
                                         rx, r2x, rkx);
@@ -524,7 +544,8 @@ __global__ __launch_bounds__(kPcThreads) void k_sketch_fe_pc(SketchArgs a) {
                     const uint64_t dr[2] = {(uint64_t)s.x | ((uint64_t)s.y << 32), (uint64_t)s.z | ((uint64_t)s.w << 32)};
 #pragma unroll
                     for (int h = 0; h < 2; h++)   // positions past the stream carry x = kx = 0: no-ops
-                        sketch_draw_lazy(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
+                        sketch_draw_lazy<(2 * PCB > 4)>(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h,
+                                                        rej, rnd0, rnd1,
                                          ax, a2x, akx);
                 }
                 ax = fe_red128(ax);

@@ -114,9 +114,22 @@ class TwoPartyResult:
     final: list = field(default_factory=list)            # Result(path, value): final_values
 
 
+# bytes per test of both parties' chunk buffers at d = 1 (gc message 81, labels 32 + 32, OT matrices
+# and messages 160, OT 2 messages / outputs 48, with headroom): the auto chunk size's divisor
+_PARTY_BYTES_PER_TEST = 512
+
+
+def chunk_windows(C: int, chunk_children: int):
+    """[(begin, count)] covering [0, C) in chunks of chunk_children (0: one window, the whole level)."""
+    if chunk_children <= 0 or C <= chunk_children:
+        return [(0, 0)]
+    return [(b, min(chunk_children, C - b)) for b in range(0, C, chunk_children)]
+
+
 def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
                     prf_seed: int = 0, levels: int = 0, cfg_fn=None, expect_counts=None,
-                    channel: str = "copy", timing: dict | None = None, record: bool = True) -> TwoPartyResult:
+                    channel: str = "copy", timing: dict | None = None, record: bool = True,
+                    chunk_children: int | None = None, chunk_bytes: int = 64 << 30) -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between
     the two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both,
     run the level's protocol through the channel, take each server's node sums from its own
@@ -129,12 +142,21 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     buffer; both shards of a pair must share a GPU). `timing` (a dict) accumulates the host wall
     seconds of each phase of the level loop: crawl, gcot, node_sums, keep, prune (every call returns
     after its device work, so these are the phases' elapsed times). record=False skips the per-level
-    v0 - v1 records (res.counts) the timed bench does not need."""
+    v0 - v1 records (res.counts) the timed bench does not need. A level's tests run in chunks of
+    `chunk_children` children (None: as many as `chunk_bytes` of both parties' buffers hold at
+    ~512 B per test; 0: the whole level), one protocol instance per chunk (fhh_gc_party_cfg
+    child_begin / child_count; the default material varies per chunk, a custom cfg_fn's does not),
+    and the node sums follow the level's last chunk."""
     L = levels or c0.depth
     n_total = nclients_total if nclients_total is not None else c0.num_clients()
     thr = max(1, int(threshold * n_total))
     thr_last = max(1, min(int(threshold * n_total), 0xFFFFFFFF))
-    cfg_fn = cfg_fn or (lambda lv, k=0: level_cfg(prf_seed ^ (k << 40), lv))
+    user_cfg = cfg_fn
+
+    def chunk_cfg(lv, k, j, S):
+        if user_cfg is None:
+            return level_cfg(prf_seed ^ (k << 40) ^ (j << 48), lv)
+        return user_cfg(lv) if S == 1 else user_cfg(lv, k)
     # a multi-device collection runs each shard's protocol over its own channel (the reference
     # splits a level's tests over several channels, collect.rs:423-430)
     S = len(c0.shard_info()[0])
@@ -151,6 +173,8 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
         tm.setdefault(k, 0.0)
     clock = time.perf_counter
     shard_clients = [a.num_clients() for a, _ in shards]
+    if chunk_children is None:
+        chunk_children = max(1, chunk_bytes // (_PARTY_BYTES_PER_TEST * max(1, max(shard_clients))))
     for lv in range(L):
         last = lv == L - 1
         t0 = clock()
@@ -162,9 +186,11 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
         for k, ((a, b), (to_gb, to_ev)) in enumerate(zip(shards, chans)):
             if shard_clients[k] == 0:
                 continue
-            cfg = cfg_fn(lv) if S == 1 else cfg_fn(lv, k)
-            for name, v in run_level(a, b, cfg, cfg, to_gb, to_ev).items():
-                sizes[name] = sizes.get(name, 0) + v
+            for j, (cb, cc) in enumerate(chunk_windows(C0, chunk_children)):
+                cfg = chunk_cfg(lv, k, j, S)
+                cfg.child_begin, cfg.child_count = cb, cc
+                for name, v in run_level(a, b, cfg, cfg, to_gb, to_ev).items():
+                    sizes[name] = sizes.get(name, 0) + v
         res.level_bytes.append(sizes)
         t2 = clock()
         s0 = party_sums(c0, C0, last)
@@ -201,4 +227,4 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     return res
 
 
-__all__ = ["Channel", "level_cfg", "run_level", "party_sums", "two_party_crawl", "TwoPartyResult"]
+__all__ = ["Channel", "level_cfg", "run_level", "party_sums", "two_party_crawl", "TwoPartyResult", "chunk_windows"]

@@ -512,7 +512,14 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
  * evaluator's the OT output (collect.rs:439-472); fhh_party_node_sums sums them on the device:
  * non-last level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm
  * (the frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own
- * channel, as the reference runs a level's tests over several channels (collect.rs:423-430). */
+ * channel, as the reference runs a level's tests over several channels (collect.rs:423-430).
+ * Chunks of children: a cfg with child_count > 0 runs the protocol for children [child_begin,
+ * child_begin + child_count) only (C above = the chunk's children, tests child-major within it) —
+ * one protocol instance per chunk, as the reference's channels each run a slice of the level's
+ * tests (collect.rs:423-430); this bounds the level's buffers (~400 B per test for both parties at
+ * d = 1) at 1M clients. Chunks run in order, each the full five-message sequence, and together
+ * cover [0, C); fhh_party_node_sums follows the last one and sums the whole level. Both parties
+ * must use the same window. child_count = 0: the whole level in one instance. */
 typedef struct fhh_gc_party_cfg {
     /* garbler only (fresh per level: AesRng::new(), collect.rs:432) */
     uint8_t label_key[16];               /* label PRG key                                          */
@@ -526,6 +533,9 @@ typedef struct fhh_gc_party_cfg {
     uint8_t base_pairs[2][128][2][16];   /* evaluator                                              */
     uint8_t base_chosen[2][128][16];     /* garbler: base_pairs[t][i][s_i]                         */
     uint8_t base_choice[2][16];          /* garbler: s (bit i % 8 of byte i / 8)                   */
+    /* both parties: the chunk of the level's children this instance covers (0 / 0 = all) */
+    uint64_t child_begin;
+    uint64_t child_count;
 } fhh_gc_party_cfg;
 int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes);
 int fhh_gb_ot_labels(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);

@@ -126,3 +126,49 @@ def test_two_party_configs1_full_size():
     tot = {k: sum(lb[k] for lb in got.level_bytes) for k in got.level_bytes[0]}
     print("configs[1] two-party channel bytes per crawl:", tot, "max per level:",
           max(sum(lb.values()) for lb in got.level_bytes))
+
+
+@pytest.mark.parametrize("chunk,devices", [(1, None), (3, None), (2, [0, 0])], ids=["1-child", "3-children", "2-shards"])
+def test_two_party_chunked_children(chunk, devices):
+    """A level's tests in chunks of children, one protocol instance per chunk (fhh_gc_party_cfg
+    child_begin / child_count; the reference splits a level's tests over its channels,
+    collect.rs:423-430), each chunk with its own label key, Delta, mask and base OTs: the leader's
+    v0 - v1 per child and the heavy hitters equal the in-process crawl's (the node sums follow the
+    level's last chunk)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    n, L = 64 * 4 + 9, 24
+    wl = workload.zipf_workload(n, 32, 1, num_sites=6, seed=41)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    c0, c1 = _keys(wl, L, 1)
+    ref = fhh.sim_crawl(c0, c1, 0.02, mode="fe", prf_seed=9, gc="ot")
+    p0, p1 = _keys(wl, L, 1, devices=devices)
+    got = fhh.two_party_crawl(p0, p1, 0.02, prf_seed=9, channel="inplace", chunk_children=chunk)
+    _assert_same_crawl(ref, got)
+    assert max(ref.level_children) > chunk   # some level really ran in several chunks
+
+
+def test_party_chunks_out_of_order_refused():
+    """Chunks run in order and cover the level before the node sums (FHH_E_STATE)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import party, workload
+    from fuzzyheavyhitters_amd._lib import lib
+    wl = workload.zipf_workload(100, 32, 1, num_sites=3, seed=1)
+    c0, c1 = _keys(wl, 32, 1)
+    c0.tree_init()
+    c1.tree_init()
+    C, _ = c0.tree_crawl()
+    c1.tree_crawl()
+    assert C == 2
+    out, nb = ctypes.c_void_p(), ctypes.c_uint64()
+    cfg = party.level_cfg(1, 0)
+    cfg.child_begin, cfg.child_count = 1, 1       # the level's first chunk must start at child 0
+    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == -2
+    cfg.child_begin, cfg.child_count = 0, 1
+    to_gb, to_ev = party.Channel(0, "inplace"), party.Channel(0, "inplace")
+    party.run_level(c0, c1, cfg, cfg, to_gb, to_ev)   # child 0 only
+    sums = np.zeros(2, np.uint64)
+    assert lib().fhh_party_node_sums(c0.handle, sums.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), None) == -2
+    cfg.child_begin = 1
+    party.run_level(c0, c1, cfg, cfg, to_gb, to_ev)   # child 1: the level is covered
+    assert lib().fhh_party_node_sums(c0.handle, sums.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), None) == 0

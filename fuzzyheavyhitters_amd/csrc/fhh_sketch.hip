@@ -15,6 +15,7 @@
 #include "fhh_internal.h"
 
 #include <atomic>
+#include <type_traits>
 #include "expand_kernel.h"
 #include "aes_tables.h"
 #include "field_arith.h"
@@ -155,13 +156,26 @@ __device__ __forceinline__ uint64_t fe_sqr62(uint64_t v) {
     return r >= kFeP_ ? r - kFeP_ : r;
 }
 
+// w mod p up to a multiple of p for w < 2^126: two folds of 2^62 = 2^30 + 1 leave
+// r < 2^62 + 2^33 + 2^63 < 2^64, no subtraction (the caller only multiplies or adds it)
+__device__ __forceinline__ uint64_t fe_fold126(unsigned __int128 w) {
+    const uint64_t mask = (1ull << 62) - 1;
+    const unsigned __int128 h = w >> 62;
+    const unsigned __int128 t = (w & mask) + h + (h << 30);
+    const uint64_t h2 = (uint64_t)(t >> 62);
+    return ((uint64_t)t & mask) + h2 + (h2 << 30);
+}
+
 // sketch_draw with the three inner-product terms accumulated unreduced, one fe_red128 per
-// accumulator per pass instead of a reduction per product. CANON = false (the fused kernel, at
-// most 4 products per accumulator per pass) multiplies the stored x / kx words as they are: x = x'
-// (mod p) gives the same sum mod p, and 4 products of a u64 word and a value below 2^62 (the draw,
-// or its canonical square) plus an accumulator below 2^62 stay below 2^128:
-// 4 (2^64 - 1)(2^62 - 1) + 2^62 = 2^128 - 2^66 - 2^64 + 2^62 + 4. CANON = true reduces x and kx
-// first (products below 2^124: room for the producer / consumer form's 6 per phase).
+// accumulator per pass instead of a reduction per product.
+// CANON = false (the fused kernel, at most 4 draws per pass) multiplies the stored x / kx words as
+// they are (x = x' mod p gives the same sums mod p) and forms x r^2 as (x r) r: t = fold(x r) < 2^64
+// is added to <r, x> and multiplied by r for <r^2, x> — 12 instead of 15 32-bit partial products
+// per draw, no squaring. Every accumulator takes at most 4 products of a u64 word and a draw below
+// 2^62 (plus a start below 2^62), so it stays below 2^128:
+// 4 (2^64 - 1)(2^62 - 1) + 2^62 = 2^128 - 2^66 - 2^64 + 2^62 + 4.
+// CANON = true (the producer / consumer form, 6 draws per phase) reduces x and kx first and squares
+// the draw (products below 2^124).
 template <bool CANON = true>
 __device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint64_t xv, uint64_t kxv, uint64_t F,
                                                  int h, bool& rej, uint64_t& rnd0, uint64_t& rnd1,
@@ -174,13 +188,17 @@ __device__ __forceinline__ void sketch_draw_lazy(uint64_t pos, uint64_t v, uint6
     rej |= live && v >= kFeP_;
     rnd0 = (is_rand && h == 0) ? v : rnd0;
     rnd1 = (is_rand && h == 1) ? v : rnd1;
-    const uint64_t r2 = fe_sqr62(v);
     if constexpr (CANON) {
+        const uint64_t r2 = fe_sqr62(v);
         xv = fe_canon_dev(xv);
         kxv = fe_canon_dev(kxv);
+        ax += (unsigned __int128)xv * v;
+        a2x += (unsigned __int128)xv * r2;
+    } else {
+        const uint64_t t = fe_fold126((unsigned __int128)xv * v);   // x r (mod p), < 2^64
+        ax += t;
+        a2x += (unsigned __int128)t * v;                            // x r^2 (mod p)
     }
-    ax += (unsigned __int128)xv * v;
-    a2x += (unsigned __int128)xv * r2;
     akx += (unsigned __int128)kxv * v;
 }
 
@@ -290,65 +308,74 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
         const uint64_t* kx = a.kx + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
         bool rej = false;
-        if (!a.force_sequential) {
-            for (uint64_t bb = sl; bb < nb; bb += NBP * LPK) {
-                // the pass's (x, kx) loads go ahead of the AES at 2 blocks per pass; at 4 their 32
-                // registers would be live across it, so they follow it (other waves hide the latency)
-                uint64_t xv[2 * NBP] = {}, kxv[2 * NBP] = {};
-                auto load_xkx = [&]() {
+        // one pass: NB keystream blocks per lane (bb, bb + LPK, ...) and their draws' products
+        auto pass = [&](uint64_t bb, auto nbc) {
+            constexpr int NB = decltype(nbc)::value;
+            // the pass's (x, kx) loads go ahead of the AES at 2 blocks per pass; at 4 their 32
+            // registers would be live across it, so they follow it (other waves hide the latency)
+            uint64_t xv[2 * NB] = {}, kxv[2 * NB] = {};
+            auto load_xkx = [&]() {
 #pragma unroll
-                    for (int q = 0; q < NBP; q++)
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const uint64_t pos = 2 * (bb + LPK * q) + h;
-                            if (pos >= 3 && pos < F + 3) {
-                                xv[2 * q + h] = x[pos - 3];
-                                kxv[2 * q + h] = kx[pos - 3];
-                            }
-                        }
-                };
-                if constexpr (NBP <= 2) load_xkx();
-                uint32_t st[NBP][4];
-#pragma unroll
-                for (int q = 0; q < NBP; q++) {
-                    const uint64_t b = bb + LPK * q;
-                    st[q][0] = 0u;
-                    st[q][1] = 0u;
-                    st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
-                    st[q][3] = __builtin_bswap32((uint32_t)b);
-                }
-                if constexpr (SCHED == 2) {
-                    // the pass's counters differ only in byte 15 (the low byte of the big-endian
-                    // block index) unless a lane's blocks straddle a multiple of 256: then rounds 1-2
-                    // of the second block reuse the first's terms (aes_ctr_shared, 293 vs 320 lookups)
-                    const bool same_hi = (bb >> 8) == ((bb + LPK * (NBP - 1)) >> 8);
-                    if (__ballot(!same_hi) == 0) aes_lds_rk_ctr<Tab, NBP, 3, 3>(st, tbl, b0, b1, rkl);
-                    else aes_lds_rk<Tab, NBP>(st, tbl, b0, b1, rkl);
-                } else if constexpr (OTF) aes_otf<Tab, NBP>(st, tbl, b0, b1, seed);
-                else aes_rk<Tab, NBP>(st, tbl, b0, b1, rk);
-                if constexpr (NBP > 2) load_xkx();
-                unsigned __int128 ax = rx, a2x = r2x, akx = rkx;
-#pragma unroll
-                for (int q = 0; q < NBP; q++) {
-                    const uint64_t b = bb + LPK * q;
-                    if (!OTF && b >= nb) break;   // OTF: positions past the stream are no-ops
-                    const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
-                                            (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
+                for (int q = 0; q < NB; q++)
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        if constexpr (OTF)
-                            sketch_draw_lazy<(2 * NBP > 4)>(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F,
-                                                            h, rej, rnd0, rnd1, ax, a2x, akx);
-                        else
-                            sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
-                                        rx, r2x, rkx);
+                        const uint64_t pos = 2 * (bb + LPK * q) + h;
+                        if (pos >= 3 && pos < F + 3) {
+                            xv[2 * q + h] = x[pos - 3];
+                            kxv[2 * q + h] = kx[pos - 3];
+                        }
                     }
+            };
+            if constexpr (NB <= 2) load_xkx();
+            uint32_t st[NB][4];
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                const uint64_t b = bb + LPK * q;
+                st[q][0] = 0u;
+                st[q][1] = 0u;
+                st[q][2] = __builtin_bswap32((uint32_t)(b >> 32));
+                st[q][3] = __builtin_bswap32((uint32_t)b);
+            }
+            if constexpr (SCHED == 2) {
+                // the pass's counters differ only in byte 15 (the low byte of the big-endian
+                // block index) unless a lane's blocks straddle a multiple of 256: then rounds 1-2
+                // of the second block reuse the first's terms (aes_ctr_shared, 293 vs 320 lookups)
+                const bool same_hi = (bb >> 8) == ((bb + LPK * (NB - 1)) >> 8);
+                if (NB == 1 || __ballot(!same_hi) == 0) aes_lds_rk_ctr<Tab, NB, 3, 3>(st, tbl, b0, b1, rkl);
+                else aes_lds_rk<Tab, NB>(st, tbl, b0, b1, rkl);
+            } else if constexpr (OTF) aes_otf<Tab, NB>(st, tbl, b0, b1, seed);
+            else aes_rk<Tab, NB>(st, tbl, b0, b1, rk);
+            if constexpr (NB > 2) load_xkx();
+            unsigned __int128 ax = rx, a2x = r2x, akx = rkx;
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                const uint64_t b = bb + LPK * q;
+                if (!OTF && b >= nb) break;   // OTF: positions past the stream are no-ops
+                const uint64_t dr[2] = {(uint64_t)st[q][0] | ((uint64_t)st[q][1] << 32),
+                                        (uint64_t)st[q][2] | ((uint64_t)st[q][3] << 32)};
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    if constexpr (OTF)
+                        sketch_draw_lazy<(2 * NB > 4)>(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h,
+                                                       rej, rnd0, rnd1, ax, a2x, akx);
+                    else
+                        sketch_draw(2 * b + h, dr[h] & mask, xv[2 * q + h], kxv[2 * q + h], F, h, rej, rnd0, rnd1,
+                                    rx, r2x, rkx);
                 }
-                if constexpr (OTF) {
-                    rx = fe_red128(ax);
-                    r2x = fe_red128(a2x);
-                    rkx = fe_red128(akx);
-                }
+            }
+            if constexpr (OTF) {
+                rx = fe_red128(ax);
+                r2x = fe_red128(a2x);
+                rkx = fe_red128(akx);
+            }
+        };
+        if (!a.force_sequential) {
+            for (uint64_t bb = sl; bb < nb; bb += NBP * LPK) {
+                // a pass whose blocks past the first are beyond the stream on every lane (the last
+                // pass of a 130-block key at LPK 8: blocks 128, 129) runs one block per lane: about
+                // half the AES and products of a full pass (OTF: past-the-stream positions are no-ops)
+                if (OTF && NBP > 1 && __ballot(bb + LPK < nb) == 0) pass(bb, std::integral_constant<int, 1>{});
+                else pass(bb, std::integral_constant<int, NBP>{});
             }
         }
         // per-key rejection flag over the key's segment

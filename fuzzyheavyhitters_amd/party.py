@@ -129,7 +129,8 @@ def chunk_windows(C: int, chunk_children: int):
 def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_total: int | None = None,
                     prf_seed: int = 0, levels: int = 0, cfg_fn=None, expect_counts=None,
                     channel: str = "copy", timing: dict | None = None, record: bool = True,
-                    chunk_children: int | None = None, chunk_bytes: int = 64 << 30) -> TwoPartyResult:
+                    chunk_children: int | None = None, chunk_bytes: int = 64 << 30,
+                    level_log: list | None = None) -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between
     the two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both,
     run the level's protocol through the channel, take each server's node sums from its own
@@ -146,7 +147,8 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     `chunk_children` children (None: as many as `chunk_bytes` of both parties' buffers hold at
     ~512 B per test; 0: the whole level), one protocol instance per chunk (fhh_gc_party_cfg
     child_begin / child_count; the default material varies per chunk, a custom cfg_fn's does not),
-    and the node sums follow the level's last chunk."""
+    and the node sums follow the level's last chunk. `level_log` (a list) receives one
+    (level, children, crawl_s, gcot_s, node_sums_s) tuple per level."""
     L = levels or c0.depth
     n_total = nclients_total if nclients_total is not None else c0.num_clients()
     thr = max(1, int(threshold * n_total))
@@ -213,6 +215,8 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
         tm["node_sums"] += t3 - t2
         tm["keep"] += t4 - t3
         tm["prune"] += t5 - t4
+        if level_log is not None:
+            level_log.append((lv, int(C0), t1 - t0, t2 - t1, t3 - t2))
         if not (record or expect_counts is not None):
             continue
         if not last:

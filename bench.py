@@ -268,7 +268,9 @@ def dropin_bench(args, world, rank, local_rank, dist):
 
     def timed(fn, reps, warm=1):
         for _ in range(warm):
+            t0 = time.perf_counter()
             fn()
+            print(f"dropin:   warm-up run {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
         best, out = None, None
         for _ in range(reps):
             torch.cuda.synchronize()
@@ -276,6 +278,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
             out = fn()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            print(f"dropin:   timed run {dt:.2f} s", file=sys.stderr, flush=True)
             best = dt if best is None else min(best, dt)
         return best, out
 

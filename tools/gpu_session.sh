@@ -11,7 +11,7 @@
 #   gcot1m       bench.py --gc ot --base-ot at the metric's 1M clients (kernel stats)  -> gcot1m_*
 #   sketch       bench.py --workload sketch (configs[4]) under rocprofv3 --stats        -> sketch_*
 #   dropin       bench.py --workload dropin --clients 100000 (configs[1])              -> dropin.json
-#   dropin1m     the same at the metric's 1M clients (chunked party protocol), one rep  -> dropin1m.json
+#   dropin1m     the same at the metric's 1M clients (chunked party protocol), 1 warm-up + 1 timed rep  -> dropin1m.json
 #   workloads    configs[1], configs[3], bincode, gc one-level lines                   -> wl_*.json
 set -u
 O=${1:?outdir}; shift
@@ -36,7 +36,7 @@ for s in "$@"; do
     gcot1m) step gcot1m stats_of gcot1m 400 --gc ot --base-ot --steps 1 --warmup 0 --no-cpu-baseline ;;
     sketch) step sketch stats_of sketch 300 --workload sketch --steps 3 --warmup 1 ;;
     dropin) step dropin bash -c "timeout -k 10 600 python3 bench.py --workload dropin --clients 100000 --steps 2 --warmup 1 > $O/dropin.json 2> $O/dropin.err" ;;
-    dropin1m) step dropin1m bash -c "timeout -k 10 900 python3 -u bench.py --workload dropin --clients 1000000 --steps 1 --warmup 0 > $O/dropin1m.json 2> $O/dropin1m.err" ;;
+    dropin1m) step dropin1m bash -c "timeout -k 10 1000 python3 -u bench.py --workload dropin --clients 1000000 --steps 1 --warmup 1 > $O/dropin1m.json 2> $O/dropin1m.err" ;;
     workloads)
       step configs1 bash -c "timeout -k 10 300 python3 bench.py --clients 100000 --steps 5 --warmup 1 --no-cpu-baseline > $O/wl_configs1.json 2> $O/wl_configs1.err"
       step configs3 bash -c "timeout -k 10 300 python3 bench.py --workload coords --steps 5 --warmup 1 --no-cpu-baseline > $O/wl_configs3.json 2> $O/wl_configs3.err"

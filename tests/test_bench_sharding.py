@@ -71,11 +71,11 @@ def test_two_rank_plan_and_aggregation():
     assert elapsed == 1.5 and blocks == 30
 
 
-def _bench_line(cmd):
+def _bench_line(cmd, timeout=240):
     import json
     import subprocess
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -99,6 +99,30 @@ def test_bench_two_rank_rehearsal_equals_one_rank():
     for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
         assert two[k] == one[k], k
     assert two["config"]["clients_total"] == one["config"]["clients_total"] == 20000
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_configs2_eight_rank_rehearsal_equals_golden():
+    """configs[2] — the metric's 1M Zipf clients sharded over 8 ranks — through bench.py's own N = 8
+    path on one GPU (--rehearse: 8 torchrun ranks share the device, the per-level all-reduce of the
+    partials through the hosted communicator): the sharded crawl recovers the north star's output
+    exactly as the committed 1M golden fixture holds it (tests/golden/zipf_1m_L512.npz: 101 998
+    children over the 512 levels, 206 heavy hitters), and the line aggregates the 8 ranks. Only
+    RCCL's xGMI transport differs on an 8-GPU node."""
+    import random
+    import sys as _sys
+    g = np.load(os.path.join(ROOT, "tests", "golden", "zipf_1m_L512.npz"), allow_pickle=False)
+    port = str(29000 + random.randrange(300))
+    line = _bench_line([_sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "8", "--rehearse",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-protocol-crawl"], timeout=540)
+    assert line["n_gpus"] == 8 and line["config"]["collective"]["comm_ranks"] == 8
+    assert line["config"]["clients_total"] == 1_000_000 and line["config"]["clients_per_gpu"] == 125_000
+    assert line["levels"] == 512
+    assert line["children_total"] == int(g["level_children"].sum()) == 101_998
+    assert line["final_heavy_hitters"] == len(g["paths"]) == 206
+    assert line["aes_blocks_per_step"] == 101_998 * 1_000_000 * 4   # children x clients x 2 sides x 2 servers
 
 
 @pytest.mark.gpu

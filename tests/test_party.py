@@ -108,10 +108,13 @@ def test_party_calls_out_of_order_refused():
     assert b"expected" in lib().fhh_last_error(c0.handle)
 
 
-def test_two_party_configs1_full_size():
+@pytest.mark.parametrize("chunk", [None, 150], ids=["whole-levels", "chunks-of-150"])
+def test_two_party_configs1_full_size(chunk):
     """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): the split
     GC + OT crawl equals the in-process GC + OT crawl level by level, and both equal the plaintext
-    recount (222 heavy hitters). Prints the bytes that would cross the channel."""
+    recount (222 heavy hitters) — with each level's tests in one protocol instance, and (r04) in
+    chunks of 150 children, one instance per chunk (the 1M configuration's shape). Prints the bytes
+    that would cross the channel."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
     n, L = 100_000, 512
@@ -120,9 +123,12 @@ def test_two_party_configs1_full_size():
     ref = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=7, gc="ot")
     del c0, c1
     p0, p1 = _keys(wl, L, 1)
-    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7, expect_counts=ref.counts)
+    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7, expect_counts=ref.counts,
+                              chunk_children=chunk, channel="inplace" if chunk else "copy")
     _assert_same_crawl(ref, got)
     assert len(got.final) == 222
+    if chunk:
+        assert max(got.level_children) > chunk
     tot = {k: sum(lb[k] for lb in got.level_bytes) for k in got.level_bytes[0]}
     print("configs[1] two-party channel bytes per crawl:", tot, "max per level:",
           max(sum(lb.values()) for lb in got.level_bytes))

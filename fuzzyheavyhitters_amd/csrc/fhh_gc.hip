@@ -110,6 +110,10 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; c++) lrk[r][c] = a.rk_label[r][c];
     constexpr int W = 2 * B + 1;
+    // label counter stride: the power of two >= W, so with label_nonce a multiple of it (the level
+    // loop and the party ABI use 0) a test's W counters differ in byte 0 alone and a pass of its
+    // label blocks shares AES rounds 1-2 (aes_rk_ctr: 133 instead of 160 lookups per extra block)
+    constexpr int WS = W <= 4 ? 4 : W <= 8 ? 8 : W <= 16 ? 16 : 32;
     const uint64_t n_act = gc_active(a);
     for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
         const uint64_t g = t / a.N;                  // group within the chunk
@@ -117,13 +121,40 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         const uint64_t tg = a.g_off * a.N + t;       // the test's index in the whole level
         // zero labels, generated per wire pair as the gates consume them (registers do not
         // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B
-        const uint64_t ctr0 = a.label_nonce + tg * W;
-        uint32_t acc[4];
+        const uint64_t ctr0 = a.label_nonce + tg * WS;
+        // wave-uniform: no lane's counters ctr0 .. ctr0 + W - 1 carry out of byte 0 (always, for an
+        // aligned label_nonce; otherwise the pass runs every round in full)
+        const bool shared = __ballot(((uint32_t)ctr0 & 0xFFu) + (W - 1) > 0xFFu) == 0;
+        uint32_t acc[4], m[1][4];
 #pragma unroll
         for (int k = 0; k < B; k++) {
-            uint32_t s[2][4] = {{(uint32_t)(ctr0 + k), (uint32_t)((ctr0 + k) >> 32), 0u, 0u},
-                                {(uint32_t)(ctr0 + B + 1 + k), (uint32_t)((ctr0 + B + 1 + k) >> 32), 0u, 0u}};
-            aes_rk<GcTab, 2>(s, tbl_gc, b0, b1, lrk);
+            // wires k (garbler) and B + 1 + k (evaluator); the last pair also takes the mask wire B
+            uint32_t s[2][4];
+            auto ctr_blk = [&](uint32_t (&b)[4], uint64_t c) {
+                b[0] = (uint32_t)c;
+                b[1] = (uint32_t)(c >> 32);
+                b[2] = 0u;
+                b[3] = 0u;
+            };
+            if (k == B - 1) {
+                uint32_t s3[3][4];
+                ctr_blk(s3[0], ctr0 + k);
+                ctr_blk(s3[1], ctr0 + B + 1 + k);
+                ctr_blk(s3[2], ctr0 + B);
+                if (shared) aes_rk_ctr<GcTab, 3, 0, 0>(s3, tbl_gc, b0, b1, lrk);
+                else aes_rk<GcTab, 3>(s3, tbl_gc, b0, b1, lrk);
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    s[0][c] = s3[0][c];
+                    s[1][c] = s3[1][c];
+                    m[0][c] = s3[2][c];
+                }
+            } else {
+                ctr_blk(s[0], ctr0 + k);
+                ctr_blk(s[1], ctr0 + B + 1 + k);
+                if (shared) aes_rk_ctr<GcTab, 2, 0, 0>(s, tbl_gc, b0, b1, lrk);
+                else aes_rk<GcTab, 2>(s, tbl_gc, b0, b1, lrk);
+            }
             // active labels: the garbler's bit (sent in the clear), the evaluator's (via OT)
             const uint32_t gb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
             const uint32_t eb = a.ev_ot ? 0u : plane_bit(a.ev_planes, a.g_off + g, B, k, a.nw, i);
@@ -169,9 +200,8 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
             st_blk(a.tables, 2 * (k - 1), n, t, TG);
             st_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
         }
-        // mask wire; out = eq ^ mask has zero label acc ^ M0, decoding bit = its colour
-        uint32_t m[1][4] = {{(uint32_t)(ctr0 + B), (uint32_t)((ctr0 + B) >> 32), 0u, 0u}};
-        aes_rk<GcTab, 1>(m, tbl_gc, b0, b1, lrk);
+        // mask wire (labelled with the last pair); out = eq ^ mask has zero label acc ^ M0, decoding
+        // bit = its colour
         a.decode[t] = (uint8_t)((acc[0] ^ m[0][0]) & 1u);
 #pragma unroll
         for (int c = 0; c < 4; c++) m[0][c] ^= a.mask ? D[c] : 0u;

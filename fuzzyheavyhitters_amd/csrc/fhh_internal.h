@@ -203,7 +203,7 @@ struct GcArgs {
     uint32_t N, nw, bits, mask;
     uint32_t rk_label[11][4];    // garbler's label PRG key schedule (AES-128-CTR)
     uint32_t delta[4];           // free-XOR offset, lsb 1
-    uint64_t label_nonce;        // label of (t, w) = AES_k(label_nonce + t * (2 bits + 1) + w)
+    uint64_t label_nonce;        // label of (t, w) = AES_k(label_nonce + t S + w), S = pow2 >= 2 bits + 1
     uint64_t gate_base;          // half-gate tweaks 2 (gate_base + t (bits - 1) + k) (+1)
     uint4* tables;               // [(bits-1)][2][n]  (T_G, T_E)
     uint4* gb_labels;            // [bits + 1][n]     garbler's active input labels (+ mask)

@@ -419,8 +419,9 @@ int fhh_sim_sketch_verify_fe255(fhh_ctx* ctx, const fhh_sketch_batch255* batch);
  * Free-XOR + half-gates, hash TCCR(x, i) = pi(pi(x) ^ i) ^ pi(x) with pi = AES-128 under the
  * all-zero key (swanky's fixed key and wire format are not restatable: DESIGN.md §5.3). Labels
  * are 16-B blocks, colour = bit 0 of byte 0; the garbler's zero label of wire w of test t is
- * AES_label_key(LE128(label_nonce + t (2 bits + 1) + w)) (w < bits: its string, w = bits: the
- * mask, w > bits: the evaluator's string); AND gate k of test t has tweaks 2 g, 2 g + 1 with
+ * AES_label_key(LE128(label_nonce + t S + w)) with S the power of two >= 2 bits + 1 (w < bits: its
+ * string, w = bits: the mask, w > bits: the evaluator's string; a label_nonce that is a multiple of
+ * S lets the kernel share AES rounds 1-2 between a test's label blocks); AND gate k of test t has tweaks 2 g, 2 g + 1 with
  * g = gate_base + t (bits - 1) + k. Tests t = g N + i (g < groups, i < clients); inputs are bit
  * planes [groups][bits][words] (bit i % 64 of word i / 64, as fhh_tree_crawl's share planes);
  * outputs are SoA over t: tables [(bits-1) * 2][t] (T_G, T_E), gb_labels [bits + 1][t] (the

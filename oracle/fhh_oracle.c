@@ -950,12 +950,14 @@ void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const u
     memcpy(D, delta_in, 16);
     D[0] |= 1;
     const uint64_t W = 2 * (uint64_t)bits + 1;
+    uint64_t WS = 4;                                 /* label counter stride: the power of two >= W */
+    while (WS < W) WS *= 2;
 #pragma omp parallel for schedule(static)
     for (int64_t t = 0; t < (int64_t)n; t++) {
         uint8_t L[17][16], acc[16];
-        for (uint64_t w = 0; w < W; w++) {           /* zero labels: AES_key(LE128(nonce + t W + w)) */
+        for (uint64_t w = 0; w < W; w++) {           /* zero labels: AES_key(LE128(nonce + t WS + w)) */
             uint8_t ctr[16] = {0};
-            const uint64_t c = label_nonce + (uint64_t)t * W + w;
+            const uint64_t c = label_nonce + (uint64_t)t * WS + w;
             for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
             aes128_encrypt_rk(rk, ctr, L[w]);
         }

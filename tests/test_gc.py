@@ -85,9 +85,11 @@ def test_gpu_gc_bit_exact(oracle, n, bits):
     rng = np.random.default_rng(n * 10 + bits)
     g, e = _cases(rng, n, bits)
     kc = fhh.KeyCollection(8, 1)
-    for mask in (0, 1):
-        out, tr = gc.equality_test(kc, g, e, mask, KEY, DELTA, label_nonce=123, gate_base=77, transcript=True)
-        t, gl, el, d = oracle.gc_garble_eq(g, e, mask, KEY, DELTA, label_nonce=123, gate_base=77)
+    # label_nonce 0 / 1 << 20 (multiples of the label counter stride: the label passes share AES
+    # rounds 1-2) and 123 (unaligned: some lanes' counters carry out of byte 0, full rounds)
+    for nonce, mask in ((123, 0), (123, 1), (0, 1), (1 << 20, 0)):
+        out, tr = gc.equality_test(kc, g, e, mask, KEY, DELTA, label_nonce=nonce, gate_base=77, transcript=True)
+        t, gl, el, d = oracle.gc_garble_eq(g, e, mask, KEY, DELTA, label_nonce=nonce, gate_base=77)
         assert np.array_equal(tr.tables, t)
         assert np.array_equal(tr.gb_labels, gl)
         assert np.array_equal(tr.ev_labels, el)

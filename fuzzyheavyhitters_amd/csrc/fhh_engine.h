@@ -254,7 +254,8 @@ struct OtOut {            // optional transcript (device pointers into the scrat
 int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev);
 int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
            const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off = 0);
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off = 0,
+           const OtFeMsg* fe = nullptr);
 
 }  // namespace eng
 }  // namespace fhh

@@ -152,7 +152,8 @@ int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t 
 // key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
 int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
            const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off) {
+           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off,
+           const OtFeMsg* fe) {
     if (m == 0) return FHH_OK;
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
@@ -178,6 +179,7 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     a.ctl = ctl;
     a.per_group = per_group;
     a.g_off = g_off;
+    if (fe) a.fe = *fe;   // the send hash computes the messages (x0 / x1 unused)
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
     HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1

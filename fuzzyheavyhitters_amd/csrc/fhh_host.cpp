@@ -1322,15 +1322,23 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         // last level, where a FieldElm travels as a BlockPair = 2 OTs): server 0
                         // sends (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
                         const uint64_t m2 = tests * per2;
-                        HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
-                        HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
                         HIP_TRY(c0, B.gc_recv.ensure(m2 * 16));
-                        if (pmode == 1)
-                            HIP_TRY(c0, launch_ot_fe_messages(ca, g.mask, B.gc_msg[0].as<uint4>(),
-                                                              B.gc_msg[1].as<uint4>(), c0->stream));
-                        else
+                        // FE levels: the send hash computes (r0, r1) itself (OtFeMsg, the PRF of
+                        // k_ot_fe_messages) instead of reading 32 B per OT that kernel wrote; the
+                        // last level's FieldElm messages (2 OTs per test) keep their kernel
+                        OtFeMsg fe{};
+                        if (pmode == 1) {
+                            fe.base = host_mix64(cfg->prf_seed ^ (uint64_t)lv);   // k_ot_fe_messages: mix64(prf_seed ^ level)
+                            fe.client_base = c0->client_base;
+                            fe.c_off = g_off;
+                            fe.n = (uint32_t)c0->n;
+                            fe.mask = g.mask;
+                        } else {
+                            HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
+                            HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
                             HIP_TRY(c0, launch_ot_fe255_messages(ca, g.mask, B.gc_msg[0].as<uint4>(),
                                                                  B.gc_msg[1].as<uint4>(), c0->stream));
+                        }
                         uint32_t sw[4];
                         ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw);
                         const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
@@ -1343,7 +1351,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         }
                         rc = ot_run(c0, m2, g.out_packed, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
                                     B.gc_recv.as<uint4>(), rk2, sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * per2,
-                                    nullptr, g_off);
+                                    nullptr, g_off, pmode == 1 ? &fe : nullptr);
                         if (rc) return rc;
                         ca.ot_recv = B.gc_recv.as<uint4>();
                     }

@@ -312,13 +312,24 @@ hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
 // key schedules are those of k_i^{s_i}). Bit matrices are [128 rows][mp / 128] uint4 blocks,
 // read per OT by the hashes (transposed on the fly). With ctl set (level loop) only the first
 // per_group * min(groups, ctl->C) OTs run.
+// The FE share conversion's sender messages (collect.rs:437-452), computed inside the send hash from
+// k_ot_fe_messages' PRF instead of being written to HBM by that kernel and read back (in-process
+// crawl): OT j of the chunk is client i = j mod n of child c_off + j / n
+struct OtFeMsg {
+    uint64_t base;          // mix64(prf_seed ^ level)
+    uint64_t client_base;
+    uint64_t c_off;         // the chunk's first child
+    uint32_t n;             // OTs (clients) per child; 0: the messages are x0 / x1
+    uint32_t mask;          // the garbler's mask bit: (r0, r1) if set, else (r1, r0)
+};
+
 struct OtArgs {
     uint64_t m;                  // OTs (capacity)
     uint64_t mp;                 // m padded to a multiple of 8192 (whole waves per row)
     const uint32_t* rk;          // [3][128][44]: receiver k_i^0, k_i^1, sender k_i^{s_i}
     uint32_t s[4];               // sender's base choice bits
     const uint32_t* choices;     // [mp / 32] receiver's choice bits (0 past m)
-    uint4 *T, *U, *Q;            // [128][mp / 128]
+    uint4 *T, *U, *Q;            // U [128][mp / 128] (row form, the wire); T, Q tile-major (fhh_ot.hip ot_tmaj)
     const uint4 *x0, *x1;        // [m]; x1 == nullptr: x1 = x0 ^ delta (correlated OT)
     uint32_t delta[4];
     uint4 *Y0, *Y1, *out;        // [m]
@@ -326,6 +337,7 @@ struct OtArgs {
     const LoopCtl* ctl;
     uint64_t per_group;
     uint64_t g_off;              // level loop chunk: OTs of groups [g_off, ctl->C) only
+    OtFeMsg fe;                  // fe.n > 0: the send hash computes x0 / x1 itself
 };
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);

@@ -46,6 +46,17 @@ __device__ __forceinline__ uint64_t ot_active(const OtArgs& a) {
     return v < a.m ? v : a.m;
 }
 
+// T and Q (internal to the parties, never on the wire) are stored tile-major: a hash's 512-OT tile
+// (4 blocks x 128 rows = 8 KiB) is one contiguous run, row r at words 16 r .. 16 r + 15, so its 32
+// row loads per lane read whole 128 B lines (rows r, r + 1) instead of 64 B from each of 128 rows
+// mp / 8 bytes apart. U, the receiver's message to the sender, stays in row form [128][mp / 128].
+// Same-box A/B at configs[1] (profiles/r04/ab_ot_tmaj/): receive hash -11 %, send hash -3 %, the
+// sender's expand +12 % (one row per wave: its Q stores are 64 B runs), all kernels -0.9 / -1.6 %;
+// T alone tile-major -0.2 %; 8-block (128 B per row) runs: hashes as before.
+__device__ __forceinline__ uint64_t ot_tmaj(uint32_t i, uint64_t c) {
+    return (c >> 2) * 512 + (uint64_t)i * 4 + (c & 3);
+}
+
 __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4]) {
 #pragma unroll
     for (int r = 0; r < 11; r++)
@@ -107,7 +118,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
                 const uint64_t c = c0 + 64 * q + lane;
-                if (c0 + 64 * q < nblk_act) a.T[(uint64_t)i * nblk + c] = make_uint4(g[q][0], g[q][1], g[q][2], g[q][3]);
+                if (c0 + 64 * q < nblk_act) a.T[ot_tmaj(i, c)] = make_uint4(g[q][0], g[q][1], g[q][2], g[q][3]);
                 g1[q][0] = (uint32_t)c;
                 g1[q][1] = (uint32_t)(c >> 32);
                 g1[q][2] = 0u;
@@ -132,14 +143,14 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
                 if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
                 uint4 u = make_uint4(0, 0, 0, 0);
                 if (si) u = a.U[(uint64_t)i * nblk + c];
-                a.Q[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
+                a.Q[ot_tmaj(i, c)] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
             }
         }
     }
 }
 
 // ---- transpose-fused hashes (r02) ------------------------------------------------------------
-// The hashes read the 128 x m bit matrices (T, Q) in their row form and transpose on the fly, so
+// The hashes read the 128 x m bit matrices (T, Q; tile-major) as row words and transpose on the fly, so
 // the separate transpose pass of r01 (k_ot_transpose: an HBM round trip of 32 B per OT, 7 % of the
 // GC + OT crawl) is gone.
 // One wave = one tile of 16 words x 128 rows = 512 OTs. Lane l = 4 q + g loads rows 32 g .. 32 g + 31
@@ -161,12 +172,11 @@ __device__ __forceinline__ uint64_t ot_tile_ot(uint64_t tile, uint32_t lane, int
     return 32 * (tile * kOtTileWords + (lane & 15)) + 8 * r + (lane >> 4) + 4 * u;
 }
 
-__device__ __forceinline__ void ot_tile_load(const uint32_t* rows, uint64_t W, uint64_t tile, uint32_t lane,
-                                             uint32_t (&x)[32]) {
+__device__ __forceinline__ void ot_tile_load(const uint32_t* rows, uint64_t tile, uint32_t lane, uint32_t (&x)[32]) {
     const uint32_t q = lane >> 2, g = lane & 3;
-    const uint32_t* p = rows + (uint64_t)(32 * g) * W + tile * kOtTileWords + q;
+    const uint32_t* p = rows + tile * (128 * kOtTileWords) + (32 * g) * kOtTileWords + q;   // ot_tmaj
 #pragma unroll
-    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + (uint64_t)i * W);
+    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + i * kOtTileWords);
     transpose32(x);   // x[k] bit i = row 32 g + i of OT 32 w + k
 }
 
@@ -184,11 +194,41 @@ __device__ __forceinline__ void ot_tile_round(uint32_t* st, uint32_t (&x)[32], u
     for (int i = 0; i < 24; i++) x[i] = x[i + 8];
 }
 
+__device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {   // SplitMix64's finaliser (as fhh_kernels.hip mix64)
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+
+// the sender's messages of OT j: x0[j], x1[j] (x1 = x0 ^ delta when absent), or with a.fe.n the FE
+// share conversion's (r0, r1) ordered by the mask bit, r0 = the PRF of k_ot_fe_messages
+// (fhh_kernels.hip) for client j mod n of child c_off + j / n, r1 = r0 + 1 mod p; blocks carry the
+// value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430)
+__device__ __forceinline__ void ot_messages(const OtArgs& a, uint64_t j, uint4& x0, uint4& x1) {
+    if (a.fe.n) {
+        constexpr uint64_t P = (1ull << 62) - (1ull << 30) - 1;
+        const uint64_t cr = (j >> 32) ? j / a.fe.n : (uint32_t)j / a.fe.n;   // a chunk's OTs: < 2^32 in practice
+        const uint64_t i = j - cr * a.fe.n;
+        const uint64_t bc = ot_mix64(a.fe.base ^ (a.fe.c_off + cr));
+        uint64_t r0 = ot_mix64(ot_mix64(bc ^ (a.fe.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
+        if (r0 >= P) r0 -= P;
+        const uint64_t r1 = (r0 + 1 == P) ? 0 : r0 + 1;
+        const uint64_t m0 = a.fe.mask ? r0 : r1, m1 = a.fe.mask ? r1 : r0;
+        x0 = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
+        x1 = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
+        return;
+    }
+    x0 = a.x0[j];
+    x1 = a.x1 ? a.x1[j] : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+}
+
 __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t m = ot_active(a);
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     if ((uint64_t)blockIdx.x * kOtWaves >= tiles) return;   // no tiles for this workgroup: skip the fill
     ot_fill(tbl_ot);
@@ -198,7 +238,7 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) 
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
     for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
-        ot_tile_load(rows, W, t, lane, x);
+        ot_tile_load(rows, t, lane, x);
 #pragma unroll 1
         for (int r = 0; r < 4; r++) {
             uint4 q[2];
@@ -210,9 +250,8 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) 
                 aes0_mmo_tab<DevOpsX, OtTab, 2>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
                 const uint64_t j = ot_tile_ot(t, lane, r, u);
                 if (j >= m) continue;
-                const uint4 x0 = a.x0[j];
-                const uint4 x1 = a.x1 ? a.x1[j]
-                                      : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+                uint4 x0, x1;
+                ot_messages(a, j, x0, x1);
                 a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
                 a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
             }
@@ -224,7 +263,7 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t m = ot_active(a);
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     if ((uint64_t)blockIdx.x * kOtWaves >= tiles) return;   // no tiles for this workgroup: skip the fill
     ot_fill(tbl_ot);
@@ -234,7 +273,7 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
     for (uint64_t t = (uint64_t)blockIdx.x * kOtWaves + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
-        ot_tile_load(rows, W, t, lane, x);
+        ot_tile_load(rows, t, lane, x);
         // the lane's 8 OTs of the tile share one choice word (ot_tile_ot: j >> 5 = 16 t + (lane & 15));
         // read once per tile, and only if the word holds an active OT (the buffer may end at m bits)
         const uint64_t cwi = t * kOtTileWords + (lane & 15);
@@ -287,12 +326,11 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
 // 168 each) and every wave keeps the NEXT tile's 32 row words and the current pass's messages in
 // flight behind the current pass's AES: the next tile's loads are issued right after this tile's
 // transpose, a pass's Y (receiver) / x0, x1 (sender) loads right before its AES.
-__device__ __forceinline__ void ot_tile_issue(const uint32_t* rows, uint64_t W, uint64_t tile, uint32_t lane,
-                                              uint32_t (&x)[32]) {
+__device__ __forceinline__ void ot_tile_issue(const uint32_t* rows, uint64_t tile, uint32_t lane, uint32_t (&x)[32]) {
     const uint32_t q = lane >> 2, g = lane & 3;
-    const uint32_t* p = rows + (uint64_t)(32 * g) * W + tile * kOtTileWords + q;
+    const uint32_t* p = rows + tile * (128 * kOtTileWords) + (32 * g) * kOtTileWords + q;   // ot_tmaj
 #pragma unroll
-    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + (uint64_t)i * W);
+    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + i * kOtTileWords);
 }
 
 template <int THREADS>
@@ -301,7 +339,7 @@ __global__ __launch_bounds__(THREADS) void k_ot_recv_hash_pf(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[WAVES][512];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t m = ot_active(a);
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
     ot_fill(tbl_ot);
@@ -311,12 +349,12 @@ __global__ __launch_bounds__(THREADS) void k_ot_recv_hash_pf(OtArgs a) {
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
     uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
     uint32_t x[32];
-    if (t < tiles) ot_tile_issue(rows, W, t, lane, x);
+    if (t < tiles) ot_tile_issue(rows, t, lane, x);
     for (; t < tiles; t += nwaves) {
         transpose32(x);
         uint32_t xn[32];
         const uint64_t tn = t + nwaves;
-        if (tn < tiles) ot_tile_issue(rows, W, tn, lane, xn);   // wave-uniform
+        if (tn < tiles) ot_tile_issue(rows, tn, lane, xn);   // wave-uniform
         const uint64_t cwi = t * kOtTileWords + (lane & 15);
         const uint32_t cw = 32 * cwi < m ? a.choices[cwi] : 0u;
 #pragma unroll 1
@@ -357,7 +395,7 @@ __global__ __launch_bounds__(THREADS) void k_ot_send_hash_pf(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[WAVES][512];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a), W = a.mp / 32;
+    const uint64_t m = ot_active(a);
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
     ot_fill(tbl_ot);
@@ -367,12 +405,12 @@ __global__ __launch_bounds__(THREADS) void k_ot_send_hash_pf(OtArgs a) {
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
     uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
     uint32_t x[32];
-    if (t < tiles) ot_tile_issue(rows, W, t, lane, x);
+    if (t < tiles) ot_tile_issue(rows, t, lane, x);
     for (; t < tiles; t += nwaves) {
         transpose32(x);
         uint32_t xn[32];
         const uint64_t tn = t + nwaves;
-        if (tn < tiles) ot_tile_issue(rows, W, tn, lane, xn);   // wave-uniform
+        if (tn < tiles) ot_tile_issue(rows, tn, lane, xn);   // wave-uniform
 #pragma unroll 1
         for (int r = 0; r < 4; r++) {
             uint4 q[2];
@@ -414,13 +452,6 @@ __global__ __launch_bounds__(THREADS) void k_ot_send_hash_pf(OtArgs a) {
 // device, so an enqueued level needs no host data; key schedules [3][128][44] (k_i^0, k_i^1,
 // k_i^{s_i}). One thread per key.
 __constant__ ByteTable c_sbox_ot = SBOX;
-
-__device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {
-    z += 0x9e3779b97f4a7c15ull;
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
 
 __device__ __forceinline__ uint64_t ot_seed_word(uint64_t prf, uint32_t level, uint32_t salt, uint32_t i, uint32_t b,
                                                  int h) {
@@ -531,7 +562,7 @@ static int ot_rows_grid_waves(const OtArgs& a, int waves) {
 
 hipError_t launch_ot_send_hash_rows(const OtArgs& a, hipStream_t stream) {
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // tiles of 16 words stay inside a row
-    switch (ot_hash_form(true)) {
+    switch (a.fe.n ? 0 : ot_hash_form(true)) {   // the prefetching forms read x0 / x1 only
         case 512: hipLaunchKernelGGL(k_ot_send_hash_pf<512>, dim3(ot_rows_grid_waves(a, 8)), dim3(512), 0, stream, a); break;
         case 768: hipLaunchKernelGGL(k_ot_send_hash_pf<768>, dim3(ot_rows_grid_waves(a, 12)), dim3(768), 0, stream, a); break;
         default: hipLaunchKernelGGL(k_ot_send_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);

@@ -4,7 +4,8 @@
 # rocprofv3 --kernel-trace --stats of `python3 bench.py <args>` with FHH_LIB_PATH =
 # ab_builds/libfhh_base.so and ab_builds/libfhh_new.so alternately; keeps only the per-kernel
 # stats CSV of each run (gpurun_out/abk_<tag>/<build>_<round>_kernel_stats.csv).
-# AB_BUILDS="base new new2 ..." alternates more builds (ab_builds/libfhh_<name>.so).
+# AB_BUILDS="base new new2 ..." alternates more builds (ab_builds/libfhh_<name>.so); AB_SCRIPT=tools/x.py
+# profiles that script instead of bench.py.
 set -u
 TAG=$1; ROUNDS=$2; shift 2
 export TMPDIR=/tmp
@@ -13,7 +14,7 @@ mkdir -p $OUT
 for r in $(seq 1 $ROUNDS); do
   for b in ${AB_BUILDS:-base new}; do
     FHH_LIB_PATH=ab_builds/libfhh_$b.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d $OUT/tmp_${b}_$r -o run -- python3 bench.py "$@" > $OUT/${b}_$r.log 2>&1
+        -d $OUT/tmp_${b}_$r -o run -- python3 ${AB_SCRIPT:-bench.py} "$@" > $OUT/${b}_$r.log 2>&1
     rc=$?
     echo "round $r $b rc=$rc"
     [ $rc -eq 0 ] || exit $rc

@@ -125,18 +125,36 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         // wave-uniform: no lane's counters ctr0 .. ctr0 + W - 1 carry out of byte 0 (always, for an
         // aligned label_nonce; otherwise the pass runs every round in full)
         const bool shared = __ballot(((uint32_t)ctr0 & 0xFFu) + (W - 1) > 0xFFu) == 0;
+        auto ctr_blk = [&](uint32_t (&b)[4], uint64_t c) {
+            b[0] = (uint32_t)c;
+            b[1] = (uint32_t)(c >> 32);
+            b[2] = 0u;
+            b[3] = 0u;
+        };
+        // B <= 2 (d = 1: the metric's configuration): all W <= 5 label blocks in one pass up front, 4
+        // sharing rounds 1-2 with the first, instead of a 2-block pass then a 3-block one (692 instead of
+        // 719 lookups, and 5 independent blocks in flight per lane)
+        constexpr bool kOnePass = W <= 5;
+        uint32_t L[kOnePass ? W : 1][4];
+        if constexpr (kOnePass) {
+#pragma unroll
+            for (int w = 0; w < W; w++) ctr_blk(L[w], ctr0 + w);
+            if (shared) aes_rk_ctr<GcTab, W, 0, 0>(L, tbl_gc, b0, b1, lrk);
+            else aes_rk<GcTab, W>(L, tbl_gc, b0, b1, lrk);
+        }
         uint32_t acc[4], m[1][4];
 #pragma unroll
         for (int k = 0; k < B; k++) {
             // wires k (garbler) and B + 1 + k (evaluator); the last pair also takes the mask wire B
             uint32_t s[2][4];
-            auto ctr_blk = [&](uint32_t (&b)[4], uint64_t c) {
-                b[0] = (uint32_t)c;
-                b[1] = (uint32_t)(c >> 32);
-                b[2] = 0u;
-                b[3] = 0u;
-            };
-            if (k == B - 1) {
+            if constexpr (kOnePass) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    s[0][c] = L[k][c];
+                    s[1][c] = L[B + 1 + k][c];
+                    if (k == B - 1) m[0][c] = L[B][c];
+                }
+            } else if (k == B - 1) {
                 uint32_t s3[3][4];
                 ctr_blk(s3[0], ctr0 + k);
                 ctr_blk(s3[1], ctr0 + B + 1 + k);

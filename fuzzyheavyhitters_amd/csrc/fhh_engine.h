@@ -143,6 +143,11 @@ struct fhh_ctx {
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> last_hist;
 
     DevBuf scratch, scratch2;
+    // level-batched sketch verification (fhh_sim_sketch_verify_fe): a second stream for the sketch
+    // tails and the verify, its events, and the odd levels' sketch outputs
+    hipStream_t side_stream = nullptr;
+    hipEvent_t side_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    DevBuf sketch_alt;
     DevBuf ot_buf[8], ot_rk;                     // OT extension scratch (T U Q - - Y0 Y1 choices)
     std::vector<uint32_t> ot_rk_host;            // key schedules staged for ot_rk
     std::vector<PinnedBuf*> stage;   // pinned staging for async H2D, recycled at every sync

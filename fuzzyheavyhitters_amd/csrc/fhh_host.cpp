@@ -1687,6 +1687,12 @@ void fhh_destroy(fhh_ctx* ctx) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
     }
+    if (ctx->side_stream) {
+        (void)hipStreamSynchronize(ctx->side_stream);
+        (void)hipStreamDestroy(ctx->side_stream);
+    }
+    for (hipEvent_t e : ctx->side_ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->own_stream);
     for (auto* b : ctx->stage) delete b;
     delete ctx;
@@ -2469,23 +2475,55 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
         return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: n_levels > 1 needs triples_levels (fresh triples per level)");
     if (b->triples_levels && b->level + nl > tl)
         return ctx->fail(FHH_E_ARG, "sim_sketch_verify_fe: levels past the triples held");
+    // Several levels: a two-stage pipeline over two streams. The main stream runs every level's two
+    // main sketch launches back to back; the side stream runs the level's sketch tails (disjoint
+    // outputs) and, once both main launches are done, its verify. Level k's sketches go to slot
+    // (nl - 1 - k) & 1 (slot 0 = the caller's sketch_dev, so the last level ends there; slot 1 =
+    // sketch_alt), so level k + 1's main launches overlap level k's verify, and a slot is reused by
+    // level k + 2 only after level k's verify has read it. FHH_SKETCH_OVERLAP=0: one stream.
+    static const bool kOverlapEnv = [] {
+        const char* e = std::getenv("FHH_SKETCH_OVERLAP");
+        return !(e && e[0] == '0');
+    }();
+    const bool overlap = nl > 1 && kOverlapEnv;
+    uint64_t* alt[2] = {nullptr, nullptr};
+    if (overlap) {
+        if (!ctx->side_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
+        for (hipEvent_t& e : ctx->side_ev)
+            if (!e) HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(ctx, ctx->sketch_alt.ensure((size_t)2 * b->n_keys * 6 * 8));
+        for (int s = 0; s < 2; s++) alt[s] = ctx->sketch_alt.as<uint64_t>() + (size_t)s * b->n_keys * 6;
+        // the side stream starts after everything already on the main stream (triples, uploads)
+        HIP_TRY(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
+    }
+    hipStream_t side = overlap ? ctx->side_stream : ctx->stream;
+    hipEvent_t* ev_main = ctx->side_ev;       // [slot]: the slot's main launches are done
+    hipEvent_t* ev_ver = ctx->side_ev + 2;    // [slot]: the slot's verify is done
     for (uint32_t k = 0; k < nl; k++) {
         const uint32_t lv = b->level + k;
+        const int slot = overlap ? (int)((nl - 1 - k) & 1) : 0;
+        uint64_t* out[2] = {slot ? alt[0] : b->sketch_dev[0], slot ? alt[1] : b->sketch_dev[1]};
+        if (overlap && k >= 2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev_ver[slot], 0));
         for (int s = 0; s < 2; s++) {
             SketchArgs a{};
             a.seeds = b->seeds_dev;
             a.x = b->x_dev[s] + (size_t)k * b->x_level_stride;
             a.kx = b->kx_dev[s] + (size_t)k * b->x_level_stride;
-            a.out = b->sketch_dev[s];
+            a.out = out[s];
             a.n_keys = b->n_keys;
             a.n_nodes = b->n_nodes;
             a.force_sequential = b->force_sequential;
             a.level = lv;
-            HIP_TRY(ctx, launch_sketch_fe(a, ctx->stream));
+            HIP_TRY(ctx, launch_sketch_fe2(a, ctx->stream, side));
+        }
+        if (overlap) {
+            HIP_TRY(ctx, hipEventRecord(ev_main[slot], ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(side, ev_main[slot], 0));
         }
         VerifyArgs v{};
         for (int s = 0; s < 2; s++) {
-            v.sketch[s] = b->sketch_dev[s];
+            v.sketch[s] = out[s];
             v.mac[s] = b->mac_dev[s];
             v.mac2[s] = b->mac2_dev[s];
             v.triples[s] = b->triples_dev[s];
@@ -2495,8 +2533,10 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
         v.n = b->n_keys;
         v.level = b->triples_levels ? lv : 0;
         v.triples_levels = tl;
-        HIP_TRY(ctx, launch_verify_fe(v, ctx->stream));
+        HIP_TRY(ctx, launch_verify_fe(v, side));
+        if (overlap) HIP_TRY(ctx, hipEventRecord(ev_ver[slot], side));
     }
+    if (overlap) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev_ver[0], 0));   // the last level's slot
     return sync(ctx);
 }
 

@@ -452,6 +452,7 @@ struct VerifyArgs {
     uint32_t triples_levels;
 };
 hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream);
+hipError_t launch_sketch_fe2(const SketchArgs& a, hipStream_t stream, hipStream_t tail_stream);
 hipError_t launch_mul_fe(const MulArgs& a, hipStream_t stream);
 hipError_t launch_verify_fe(const VerifyArgs& a, hipStream_t stream);
 hipError_t launch_deal_triples_fe(uint64_t n, uint32_t levels, uint64_t seed, uint64_t* t0, uint64_t* t1,

@@ -792,7 +792,11 @@ static hipError_t launch_sketch_pc(const SketchArgs& a, hipStream_t stream) {
     return launch_sketch_pc_lpk(p.lpk_tail, t, cus, stream);
 }
 
-hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
+hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) { return launch_sketch_fe2(a, stream, stream); }
+
+// the default form's main launch on `stream`, its tail launch (the keys past n_main, disjoint outputs)
+// on `tail_stream`: a caller with a second stream lets the tail fill the main launch's ragged end
+hipError_t launch_sketch_fe2(const SketchArgs& a, hipStream_t stream, hipStream_t tail_stream) {
     if (a.n_keys == 0) return hipSuccess;
     if (g_sketch_impl == 4) return launch_sketch_pc(a, stream);
     if (g_sketch_impl == 1)
@@ -814,7 +818,7 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) {
     t.n_keys = a.n_keys - p.n_main;
     // (r03, configs[4]: its 3 blocks per lane cover a 130-block key at LPK 64 in one pass where the
     // fused form takes two: 16.2 vs 28.8 us; the main launch stays fused, 227 vs 236 us)
-    return launch_sketch_pc_lpk(p.lpk_tail, t, sketch_cus(), stream);
+    return launch_sketch_pc_lpk(p.lpk_tail, t, sketch_cus(), tail_stream);
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

@@ -67,6 +67,8 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
 // one wave per (row i, kOtSlices consecutive 64-block slices): lane l computes blocks
 // c = c0 + 64 q + l, q < kOtSlices, in lockstep. nblk = mp / 128 is a multiple of 64, so a slice
 // is wholly inside or outside the row and the row's key schedules are uniform (scalar loads)
+// (launched for the receiver; the sender runs k_ot_send_expand_pair below, RECV = false is the
+// one-row sender form it replaced)
 template <bool RECV>
 __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
     // 4 slices per wave (4 blocks per lane in lockstep). The receiver runs its two row keys one
@@ -145,6 +147,57 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
                 if (si) u = a.U[(uint64_t)i * nblk + c];
                 a.Q[ot_tmaj(i, c)] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
             }
+        }
+    }
+}
+
+// The sender's expand in row pairs (r04): a wave takes rows 2 p (lanes 0-31) and 2 p + 1 (lanes
+// 32-63) over the same 128 blocks, lane l computing blocks c0 + 32 q + (l & 31), q < 4 (c0 a multiple
+// of 128: the four counters differ in byte 0 alone, as aes_rk_ctr needs). Both rows' schedules come by
+// scalar loads, selected per half-wave (RkHalves). In the tile-major Q (ot_tmaj) rows 2 p and 2 p + 1
+// of a tile are adjacent, so each store instruction writes 8 whole 128-B lines instead of 16 half
+// lines: 263 -> 246 us per configs[1] launch against k_ot_expand<false> (the receiver's pair form
+// measured +0.8 %: its two keys per block keep the one-row form; profiles/r04/ab_ot_expand_pair/).
+__global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
+    constexpr int kSlices = 4;
+    __shared__ uint32_t tbl_ot[OtTab::kWords];
+    const uint32_t lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
+    const uint64_t nblk = a.mp / 128;
+    const uint64_t nblk_act = (ot_active(a) + 127) / 128;
+    const uint64_t tiles_per_pair = (nblk_act + 32 * kSlices - 1) / (32 * kSlices);
+    const uint64_t tiles = 64 * tiles_per_pair;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
+    const uint64_t wave = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6);
+    const uint64_t run = (tiles + nwaves - 1) / nwaves;
+    if ((uint64_t)blockIdx.x * (kOtThreads / 64) * run >= tiles) return;
+    ot_fill(tbl_ot);
+    uint32_t b0, b1;
+    OtTab::bases(lane, b0, b1);
+    const uint64_t t_end = min(tiles, (wave + 1) * run);
+    for (uint64_t t = wave * run; t < t_end; t++) {
+        const uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_pair));
+        const uint64_t c0 = (t - (uint64_t)p * tiles_per_pair) * 32 * kSlices;
+        if (c0 >= nblk_act) continue;   // wave-uniform
+        const uint32_t i = 2 * p + half;
+        uint32_t g[kSlices][4];
+#pragma unroll
+        for (int q = 0; q < kSlices; q++) {
+            const uint64_t c = c0 + 32 * q + l;
+            g[q][0] = (uint32_t)c;
+            g[q][1] = (uint32_t)(c >> 32);
+            g[q][2] = 0u;
+            g[q][3] = 0u;
+        }
+        aes_halves_rk_ctr<OtTab, kSlices, 0, 0>(g, tbl_ot, b0, b1, a.rk + (size_t)(256 + 2 * p) * 44,
+                                                a.rk + (size_t)(257 + 2 * p) * 44, half != 0);   // G(k_i^{s_i})
+        const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
+#pragma unroll
+        for (int q = 0; q < kSlices; q++) {
+            const uint64_t c = c0 + 32 * q + l;
+            if (c0 + 32 * q >= nblk_act) break;   // wave-uniform
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (si) u = a.U[(uint64_t)i * nblk + c];
+            a.Q[ot_tmaj(i, c)] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
         }
     }
 }
@@ -519,7 +572,7 @@ hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_expand<false>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
+    hipLaunchKernelGGL(k_ot_send_expand_pair, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
                        stream, a);
     return hipGetLastError();
 }

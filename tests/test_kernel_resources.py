@@ -61,7 +61,8 @@ def test_ot_hash_rows_do_not_spill(tmp_path):
 
 
 def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
-    """k_gc_garble / k_gc_eval at every share-string width b = 1..8 and both OT expand forms stay
+    """k_gc_garble / k_gc_eval at every share-string width b = 1..8 and both OT expands (the receiver's
+    one-row form, the sender's row-pair form) stay
     in registers at 4 waves per SIMD."""
     if not shutil.which("hipcc"):
         pytest.skip("hipcc not available")
@@ -70,7 +71,7 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     names += [f"_ZN3fhh9k_gc_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
-    names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh11k_ot_expandILb0EEEvNS_6OtArgsE"]
+    names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE"]
     for name in names:
         assert name in u, f"{name} not found"
         k = u[name]

@@ -99,6 +99,11 @@ def test_bench_two_rank_rehearsal_equals_one_rank():
     for k in ("final_heavy_hitters", "children_total", "levels", "aes_blocks_per_step"):
         assert two[k] == one[k], k
     assert two["config"]["clients_total"] == one["config"]["clients_total"] == 20000
+    # the real protocol's crawl (GC + OT + real base OTs every level) over the two ranks' shards with
+    # the per-level all-reduce: the same heavy hitters as the plaintext headline and as one rank
+    for line in (one, two):
+        assert line["protocol_crawl"]["heavy_hitters_equal_headline"], line["protocol_crawl"]
+    assert two["protocol_crawl"]["heavy_hitters"] == one["protocol_crawl"]["heavy_hitters"]
 
 
 @pytest.mark.gpu

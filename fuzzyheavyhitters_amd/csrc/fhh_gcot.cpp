@@ -387,7 +387,8 @@ struct PartyState {
     DevBuf planes;              // own share planes [C][bits][nw] (evaluator: OT 1's choice bits)
     DevBuf gc;                  // garbler: the gc message; evaluator: unused
     DevBuf labels;              // garbler: OT 1 inputs (evaluator zero labels); evaluator: OT 1 outputs
-    DevBuf x0, x1;              // garbler: OT 2 messages (r0 / r1 ordered by the mask)
+    DevBuf x0, x1;              // garbler: OT 2 messages (r0 / r1 ordered by the mask), last level only
+    OtFeMsg fe{};               // garbler, FE levels: OT 2's messages drawn inside the send hash
     DevBuf rk;                  // base-OT key schedules [3][128][44] of the current OT, own rows only
     DevBuf T, U, Q, Y;          // OT matrices (T / Q private) and messages (U or Y0 | Y1)
     DevBuf choices2;            // evaluator: the GC outputs packed as OT 2's choice words
@@ -460,10 +461,11 @@ int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
 }
 
 // a finished chunk's node values into the level's rows [c_off, c_off + C) (the evaluator's OT 2
-// outputs, or the garbler's r1 = its message for the mask's other side, collect.rs:439-472)
+// outputs, or the garbler's r1 = its message for the mask's other side, collect.rs:439-472);
+// chunk_vals == nullptr: already written there (the garbler's FE levels)
 int party_chunk_done(fhh_ctx* ctx, PartyState& P, const void* chunk_vals) {
     const uint64_t bytes = P.C * P.n * P.per2 * 16;
-    if (bytes)
+    if (bytes && chunk_vals)
         HIP_TRY(ctx, hipMemcpyAsync(P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * 16, chunk_vals, bytes,
                                     hipMemcpyDeviceToDevice, ctx->stream));
     P.covered = P.c_off + P.C;
@@ -574,17 +576,30 @@ int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_
     for (int c = 0; c < 4; c++) P.delta[c] = P.g.delta[c];
     if (P.tests) HIP_TRY(ctx, launch_gc_garble(P.g, ctx->stream));
     // OT 2's messages: (r0, r1) if the mask is set, else (r1, r0) (collect.rs:439-452, 846-866); the
-    // garbler's node value is r1
-    HIP_TRY(ctx, P.x0.ensure(std::max<uint64_t>(P.m2, 1) * 16));
-    HIP_TRY(ctx, P.x1.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+    // garbler's node value is r1. FE levels: r1 straight into the level's rows, and the send hash
+    // draws (r0, r1) from the same PRF (OtFeMsg) instead of reading 32 B per OT back; the last
+    // level's FieldElm messages keep their buffers
+    P.fe = OtFeMsg{};
+    if (P.last) {
+        HIP_TRY(ctx, P.x0.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+        HIP_TRY(ctx, P.x1.ensure(std::max<uint64_t>(P.m2, 1) * 16));
+    }
     if (P.tests) {
         ChildArgs a = ctx_child_args(ctx);   // the chunk's children
         a.c_off = P.c_off;
         a.c_cnt = P.C;
         a.prf_seed = cfg->share_seed;
         a.gc_N = (uint32_t)P.n;
-        if (P.last) HIP_TRY(ctx, launch_ot_fe255_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
-        else HIP_TRY(ctx, launch_ot_fe_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
+        if (P.last) {
+            HIP_TRY(ctx, launch_ot_fe255_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
+        } else {
+            HIP_TRY(ctx, launch_ot_fe_messages(a, P.mask, P.vals.as<uint4>() + P.c_off * P.n, nullptr, ctx->stream));
+            P.fe.base = host_mix64(cfg->share_seed ^ (uint64_t)a.level);   // k_ot_fe_messages: mix64(prf ^ level)
+            P.fe.client_base = a.client_base;
+            P.fe.c_off = P.c_off;
+            P.fe.n = (uint32_t)P.n;
+            P.fe.mask = P.mask;
+        }
     }
     // both OTs' sender schedules now (OtSender::init per OT, collect.rs:454-471)
     rc = party_keys(ctx, P, nullptr, &cfg->base_chosen[0][0][0]);
@@ -629,9 +644,11 @@ static int gb_ot_send(fhh_ctx* ctx, int which, const uint8_t* u_dev, uint64_t u_
         for (int c = 0; c < 4; c++) a.s[c] = P.s[which][c];
         a.Y0 = P.Y.as<uint4>();
         a.Y1 = P.Y.as<uint4>() + m;
-        if (which) {
+        if (which && P.last) {
             a.x0 = P.x0.as<uint4>();
             a.x1 = P.x1.as<uint4>();
+        } else if (which) {
+            a.fe = P.fe;   // (r0, r1) from the PRF inside the send hash
         } else {   // correlated: x1 = x0 ^ Delta (the evaluator's one labels)
             a.x0 = P.labels.as<uint4>();
             a.x1 = nullptr;
@@ -641,7 +658,7 @@ static int gb_ot_send(fhh_ctx* ctx, int which, const uint8_t* u_dev, uint64_t u_
         HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // Y0, Y1
     }
     if (which) {   // the chunk is done on this side: its node values r1 into the level's rows
-        rc = party_chunk_done(ctx, P, P.mask ? P.x1.p : P.x0.p);
+        rc = party_chunk_done(ctx, P, P.last ? (P.mask ? P.x1.p : P.x0.p) : nullptr);
         if (rc) return rc;
     }
     rc = ctx_sync(ctx);

@@ -695,7 +695,8 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
 
 // the garbler's OT messages of the FE share conversion (collect.rs:437-452): r0 from the same
 // PRF as k_sim_ot_fe, r1 = r0 + 1; (r0, r1) if the mask bit is set, else (r1, r0); blocks carry
-// the value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430)
+// the value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430). x1 == nullptr: r1
+// alone into x0 (the party garbler's node values; its send hash then draws (r0, r1) itself, OtFeMsg)
 __global__ __launch_bounds__(kReduceThreads) void k_ot_fe_messages(ChildArgs a, uint32_t mask, uint4* x0, uint4* x1) {
     const uint64_t base = mix64(a.prf_seed ^ a.level);
     const uint64_t C_ = child_end(a);
@@ -705,6 +706,10 @@ __global__ __launch_bounds__(kReduceThreads) void k_ot_fe_messages(ChildArgs a, 
             uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
             if (r0 >= kFeP) r0 -= kFeP;
             const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;
+            if (!x1) {
+                x0[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)r1, (uint32_t)(r1 >> 32), 0u, 0u);
+                continue;
+            }
             const uint64_t m0 = mask ? r0 : r1, m1 = mask ? r1 : r0;
             x0[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
             x1[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);

@@ -67,10 +67,11 @@ __device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4
 // one wave per (row i, kOtSlices consecutive 64-block slices): lane l computes blocks
 // c = c0 + 64 q + l, q < kOtSlices, in lockstep. nblk = mp / 128 is a multiple of 64, so a slice
 // is wholly inside or outside the row and the row's key schedules are uniform (scalar loads)
-// (launched for the receiver; the sender runs k_ot_send_expand_pair below, RECV = false is the
-// one-row sender form it replaced)
+// The receiver's expand (the sender's is k_ot_send_expand_pair below; the template parameter keeps
+// the kernel's name, k_ot_expand<true>, that every profile since r01 reports)
 template <bool RECV>
 __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
+    static_assert(RECV, "the sender's expand is k_ot_send_expand_pair");
     // 4 slices per wave (4 blocks per lane in lockstep). The receiver runs its two row keys one
     // after the other over the same 4 blocks (T = G(k0) is stored, U = T ^ G(k1) ^ r): only one
     // 44-word schedule is live in SGPRs at a time (both at once spilled it into VGPRs: 128 VGPRs
@@ -112,10 +113,10 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
         }
         {
             uint32_t rk[11][4];
-            ld_rk(a.rk + (size_t)(RECV ? i : 256 + i) * 44, rk);
-            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g, tbl_ot, b0, b1, rk);   // G(k_i^0) (receiver) / G(k_i^{s_i})
+            ld_rk(a.rk + (size_t)i * 44, rk);
+            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g, tbl_ot, b0, b1, rk);   // G(k_i^0)
         }
-        if (RECV) {
+        {
             uint32_t g1[kOtSlices][4];
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
@@ -136,16 +137,6 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
                 const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
                 a.U[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ g1[q][0] ^ r.x, g[q][1] ^ g1[q][1] ^ r.y,
                                                          g[q][2] ^ g1[q][2] ^ r.z, g[q][3] ^ g1[q][3] ^ r.w);
-            }
-        } else {
-            const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
-#pragma unroll
-            for (int q = 0; q < kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * q + lane;
-                if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
-                uint4 u = make_uint4(0, 0, 0, 0);
-                if (si) u = a.U[(uint64_t)i * nblk + c];
-                a.Q[ot_tmaj(i, c)] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
             }
         }
     }

@@ -2500,6 +2500,14 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
     hipStream_t side = overlap ? ctx->side_stream : ctx->stream;
     hipEvent_t* ev_main = ctx->side_ev;       // [slot]: the slot's main launches are done
     hipEvent_t* ev_ver = ctx->side_ev + 2;    // [slot]: the slot's verify is done
+    // a failure part way leaves no side-stream work running on the caller's buffers
+    struct SideDrain {
+        hipStream_t st;
+        bool armed;
+        ~SideDrain() {
+            if (armed && st) (void)hipStreamSynchronize(st);
+        }
+    } drain{overlap ? ctx->side_stream : nullptr, overlap};
     for (uint32_t k = 0; k < nl; k++) {
         const uint32_t lv = b->level + k;
         const int slot = overlap ? (int)((nl - 1 - k) & 1) : 0;
@@ -2537,6 +2545,7 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
         if (overlap) HIP_TRY(ctx, hipEventRecord(ev_ver[slot], side));
     }
     if (overlap) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev_ver[0], 0));   // the last level's slot
+    drain.armed = false;   // the main stream now waits for the side stream's last verify
     return sync(ctx);
 }
 

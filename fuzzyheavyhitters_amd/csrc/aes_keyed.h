@@ -84,18 +84,6 @@ struct RkLds {
     }
 };
 
-// two uniform schedules, one per half-wave (lanes 0-31: a, 32-63: b): both rows' round-key words by
-// scalar loads, selected per lane (4 v_cndmask per round)
-struct RkHalves {
-    const uint32_t* a;
-    const uint32_t* b;
-    bool hi;
-    __device__ __forceinline__ void get(int r, uint32_t (&w)[4]) const {
-#pragma unroll
-        for (int c = 0; c < 4; c++) w[c] = hi ? b[4 * r + c] : a[4 * r + c];
-    }
-};
-
 template <class Tab, int NB, int R, int C, class Rk>
 __device__ __forceinline__ void aes_ctr_shared(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
                                                const Rk& src) {
@@ -178,12 +166,6 @@ template <class Tab, int NB, int R, int C>
 __device__ __forceinline__ void aes_rk_ctr(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
                                            const uint32_t (&rk)[11][4]) {
     aes_ctr_shared<Tab, NB, R, C>(s, tbl, b0, b1, RkRegs{rk});
-}
-
-template <class Tab, int NB, int R, int C>
-__device__ __forceinline__ void aes_halves_rk_ctr(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
-                                                  const uint32_t* rka, const uint32_t* rkb, bool hi) {
-    aes_ctr_shared<Tab, NB, R, C>(s, tbl, b0, b1, RkHalves{rka, rkb, hi});
 }
 
 template <class Tab, int NB, int R, int C>

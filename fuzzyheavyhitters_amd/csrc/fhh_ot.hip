@@ -144,15 +144,20 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
 
 // The sender's expand in row pairs (r04): a wave takes rows 2 p (lanes 0-31) and 2 p + 1 (lanes
 // 32-63) over the same 128 blocks, lane l computing blocks c0 + 32 q + (l & 31), q < 4 (c0 a multiple
-// of 128: the four counters differ in byte 0 alone, as aes_rk_ctr needs). Both rows' schedules come by
-// scalar loads, selected per half-wave (RkHalves). In the tile-major Q (ot_tmaj) rows 2 p and 2 p + 1
+// of 128: the four counters differ in byte 0 alone, as aes_rk_ctr needs). Both rows' schedules are
+// staged in LDS per row pair and read as one ds_read_b128 per round (-5.7 % against per-half-wave
+// global key loads, profiles/r04/ab_ot_expand_pair/). In the tile-major Q (ot_tmaj) rows 2 p and 2 p + 1
 // of a tile are adjacent, so each store instruction writes 8 whole 128-B lines instead of 16 half
 // lines: 263 -> 246 us per configs[1] launch against k_ot_expand<false> (the receiver's pair form
 // measured +0.8 %: its two keys per block keep the one-row form; profiles/r04/ab_ot_expand_pair/).
 __global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
     constexpr int kSlices = 4;
     __shared__ uint32_t tbl_ot[OtTab::kWords];
-    const uint32_t lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
+    // the wave's two row schedules, staged once per row pair: a per-half-wave key read by global
+    // loads put an L2 round trip on every round (vmcnt waits in the AES)
+    __shared__ __attribute__((aligned(16))) uint32_t rk_pair[kOtThreads / 64][2][44];
+    const uint32_t lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31, wv = threadIdx.x >> 6;
+    uint32_t cur_p = ~0u;
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
     const uint64_t tiles_per_pair = (nblk_act + 32 * kSlices - 1) / (32 * kSlices);
@@ -170,6 +175,14 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
         const uint64_t c0 = (t - (uint64_t)p * tiles_per_pair) * 32 * kSlices;
         if (c0 >= nblk_act) continue;   // wave-uniform
         const uint32_t i = 2 * p + half;
+        if (p != cur_p) {   // wave-uniform: the wave's tiles run in contiguous order, mostly one pair
+            if (lane < 44) {
+                rk_pair[wv][0][lane] = a.rk[(size_t)(256 + 2 * p) * 44 + lane];
+                rk_pair[wv][1][lane] = a.rk[(size_t)(257 + 2 * p) * 44 + lane];
+            }
+            cur_p = p;
+            __builtin_amdgcn_wave_barrier();   // one wave's LDS accesses retire in order
+        }
         uint32_t g[kSlices][4];
 #pragma unroll
         for (int q = 0; q < kSlices; q++) {
@@ -179,8 +192,8 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
             g[q][2] = 0u;
             g[q][3] = 0u;
         }
-        aes_halves_rk_ctr<OtTab, kSlices, 0, 0>(g, tbl_ot, b0, b1, a.rk + (size_t)(256 + 2 * p) * 44,
-                                                a.rk + (size_t)(257 + 2 * p) * 44, half != 0);   // G(k_i^{s_i})
+        aes_lds_rk_ctr<OtTab, kSlices, 0, 0>(g, tbl_ot, b0, b1,
+                                             reinterpret_cast<const uint4*>(&rk_pair[wv][half][0]));   // G(k_i^{s_i})
         const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
 #pragma unroll
         for (int q = 0; q < kSlices; q++) {

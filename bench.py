@@ -291,7 +291,9 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic Zipf workload (leader.rs shape), GPU keygen",
         "config": {"workload": f"{n} Zipf clients, data_len {L}, d {d}, threshold {args.threshold}, both servers, "
-                               "GC + OT (ideal base-OT material) every level", "parallelism": "single GPU"},
+                               "GC + correlated OTs every level; drop-in legs: each server's own material and "
+                               "real Chou-Orlandi base OTs over the channel; fused leg: one-seed material, ideal "
+                               "base OTs", "parallelism": "single GPU"},
     }
     c0, c1 = pair()
     t_fused, res = timed(lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False),
@@ -303,17 +305,23 @@ def dropin_bench(args, world, rank, local_rank, dist):
     def dropin_leg(devices=None, channel="inplace"):
         p0, p1 = pair(devices)
         tm = {}
+        last = {}
 
         def run():
             tm.clear()
-            return fhh.two_party_crawl(p0, p1, args.threshold, prf_seed=7, channel=channel, timing=tm, record=False)
+            r = fhh.two_party_crawl(p0, p1, args.threshold, channel=channel, timing=tm, record=False,
+                                    material="fresh")
+            last["r"] = r
+            return r
         t, r = timed(run, reps, warm)
         assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
         tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
-        print(f"dropin: leg devices={devices} channel={channel}: {t:.2f} s", file=sys.stderr, flush=True)
-        return t, {k: v / L * 1e3 for k, v in tm.items()}, tot
+        tot["base_ot"] = r.base_ot_bytes
+        print(f"dropin: leg devices={devices} channel={channel}: {t:.2f} s ({r.base_ot_runs} CO15 runs, "
+              f"crawl waited {r.base_ot_wait_s:.3f} s for them)", file=sys.stderr, flush=True)
+        return t, {k: v / L * 1e3 for k, v in tm.items()}, tot, r
 
-    t_d, per_d, bytes_d = dropin_leg()
+    t_d, per_d, bytes_d, r_d = dropin_leg()
     out.update({
         "value": t_d, "ms_per_step": t_d * 1e3,
         "fused_protocol_crawl_s": t_fused, "dropin_crawl_s": t_d, "dropin_over_fused": t_d / t_fused,
@@ -322,15 +330,18 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",
         "channel_bytes_per_crawl": bytes_d, "channel_bytes_total": sum(bytes_d.values()),
         "heavy_hitters": hh,
+        "dropin_material": "each server its own (os.urandom: label key, Delta, mask per chunk); every level's two OT "
+                           "extensions on Chou-Orlandi base OTs between the servers over the channel",
+        "dropin_base_ot_runs": r_d.base_ot_runs, "dropin_base_ot_wait_s": r_d.base_ot_wait_s,
     })
     if not args.no_party:
-        t_2, per_2, _ = dropin_leg(devices=[local_rank, local_rank])
+        t_2, per_2, _, _ = dropin_leg(devices=[local_rank, local_rank])
         out.update({"dropin_2shard_crawl_s": t_2, "dropin_2shard_over_fused": t_2 / t_fused,
                     "dropin_2shard_ms_per_level": per_2,
                     "dropin_2shard_note": "fhh_create_multi over [this GPU, this GPU]: host reduction of the shards' "
                                           "device-resident sums, one protocol instance per shard"})
     if args.dropin_copy:
-        t_c, per_c, _ = dropin_leg(channel="copy")
+        t_c, per_c, _, _ = dropin_leg(channel="copy")
         out.update({"dropin_copy_crawl_s": t_c, "dropin_copy_over_fused": t_c / t_fused,
                     "dropin_copy_ms_per_level": per_c})
     if args.dropin_host_values:
@@ -551,8 +562,14 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
         "wall_s": wall,
         "heavy_hitters": hh,
         "heavy_hitters_equal_headline": hh == headline_hh,
-        "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per OT extension per level and chunk)",
-        "base_ot_host_ms": s0["base_ot_ms"],
+        "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per OT kind per level; chunks on "
+                   "disjoint row-PRG counters)",
+        "base_ot_instances": s0["base_ot_instances"],
+        "base_ot_compute_ms": s0["base_ot_ms"],
+        "base_ot_stall_ms": s0["base_ot_stall_ms"],
+        "base_ot_note": "compute = summed per-instance CO15 + key-schedule time over the host threads; stall = time "
+                        "the level loop waited for an instance it needed (the base OTs on the critical path)",
+        "protocol": "GC (half-gates, TCCR) + ALSZ correlated OT for the evaluator's labels and the FE share",
         "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
         "expand_gpu_ms": s0["expand_ms"],
         "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,

@@ -52,7 +52,8 @@ EXPORTS = [
     "fhh_gc_equality_device", "fhh_gc_equality_host", "fhh_ot_extend_device", "fhh_ot_extend_host",
     "fhh_create_multi", "fhh_shard_info", "fhh_shard_ctx", "fhh_node_sums_fe_device", "fhh_node_sums_fe255_device",
     "fhh_gb_garble", "fhh_gb_ot_labels", "fhh_gb_ot_shares", "fhh_ev_ot_labels", "fhh_ev_evaluate", "fhh_ev_ot_shares",
-    "fhh_party_node_sums", "fhh_party_bytes_sent", "fhh_gc_party_level_cfg", "fhh_memcpy_device",
+    "fhh_party_node_sums", "fhh_party_bytes_sent", "fhh_gc_party_test_cfgs", "fhh_memcpy_device",
+    "fhh_cot_extend_host", "fhh_gc_cot_host",
     "fhh_shard_plan",
 ]
 
@@ -72,6 +73,8 @@ class FhhStats(ctypes.Structure):
         ("allreduce_timed", ctypes.c_uint64),
         ("gcot_ms", ctypes.c_double),
         ("gcot_timed", ctypes.c_uint64),
+        ("base_ot_stall_ms", ctypes.c_double),
+        ("base_ot_instances", ctypes.c_uint64),
     ]
 
 
@@ -186,19 +189,31 @@ class FhhOtBatch(ctypes.Structure):
     ]
 
 
-class FhhGcPartyCfg(ctypes.Structure):
+class FhhGbCfg(ctypes.Structure):
+    """fhh_gb_cfg: the garbler's (server 0's) own material for one chunk (include/fhh.h)."""
     _fields_ = [
         ("label_key", ctypes.c_uint8 * 16),
         ("delta", ctypes.c_uint8 * 16),
         ("mask", ctypes.c_uint32),
         ("pad_", ctypes.c_uint32),
-        ("share_seed", ctypes.c_uint64),
-        ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
         ("base_chosen", ctypes.c_uint8 * (2 * 128 * 16)),
         ("base_choice", ctypes.c_uint8 * (2 * 16)),
         ("child_begin", ctypes.c_uint64),
         ("child_count", ctypes.c_uint64),
     ]
+
+
+class FhhEvCfg(ctypes.Structure):
+    """fhh_ev_cfg: the evaluator's (server 1's) own material: its base-OT key pairs, nothing else."""
+    _fields_ = [
+        ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
+        ("child_begin", ctypes.c_uint64),
+        ("child_count", ctypes.c_uint64),
+    ]
+
+
+# fhh_cot_extend_host modes (include/fhh.h)
+FHH_COT_LABELS, FHH_COT_FE, FHH_COT_FE255 = 1, 2, 3
 
 
 def build(verbose: bool = False) -> str:
@@ -259,15 +274,18 @@ def lib():
         "fhh_shard_ctx": (i, [vp, i, P(vp)]),
         "fhh_node_sums_fe_device": (i, [vp, P(vp), u64, u32, u64p]),
         "fhh_node_sums_fe255_device": (i, [vp, P(vp), u64, u32, u32p, u32p]),
-        "fhh_gb_garble": (i, [vp, P(FhhGcPartyCfg), P(vp), u64p]),
-        "fhh_gb_ot_labels": (i, [vp, vp, u64, P(vp), u64p]),
+        "fhh_gb_garble": (i, [vp, P(vp), u64p]),
+        "fhh_gb_ot_labels": (i, [vp, P(FhhGbCfg), vp, u64, P(vp), u64p]),
         "fhh_gb_ot_shares": (i, [vp, vp, u64, P(vp), u64p]),
-        "fhh_ev_ot_labels": (i, [vp, P(FhhGcPartyCfg), P(vp), u64p]),
+        "fhh_ev_ot_labels": (i, [vp, P(FhhEvCfg), P(vp), u64p]),
         "fhh_ev_evaluate": (i, [vp, vp, u64, vp, u64, P(vp), u64p]),
         "fhh_ev_ot_shares": (i, [vp, vp, u64]),
         "fhh_party_node_sums": (i, [vp, vp, vp]),
         "fhh_party_bytes_sent": (i, [vp, u64p]),
-        "fhh_gc_party_level_cfg": (i, [u64, u32, P(FhhGcPartyCfg)]),
+        "fhh_gc_party_test_cfgs": (i, [u64, u32, P(FhhGbCfg), P(FhhEvCfg)]),
+        "fhh_cot_extend_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
+        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p,
+                                u8p, u8p]),
         "fhh_memcpy_device": (i, [i, vp, vp, u64]),
         "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),

@@ -2,7 +2,7 @@
 //   fhh_host.cpp   one server's KeyCollection on one GPU (engine, device level loop, C ABI)
 //   fhh_group.cpp  one KeyCollection over several GPUs: clients sharded in 64-client words,
 //                  per-child partials reduced over an in-process RCCL communicator
-//   fhh_party.cpp  the two-party split of the GC equality test + OT extension of tree_crawl
+//   fhh_gcot.cpp   the GC equality test + OT extension of tree_crawl and their two-party split
 //                  (each server's half on its own ctx; only byte buffers cross)
 #pragma once
 #include "fhh_internal.h"
@@ -198,7 +198,7 @@ namespace eng {
 // ---- fhh_host.cpp ----------------------------------------------------------------------------
 int ctx_sync(fhh_ctx* ctx);         // drain the ctx stream, retire its timing events and staging
 int ctx_set_device(fhh_ctx* ctx);   // hipSetDevice(ctx->device)
-ChildArgs ctx_child_args(fhh_ctx* ctx);   // the pending crawl's children as k_share_planes / k_ot_fe_messages read them
+ChildArgs ctx_child_args(fhh_ctx* ctx);   // the pending crawl's children as k_share_planes reads them
 
 // tree_crawl(_last)'s expansion; the share planes [C][2d][nw] (NULL: none) go to a host buffer
 // whose rows are pitch_words u64 wide, this ctx's words starting at word_off (a shard of a
@@ -257,10 +257,11 @@ struct OtOut {            // optional transcript (device pointers into the scrat
     uint64_t nblk = 0;
 };
 int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev);
-int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
-           const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off = 0,
-           const OtFeMsg* fe = nullptr);
+// m OTs of OtArgs a's mode on ctx's stream (fhh_gcot.cpp): sizes, scratch matrices and messages are
+// set here; tr (optional) receives the transcript's device pointers
+int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr);
+// row-PRG blocks a batch of m OTs takes from its base-OT session (a multiple of 256)
+uint64_t ot_session_blocks(uint64_t m);
 
 }  // namespace eng
 }  // namespace fhh

@@ -90,7 +90,10 @@ __device__ __forceinline__ void ld_blk(const uint4* base, uint64_t row, uint64_t
     v[3] = q.w;
 }
 
-template <int B>
+// EVIN (r05, the labels OT is a correlated OT): the evaluator's zero labels are inputs — the C-OT's
+// sender messages H(q_j), at OT index (g B + k) Npad + i of a.ev_labels — and the garbler draws only
+// its own B wires and the mask: W = B + 1 label blocks per test (3 instead of 5 at d = 1).
+template <int B, bool EVIN>
 __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
     // a workgroup without tests leaves before filling 128 KiB of tables (the level loop enqueues a
@@ -103,13 +106,14 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     uint32_t zrk[11][4];
     zero_rk(zrk);
     const uint64_t n = a.G * a.N;
+    const uint64_t Npad = (uint64_t)a.nw * 64;
     const uint32_t D[4] = {a.delta[0], a.delta[1], a.delta[2], a.delta[3]};
     uint32_t lrk[11][4];   // uniform: the label key schedule stays in SGPRs
 #pragma unroll
     for (int r = 0; r < 11; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) lrk[r][c] = a.rk_label[r][c];
-    constexpr int W = 2 * B + 1;
+    constexpr int W = EVIN ? B + 1 : 2 * B + 1;
     // label counter stride: the power of two >= W, so with label_nonce a multiple of it (the level
     // loop and the party ABI use 0) a test's W counters differ in byte 0 alone and a pass of its
     // label blocks shares AES rounds 1-2 (aes_rk_ctr: 133 instead of 160 lookups per extra block)
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         const uint32_t i = (uint32_t)(t - g * a.N);
         const uint64_t tg = a.g_off * a.N + t;       // the test's index in the whole level
         // zero labels, generated per wire pair as the gates consume them (registers do not
-        // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B
+        // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B (EVIN: loaded)
         const uint64_t ctr0 = a.label_nonce + tg * WS;
         // wave-uniform: no lane's counters ctr0 .. ctr0 + W - 1 carry out of byte 0 (always, for an
         // aligned label_nonce; otherwise the pass runs every round in full)
@@ -131,9 +135,9 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
             b[2] = 0u;
             b[3] = 0u;
         };
-        // B <= 2 (d = 1: the metric's configuration): all W <= 5 label blocks in one pass up front, 4
-        // sharing rounds 1-2 with the first, instead of a 2-block pass then a 3-block one (692 instead of
-        // 719 lookups, and 5 independent blocks in flight per lane)
+        // W <= 5 (d = 1, and d = 2 with EVIN): all label blocks in one pass up front, sharing rounds 1-2
+        // with the first (692 instead of 719 lookups at d = 1 without EVIN; 5 / 3 independent blocks in
+        // flight per lane)
         constexpr bool kOnePass = W <= 5;
         uint32_t L[kOnePass ? W : 1][4];
         if constexpr (kOnePass) {
@@ -147,12 +151,34 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         for (int k = 0; k < B; k++) {
             // wires k (garbler) and B + 1 + k (evaluator); the last pair also takes the mask wire B
             uint32_t s[2][4];
+            if constexpr (EVIN) {   // the evaluator's zero label: the C-OT's sender message
+                ld_blk(a.ev_labels, g * B + k, Npad, i, s[1]);
+            }
             if constexpr (kOnePass) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     s[0][c] = L[k][c];
-                    s[1][c] = L[B + 1 + k][c];
+                    if constexpr (!EVIN) s[1][c] = L[B + 1 + k][c];
                     if (k == B - 1) m[0][c] = L[B][c];
+                }
+            } else if constexpr (EVIN) {
+                if (k == B - 1) {   // the garbler's last wire and the mask
+                    uint32_t s2[2][4];
+                    ctr_blk(s2[0], ctr0 + k);
+                    ctr_blk(s2[1], ctr0 + B);
+                    if (shared) aes_rk_ctr<GcTab, 2, 0, 0>(s2, tbl_gc, b0, b1, lrk);
+                    else aes_rk<GcTab, 2>(s2, tbl_gc, b0, b1, lrk);
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        s[0][c] = s2[0][c];
+                        m[0][c] = s2[1][c];
+                    }
+                } else {
+                    uint32_t s1[1][4];
+                    ctr_blk(s1[0], ctr0 + k);
+                    aes_rk<GcTab, 1>(s1, tbl_gc, b0, b1, lrk);
+#pragma unroll
+                    for (int c = 0; c < 4; c++) s[0][c] = s1[0][c];
                 }
             } else if (k == B - 1) {
                 uint32_t s3[3][4];
@@ -175,19 +201,20 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
             }
             // active labels: the garbler's bit (sent in the clear), the evaluator's (via OT)
             const uint32_t gb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
-            const uint32_t eb = a.ev_ot ? 0u : plane_bit(a.ev_planes, a.g_off + g, B, k, a.nw, i);
-            uint32_t x[4], y[4], bz[4];
+            uint32_t x[4], bz[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 x[c] = s[0][c] ^ (gb ? D[c] : 0u);
-                y[c] = s[1][c] ^ (eb ? D[c] : 0u);
                 bz[c] = s[0][c] ^ s[1][c] ^ D[c];   // z_k = NOT(x_k ^ y_k): free XOR, NOT = ^Delta
             }
             st_blk(a.gb_labels, k, n, t, x);
-            // OT sender input x0 = zero label, at OT index (g B + k) Npad + i: the evaluator's share
-            // planes are then the OT's choice bits as they stand (no repacking)
-            if (a.ev_ot) st_blk(a.ev_labels, g * B + k, (uint64_t)a.nw * 64, i, y);
-            else st_blk(a.ev_labels, k, n, t, y);
+            if constexpr (!EVIN) {   // ideal OT: the evaluator's active label (what an OT would deliver)
+                const uint32_t eb = plane_bit(a.ev_planes, a.g_off + g, B, k, a.nw, i);
+                uint32_t y[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++) y[c] = s[1][c] ^ (eb ? D[c] : 0u);
+                st_blk(a.ev_labels, k, n, t, y);
+            }
             if (k == 0) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) acc[c] = bz[c];
@@ -320,7 +347,8 @@ static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     // evaluate at configs[1] but +3.2 % for evaluate and +0.7 % for the whole GC + OT crawl at 1M
     // clients, alternated twice; r03)
     const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
-    if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    if (garble && a.ev_ot) hipLaunchKernelGGL((k_gc_garble<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else if (garble) hipLaunchKernelGGL((k_gc_garble<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
     else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
     return hipGetLastError();
 }

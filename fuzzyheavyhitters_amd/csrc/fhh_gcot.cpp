@@ -148,41 +148,30 @@ int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t 
     return FHH_OK;
 }
 
-// m OTs on ctx's stream. choices: the padded buffer from ot_choices_buffer; rk_dev: the base-OT
-// key schedules [3][128][44] (ideal base OTs); s: the sender's base choice words.
-int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, const uint4* x1,
-           const uint32_t* delta_words, uint4* out, const uint32_t* rk_dev, const uint32_t s_words[4],
-           uint64_t tweak_base, const LoopCtl* ctl, uint64_t per_group, OtOut* tr, uint64_t g_off,
-           const OtFeMsg* fe) {
+// m OTs on ctx's stream (OtArgs in include fhh_internal.h): the caller fills the mode's fields of
+// `a` (mode, choices from ot_choices_buffer or a padded buffer of its own, x0 / x1 / delta, mask, sx,
+// out, rk, s, ctr_off, ctl / per_group / g_off); ot_run sets the sizes and the scratch matrices and
+// messages, then launches receiver expand -> sender expand -> send hash (-> the FieldElm finish) ->
+// receive hash. Mode 0 keeps Y0 | Y1 in ot_buf[5 / 6]; the C-OT modes one y buffer in ot_buf[5].
+int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
     if (m == 0) return FHH_OK;
+    if (a.ctr_off % 256) return ctx->fail(FHH_E_ARG, "ot: the row PRG offset must be a multiple of 256 blocks");
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
     for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
-    for (int k = 5; k < 7; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(m * 16));
-    OtArgs a{};
+    HIP_TRY(ctx, ctx->ot_buf[5].ensure(m * 16));
+    if (a.mode == 0) HIP_TRY(ctx, ctx->ot_buf[6].ensure(m * 16));
     a.m = m;
     a.mp = mp;
-    a.rk = rk_dev;
-    for (int c = 0; c < 4; c++) a.s[c] = s_words[c];
-    a.choices = choices;
     a.T = ctx->ot_buf[0].as<uint4>();
     a.U = ctx->ot_buf[1].as<uint4>();
     a.Q = ctx->ot_buf[2].as<uint4>();
-    a.x0 = x0;
-    a.x1 = x1;
-    if (delta_words)
-        for (int c = 0; c < 4; c++) a.delta[c] = delta_words[c];
     a.Y0 = ctx->ot_buf[5].as<uint4>();
-    a.Y1 = ctx->ot_buf[6].as<uint4>();
-    a.out = out;
-    a.tweak_base = tweak_base;
-    a.ctl = ctl;
-    a.per_group = per_group;
-    a.g_off = g_off;
-    if (fe) a.fe = *fe;   // the send hash computes the messages (x0 / x1 unused)
+    a.Y1 = a.mode == 0 ? ctx->ot_buf[6].as<uint4>() : nullptr;
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
-    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: Y0, Y1
+    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: y (Y0 | Y1)
+    if (a.mode == 3) HIP_TRY(ctx, launch_cot_fe255_finish(a, ctx->stream));
     HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     if (tr) {
         tr->U = a.U;
@@ -192,6 +181,10 @@ int ot_run(fhh_ctx* ctx, uint64_t m, const uint32_t* choices, const uint4* x0, c
     }
     return FHH_OK;
 }
+
+// row-PRG blocks one batch of m OTs takes from its base-OT session (a multiple of 256, the expand
+// kernels' shared-rounds alignment)
+uint64_t ot_session_blocks(uint64_t m) { return (ot_padded(m) / 128 + 255) / 256 * 256; }
 
 }  // namespace eng
 }  // namespace fhh
@@ -297,12 +290,16 @@ int fhh_ot_extend_device(fhh_ctx* ctx, const fhh_ot_batch* b) {
     const uint32_t* rk = nullptr;
     rc = ot_host_keys(ctx, &b->base_seeds[0][0][0], b->base_choice, &rk);
     if (rc) return rc;
-    uint32_t sw[4], dw[4];
-    words_from_bytes(b->base_choice, sw);
-    words_from_bytes(b->delta, dw);
-    rc = ot_run(ctx, b->m, ch, reinterpret_cast<const uint4*>(b->x0_dev), reinterpret_cast<const uint4*>(b->x1_dev),
-                b->x1_dev ? nullptr : dw, reinterpret_cast<uint4*>(b->out_dev), rk, sw, b->tweak_base, nullptr, 0,
-                nullptr);
+    OtArgs a{};
+    a.rk = rk;
+    words_from_bytes(b->base_choice, a.s);
+    a.choices = ch;
+    a.x0 = reinterpret_cast<const uint4*>(b->x0_dev);
+    a.x1 = reinterpret_cast<const uint4*>(b->x1_dev);
+    words_from_bytes(b->delta, a.delta);
+    a.out = reinterpret_cast<uint4*>(b->out_dev);
+    a.tweak_base = b->tweak_base;
+    rc = ot_run(ctx, a, b->m, nullptr);
     if (rc) return rc;
     return ctx_sync(ctx);
 }
@@ -335,11 +332,16 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
     const uint32_t* rk = nullptr;
     rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
     if (rc) return rc;
-    uint32_t sw[4], dw[4] = {0, 0, 0, 0};
-    words_from_bytes(base_choice, sw);
-    if (!x1) words_from_bytes(delta, dw);
-    rc = ot_run(ctx, m, ch, d0.as<uint4>(), x1 ? d1.as<uint4>() : nullptr, x1 ? nullptr : dw, dout.as<uint4>(), rk, sw,
-                tweak_base, nullptr, 0, &tr);
+    OtArgs a{};
+    a.rk = rk;
+    words_from_bytes(base_choice, a.s);
+    a.choices = ch;
+    a.x0 = d0.as<uint4>();
+    a.x1 = x1 ? d1.as<uint4>() : nullptr;
+    if (!x1) words_from_bytes(delta, a.delta);
+    a.out = dout.as<uint4>();
+    a.tweak_base = tweak_base;
+    rc = ot_run(ctx, a, m, &tr);
     if (rc) return rc;
     rc = ctx_sync(ctx);
     if (rc) return rc;
@@ -353,19 +355,172 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
     return FHH_OK;
 }
 
+int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
+                        uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                        uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (mode < FHH_COT_LABELS || mode > FHH_COT_FE255) return ctx->fail(FHH_E_ARG, "cot_extend: mode must be 1, 2 or 3");
+    if (m == 0) return FHH_OK;
+    if (!choices || !out || !base_seeds || !base_choice || (mode == FHH_COT_LABELS && !delta))
+        return ctx->fail(FHH_E_ARG, "cot_extend: NULL argument");
+    if (mode == FHH_COT_FE255 && (m % 2)) return ctx->fail(FHH_E_ARG, "cot_extend: FieldElm shares take OT pairs (m even)");
+    const uint64_t mp = ot_padded(m);
+    std::vector<uint32_t> bits(mp / 32, 0);
+    for (uint64_t j = 0; j < m; j++)
+        if (choices[j] & 1) bits[j / 32] |= 1u << (j % 32);
+    if (mode == FHH_COT_FE255)
+        for (uint64_t t = 0; 2 * t < m; t++)
+            if (((bits[(2 * t) / 32] >> ((2 * t) % 32)) & 1u) != ((bits[(2 * t + 1) / 32] >> ((2 * t + 1) % 32)) & 1u))
+                return ctx->fail(FHH_E_ARG, "cot_extend: a FieldElm OT pair needs one choice for both halves");
+    uint32_t* ch = nullptr;
+    HIP_TRY(ctx, ot_choices_buffer(ctx, m, &ch));
+    HIP_TRY(ctx, hipMemcpyAsync(ch, bits.data(), mp / 8, hipMemcpyHostToDevice, ctx->stream));
+    const size_t per = mode == FHH_COT_FE ? 8 : 16;   // bytes per OT of out / sender values / y
+    DevBuf dsx, dout;
+    HIP_TRY(ctx, dsx.ensure(m * per));
+    HIP_TRY(ctx, dout.ensure(m * per));
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
+    if (rc) return rc;
+    OtArgs a{};
+    a.mode = mode;
+    a.mask = mask & 1u;
+    a.rk = rk;
+    words_from_bytes(base_choice, a.s);
+    a.choices = ch;
+    if (delta) words_from_bytes(delta, a.delta);
+    a.ctr_off = ctr_off;
+    a.sx = dsx.p;
+    a.out = dout.as<uint4>();
+    OtOut tr;
+    rc = ot_run(ctx, a, m, &tr);
+    if (rc) return rc;
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, m * per, hipMemcpyDeviceToHost));
+    if (sender_out) HIP_TRY(ctx, hipMemcpy(sender_out, dsx.p, m * per, hipMemcpyDeviceToHost));
+    if (y_out) HIP_TRY(ctx, hipMemcpy(y_out, tr.Y0, m * per, hipMemcpyDeviceToHost));
+    if (u_out) {
+        const uint64_t nb = (m + 127) / 128;
+        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
+    }
+    return FHH_OK;
+}
+
+int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                    uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
+                    uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                    uint64_t ctr_off, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_zero, uint8_t* ev_active,
+                    uint8_t* decode, uint8_t* out) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc_cot: bits must be in [1, 8]");
+    if (n == 0) return FHH_OK;
+    if (!gb_bits || !ev_bits || !label_key || !delta || !base_seeds || !base_choice || !out)
+        return ctx->fail(FHH_E_ARG, "gc_cot: NULL argument");
+    if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc_cot: n must fit 32 bits");
+    const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad;
+    std::vector<uint64_t> planes[2];
+    const uint8_t* src[2] = {gb_bits, ev_bits};
+    for (int s = 0; s < 2; s++) {
+        planes[s].assign((size_t)bits * nw + ot_padded(m) / 64, 0);   // the evaluator's: OT choice words, padded
+        for (uint64_t t = 0; t < n; t++)
+            for (uint32_t j = 0; j < bits; j++)
+                if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
+    }
+    DevBuf dp[2], dt, dg, de, da, dd, dout, dch;
+    for (int s = 0; s < 2; s++) {
+        HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
+        HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, dt.ensure((size_t)std::max(bits - 1, 1u) * 2 * n * 16));
+    HIP_TRY(ctx, dg.ensure((size_t)(bits + 1) * n * 16));
+    HIP_TRY(ctx, de.ensure(m * 16));
+    HIP_TRY(ctx, da.ensure(m * 16));
+    HIP_TRY(ctx, dd.ensure(n));
+    HIP_TRY(ctx, dout.ensure(n));
+    // 1. the labels C-OT (OtArgs mode 1): choice bits = the evaluator's planes at OT index j npad + i
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
+    if (rc) return rc;
+    fhh_gc_batch gb{};
+    gb.groups = 1;
+    gb.clients = (uint32_t)n;
+    gb.words = (uint32_t)nw;
+    gb.bits = bits;
+    gb.mask = mask;
+    std::memcpy(gb.label_key, label_key, 16);
+    std::memcpy(gb.delta, delta, 16);
+    gb.label_nonce = label_nonce;
+    gb.gate_base = gate_base;
+    gb.gb_planes_dev = dp[0].as<uint64_t>();
+    gb.ev_planes_dev = dp[1].as<uint64_t>();
+    gb.tables_dev = dt.as<uint8_t>();
+    gb.gb_labels_dev = dg.as<uint8_t>();
+    gb.ev_labels_dev = de.as<uint8_t>();
+    gb.decode_dev = dd.as<uint8_t>();
+    gb.out_dev = dout.as<uint8_t>();
+    GcArgs g;
+    rc = gc_args(ctx, &gb, g);
+    if (rc) return rc;
+    OtArgs a{};
+    a.mode = 1;
+    a.rk = rk;
+    words_from_bytes(base_choice, a.s);
+    a.choices = dp[1].as<uint32_t>();
+    for (int c = 0; c < 4; c++) a.delta[c] = g.delta[c];   // the colour-forced Delta
+    a.ctr_off = ctr_off;
+    a.sx = de.p;
+    a.out = da.as<uint4>();
+    rc = ot_run(ctx, a, m, nullptr);
+    if (rc) return rc;
+    // 2. garble on the C-OT's zero labels, 3. evaluate on the OT'd active labels
+    g.ev_ot = 1;
+    HIP_TRY(ctx, launch_gc_garble(g, ctx->stream));
+    g.ev_labels = da.as<uint4>();
+    HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    if (decode) HIP_TRY(ctx, hipMemcpy(decode, dd.p, n, hipMemcpyDeviceToHost));
+    auto soa_to_aos = [&](const DevBuf& d, uint32_t rows_, uint64_t stride, uint8_t* dst) -> int {
+        if (!dst || rows_ == 0) return FHH_OK;
+        std::vector<uint8_t> h((size_t)rows_ * stride * 16);
+        HIP_TRY(ctx, hipMemcpy(h.data(), d.p, h.size(), hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < rows_; r++)
+            for (uint64_t t = 0; t < n; t++)
+                std::memcpy(dst + (t * rows_ + r) * 16, h.data() + ((size_t)r * stride + t) * 16, 16);
+        return FHH_OK;
+    };
+    rc = soa_to_aos(dt, 2 * (bits - 1), n, tables);
+    if (!rc) rc = soa_to_aos(dg, bits + 1, n, gb_labels);
+    if (!rc) rc = soa_to_aos(de, bits, npad, ev_zero);
+    if (!rc) rc = soa_to_aos(da, bits, npad, ev_active);
+    return rc;
+}
+
 }  // extern "C"
 
 // ================================================================================================
 // Two-party split of a level's GC equality test + OT (collect.rs:419-482 with gc_sender = true on
-// server 0 and false on server 1; equalitytest.rs:25-106). Each server's ctx runs only its own
-// half and keeps its own secrets; what crosses is five byte buffers per level, in protocol order:
+// server 0 and false on server 1; equalitytest.rs:25-106). Each server's ctx runs only its own half
+// and holds only its own secrets: the garbler's fhh_gb_cfg (label key, Delta, mask, its base-OT
+// outputs) never reaches the evaluator's ctx, the evaluator's fhh_ev_cfg (its base-OT key pairs)
+// never the garbler's. Five buffers cross per chunk, in protocol order (r05: both OTs correlated):
+//   E -> G  u1      labels C-OT: U (the evaluator's share planes are its choice bits)
+//   G -> E  y1      labels C-OT: y = H(q) ^ Delta ^ H(q ^ s), 16 B per OT
 //   G -> E  gc      the garbled tables, the garbler's active labels (+ mask wire), decode bits
-//   E -> G  u1      OT 1 (the evaluator's input labels, equalitytest.rs:67-82, 108-119): U
-//   G -> E  y1      OT 1: Y0 | Y1
-//   E -> G  u2      OT 2 (the share conversion, collect.rs:437-471 / 846-876): U
-//   G -> E  y2      OT 2: Y0 | Y1
+//   E -> G  u2      share C-OT (collect.rs:437-471 / 846-876): U
+//   G -> E  y2      share C-OT: 8 B per OT (FE), 16 B per OT (FieldElm: 2 OTs per test)
 // Buffers are device memory owned by the producing ctx (valid until its next party call); the
 // caller moves them (a network in a deployment, a device copy in the in-process tests).
+// Counters: each OT kind's base-OT session (the cfg's base material) keeps a running row-PRG
+// counter per ctx, so chunks and levels that extend the same base OTs never repeat pads (ocelot's
+// AlszSender keeps its PRG across `send` calls the same way); a new set of base OTs starts at 0. The
+// garbler's labels and gate tweaks use the test's index in the whole level (child_begin x n + t).
 // ================================================================================================
 namespace fhh {
 namespace eng {
@@ -375,26 +530,26 @@ struct PartyState {
     int step = 0;               // protocol position (calls must come in order)
     bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
     // C = this instance's children: the chunk [c_off, c_off + C) of the level's level_C children
-    // (fhh_gc_party_cfg.child_begin / child_count); covered = children whose OTs are finished
+    // (child_begin / child_count); covered = children whose OTs are finished
     uint64_t c_off = 0, level_C = 0, covered = 0;
     uint32_t level_id = 0;
     bool level_last = false;
     uint64_t C = 0, n = 0, npad = 0, nw = 0, tests = 0, m1 = 0, m2 = 0;
     uint32_t bits = 0, mask = 0, per2 = 1;
-    uint32_t delta[4] = {0, 0, 0, 0};
-    uint32_t s[2][4] = {};      // sender's base choice words per OT
-    GcArgs g{};                 // garbler: the level's garbling arguments
-    DevBuf planes;              // own share planes [C][bits][nw] (evaluator: OT 1's choice bits)
-    DevBuf gc;                  // garbler: the gc message; evaluator: unused
-    DevBuf labels;              // garbler: OT 1 inputs (evaluator zero labels); evaluator: OT 1 outputs
-    DevBuf x0, x1;              // garbler: OT 2 messages (r0 / r1 ordered by the mask), last level only
-    OtFeMsg fe{};               // garbler, FE levels: OT 2's messages drawn inside the send hash
-    DevBuf rk;                  // base-OT key schedules [3][128][44] of the current OT, own rows only
-    DevBuf T, U, Q, Y;          // OT matrices (T / Q private) and messages (U or Y0 | Y1)
+    uint32_t s[2][4] = {};      // garbler: the OT-extension sender's base choice words per OT kind
+    uint64_t ctr[2] = {0, 0};   // this chunk's row-PRG offsets per OT kind (blocks)
+    // per OT kind: the base material of the running session and its next free counter
+    std::vector<uint8_t> sess[2];
+    uint64_t sess_next[2] = {0, 0};
+    GcArgs g{};                 // garbler: the chunk's garbling arguments
+    DevBuf planes;              // own share planes [C][bits][nw] (+ padding: OT 1's choice words)
+    DevBuf gc;                  // garbler: the gc message
+    DevBuf labels;              // garbler: the evaluator's zero labels (C-OT 1 sender messages); evaluator: its active labels
+    DevBuf rk[2];               // base-OT key schedules [3][128][44] per OT kind, own rows only
+    DevBuf T, U, Q, Y;          // OT matrices (T / Q private) and messages (U or y)
     DevBuf choices2;            // evaluator: the GC outputs packed as OT 2's choice words
     DevBuf out;                 // evaluator: GC output bytes (eq ^ mask)
-    DevBuf recv;                // evaluator: OT 2 outputs of the chunk
-    DevBuf vals;                // the level's node values [level_C][n] (x per2 blocks), filled per chunk
+    DevBuf vals;                // the level's node values [level_C][n] (u64, or a BlockPair at the last level)
     std::vector<uint32_t> rk_host;
     uint64_t bytes_sent = 0;    // this ctx's outgoing message bytes for the level
 };
@@ -411,7 +566,7 @@ PartyState& party_of(fhh_ctx* ctx) {
     return *ctx->party;
 }
 
-int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
+int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_count) {
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     if (ctx->group) return ctx->fail(FHH_E_ARG, "party: run the GC + OT per shard (fhh_shard_ctx)");
@@ -421,12 +576,13 @@ int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
     PartyState& P = party_of(ctx);
     const bool last = ctx->phase == Phase::kPendingLast;
     // the chunk of children (collect.rs:423-430: a level's tests split over channels), in order
-    const uint64_t LC = ctx->pending_C, b = cfg->child_begin;
-    if (cfg->child_count == 0 && b != 0) return ctx->fail(FHH_E_ARG, "party: child_begin without child_count");
-    if (b > LC || (cfg->child_count && b == LC && LC))
+    const uint64_t LC = ctx->pending_C, b = child_begin;
+    if (child_count == 0 && b != 0) return ctx->fail(FHH_E_ARG, "party: child_begin without child_count");
+    if (b > LC || (child_count && b == LC && LC))
         return ctx->fail(FHH_E_ARG, "party: child_begin " + std::to_string(b) + " past the level's " +
                                         std::to_string(LC) + " children");
-    if (b != 0 && (P.level_id != ctx->level || P.level_last != last || P.level_C != LC || P.covered != b))
+    if (b != 0 && (P.role != role || P.level_id != ctx->level || P.level_last != last || P.level_C != LC ||
+                   P.covered != b))
         return ctx->fail(FHH_E_STATE, "party: chunk at child " + std::to_string(b) + " does not follow the level's " +
                                           "finished children (" + std::to_string(P.covered) + ")");
     P.role = role;
@@ -437,7 +593,7 @@ int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
     P.level_C = LC;
     if (b == 0) P.covered = 0;
     P.c_off = b;
-    P.C = cfg->child_count ? std::min<uint64_t>(cfg->child_count, LC - b) : LC;
+    P.C = child_count ? std::min<uint64_t>(child_count, LC - b) : LC;
     P.n = ctx->n;
     P.npad = ctx->npad;
     P.nw = ctx->nw;
@@ -447,62 +603,65 @@ int party_begin(fhh_ctx* ctx, int role, const fhh_gc_party_cfg* cfg) {
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
     P.m2 = P.tests * P.per2;
     if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
-    // this server's share planes [C][bits][nw] of the chunk (collect.rs:393-418)
-    HIP_TRY(ctx, P.planes.ensure(std::max<uint64_t>(P.C * P.bits * P.nw, 1) * 8));
+    // this server's share planes [C][bits][nw] of the chunk (collect.rs:393-418), zero-padded to the
+    // OT's whole choice words (ot_padded(m1) bits)
+    const uint64_t plane_words = P.C * P.bits * P.nw, pad_words = ot_padded(std::max<uint64_t>(P.m1, 1)) / 64;
+    HIP_TRY(ctx, P.planes.ensure(std::max(plane_words, pad_words) * 8));
+    HIP_TRY(ctx, hipMemsetAsync(P.planes.p, 0, std::max(plane_words, pad_words) * 8, ctx->stream));
     if (P.C) {
         ChildArgs a = ctx_child_args(ctx);
         a.c_off = P.c_off;
         a.c_cnt = P.C;
         HIP_TRY(ctx, launch_share_planes(a, P.planes.as<uint64_t>(), ctx->stream));
     }
-    // the level's node values, one row of n per child (a block, or a BlockPair at the last level)
-    if (b == 0) HIP_TRY(ctx, P.vals.ensure(std::max<uint64_t>(LC * P.n * P.per2, 1) * 16));
+    // the level's node values, one row of n per child (u64 FE, or a BlockPair at the last level)
+    if (b == 0) HIP_TRY(ctx, P.vals.ensure(std::max<uint64_t>(LC * P.n * P.per2, 1) * (P.last ? 16 : 8)));
     return FHH_OK;
 }
 
-// a finished chunk's node values into the level's rows [c_off, c_off + C) (the evaluator's OT 2
-// outputs, or the garbler's r1 = its message for the mask's other side, collect.rs:439-472);
-// chunk_vals == nullptr: already written there (the garbler's FE levels)
-int party_chunk_done(fhh_ctx* ctx, PartyState& P, const void* chunk_vals) {
-    const uint64_t bytes = P.C * P.n * P.per2 * 16;
-    if (bytes && chunk_vals)
-        HIP_TRY(ctx, hipMemcpyAsync(P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * 16, chunk_vals, bytes,
-                                    hipMemcpyDeviceToDevice, ctx->stream));
-    P.covered = P.c_off + P.C;
-    return FHH_OK;
+// base-OT session of OT kind w: the same material as the running session continues its counter,
+// new material starts a session at 0; the chunk's m OTs take the next blocks
+void party_session(PartyState& P, int w, const uint8_t* mat, size_t bytes, uint64_t m) {
+    if (P.sess[w].size() != bytes || std::memcmp(P.sess[w].data(), mat, bytes) != 0) {
+        P.sess[w].assign(mat, mat + bytes);
+        P.sess_next[w] = 0;
+    }
+    P.ctr[w] = P.sess_next[w];
+    P.sess_next[w] += m ? ot_session_blocks(m) : 0;
 }
 
-// key schedules of one OT's base OTs into P.rk: receiver rows 0 / 1 from both seeds of each base
-// OT, sender row 2 from its chosen seeds (the other party's rows stay zero: never read)
-int party_keys(fhh_ctx* ctx, PartyState& P, const uint8_t* pairs /*[128][2][16] or null*/,
+// key schedules of OT kind w's base OTs into P.rk[w]: receiver rows 0 / 1 from both seeds of each
+// base OT, sender row 2 from its chosen seeds (the other party's rows stay zero: never read)
+int party_keys(fhh_ctx* ctx, PartyState& P, int w, const uint8_t* pairs /*[128][2][16] or null*/,
                const uint8_t* chosen /*[128][16] or null*/) {
     P.rk_host.assign((size_t)3 * 128 * 44, 0);
     for (int i = 0; i < 128; i++) {
-        uint32_t w[11][4];
+        uint32_t k[11][4];
         for (int b = 0; b < 2 && pairs; b++) {
-            host_key_schedule(pairs + ((size_t)i * 2 + b) * 16, w);
-            std::memcpy(P.rk_host.data() + ((size_t)b * 128 + i) * 44, w, 44 * 4);
+            host_key_schedule(pairs + ((size_t)i * 2 + b) * 16, k);
+            std::memcpy(P.rk_host.data() + ((size_t)b * 128 + i) * 44, k, 44 * 4);
         }
         if (chosen) {
-            host_key_schedule(chosen + (size_t)i * 16, w);
-            std::memcpy(P.rk_host.data() + ((size_t)2 * 128 + i) * 44, w, 44 * 4);
+            host_key_schedule(chosen + (size_t)i * 16, k);
+            std::memcpy(P.rk_host.data() + ((size_t)2 * 128 + i) * 44, k, 44 * 4);
         }
     }
-    HIP_TRY(ctx, P.rk.ensure(P.rk_host.size() * 4));
-    HIP_TRY(ctx, hipMemcpyAsync(P.rk.p, P.rk_host.data(), P.rk_host.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, P.rk[w].ensure(P.rk_host.size() * 4));
+    HIP_TRY(ctx, hipMemcpyAsync(P.rk[w].p, P.rk_host.data(), P.rk_host.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     // the staging vector is rewritten by the next call: finish the copy now
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return FHH_OK;
 }
 
-OtArgs party_ot(PartyState& P, uint64_t m) {
+OtArgs party_ot(PartyState& P, int w, uint64_t m) {
     OtArgs a{};
     a.m = m;
     a.mp = ot_padded(m);
-    a.rk = P.rk.as<uint32_t>();
+    a.rk = P.rk[w].as<uint32_t>();
     a.T = P.T.as<uint4>();
     a.U = P.U.as<uint4>();
     a.Q = P.Q.as<uint4>();
+    a.ctr_off = P.ctr[w];
     return a;
 }
 
@@ -510,13 +669,14 @@ int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver) {
     const uint64_t rows = 16 * ot_padded(m);   // [128][mp / 128] blocks
     HIP_TRY(ctx, (receiver ? P.T : P.Q).ensure(rows));
     if (receiver) HIP_TRY(ctx, P.U.ensure(rows));
-    else HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 32));
+    else HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 16));
     return FHH_OK;
 }
 
 // message sizes
 uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
 uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)(2 * (P.bits - 1) + P.bits + 1) * 16 + 1); }
+uint64_t y2_bytes(const PartyState& P) { return P.m2 * (P.last ? 16 : 8); }
 
 int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const char* what) {
     if (want && !p) return ctx->fail(FHH_E_ARG, std::string("party: NULL ") + what);
@@ -534,23 +694,71 @@ void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
     g.decode = base + (uint64_t)(2 * (P.bits - 1) + P.bits + 1) * t * 16;
 }
 
+// the chunk's label nonce and gate tweaks: the test's index in the whole level (c_off n + t)
+uint64_t party_label_nonce(const PartyState& P) {
+    const uint64_t W = P.bits + 1;
+    uint64_t WS = 4;
+    while (WS < W) WS *= 2;
+    return P.c_off * P.n * WS;
+}
+uint64_t party_gate_base(const PartyState& P) { return P.c_off * P.n * (P.bits - 1); }
+
 }  // namespace
 }  // namespace eng
 }  // namespace fhh
 
 extern "C" {
 
-int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes) {
+int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev, uint64_t* u_len) {
     CTX_CHECK(ctx);
-    if (!cfg || !gc_msg_dev || !gc_msg_bytes) return ctx->fail(FHH_E_ARG, "gb_garble: NULL argument");
-    int rc = party_begin(ctx, 0, cfg);
+    if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
+    int rc = party_begin(ctx, 1, cfg->child_begin, cfg->child_count);
     if (rc) return rc;
     PartyState& P = *ctx->party;
+    // both OT kinds' receiver schedules and session counters (OtReceiver::init, collect.rs:460)
+    party_session(P, 0, &cfg->base_pairs[0][0][0][0], 128 * 32, P.m1);
+    party_session(P, 1, &cfg->base_pairs[1][0][0][0], 128 * 32, P.m2);
+    rc = party_keys(ctx, P, 0, &cfg->base_pairs[0][0][0][0], nullptr);
+    if (!rc) rc = party_keys(ctx, P, 1, &cfg->base_pairs[1][0][0][0], nullptr);
+    if (rc) return rc;
+    rc = party_ot_buffers(ctx, P, P.m1, true);
+    if (rc) return rc;
+    if (P.m1) {   // OT 1's receiver: choice bits = this server's share planes as they stand
+        OtArgs a = party_ot(P, 0, P.m1);
+        a.choices = P.planes.as<uint32_t>();
+        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));   // T, U
+    }
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 1;
+    *u_dev = P.U.as<uint8_t>();
+    *u_len = P.m1 ? u_bytes(P.m1) : 0;
+    P.bytes_sent += *u_len;
+    return FHH_OK;
+}
+
+int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev,
+                     uint64_t* y_len) {
+    CTX_CHECK(ctx);
+    if (!cfg || !y_dev || !y_len) return ctx->fail(FHH_E_ARG, "gb_ot_labels: NULL argument");
+    int rc = party_begin(ctx, 0, cfg->child_begin, cfg->child_count);
+    if (rc) return rc;
+    PartyState& P = *ctx->party;
+    rc = check_in(ctx, u_dev, u_len, P.m1 ? u_bytes(P.m1) : 0, "U (labels OT)");
+    if (rc) return rc;
     P.mask = cfg->mask & 1u;
-    words_from_bytes(cfg->base_choice[0], P.s[0]);
-    words_from_bytes(cfg->base_choice[1], P.s[1]);
-    // garbling (multiple_gb_equality_test, equalitytest.rs:25-65): the evaluator's zero labels are
-    // stored as OT 1's sender inputs at the OT index of the evaluator's choice bits
+    // both OT kinds' sender schedules and session counters (OtSender::init, collect.rs:454)
+    for (int w = 0; w < 2; w++) {
+        std::vector<uint8_t> mat((size_t)128 * 16 + 16);
+        std::memcpy(mat.data(), &cfg->base_chosen[w][0][0], 128 * 16);
+        std::memcpy(mat.data() + 128 * 16, cfg->base_choice[w], 16);
+        party_session(P, w, mat.data(), mat.size(), w ? P.m2 : P.m1);
+        words_from_bytes(cfg->base_choice[w], P.s[w]);
+        rc = party_keys(ctx, P, w, nullptr, &cfg->base_chosen[w][0][0]);
+        if (rc) return rc;
+    }
+    // the garbling arguments of the chunk (multiple_gb_equality_test, equalitytest.rs:25-65); the
+    // evaluator's zero labels are OT 1's sender messages, at the OT index of its choice bits
     HIP_TRY(ctx, P.gc.ensure(std::max<uint64_t>(gc_bytes(P), 1)));
     HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
     fhh_gc_batch gb{};
@@ -561,6 +769,8 @@ int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_
     gb.mask = P.mask;
     std::memcpy(gb.label_key, cfg->label_key, 16);
     std::memcpy(gb.delta, cfg->delta, 16);
+    gb.label_nonce = party_label_nonce(P);
+    gb.gate_base = party_gate_base(P);
     gb.gb_planes_dev = P.planes.as<uint64_t>();
     gb.ev_planes_dev = P.planes.as<uint64_t>();   // not read: the evaluator's labels go by OT
     gb.tables_dev = P.gc.as<uint8_t>();
@@ -573,137 +783,45 @@ int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_
     gc_layout(P, P.gc.as<uint8_t>(), P.g);
     P.g.ev_ot = 1;
     P.g.out = nullptr;
-    for (int c = 0; c < 4; c++) P.delta[c] = P.g.delta[c];
-    if (P.tests) HIP_TRY(ctx, launch_gc_garble(P.g, ctx->stream));
-    // OT 2's messages: (r0, r1) if the mask is set, else (r1, r0) (collect.rs:439-452, 846-866); the
-    // garbler's node value is r1. FE levels: r1 straight into the level's rows, and the send hash
-    // draws (r0, r1) from the same PRF (OtFeMsg) instead of reading 32 B per OT back; the last
-    // level's FieldElm messages keep their buffers
-    P.fe = OtFeMsg{};
-    if (P.last) {
-        HIP_TRY(ctx, P.x0.ensure(std::max<uint64_t>(P.m2, 1) * 16));
-        HIP_TRY(ctx, P.x1.ensure(std::max<uint64_t>(P.m2, 1) * 16));
-    }
-    if (P.tests) {
-        ChildArgs a = ctx_child_args(ctx);   // the chunk's children
-        a.c_off = P.c_off;
-        a.c_cnt = P.C;
-        a.prf_seed = cfg->share_seed;
-        a.gc_N = (uint32_t)P.n;
-        if (P.last) {
-            HIP_TRY(ctx, launch_ot_fe255_messages(a, P.mask, P.x0.as<uint4>(), P.x1.as<uint4>(), ctx->stream));
-        } else {
-            HIP_TRY(ctx, launch_ot_fe_messages(a, P.mask, P.vals.as<uint4>() + P.c_off * P.n, nullptr, ctx->stream));
-            P.fe.base = host_mix64(cfg->share_seed ^ (uint64_t)a.level);   // k_ot_fe_messages: mix64(prf ^ level)
-            P.fe.client_base = a.client_base;
-            P.fe.c_off = P.c_off;
-            P.fe.n = (uint32_t)P.n;
-            P.fe.mask = P.mask;
-        }
-    }
-    // both OTs' sender schedules now (OtSender::init per OT, collect.rs:454-471)
-    rc = party_keys(ctx, P, nullptr, &cfg->base_chosen[0][0][0]);
+    // OT 1 as a correlated OT (gb_set_fancy_inputs, equalitytest.rs:67-82): x0 = H(q_j) becomes the
+    // evaluator's zero label of its share bit j, x1 = x0 ^ Delta; y = x0 ^ Delta ^ H(q_j ^ s)
+    rc = party_ot_buffers(ctx, P, P.m1, false);
     if (rc) return rc;
+    if (P.m1) {
+        OtArgs a = party_ot(P, 0, P.m1);
+        a.mode = 1;
+        a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
+        for (int c = 0; c < 4; c++) a.s[c] = P.s[0][c];
+        for (int c = 0; c < 4; c++) a.delta[c] = P.g.delta[c];
+        a.sx = P.labels.p;
+        a.Y0 = P.Y.as<uint4>();
+        HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
+        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // zero labels, y
+    }
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 1;
-    *gc_msg_dev = P.gc.as<uint8_t>();
-    *gc_msg_bytes = gc_bytes(P);
-    P.bytes_sent += *gc_msg_bytes;
-    // keep OT 2's chosen seeds for fhh_gb_ot_shares
-    P.rk_host.resize((size_t)3 * 128 * 44 + 128 * 16);
-    std::memcpy(reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), &cfg->base_chosen[1][0][0],
-                128 * 16);
+    *y_dev = P.Y.as<uint8_t>();
+    *y_len = P.m1 * 16;
+    P.bytes_sent += *y_len;
     return FHH_OK;
 }
 
-static int gb_ot_send(fhh_ctx* ctx, int which, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev,
-                      uint64_t* y_bytes) {
+int fhh_gb_garble(fhh_ctx* ctx, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes) {
     CTX_CHECK(ctx);
-    if (!y_dev || !y_bytes) return ctx->fail(FHH_E_ARG, "gb_ot: NULL output");
+    if (!gc_msg_dev || !gc_msg_bytes) return ctx->fail(FHH_E_ARG, "gb_garble: NULL argument");
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     PartyState* Pp = ctx->party;
-    if (!Pp || Pp->role != 0 || Pp->step != 1 + which)
-        return ctx->fail(FHH_E_STATE, which ? "gb_ot_shares: call after fhh_gb_ot_labels" : "gb_ot_labels: call after fhh_gb_garble");
+    if (!Pp || Pp->role != 0 || Pp->step != 1) return ctx->fail(FHH_E_STATE, "gb_garble: call after fhh_gb_ot_labels");
     PartyState& P = *Pp;
-    const uint64_t m = which ? P.m2 : P.m1;
-    rc = check_in(ctx, u_dev, u_len, m ? u_bytes(m) : 0, "U");
-    if (rc) return rc;
-    if (which) {   // OT 2's schedules from the chosen seeds kept by fhh_gb_garble
-        std::vector<uint8_t> chosen(128 * 16);
-        std::memcpy(chosen.data(), reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), 128 * 16);
-        rc = party_keys(ctx, P, nullptr, chosen.data());
-        if (rc) return rc;
-    }
-    rc = party_ot_buffers(ctx, P, m, false);
-    if (rc) return rc;
-    if (m) {
-        OtArgs a = party_ot(P, m);
-        a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
-        for (int c = 0; c < 4; c++) a.s[c] = P.s[which][c];
-        a.Y0 = P.Y.as<uint4>();
-        a.Y1 = P.Y.as<uint4>() + m;
-        if (which && P.last) {
-            a.x0 = P.x0.as<uint4>();
-            a.x1 = P.x1.as<uint4>();
-        } else if (which) {
-            a.fe = P.fe;   // (r0, r1) from the PRF inside the send hash
-        } else {   // correlated: x1 = x0 ^ Delta (the evaluator's one labels)
-            a.x0 = P.labels.as<uint4>();
-            a.x1 = nullptr;
-            for (int c = 0; c < 4; c++) a.delta[c] = P.delta[c];
-        }
-        HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
-        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // Y0, Y1
-    }
-    if (which) {   // the chunk is done on this side: its node values r1 into the level's rows
-        rc = party_chunk_done(ctx, P, P.last ? (P.mask ? P.x1.p : P.x0.p) : nullptr);
-        if (rc) return rc;
-    }
+    if (P.tests) HIP_TRY(ctx, launch_gc_garble(P.g, ctx->stream));
     rc = ctx_sync(ctx);
     if (rc) return rc;
-    P.step = 2 + which;
-    *y_dev = P.Y.as<uint8_t>();
-    *y_bytes = m * 32;
-    P.bytes_sent += *y_bytes;
-    return FHH_OK;
-}
-
-int fhh_gb_ot_labels(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev, uint64_t* y_bytes) {
-    return gb_ot_send(ctx, 0, u_dev, u_len, y_dev, y_bytes);
-}
-
-int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev, uint64_t* y_bytes) {
-    return gb_ot_send(ctx, 1, u_dev, u_len, y_dev, y_bytes);
-}
-
-int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** u_dev, uint64_t* u_len) {
-    CTX_CHECK(ctx);
-    if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
-    int rc = party_begin(ctx, 1, cfg);
-    if (rc) return rc;
-    PartyState& P = *ctx->party;
-    // OT 1's receiver: choice bits = this server's share planes as they stand (m1 = C bits npad)
-    rc = party_keys(ctx, P, &cfg->base_pairs[0][0][0][0], nullptr);
-    if (rc) return rc;
-    // keep OT 2's seed pairs for fhh_ev_evaluate
-    P.rk_host.resize((size_t)3 * 128 * 44 + 128 * 32);
-    std::memcpy(reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), &cfg->base_pairs[1][0][0][0],
-                128 * 32);
-    rc = party_ot_buffers(ctx, P, P.m1, true);
-    if (rc) return rc;
-    if (P.m1) {
-        OtArgs a = party_ot(P, P.m1);
-        a.choices = P.planes.as<uint32_t>();
-        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));   // T, U
-    }
-    rc = ctx_sync(ctx);
-    if (rc) return rc;
-    P.step = 1;
-    *u_dev = P.U.as<uint8_t>();
-    *u_len = P.m1 ? u_bytes(P.m1) : 0;
-    P.bytes_sent += *u_len;
+    P.step = 2;
+    *gc_msg_dev = P.gc.as<uint8_t>();
+    *gc_msg_bytes = gc_bytes(P);
+    P.bytes_sent += *gc_msg_bytes;
     return FHH_OK;
 }
 
@@ -718,15 +836,15 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     PartyState& P = *Pp;
     rc = check_in(ctx, gc_msg_dev, gc_len, gc_bytes(P), "gc message");
     if (rc) return rc;
-    rc = check_in(ctx, y_dev, y_len, P.m1 * 32, "Y (labels OT)");
+    rc = check_in(ctx, y_dev, y_len, P.m1 * 16, "y (labels OT)");
     if (rc) return rc;
     // 1. OT 1 output: the evaluator's active input labels (ev_set_fancy_inputs, equalitytest.rs:108-119)
     HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
     if (P.m1) {
-        OtArgs a = party_ot(P, P.m1);
+        OtArgs a = party_ot(P, 0, P.m1);
+        a.mode = 1;
         a.choices = P.planes.as<uint32_t>();
         a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
-        a.Y1 = a.Y0 + P.m1;
         a.out = P.labels.as<uint4>();
         HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     }
@@ -740,6 +858,7 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     g.N = (uint32_t)P.n;
     g.nw = (uint32_t)P.nw;
     g.bits = P.bits;
+    g.gate_base = party_gate_base(P);
     gc_layout(P, const_cast<uint8_t*>(gc_msg_dev), g);
     g.ev_labels = P.labels.as<uint4>();
     g.ev_ot = 1;
@@ -748,16 +867,10 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     g.out_dup = P.per2;
     if (P.tests) HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
     // 3. OT 2's receiver: choice = the GC output (collect.rs:461-471); T and U reused
-    std::vector<uint8_t> pairs(128 * 32);
-    std::memcpy(pairs.data(), reinterpret_cast<uint8_t*>(P.rk_host.data() + (size_t)3 * 128 * 44), 128 * 32);
-    rc = ctx_sync(ctx);   // the evaluation read the previous schedules' neighbours only; drain before re-keying
-    if (rc) return rc;
-    rc = party_keys(ctx, P, pairs.data(), nullptr);
-    if (rc) return rc;
     rc = party_ot_buffers(ctx, P, P.m2, true);
     if (rc) return rc;
     if (P.m2) {
-        OtArgs a = party_ot(P, P.m2);
+        OtArgs a = party_ot(P, 1, P.m2);
         a.choices = P.choices2.as<uint32_t>();
         HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));
     }
@@ -770,6 +883,43 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     return FHH_OK;
 }
 
+int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const uint8_t** y_dev, uint64_t* y_len) {
+    CTX_CHECK(ctx);
+    if (!y_dev || !y_len) return ctx->fail(FHH_E_ARG, "gb_ot_shares: NULL output");
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    PartyState* Pp = ctx->party;
+    if (!Pp || Pp->role != 0 || Pp->step != 2) return ctx->fail(FHH_E_STATE, "gb_ot_shares: call after fhh_gb_garble");
+    PartyState& P = *Pp;
+    rc = check_in(ctx, u_dev, u_len, P.m2 ? u_bytes(P.m2) : 0, "U (shares OT)");
+    if (rc) return rc;
+    rc = party_ot_buffers(ctx, P, P.m2, false);
+    if (rc) return rc;
+    if (P.m2) {
+        // OT 2 as a correlated OT (collect.rs:439-471): pair[0] = H(q_j) read as the share (FE: a LE u128
+        // mod p; FieldElm: the OT pair's 32 big-endian bytes mod p), pair[1] = pair[0] +- 1 as the mask
+        // orders (r0, r1); this server's node value r1 goes straight into the level's rows
+        OtArgs a = party_ot(P, 1, P.m2);
+        a.mode = P.last ? 3 : 2;
+        a.mask = P.mask;
+        a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
+        for (int c = 0; c < 4; c++) a.s[c] = P.s[1][c];
+        a.sx = P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * (P.last ? 16 : 8);
+        a.Y0 = P.Y.as<uint4>();
+        HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));
+        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));
+        if (P.last) HIP_TRY(ctx, launch_cot_fe255_finish(a, ctx->stream));
+    }
+    P.covered = P.c_off + P.C;
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    P.step = 3;
+    *y_dev = P.Y.as<uint8_t>();
+    *y_len = y2_bytes(P);
+    P.bytes_sent += *y_len;
+    return FHH_OK;
+}
+
 int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_len) {
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
@@ -777,19 +927,17 @@ int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_len) {
     PartyState* Pp = ctx->party;
     if (!Pp || Pp->role != 1 || Pp->step != 2) return ctx->fail(FHH_E_STATE, "ev_ot_shares: call after fhh_ev_evaluate");
     PartyState& P = *Pp;
-    rc = check_in(ctx, y_dev, y_len, P.m2 * 32, "Y (shares OT)");
+    rc = check_in(ctx, y_dev, y_len, y2_bytes(P), "y (shares OT)");
     if (rc) return rc;
-    HIP_TRY(ctx, P.recv.ensure(std::max<uint64_t>(P.m2, 1) * 16));
-    if (P.m2) {
-        OtArgs a = party_ot(P, P.m2);
+    if (P.m2) {   // the OT outputs are this server's node values, straight into the level's rows
+        OtArgs a = party_ot(P, 1, P.m2);
+        a.mode = P.last ? 3 : 2;
         a.choices = P.choices2.as<uint32_t>();
         a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
-        a.Y1 = a.Y0 + P.m2;
-        a.out = P.recv.as<uint4>();
+        a.out = reinterpret_cast<uint4*>(P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * (P.last ? 16 : 8));
         HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     }
-    rc = party_chunk_done(ctx, P, P.recv.p);   // the OT outputs are this server's node values
-    if (rc) return rc;
+    P.covered = P.c_off + P.C;
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 3;
@@ -821,21 +969,20 @@ int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
             v[(size_t)k] = P->vals.p;
         }
         if (last < 0) return ctx->fail(FHH_E_STATE, "party_node_sums: no shard holds clients");
-        const uint32_t fmt = last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
+        const uint32_t fmt = last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_U64;
         return group_node_sums(ctx, v.data(), false, 0, fmt, sums_a, sums_b);   // ld 0: each shard's n
     }
     PartyState* Pp = ctx->party;
     if (!Pp || Pp->step != 3 || Pp->covered != Pp->level_C)
         return ctx->fail(FHH_E_STATE, "party_node_sums: the level's OTs are not finished for every child");
     PartyState& P = *Pp;
-    // the garbler's value is r1 = its message for the mask's other side, the evaluator's its OT output
-    // (gathered per chunk into P.vals); rows of n values, FE in a block's low 8 bytes, FieldElm as a
-    // BlockPair (2 blocks)
-    const void* v = P.vals.p;
-    const uint32_t fmt = P.last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_BLOCK;
-    const void* vv[1] = {v};
-    if (P.last) return fhh_node_sums_fe255_device(ctx, vv, P.n, fmt, static_cast<uint32_t*>(sums_a), static_cast<uint32_t*>(sums_b));
-    return fhh_node_sums_fe_device(ctx, vv, P.n, fmt, static_cast<uint64_t*>(sums_a));
+    // the garbler's value is r1 = v + mask, the evaluator's its C-OT output (written per chunk into
+    // P.vals); rows of n values: FE as u64, FieldElm as a BlockPair (2 blocks)
+    const void* vv[1] = {P.vals.p};
+    if (P.last)
+        return fhh_node_sums_fe255_device(ctx, vv, P.n, FHH_VALS_FE255_BLOCKPAIR, static_cast<uint32_t*>(sums_a),
+                                          static_cast<uint32_t*>(sums_b));
+    return fhh_node_sums_fe_device(ctx, vv, P.n, FHH_VALS_FE_U64, static_cast<uint64_t*>(sums_a));
 }
 
 int fhh_party_bytes_sent(const fhh_ctx* ctx, uint64_t* bytes) {
@@ -844,18 +991,21 @@ int fhh_party_bytes_sent(const fhh_ctx* ctx, uint64_t* bytes) {
     return FHH_OK;
 }
 
-int fhh_gc_party_level_cfg(uint64_t prf_seed, uint32_t level, fhh_gc_party_cfg* out) {
-    if (!out) {
-        g_err = "gc_party_level_cfg: NULL output";
+// TEST MODE: the in-process level loop's material (fhh_sim_crawl gc = 2 with ideal base OTs) for
+// prf_seed and level, split into the two parties' configs. Deterministic from one seed, so NOT private:
+// a deployment draws each party's material on its own side (fuzzyheavyhitters_amd.party).
+int fhh_gc_party_test_cfgs(uint64_t prf_seed, uint32_t level, fhh_gb_cfg* gb, fhh_ev_cfg* ev) {
+    if (!gb || !ev) {
+        g_err = "gc_party_test_cfgs: NULL output";
         return FHH_E_ARG;
     }
-    std::memset(out, 0, sizeof(*out));
-    gc_level_material(prf_seed, level, out->label_key, out->delta, &out->mask);
-    out->share_seed = prf_seed;
+    std::memset(gb, 0, sizeof(*gb));
+    std::memset(ev, 0, sizeof(*ev));
+    gc_level_material(prf_seed, level, gb->label_key, gb->delta, &gb->mask);
     for (uint32_t salt = 0; salt < 2; salt++) {
         uint32_t sw[4];
         ot_level_choice(prf_seed, level, salt, sw);
-        std::memcpy(out->base_choice[salt], sw, 16);
+        std::memcpy(gb->base_choice[salt], sw, 16);
         for (uint32_t i = 0; i < 128; i++) {
             const uint32_t si = (sw[i >> 5] >> (i & 31)) & 1u;
             for (uint32_t b = 0; b < 2; b++) {
@@ -863,10 +1013,10 @@ int fhh_gc_party_level_cfg(uint64_t prf_seed, uint32_t level, fhh_gc_party_cfg* 
                 const uint64_t z = host_mix64(prf_seed ^ 0x6f745f62617365ull ^ ((uint64_t)level << 24) ^
                                               ((uint64_t)salt << 20) ^ ((uint64_t)i << 2) ^ b);
                 const uint64_t lo = z, hi = host_mix64(z);
-                std::memcpy(out->base_pairs[salt][i][b], &lo, 8);
-                std::memcpy(out->base_pairs[salt][i][b] + 8, &hi, 8);
+                std::memcpy(ev->base_pairs[salt][i][b], &lo, 8);
+                std::memcpy(ev->base_pairs[salt][i][b] + 8, &hi, 8);
             }
-            std::memcpy(out->base_chosen[salt][i], out->base_pairs[salt][i][si], 16);
+            std::memcpy(gb->base_chosen[salt][i], ev->base_pairs[salt][i][si], 16);
         }
     }
     return FHH_OK;

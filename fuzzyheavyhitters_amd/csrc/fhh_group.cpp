@@ -525,6 +525,8 @@ int group_get_stats(const fhh_ctx* g, fhh_stats* out) {
         t.keygen_ms += v.keygen_ms;
         t.expand_launches_timed += v.expand_launches_timed;
         t.base_ot_ms += v.base_ot_ms;
+        t.base_ot_stall_ms += v.base_ot_stall_ms;
+        t.base_ot_instances += v.base_ot_instances;
         t.allreduce_ms += v.allreduce_ms;
         t.allreduce_timed += v.allreduce_timed;
         t.gcot_ms += v.gcot_ms;

@@ -732,13 +732,16 @@ struct PhaseClock {
     }
 };
 
-// Host producer of the real base OTs (fhh_sim_config.base_ot). Every OT extension of the crawl —
-// level lv, chunk k: the evaluator's labels (salt 2 k) and the share conversion (salt 2 k + 1) —
-// starts from its own 128 Chou–Orlandi OTs (AlszSender/AlszReceiver::init per channel and level,
-// collect.rs:454-471). The level loop requests instances (lv, salt) ahead of the level it enqueues
-// (the chunk count of a level follows the loop's capacity, so it is known only then); worker threads
-// compute them in request order with their key schedules [3][128][44] (receiver k_i^0, k_i^1; sender
-// k_i^{s_i}); wait(i) blocks until request i is done.
+// Host producer of the real base OTs (fhh_sim_config.base_ot). Each level's two OT extensions — kind
+// 0 the evaluator's labels, kind 1 the share conversion — start from their own 128 Chou–Orlandi OTs
+// (AlszSender/AlszReceiver::init per channel and level, collect.rs:454-471); the level's chunks extend
+// them from disjoint row-PRG counters. The level loop requests instances (lv, kind) a few levels ahead
+// of the level it enqueues; worker threads compute them in request order with their key schedules
+// [3][128][44] (receiver k_i^0, k_i^1; sender k_i^{s_i}); wait(i) blocks until request i is done.
+// Accounting (fhh_stats): compute_ms sums every instance's own CO15 + key-schedule time over the
+// workers (the host CPU the base OTs cost), stall_ms is the time the enqueueing thread spent blocked
+// in wait() — the base OTs' share of the crawl's critical path. An instance's schedules are released
+// once uploaded (release()); a resumed level re-requests and recomputes them.
 struct BaseOtProducer {
     struct Inst {
         uint32_t lv, salt;
@@ -748,7 +751,7 @@ struct BaseOtProducer {
     uint64_t prf;
     uint8_t seed[32];
     std::deque<Inst> insts;                          // stable addresses under push_back
-    std::map<uint64_t, size_t> index;                // (lv << 32 | salt) -> request
+    std::map<uint64_t, size_t> index;                // (lv << 32 | salt) -> request (until released)
     size_t next_work = 0;
     bool stop = false;
     std::mutex mu;
@@ -756,8 +759,9 @@ struct BaseOtProducer {
     int rc = FHH_OK;
     std::string err;
     std::vector<std::thread> workers;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    double busy_ms = 0;                              // wall time until the last instance finished
+    double compute_ms = 0;                           // summed per-instance compute (all workers)
+    double stall_ms = 0;                             // enqueueing thread blocked in wait()
+    uint64_t computed = 0;                           // instances finished
     BaseOtProducer(uint64_t prf_seed, const uint8_t s[32]) : prf(prf_seed) {
         std::memcpy(seed, s, 32);
         unsigned nt = std::thread::hardware_concurrency();
@@ -793,6 +797,7 @@ struct BaseOtProducer {
                 if (stop) return;
                 in = &insts[next_work++];
             }
+            const auto t_begin = std::chrono::steady_clock::now();
             // the OT-extension sender's base choice bits: the words the ideal mode uses (ot_level_choice)
             uint32_t sw[4];
             ot_level_choice(prf, in->lv, in->salt, sw);
@@ -811,6 +816,7 @@ struct BaseOtProducer {
                     }
                 }
             }
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
             std::lock_guard<std::mutex> lk(mu);
             if (r && !rc) {
                 rc = r;
@@ -818,18 +824,29 @@ struct BaseOtProducer {
             }
             in->rk.swap(rk);
             in->done = true;
-            busy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            compute_ms += ms;
+            computed++;
             cv_done.notify_all();
         }
     }
     int wait(size_t i) {
         std::unique_lock<std::mutex> lk(mu);
+        if (insts[i].done || rc != FHH_OK) return rc;
+        const auto t_begin = std::chrono::steady_clock::now();
         cv_done.wait(lk, [&] { return insts[i].done || rc != FHH_OK; });
+        stall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
         return rc;
     }
     const uint32_t* schedules(size_t i) {
         std::lock_guard<std::mutex> lk(mu);
         return insts[i].rk.data();
+    }
+    // the schedules have left the host (their upload returned): free them, and let a later request for
+    // the same (lv, salt) compute a fresh instance
+    void release(size_t i) {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<uint32_t>().swap(insts[i].rk);
+        index.erase((uint64_t)insts[i].lv << 32 | insts[i].salt);
     }
 };
 
@@ -837,7 +854,7 @@ struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
     DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
     DevBuf gc_planes[2], gc_tables, gc_gbl, gc_evl, gc_decode, gc_out;   // cfg->gc (row f1)
-    DevBuf gc_evact, gc_msg[2], gc_recv;                                  // cfg->gc = 2: OT buffers
+    DevBuf gc_evact, gc_val[2];                                           // cfg->gc = 2: OT buffers
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
@@ -870,7 +887,7 @@ struct LoopBuffers {
 
 // wait for the base OTs of OT extension (lv, salt) and copy their key schedules to the next ring
 // slot; returns the slot's device address. The copy is from pageable memory, so it has left the host
-// buffer on return.
+// buffer on return, and the instance is released.
 int upload_base_ot(fhh_ctx* c0, LoopBuffers& B, uint32_t lv, uint32_t salt, const uint32_t** rk_dev) {
     const size_t i = B.bot->request(lv, salt);
     const int rc = B.bot->wait(i);
@@ -878,6 +895,7 @@ int upload_base_ot(fhh_ctx* c0, LoopBuffers& B, uint32_t lv, uint32_t salt, cons
     const size_t words = (size_t)3 * 128 * 44;
     uint32_t* dst = B.base_rk.as<uint32_t>() + (size_t)(B.base_slot++ % LoopBuffers::kBaseRing) * words;
     HIP_TRY(c0, hipMemcpyAsync(dst, B.bot->schedules(i), words * 4, hipMemcpyHostToDevice, c0->stream));
+    B.bot->release(i);   // a pageable copy has left the host buffer on return
     *rk_dev = dst;
     return FHH_OK;
 }
@@ -1229,7 +1247,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 // servers' share planes, server 0 garbles, server 1 evaluates. The level's tests
                 // run in chunks of gc_groups children (bounded memory at 1M clients; the reference
                 // splits a level's tests over its channels the same way, collect.rs:423-430), each
-                // chunk a fresh protocol instance: its own garbler key / Delta / mask and base OTs
+                // chunk a fresh protocol instance: its own garbler key / Delta / mask, and its own
+                // row-PRG range of the level's base-OT sessions
                 const uint32_t bits = 2 * d;
                 const size_t plane_bytes = (size_t)C_cap * bits * c0->nw * 8;
                 for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
@@ -1242,22 +1261,41 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 const uint64_t Gc = std::min<uint64_t>(C_cap, gc_groups);
                 const uint64_t chunks = (C_cap + Gc - 1) / Gc;
                 const bool real_ot = cfg->gc >= 2;
-                if (B.base_ot) {
-                    // keep the producer a few levels ahead of the enqueueing (at this capacity's chunk
-                    // count; a level enqueued after a growth requests its extra chunks itself)
-                    constexpr uint32_t kAhead = 4;
-                    for (uint32_t l = lv; l < std::min(levels, lv + kAhead); l++)
-                        for (uint64_t salt = 0; salt < 2 * chunks; salt++) (void)B.bot->request(l, (uint32_t)salt);
-                }
                 const uint64_t tests = Gc * c0->n;
                 const uint32_t per2 = pmode == 1 ? 1 : 2;   // OTs per test of the share conversion
+                const uint64_t m1 = Gc * bits * c0->npad, m2 = tests * per2;
+                // the level's two base-OT sessions (OtSender / OtReceiver::init per level and kind,
+                // collect.rs:454,460): kind 0 the labels OT, kind 1 the share OT; chunk k extends them
+                // from row-PRG block k x (the chunk's blocks), so no two chunks share a pad
+                const uint32_t* rk_ot[2] = {nullptr, nullptr};
+                uint32_t sw_ot[2][4];
+                if (real_ot) {
+                    HIP_TRY(c0, c0->ot_rk.ensure((size_t)2 * 3 * 128 * 44 * 4));
+                    if (B.base_ot) {
+                        // keep the producer a few levels ahead of the enqueueing
+                        constexpr uint32_t kAhead = 4;
+                        for (uint32_t l = lv; l < std::min(levels, lv + kAhead); l++)
+                            for (uint32_t w = 0; w < 2; w++) (void)B.bot->request(l, w);
+                    }
+                    for (uint32_t w = 0; w < 2; w++) {
+                        ot_level_choice(cfg->prf_seed, lv, w, sw_ot[w]);
+                        if (B.base_ot) {
+                            rc = upload_base_ot(c0, B, lv, w, &rk_ot[w]);
+                            if (rc) return rc;
+                        } else {
+                            uint32_t* rk = c0->ot_rk.as<uint32_t>() + (size_t)w * 3 * 128 * 44;
+                            HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, w, sw_ot[w], rk, c0->stream));
+                            rk_ot[w] = rk;
+                        }
+                    }
+                }
                 HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
                 HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
-                // OT mode: the evaluator's zero labels at OT index (g bits + j) npad + i
-                HIP_TRY(c0, B.gc_evl.ensure((size_t)bits * Gc * c0->npad * 16));
+                // ideal OT: the evaluator's active labels [bits][tests]; OT mode: its zero labels (the
+                // labels C-OT's sender messages) at OT index (g bits + j) npad + i
+                HIP_TRY(c0, B.gc_evl.ensure(std::max<size_t>((size_t)bits * tests, real_ot ? m1 : 0) * 16));
                 HIP_TRY(c0, B.gc_decode.ensure(tests));
                 HIP_TRY(c0, B.gc_out.ensure(tests));
-                HIP_TRY(c0, c0->ot_rk.ensure((size_t)3 * 128 * 44 * 4));
                 for (uint64_t k = 0; k < chunks; k++) {
                     const uint64_t g_off = k * Gc;
                     fhh_gc_batch gb{};
@@ -1278,35 +1316,35 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     if (rc) return rc;
                     g.ctl = B.ctl.as<LoopCtl>();
                     g.g_off = g_off;
-                    g.ev_ot = real_ot ? 1u : 0u;
+                    if (real_ot) {
+                        // 1. the evaluator's input labels by correlated OT (gb_set_fancy_inputs /
+                        // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1's choice bits are
+                        // its share planes [C][bits][nw] from the chunk's first group on, as they stand
+                        // (m1 a multiple of 128: npad of 64, bits even); server 0's sender messages
+                        // x0 = H(q_j) are the zero labels it garbles with, x1 = x0 ^ Delta
+                        HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
+                        OtArgs a1{};
+                        a1.mode = 1;
+                        a1.rk = rk_ot[0];
+                        for (int c = 0; c < 4; c++) a1.s[c] = sw_ot[0][c];
+                        a1.choices = B.gc_planes[1].as<uint32_t>() + g_off * bits * c0->nw * 2;
+                        for (int c = 0; c < 4; c++) a1.delta[c] = g.delta[c];
+                        a1.ctr_off = k * ot_session_blocks(m1);
+                        a1.sx = B.gc_evl.p;
+                        a1.out = B.gc_evact.as<uint4>();
+                        a1.ctl = B.ctl.as<LoopCtl>();
+                        a1.per_group = (uint64_t)c0->npad * bits;
+                        a1.g_off = g_off;
+                        rc = ot_run(c0, a1, m1, nullptr);
+                        if (rc) return rc;
+                        g.ev_ot = 1;
+                    }
                     HIP_TRY(c0, launch_gc_garble(g, c0->stream));
                     if (real_ot) {
-                        // the evaluator's input labels by OT extension (gb_set_fancy_inputs /
-                        // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1 receives the
-                        // labels of its share bits, server 0 sends (zero label, zero label ^ Delta);
-                        // OT index (g bits + j) npad + i: the choice bits are server 1's share planes
-                        // [C][bits][nw] from the chunk's first group on, as they stand (m1 is a
-                        // multiple of 128: npad of 64, bits even)
-                        const uint64_t m1 = Gc * bits * c0->npad;
-                        const uint32_t* ch = B.gc_planes[1].as<uint32_t>() + g_off * bits * c0->nw * 2;
-                        uint32_t sw[4];
-                        ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k), sw);
-                        const uint32_t* rk1 = c0->ot_rk.as<uint32_t>();
-                        if (B.base_ot) {
-                            rc = upload_base_ot(c0, B, lv, (uint32_t)(2 * k), &rk1);
-                            if (rc) return rc;
-                        } else {
-                            HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k), sw,
-                                                             c0->ot_rk.as<uint32_t>(), c0->stream));
-                        }
-                        HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
-                        rc = ot_run(c0, m1, ch, g.ev_labels, nullptr, g.delta, B.gc_evact.as<uint4>(), rk1, sw, 0,
-                                    B.ctl.as<LoopCtl>(), (uint64_t)c0->npad * bits, nullptr, g_off);
-                        if (rc) return rc;
                         g.ev_labels = B.gc_evact.as<uint4>();
                         // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
                         uint32_t* och = nullptr;
-                        HIP_TRY(c0, ot_choices_buffer(c0, tests * per2, &och));
+                        HIP_TRY(c0, ot_choices_buffer(c0, m2, &och));
                         g.out_packed = och;
                         g.out_dup = per2;
                     }
@@ -1318,42 +1356,28 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     ca.gc_N = g.N;
                     ca.gc_mask = g.mask;
                     if (real_ot) {
-                        // the share conversion by OT extension (collect.rs:437-471; 846-876 at the
-                        // last level, where a FieldElm travels as a BlockPair = 2 OTs): server 0
-                        // sends (r0, r1) ordered by its mask, server 1 chooses with its GC output bit
-                        const uint64_t m2 = tests * per2;
-                        HIP_TRY(c0, B.gc_recv.ensure(m2 * 16));
-                        // FE levels: the send hash computes (r0, r1) itself (OtFeMsg, the PRF of
-                        // k_ot_fe_messages) instead of reading 32 B per OT that kernel wrote; the
-                        // last level's FieldElm messages (2 OTs per test) keep their kernel
-                        OtFeMsg fe{};
-                        if (pmode == 1) {
-                            fe.base = host_mix64(cfg->prf_seed ^ (uint64_t)lv);   // k_ot_fe_messages: mix64(prf_seed ^ level)
-                            fe.client_base = c0->client_base;
-                            fe.c_off = g_off;
-                            fe.n = (uint32_t)c0->n;
-                            fe.mask = g.mask;
-                        } else {
-                            HIP_TRY(c0, B.gc_msg[0].ensure(m2 * 16));
-                            HIP_TRY(c0, B.gc_msg[1].ensure(m2 * 16));
-                            HIP_TRY(c0, launch_ot_fe255_messages(ca, g.mask, B.gc_msg[0].as<uint4>(),
-                                                                 B.gc_msg[1].as<uint4>(), c0->stream));
-                        }
-                        uint32_t sw[4];
-                        ot_level_choice(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw);
-                        const uint32_t* rk2 = c0->ot_rk.as<uint32_t>();
-                        if (B.base_ot) {
-                            rc = upload_base_ot(c0, B, lv, (uint32_t)(2 * k + 1), &rk2);
-                            if (rc) return rc;
-                        } else {
-                            HIP_TRY(c0, launch_ot_level_keys(cfg->prf_seed, lv, (uint32_t)(2 * k + 1), sw,
-                                                             c0->ot_rk.as<uint32_t>(), c0->stream));
-                        }
-                        rc = ot_run(c0, m2, g.out_packed, B.gc_msg[0].as<uint4>(), B.gc_msg[1].as<uint4>(), nullptr,
-                                    B.gc_recv.as<uint4>(), rk2, sw, 0, B.ctl.as<LoopCtl>(), (uint64_t)c0->n * per2,
-                                    nullptr, g_off, pmode == 1 ? &fe : nullptr);
+                        // 2. the share conversion by correlated OT (collect.rs:437-471; 846-876 at the
+                        // last level, where a FieldElm travels as a BlockPair = 2 OTs): server 0's pair is
+                        // (H(q_j), H(q_j) +- 1) ordered by its mask, its node value r1 = H(q_j) + mask;
+                        // server 1 chooses with its GC output bit
+                        const size_t vb = pmode == 1 ? 8 : 16;
+                        for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(m2 * vb));
+                        OtArgs a2{};
+                        a2.mode = pmode == 1 ? 2 : 3;
+                        a2.mask = g.mask;
+                        a2.rk = rk_ot[1];
+                        for (int c = 0; c < 4; c++) a2.s[c] = sw_ot[1][c];
+                        a2.choices = g.out_packed;
+                        a2.ctr_off = k * ot_session_blocks(m2);
+                        a2.sx = B.gc_val[0].p;
+                        a2.out = B.gc_val[1].as<uint4>();
+                        a2.ctl = B.ctl.as<LoopCtl>();
+                        a2.per_group = (uint64_t)c0->n * per2;
+                        a2.g_off = g_off;
+                        rc = ot_run(c0, a2, m2, nullptr);
                         if (rc) return rc;
-                        ca.ot_recv = B.gc_recv.as<uint4>();
+                        ca.ot_val[0] = B.gc_val[0].p;
+                        ca.ot_val[1] = B.gc_val[1].p;
                     }
                     // the chunk's children's sums (FE: atomics into the partials k_prune zeroed;
                     // FE255: one store per child)
@@ -1489,7 +1513,9 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         // every instance the crawl used was waited for at its upload; lookahead ones still running
         // are abandoned (the destructor stops the workers after their current instance)
         std::lock_guard<std::mutex> lk(B.bot->mu);
-        c0->stats.base_ot_ms += B.bot->busy_ms;
+        c0->stats.base_ot_ms += B.bot->compute_ms;
+        c0->stats.base_ot_stall_ms += B.bot->stall_ms;
+        c0->stats.base_ot_instances += B.bot->computed;
     }
     c0->loop_cap_hint = std::max(B.E_cap, B.F_cap);   // the next crawl starts at this size
     pc.mark("loop");

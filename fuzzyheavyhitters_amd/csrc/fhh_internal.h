@@ -182,8 +182,11 @@ struct ChildArgs {
     const uint8_t* gc_out;
     uint32_t gc_N;
     uint32_t gc_mask;
-    // OT mode: the receiver's FE share of (c, i) is the OT output ot_recv[c * gc_N + i] (low 8 B)
-    const uint4* ot_recv;
+    // OT mode (r05: correlated OT, OtArgs modes 2 / 3): the two servers' node values of (c, i) are
+    // the C-OT's outputs — FE levels u64 ot_val[s][(c - c_off) * gc_N + i] (s = 0 the garbler's
+    // v + mask, s = 1 the receiver's); the last level BlockPairs (2 blocks per value: the garbler's
+    // canonical V + mask, the receiver's raw FieldElm::try_from(BlockPair))
+    const void* ot_val[2];
     // child window of the GC + OT kernels (a chunk of the level's children, as the reference splits
     // a level's tests over its channels, collect.rs:423-430): children [c_off, c_off + c_cnt) only,
     // gc_out / ot_recv / OT messages indexed (c - c_off) * gc_N + i; c_cnt = 0: every child
@@ -203,7 +206,7 @@ struct GcArgs {
     uint32_t N, nw, bits, mask;
     uint32_t rk_label[11][4];    // garbler's label PRG key schedule (AES-128-CTR)
     uint32_t delta[4];           // free-XOR offset, lsb 1
-    uint64_t label_nonce;        // label of (t, w) = AES_k(label_nonce + t S + w), S = pow2 >= 2 bits + 1
+    uint64_t label_nonce;        // label of (t, w) = AES_k(label_nonce + t S + w), S = pow2 >= W (W = 2 bits + 1, ev_ot: bits + 1)
     uint64_t gate_base;          // half-gate tweaks 2 (gate_base + t (bits - 1) + k) (+1)
     uint4* tables;               // [(bits-1)][2][n]  (T_G, T_E)
     uint4* gb_labels;            // [bits + 1][n]     garbler's active input labels (+ mask)
@@ -212,10 +215,13 @@ struct GcArgs {
     uint8_t* out;                // [n]               evaluator's output bit = eq ^ mask
     const LoopCtl* ctl;          // non-null (level loop): groups = min(G, ctl->C), 0 once aborted;
                                  // G * N stays the SoA stride
-    uint32_t ev_ot;              // 1: ev_labels holds the evaluator's ZERO labels (OT sender input)
-                                 // at OT index (g bits + j) Npad + i (Npad = 64 nw: the evaluator's
-                                 // share planes are the choice bits); k_gc_eval reads its OT'd
-                                 // labels there
+    uint32_t ev_ot;              // 1 (r05, the labels OT is a correlated OT): ev_labels holds the
+                                 // evaluator's labels at OT index (g bits + j) Npad + i (Npad = 64 nw:
+                                 // its share planes are the OT's choice bits) — k_gc_garble reads the
+                                 // ZERO labels there (the C-OT's sender messages) and draws only its
+                                 // own wires and the mask (label stride pow2 >= bits + 1), k_gc_eval
+                                 // reads its OT'd active labels there. 0: ideal OT (every label drawn
+                                 // by the garbler, the evaluator's active ones written to ev_labels)
     uint32_t out_dup;            // out_packed: each output bit repeated out_dup (1 or 2) times
     uint32_t* out_packed;        // non-null: k_gc_eval also writes the outputs as bit words
                                  // (tests t0.. of a 64-aligned wave slice; the FE-share OT choices)
@@ -308,21 +314,19 @@ int comm_rank(const ::fhh_comm* c);   // the rank given at creation
 // device-resident level loop (fhh_loop.hip); `unit` = items per entry group, `max_group` =
 // entries per item cap (see expand_unit)
 hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
-// IKNP / ALSZ OT extension (row f1's OT): m OTs of 16-B messages; base OTs ideal (the sender's
-// key schedules are those of k_i^{s_i}). Bit matrices are [128 rows][mp / 128] uint4 blocks,
-// read per OT by the hashes (transposed on the fly). With ctl set (level loop) only the first
+// IKNP / ALSZ OT extension (row f1's OT): m OTs of 16-B messages; base OTs given as key schedules
+// (the sender's are those of k_i^{s_i}). Bit matrices are [128 rows][mp / 128] uint4 blocks, read per
+// OT by the hashes (transposed on the fly). With ctl set (level loop) only the first
 // per_group * min(groups, ctl->C) OTs run.
-// The FE share conversion's sender messages (collect.rs:437-452), computed inside the send hash from
-// k_ot_fe_messages' PRF instead of being written to HBM by that kernel and read back (in-process
-// crawl): OT j of the chunk is client i = j mod n of child c_off + j / n
-struct OtFeMsg {
-    uint64_t base;          // mix64(prf_seed ^ level)
-    uint64_t client_base;
-    uint64_t c_off;         // the chunk's first child
-    uint32_t n;             // OTs (clients) per child; 0: the messages are x0 / x1
-    uint32_t mask;          // the garbler's mask bit: (r0, r1) if set, else (r1, r0)
-};
-
+// Modes (r05; oracle/fhh_oracle.c orc_ot_extend / orc_cot_extend):
+//   0  plain OT: y_j^b = x_j^b ^ H(q_j ^ b s) (x1 == nullptr: x1 = x0 ^ delta); out = y_j^{r_j} ^ H(t_j)
+//   1  correlated OT, XOR delta (the labels OT): sender writes sx[j] = H(q_j) (the evaluator's zero
+//      label) and Y0[j] = H(q_j) ^ delta ^ H(q_j ^ s); out = r_j ? Y0[j] ^ H(t_j) : H(t_j)
+//   2  correlated OT, FE share: v = H(q_j) as LE u128 mod p; sender value v + mask -> sx (u64 [m]),
+//      Y0 (8 B [m]) = lo64(H(q_j ^ s)) ^ (mask ? v + 1 : v - 1); out (u64 [m]) = r_j ? lo64(Y0[j] ^
+//      H(t_j)) : H(t_j) mod p
+//   3  correlated OT, FieldElm share, raw pass: sx[j] = H(q_j), Y0[j] = H(q_j ^ s); k_cot_fe255_finish
+//      turns OT pairs (2t, 2t + 1) into the sender's node values and y; out = r_j ? Y0[j] ^ H(t_j) : H(t_j)
 struct OtArgs {
     uint64_t m;                  // OTs (capacity)
     uint64_t mp;                 // m padded to a multiple of 8192 (whole waves per row)
@@ -330,14 +334,18 @@ struct OtArgs {
     uint32_t s[4];               // sender's base choice bits
     const uint32_t* choices;     // [mp / 32] receiver's choice bits (0 past m)
     uint4 *T, *U, *Q;            // U [128][mp / 128] (row form, the wire); T, Q tile-major (fhh_ot.hip ot_tmaj)
-    const uint4 *x0, *x1;        // [m]; x1 == nullptr: x1 = x0 ^ delta (correlated OT)
-    uint32_t delta[4];
-    uint4 *Y0, *Y1, *out;        // [m]
+    const uint4 *x0, *x1;        // mode 0: [m]; x1 == nullptr: x1 = x0 ^ delta (correlated messages)
+    uint32_t delta[4];           // modes 0 (x1 == nullptr) and 1
+    uint4 *Y0, *Y1, *out;        // mode 0: Y0, Y1 [m]; modes 1-3: y in Y0 (mode 2: 8 B per OT); out [m]
     uint64_t tweak_base;
     const LoopCtl* ctl;
     uint64_t per_group;
     uint64_t g_off;              // level loop chunk: OTs of groups [g_off, ctl->C) only
-    OtFeMsg fe;                  // fe.n > 0: the send hash computes x0 / x1 itself
+    uint32_t mode;               // 0..3 above
+    uint32_t mask;               // modes 2, 3: the garbler's mask bit
+    uint64_t ctr_off;            // the row PRG's first block (a multiple of 256): a base-OT session's
+                                 // running counter, so batches extending one session never repeat pads
+    void* sx;                    // modes 1, 3: uint4 [m]; mode 2: u64 [m] (the sender's node values)
 };
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
@@ -351,9 +359,10 @@ int base_ot_instance(uint64_t k, const uint8_t seed[32], const uint8_t choices[1
                      std::string* err);
 hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, const uint32_t s[4], uint32_t* rk,
                                 hipStream_t stream);
-// GC + OT glue (level loop): the garbler's OT messages for the FE share conversion
-hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
-hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream);
+// mode 3's second pass (the garbler, FieldElm share): per test t, V = H(q_2t) || H(q_2t+1) (32
+// big-endian bytes, sx) mod p255 -> sx pair = V + mask (its node value, a canonical BlockPair), Y0 pair
+// ^= (mask ? V + 1 : V - 1); tests = the active OT pairs (ctl-aware as the hashes)
+hipError_t launch_cot_fe255_finish(const OtArgs& a, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,

@@ -672,15 +672,16 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         const uint64_t bc = mix64(base ^ c);
         uint64_t v[4] = {0, 0, 0, 0};
         for (uint32_t i = i_begin + threadIdx.x; i < i_end; i += blockDim.x) {
-            uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
-            if (r0 >= kFeP) r0 -= kFeP;
-            const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;   // r1 = r0 + one (collect.rs:443-444)
-            uint64_t v1;                                         // receiver gets pair[o] (A.5)
-            if (a.ot_recv) {                                     // ... through the OT extension
-                const uint4 b = a.ot_recv[(c - a.c_off) * a.gc_N + i];
-                v1 = (uint64_t)b.x | ((uint64_t)b.y << 32);      // FE::try_from(Block), fastfield.rs:414-421
-            } else {
-                v1 = sim_eq_bit(a, e, c, i) ? r0 : r1;
+            uint64_t r1, v1;
+            if (a.ot_val[0]) {   // the correlated OT's node values (OtArgs mode 2): garbler v + mask, receiver
+                const size_t t = (c - a.c_off) * a.gc_N + i;
+                r1 = static_cast<const uint64_t*>(a.ot_val[0])[t];
+                v1 = static_cast<const uint64_t*>(a.ot_val[1])[t];
+            } else {             // simulated OT shares (ideal OT harness)
+                uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
+                if (r0 >= kFeP) r0 -= kFeP;
+                r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;              // r1 = r0 + one (collect.rs:443-444)
+                v1 = sim_eq_bit(a, e, c, i) ? r0 : r1;           // receiver gets pair[o] (A.5)
             }
             v[0] += r1 & 0xFFFFFFFFull;
             v[1] += r1 >> 32;
@@ -691,37 +692,6 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
         if (threadIdx.x == 0)
             for (int k = 0; k < 4; k++) atomicAdd(reinterpret_cast<unsigned long long*>(partials + c * 4 + k), v[k]);
     }
-}
-
-// the garbler's OT messages of the FE share conversion (collect.rs:437-452): r0 from the same
-// PRF as k_sim_ot_fe, r1 = r0 + 1; (r0, r1) if the mask bit is set, else (r1, r0); blocks carry
-// the value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430). x1 == nullptr: r1
-// alone into x0 (the party garbler's node values; its send hash then draws (r0, r1) itself, OtFeMsg)
-__global__ __launch_bounds__(kReduceThreads) void k_ot_fe_messages(ChildArgs a, uint32_t mask, uint4* x0, uint4* x1) {
-    const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_end(a);
-    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
-        const uint64_t bc = mix64(base ^ c);
-        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            uint64_t r0 = mix64(mix64(bc ^ (a.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
-            if (r0 >= kFeP) r0 -= kFeP;
-            const uint64_t r1 = (r0 + 1 == kFeP) ? 0 : r0 + 1;
-            if (!x1) {
-                x0[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)r1, (uint32_t)(r1 >> 32), 0u, 0u);
-                continue;
-            }
-            const uint64_t m0 = mask ? r0 : r1, m1 = mask ? r1 : r0;
-            x0[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
-            x1[(c - a.c_off) * a.gc_N + i] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
-        }
-    }
-}
-
-hipError_t launch_ot_fe_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
-    if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ot_fe_messages, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, mask, x0,
-                       x1);
-    return hipGetLastError();
 }
 
 hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream, bool zero) {
@@ -770,48 +740,6 @@ __device__ __forceinline__ void blockpair_to_limbs(uint4 b0, uint4 b1, uint64_t 
     r[0] = ((uint64_t)__builtin_bswap32(b1.z) << 32) | __builtin_bswap32(b1.w);
 }
 
-// the last level's OT messages (collect.rs:846-866): FieldElm r0 (the k_sim_ot_fe255 PRF),
-// r1 = r0 + 1, each as a BlockPair; two OTs per test (2t: block 0, 2t + 1: block 1), pairs
-// (r0, r1) if the mask bit is set, else (r1, r0)
-__global__ __launch_bounds__(kReduceThreads) void k_ot_fe255_messages(ChildArgs a, uint32_t mask, uint4* x0,
-                                                                      uint4* x1) {
-    const uint64_t base = mix64(a.prf_seed ^ a.level);
-    const uint64_t C_ = child_end(a);
-    for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
-        const uint64_t bc = mix64(base ^ c);
-        for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const uint64_t bi = mix64(bc ^ (a.client_base + i));
-            uint64_t r0[4], r1[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) r0[k] = mix64(bi ^ (uint64_t)k);
-            r0[3] &= 0x7FFFFFFFFFFFFFFFull;
-            fe255_canon(r0);
-            unsigned __int128 acc = (unsigned __int128)r0[0] + 1;
-            r1[0] = (uint64_t)acc;
-#pragma unroll
-            for (int k = 1; k < 4; k++) {
-                acc = (unsigned __int128)r0[k] + (uint64_t)(acc >> 64);
-                r1[k] = (uint64_t)acc;
-            }
-            fe255_canon(r1);
-            const uint64_t* m0 = mask ? r0 : r1;
-            const uint64_t* m1 = mask ? r1 : r0;
-            const size_t t = (c - a.c_off) * a.gc_N + i;
-            x0[2 * t] = limbs_to_block(m0[3], m0[2]);
-            x0[2 * t + 1] = limbs_to_block(m0[1], m0[0]);
-            x1[2 * t] = limbs_to_block(m1[3], m1[2]);
-            x1[2 * t + 1] = limbs_to_block(m1[1], m1[0]);
-        }
-    }
-}
-
-hipError_t launch_ot_fe255_messages(const ChildArgs& a, uint32_t mask, uint4* x0, uint4* x1, hipStream_t stream) {
-    if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ot_fe255_messages, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, mask,
-                       x0, x1);
-    return hipGetLastError();
-}
-
 __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[16 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
@@ -824,28 +752,31 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = 0;
         for (uint32_t i = threadIdx.x; i < a.n; i += blockDim.x) {
-            const bool eq = a.ot_recv ? false : sim_eq_bit(a, e, c, i);
-            const uint64_t bi = mix64(bc ^ (a.client_base + i));
-            uint64_t r0[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) r0[k] = mix64(bi ^ (uint64_t)k);
-            r0[3] &= 0x7FFFFFFFFFFFFFFFull;
-            fe255_canon(r0);
-            // r1 = r0 + 1 mod p
-            uint64_t r1[4];
-            unsigned __int128 acc = (unsigned __int128)r0[0] + 1;
-            r1[0] = (uint64_t)acc;
-#pragma unroll
-            for (int k = 1; k < 4; k++) {
-                acc = (unsigned __int128)r0[k] + (uint64_t)(acc >> 64);
-                r1[k] = (uint64_t)acc;
-            }
-            fe255_canon(r1);
-            uint64_t got[4];
-            if (a.ot_recv) {   // FieldElm::try_from(BlockPair): big-endian 32 bytes (field.rs:466-476)
+            uint64_t r1[4], got[4];
+            if (a.ot_val[0]) {   // the correlated OT's node values (OtArgs mode 3), BlockPairs; the receiver's
+                                 // unreduced, as FieldElm::try_from(BlockPair) reads them (field.rs:466-476)
                 const size_t t = (c - a.c_off) * a.gc_N + i;
-                blockpair_to_limbs(a.ot_recv[2 * t], a.ot_recv[2 * t + 1], got);
-            } else {
+                const uint4* g = static_cast<const uint4*>(a.ot_val[0]);
+                const uint4* r = static_cast<const uint4*>(a.ot_val[1]);
+                blockpair_to_limbs(g[2 * t], g[2 * t + 1], r1);
+                blockpair_to_limbs(r[2 * t], r[2 * t + 1], got);
+            } else {             // simulated OT shares (ideal OT harness)
+                const bool eq = sim_eq_bit(a, e, c, i);
+                const uint64_t bi = mix64(bc ^ (a.client_base + i));
+                uint64_t r0[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) r0[k] = mix64(bi ^ (uint64_t)k);
+                r0[3] &= 0x7FFFFFFFFFFFFFFFull;
+                fe255_canon(r0);
+                // r1 = r0 + 1 mod p
+                unsigned __int128 acc = (unsigned __int128)r0[0] + 1;
+                r1[0] = (uint64_t)acc;
+#pragma unroll
+                for (int k = 1; k < 4; k++) {
+                    acc = (unsigned __int128)r0[k] + (uint64_t)(acc >> 64);
+                    r1[k] = (uint64_t)acc;
+                }
+                fe255_canon(r1);
 #pragma unroll
                 for (int k = 0; k < 4; k++) got[k] = eq ? r0[k] : r1[k];
             }

@@ -19,7 +19,6 @@
 #include "fhh_internal.h"
 
 #include <atomic>
-#include <cstdlib>
 
 #include "aes_keyed.h"
 #include "bitslice.h"
@@ -105,7 +104,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
         uint32_t g[kOtSlices][4];
 #pragma unroll
         for (int q = 0; q < kOtSlices; q++) {
-            const uint64_t c = c0 + 64 * q + lane;
+            const uint64_t c = a.ctr_off + c0 + 64 * q + lane;   // the session's running counter
             g[q][0] = (uint32_t)c;
             g[q][1] = (uint32_t)(c >> 32);
             g[q][2] = 0u;
@@ -120,10 +119,10 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
             uint32_t g1[kOtSlices][4];
 #pragma unroll
             for (int q = 0; q < kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * q + lane;
+                const uint64_t c = c0 + 64 * q + lane, cc = a.ctr_off + c;
                 if (c0 + 64 * q < nblk_act) a.T[ot_tmaj(i, c)] = make_uint4(g[q][0], g[q][1], g[q][2], g[q][3]);
-                g1[q][0] = (uint32_t)c;
-                g1[q][1] = (uint32_t)(c >> 32);
+                g1[q][0] = (uint32_t)cc;
+                g1[q][1] = (uint32_t)(cc >> 32);
                 g1[q][2] = 0u;
                 g1[q][3] = 0u;
             }
@@ -186,7 +185,7 @@ __global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
         uint32_t g[kSlices][4];
 #pragma unroll
         for (int q = 0; q < kSlices; q++) {
-            const uint64_t c = c0 + 32 * q + l;
+            const uint64_t c = a.ctr_off + c0 + 32 * q + l;   // the session's running counter
             g[q][0] = (uint32_t)c;
             g[q][1] = (uint32_t)(c >> 32);
             g[q][2] = 0u;
@@ -251,36 +250,30 @@ __device__ __forceinline__ void ot_tile_round(uint32_t* st, uint32_t (&x)[32], u
     for (int i = 0; i < 24; i++) x[i] = x[i + 8];
 }
 
-__device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {   // SplitMix64's finaliser (as fhh_kernels.hip mix64)
+__device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {   // SplitMix64's finaliser (ideal base OTs only)
     z += 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
 
+constexpr uint64_t kOtFeP = (1ull << 62) - (1ull << 30) - 1;
 
-// the sender's messages of OT j: x0[j], x1[j] (x1 = x0 ^ delta when absent), or with a.fe.n the FE
-// share conversion's (r0, r1) ordered by the mask bit, r0 = the PRF of k_ot_fe_messages
-// (fhh_kernels.hip) for client j mod n of child c_off + j / n, r1 = r0 + 1 mod p; blocks carry the
-// value little-endian in bytes 0..7 (From<FE> for Block, fastfield.rs:424-430)
-__device__ __forceinline__ void ot_messages(const OtArgs& a, uint64_t j, uint4& x0, uint4& x1) {
-    if (a.fe.n) {
-        constexpr uint64_t P = (1ull << 62) - (1ull << 30) - 1;
-        const uint64_t cr = (j >> 32) ? j / a.fe.n : (uint32_t)j / a.fe.n;   // a chunk's OTs: < 2^32 in practice
-        const uint64_t i = j - cr * a.fe.n;
-        const uint64_t bc = ot_mix64(a.fe.base ^ (a.fe.c_off + cr));
-        uint64_t r0 = ot_mix64(ot_mix64(bc ^ (a.fe.client_base + i)) ^ 0ull) & ((1ull << 62) - 1);
-        if (r0 >= P) r0 -= P;
-        const uint64_t r1 = (r0 + 1 == P) ? 0 : r0 + 1;
-        const uint64_t m0 = a.fe.mask ? r0 : r1, m1 = a.fe.mask ? r1 : r0;
-        x0 = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), 0u, 0u);
-        x1 = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), 0u, 0u);
-        return;
-    }
-    x0 = a.x0[j];
-    x1 = a.x1 ? a.x1[j] : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2], x0.w ^ a.delta[3]);
+// a 16-B hash output as a little-endian u128, mod p_FE (p = 2^62 - 2^30 - 1: 2^64 = 2^32 + 4 and
+// 2^62 = 2^30 + 1 mod p); the C-OT's FE value (statistically 2^-66 from uniform)
+__device__ __forceinline__ uint64_t ot_fe_of_u128(uint64_t lo, uint64_t hi) {
+    constexpr uint64_t M62 = (1ull << 62) - 1;
+    const unsigned __int128 x = (unsigned __int128)hi * ((1ull << 32) + 4) + lo;     // < 2^98
+    const unsigned __int128 y = (unsigned __int128)(uint64_t)(x >> 62) * ((1ull << 30) + 1) + ((uint64_t)x & M62);
+    uint64_t z = ((uint64_t)y & M62) + (uint64_t)(y >> 62) * ((1ull << 30) + 1);       // < 2^62 + 2^36
+    return z >= kOtFeP ? z - kOtFeP : z;
 }
 
+// The send hash: one wave per 512-OT tile (transposed in registers + LDS), one OT (2 blocks: q, q ^ s)
+// per pass. MODE (OtArgs::mode): 0 plain OT (y^b = x^b ^ H(q ^ b s)), 1 C-OT labels (sx = H(q),
+// y = H(q) ^ delta ^ H(q ^ s)), 2 C-OT FE share (sx = v + mask, y = lo64(H(q ^ s)) ^ pair[1], 8 B),
+// 3 C-OT raw (sx = H(q), y = H(q ^ s); k_cot_fe255_finish completes the FieldElm share)
+template <int MODE>
 __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
@@ -307,15 +300,36 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_send_hash_rows(OtArgs a) 
                 aes0_mmo_tab<DevOpsX, OtTab, 2>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x
                 const uint64_t j = ot_tile_ot(t, lane, r, u);
                 if (j >= m) continue;
-                uint4 x0, x1;
-                ot_messages(a, j, x0, x1);
-                a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
-                a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
+                if constexpr (MODE == 0) {
+                    const uint4 x0 = a.x0[j];
+                    const uint4 x1 = a.x1 ? a.x1[j]
+                                          : make_uint4(x0.x ^ a.delta[0], x0.y ^ a.delta[1], x0.z ^ a.delta[2],
+                                                       x0.w ^ a.delta[3]);
+                    a.Y0[j] = make_uint4(x0.x ^ h[0][0], x0.y ^ h[0][1], x0.z ^ h[0][2], x0.w ^ h[0][3]);
+                    a.Y1[j] = make_uint4(x1.x ^ h[1][0], x1.y ^ h[1][1], x1.z ^ h[1][2], x1.w ^ h[1][3]);
+                } else if constexpr (MODE == 1) {
+                    static_cast<uint4*>(a.sx)[j] = make_uint4(h[0][0], h[0][1], h[0][2], h[0][3]);
+                    a.Y0[j] = make_uint4(h[0][0] ^ a.delta[0] ^ h[1][0], h[0][1] ^ a.delta[1] ^ h[1][1],
+                                         h[0][2] ^ a.delta[2] ^ h[1][2], h[0][3] ^ a.delta[3] ^ h[1][3]);
+                } else if constexpr (MODE == 2) {
+                    const uint64_t v = ot_fe_of_u128((uint64_t)h[0][0] | ((uint64_t)h[0][1] << 32),
+                                                     (uint64_t)h[0][2] | ((uint64_t)h[0][3] << 32));
+                    const uint64_t vp = v + 1 == kOtFeP ? 0 : v + 1, vm = v ? v - 1 : kOtFeP - 1;
+                    const uint64_t gv = a.mask ? vp : v, p1 = a.mask ? vp : vm;   // r1 = v + mask; pair[1]
+                    static_cast<uint64_t*>(a.sx)[j] = gv;
+                    reinterpret_cast<uint2*>(a.Y0)[j] = make_uint2(h[1][0] ^ (uint32_t)p1, h[1][1] ^ (uint32_t)(p1 >> 32));
+                } else {
+                    static_cast<uint4*>(a.sx)[j] = make_uint4(h[0][0], h[0][1], h[0][2], h[0][3]);
+                    a.Y0[j] = make_uint4(h[1][0], h[1][1], h[1][2], h[1][3]);
+                }
             }
         }
     }
 }
 
+// The receive hash: one wave per 512-OT tile, 4 OTs (4 blocks) per AES pass. MODE 0: out = y^{r} ^
+// H(t); 1 / 3: out = r ? y ^ H(t) : H(t); 2: out (u64) = r ? lo64(y ^ H(t)) : H(t) mod p.
+template <int MODE>
 __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) {
     __shared__ uint32_t tbl_ot[OtTab::kWords];
     __shared__ uint32_t stage[kOtWaves][512];
@@ -348,160 +362,159 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
                     h[2 * rr + u][2] = tv[u].z; h[2 * rr + u][3] = tv[u].w;
                 }
             }
-            // OTs 0, 1 of the pass have their chosen Y in flight while the AES runs (r03: without the
-            // Y loads the kernel was 18 % faster, `profiles/r03/ot_diag/`): straight into the exchange
-            // stage, idle until the next pass (global_load_lds, 1 KiB per wave and OT, lane-linear);
-            // OTs 2, 3 load after it (16 more VGPRs, or 8 for just these two, spill beside the tile)
-            auto ysrc = [&](int b) -> const uint4* {   // the OT's chosen Y (inactive OTs: a valid block)
-                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
-                return j < m ? (((cw >> (j & 31)) & 1u) ? a.Y1 : a.Y0) + j : a.Y0;
+            auto otj = [&](int b) -> uint64_t { return ot_tile_ot(t, lane, r + (b >> 1), b & 1); };
+            auto chosen = [&](int b) -> uint32_t {   // the OT is active and its choice bit is set
+                const uint64_t j = otj(b);
+                return j < m ? (cw >> (j & 31)) & 1u : 0u;
             };
+            // the Y blocks the pass needs are in flight while its AES runs (r03: without the Y loads the
+            // plain kernel was 18 % faster, `profiles/r03/ot_diag/`): straight into the exchange stage,
+            // idle until the next pass (global_load_lds, lane-linear). Plain OT: OTs 0, 1 of the pass
+            // (16 B each; 2, 3 load after the AES). C-OT: a lane loads only when its choice bit is set
+            // (modes 1 / 3: 16 B for OTs 0, 1; mode 2: 8 B for all four OTs as two dwords)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the exchange's stage reads are done
+            if constexpr (MODE == 0) {
+                auto ysrc = [&](int b) -> const uint4* {   // the OT's chosen Y (inactive OTs: a valid block)
+                    const uint64_t j = otj(b);
+                    return j < m ? (((cw >> (j & 31)) & 1u) ? a.Y1 : a.Y0) + j : a.Y0;
+                };
 #pragma unroll
-            for (int b = 0; b < 2; b++)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ysrc(b)), &stage[wv][256 * b], 16, 0, 0);
-            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stage's Y blocks have landed
+                for (int b = 0; b < 2; b++)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ysrc(b)), &stage[wv][256 * b], 16, 0, 0);
+                aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stage's Y blocks have landed
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const uint4 y = b < 2 ? *reinterpret_cast<const uint4*>(&stage[wv][256 * b + 4 * lane]) : *ysrc(b);
-                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
-                if (j >= m) continue;
-                a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
+                for (int b = 0; b < 4; b++) {
+                    const uint4 y = b < 2 ? *reinterpret_cast<const uint4*>(&stage[wv][256 * b + 4 * lane]) : *ysrc(b);
+                    const uint64_t j = otj(b);
+                    if (j >= m) continue;
+                    a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
+                }
+            } else if constexpr (MODE == 2) {
+                const uint32_t* y32 = reinterpret_cast<const uint32_t*>(a.Y0);
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    if (chosen(b)) {
+                        const uint64_t j = otj(b);
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(y32 + 2 * j), &stage[wv][128 * b], 4, 0, 0);
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(y32 + 2 * j + 1), &stage[wv][128 * b + 64], 4, 0, 0);
+                    }
+                aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                uint64_t* o = reinterpret_cast<uint64_t*>(a.out);
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint64_t j = otj(b);
+                    if (j >= m) continue;
+                    const uint64_t hl = (uint64_t)h[b][0] | ((uint64_t)h[b][1] << 32);
+                    if (chosen(b)) {
+                        const uint64_t y = (uint64_t)stage[wv][128 * b + lane] | ((uint64_t)stage[wv][128 * b + 64 + lane] << 32);
+                        o[j] = y ^ hl;
+                    } else {
+                        o[j] = ot_fe_of_u128(hl, (uint64_t)h[b][2] | ((uint64_t)h[b][3] << 32));
+                    }
+                }
+            } else {   // modes 1, 3
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    if (chosen(b))
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(a.Y0 + otj(b)), &stage[wv][256 * b], 16, 0, 0);
+                aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint64_t j = otj(b);
+                    if (j >= m) continue;
+                    uint4 y = make_uint4(0, 0, 0, 0);
+                    if (chosen(b)) y = b < 2 ? *reinterpret_cast<const uint4*>(&stage[wv][256 * b + 4 * lane]) : a.Y0[j];
+                    a.out[j] = make_uint4(y.x ^ h[b][0], y.y ^ h[b][1], y.z ^ h[b][2], y.w ^ h[b][3]);
+                }
             }
             __builtin_amdgcn_wave_barrier();   // the Y reads precede the next pass's stage writes
         }
     }
 }
 
-// ---- prefetching forms (r04): fewer, register-richer waves --------------------------------------
-// PMC of the r03 hashes (profiles/r03/gcot_1m_pmc_means.json): the receive hash's waves issue VALU / LDS
-// in 25 % of their cycles and sit in s_waitcnt for ~57 % (SQ_WAIT_INST_ANY only 18 %): they wait on
-// memory — the tile's 32 row loads at every tile start and the chosen Y blocks after each pass's AES —
-// and with 4 waves per SIMD at 128 VGPRs there is no room to keep a second tile or the Y blocks in
-// flight. Here a workgroup has THREADS / 64 waves (512: 2 per SIMD, 256 VGPRs each; 768: 3 per SIMD,
-// 168 each) and every wave keeps the NEXT tile's 32 row words and the current pass's messages in
-// flight behind the current pass's AES: the next tile's loads are issued right after this tile's
-// transpose, a pass's Y (receiver) / x0, x1 (sender) loads right before its AES.
-__device__ __forceinline__ void ot_tile_issue(const uint32_t* rows, uint64_t tile, uint32_t lane, uint32_t (&x)[32]) {
-    const uint32_t q = lane >> 2, g = lane & 3;
-    const uint32_t* p = rows + tile * (128 * kOtTileWords) + (32 * g) * kOtTileWords + q;   // ot_tmaj
-#pragma unroll
-    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(p + i * kOtTileWords);
+// mode 3's second pass (the garbler's FieldElm share, collect.rs:846-876): test t = OT pair (2t, 2t + 1).
+// V = H(q_2t) || H(q_2t+1) read as 32 big-endian bytes (the BlockPair convention, field.rs:466-492),
+// reduced mod p255; the garbler's node value r1 = V + mask replaces the H(q) pair in sx (canonical
+// BlockPair), pair[1] = mask ? V + 1 : V - 1 is XORed into y = H(q ^ s). One lane per test.
+__device__ __forceinline__ void ot_bp_to_limbs(uint4 b0, uint4 b1, uint64_t (&r)[4]) {
+    r[3] = ((uint64_t)__builtin_bswap32(b0.x) << 32) | __builtin_bswap32(b0.y);
+    r[2] = ((uint64_t)__builtin_bswap32(b0.z) << 32) | __builtin_bswap32(b0.w);
+    r[1] = ((uint64_t)__builtin_bswap32(b1.x) << 32) | __builtin_bswap32(b1.y);
+    r[0] = ((uint64_t)__builtin_bswap32(b1.z) << 32) | __builtin_bswap32(b1.w);
 }
-
-template <int THREADS>
-__global__ __launch_bounds__(THREADS) void k_ot_recv_hash_pf(OtArgs a) {
-    constexpr int WAVES = THREADS / 64;
-    __shared__ uint32_t tbl_ot[OtTab::kWords];
-    __shared__ uint32_t stage[WAVES][512];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a);
-    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
-    if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
-    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.T);
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
-    uint32_t x[32];
-    if (t < tiles) ot_tile_issue(rows, t, lane, x);
-    for (; t < tiles; t += nwaves) {
-        transpose32(x);
-        uint32_t xn[32];
-        const uint64_t tn = t + nwaves;
-        if (tn < tiles) ot_tile_issue(rows, tn, lane, xn);   // wave-uniform
-        const uint64_t cwi = t * kOtTileWords + (lane & 15);
-        const uint32_t cw = 32 * cwi < m ? a.choices[cwi] : 0u;
-#pragma unroll 1
-        for (int r = 0; r < 4; r += 2) {
-            uint32_t h[4][4];
+__device__ __forceinline__ uint4 ot_limbs_to_block(uint64_t hi, uint64_t lo) {
+    return make_uint4(__builtin_bswap32((uint32_t)(hi >> 32)), __builtin_bswap32((uint32_t)hi),
+                      __builtin_bswap32((uint32_t)(lo >> 32)), __builtin_bswap32((uint32_t)lo));
+}
+// x (< 2^256) - p255 when x >= p255, at most twice (2^256 = 2 p + 38)
+__device__ __forceinline__ void ot_fe255_canon(uint64_t (&x)[4]) {
+    constexpr uint64_t P[4] = {0xFFFFFFFFFFFFFFEDull, ~0ull, ~0ull, 0x7FFFFFFFFFFFFFFFull};
 #pragma unroll
-            for (int rr = 0; rr < 2; rr++) {
-                uint4 tv[2];
-                ot_tile_round(stage[wv], x, lane, tv);
+    for (int it = 0; it < 2; it++) {
+        uint64_t t[4], borrow = 0;
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    h[2 * rr + u][0] = tv[u].x; h[2 * rr + u][1] = tv[u].y;
-                    h[2 * rr + u][2] = tv[u].z; h[2 * rr + u][3] = tv[u].w;
-                }
-            }
-            uint4 y[4];
-#pragma unroll
-            for (int b = 0; b < 4; b++) {   // the chosen Y of the pass's 4 OTs, in flight during its AES
-                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
-                y[b] = j < m ? (((cw >> (j & 31)) & 1u) ? a.Y1 : a.Y0)[j] : make_uint4(0, 0, 0, 0);
-            }
-            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const uint64_t j = ot_tile_ot(t, lane, r + (b >> 1), b & 1);
-                if (j >= m) continue;
-                a.out[j] = make_uint4(y[b].x ^ h[b][0], y[b].y ^ h[b][1], y[b].z ^ h[b][2], y[b].w ^ h[b][3]);
-            }
+        for (int k = 0; k < 4; k++) {
+            const unsigned __int128 v = (unsigned __int128)x[k] - P[k] - borrow;
+            t[k] = (uint64_t)v;
+            borrow = (uint64_t)(v >> 64) & 1;
         }
+        if (!borrow) {
 #pragma unroll
-        for (int i = 0; i < 32; i++) x[i] = xn[i];
+            for (int k = 0; k < 4; k++) x[k] = t[k];
+        }
+    }
+}
+// x +- 1 mod p255 for canonical x
+__device__ __forceinline__ void ot_fe255_inc(const uint64_t (&x)[4], uint64_t (&o)[4]) {
+    unsigned __int128 acc = (unsigned __int128)x[0] + 1;
+    o[0] = (uint64_t)acc;
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        acc = (unsigned __int128)x[k] + (uint64_t)(acc >> 64);
+        o[k] = (uint64_t)acc;
+    }
+    ot_fe255_canon(o);
+}
+__device__ __forceinline__ void ot_fe255_dec(const uint64_t (&x)[4], uint64_t (&o)[4]) {
+    if ((x[0] | x[1] | x[2] | x[3]) == 0) {   // 0 - 1 = p - 1
+        o[0] = 0xFFFFFFFFFFFFFFECull;
+        o[1] = o[2] = ~0ull;
+        o[3] = 0x7FFFFFFFFFFFFFFFull;
+        return;
+    }
+    uint64_t borrow = 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        o[k] = x[k] - borrow;
+        borrow = (x[k] < borrow) ? 1 : 0;
     }
 }
 
-template <int THREADS>
-__global__ __launch_bounds__(THREADS) void k_ot_send_hash_pf(OtArgs a) {
-    constexpr int WAVES = THREADS / 64;
-    __shared__ uint32_t tbl_ot[OtTab::kWords];
-    __shared__ uint32_t stage[WAVES][512];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t m = ot_active(a);
-    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
-    if ((uint64_t)blockIdx.x * WAVES >= tiles) return;
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
-    const uint32_t* rows = reinterpret_cast<const uint32_t*>(a.Q);
-    uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
-    uint32_t x[32];
-    if (t < tiles) ot_tile_issue(rows, t, lane, x);
-    for (; t < tiles; t += nwaves) {
-        transpose32(x);
-        uint32_t xn[32];
-        const uint64_t tn = t + nwaves;
-        if (tn < tiles) ot_tile_issue(rows, tn, lane, xn);   // wave-uniform
-#pragma unroll 1
-        for (int r = 0; r < 4; r++) {
-            uint4 q[2];
-            ot_tile_round(stage[wv], x, lane, q);
-            uint4 m0[2], m1[2];
+__global__ __launch_bounds__(256) void k_cot_fe255_finish(OtArgs a) {
+    const uint64_t tests = ot_active(a) / 2;
+    uint4* sx = static_cast<uint4*>(a.sx);
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tests; t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t V[4], G[4], P1[4];
+        ot_bp_to_limbs(sx[2 * t], sx[2 * t + 1], V);
+        ot_fe255_canon(V);
+        if (a.mask) {
+            ot_fe255_inc(V, G);
 #pragma unroll
-            for (int u = 0; u < 2; u++) {   // the pass's messages, in flight during its AES
-                const uint64_t j = ot_tile_ot(t, lane, r, u);
-                const uint64_t jj = j < m ? j : 0;
-                m0[u] = a.x0[jj];
-                m1[u] = a.x1 ? a.x1[jj]
-                             : make_uint4(m0[u].x ^ a.delta[0], m0[u].y ^ a.delta[1], m0[u].z ^ a.delta[2],
-                                          m0[u].w ^ a.delta[3]);
-            }
-            uint32_t h[4][4];
+            for (int k = 0; k < 4; k++) P1[k] = G[k];
+        } else {
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                h[2 * u][0] = q[u].x; h[2 * u][1] = q[u].y; h[2 * u][2] = q[u].z; h[2 * u][3] = q[u].w;
-                h[2 * u + 1][0] = q[u].x ^ a.s[0]; h[2 * u + 1][1] = q[u].y ^ a.s[1];
-                h[2 * u + 1][2] = q[u].z ^ a.s[2]; h[2 * u + 1][3] = q[u].w ^ a.s[3];
-            }
-            aes0_mmo_tab<DevOpsX, OtTab, 4>(h, tbl_ot, b0, b1);   // cr_hash: pi(x) ^ x, 2 OTs x 2 blocks
-#pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const uint64_t j = ot_tile_ot(t, lane, r, u);
-                if (j >= m) continue;
-                a.Y0[j] = make_uint4(m0[u].x ^ h[2 * u][0], m0[u].y ^ h[2 * u][1], m0[u].z ^ h[2 * u][2],
-                                     m0[u].w ^ h[2 * u][3]);
-                a.Y1[j] = make_uint4(m1[u].x ^ h[2 * u + 1][0], m1[u].y ^ h[2 * u + 1][1], m1[u].z ^ h[2 * u + 1][2],
-                                     m1[u].w ^ h[2 * u + 1][3]);
-            }
+            for (int k = 0; k < 4; k++) G[k] = V[k];
+            ot_fe255_dec(V, P1);
         }
-#pragma unroll
-        for (int i = 0; i < 32; i++) x[i] = xn[i];
+        sx[2 * t] = ot_limbs_to_block(G[3], G[2]);
+        sx[2 * t + 1] = ot_limbs_to_block(G[1], G[0]);
+        const uint4 e0 = ot_limbs_to_block(P1[3], P1[2]), e1 = ot_limbs_to_block(P1[1], P1[0]);
+        const uint4 y0 = a.Y0[2 * t], y1 = a.Y0[2 * t + 1];
+        a.Y0[2 * t] = make_uint4(y0.x ^ e0.x, y0.y ^ e0.y, y0.z ^ e0.z, y0.w ^ e0.w);
+        a.Y0[2 * t + 1] = make_uint4(y1.x ^ e1.x, y1.y ^ e1.y, y1.z ^ e1.z, y1.w ^ e1.w);
     }
 }
 
@@ -590,50 +603,44 @@ hipError_t launch_mask_word(uint32_t* word, uint32_t mask, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// fused forms: one 1024-thread workgroup per CU (160 KiB of LDS), waves stride over the tiles
+// the hashes: one 1024-thread workgroup per CU (160 KiB of LDS), waves stride over the tiles
 static int ot_rows_grid(const OtArgs& a) {
     const uint64_t tiles = (a.m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     const uint64_t need = (tiles + kOtWaves - 1) / kOtWaves, cap = (uint64_t)device_cus();
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 
-// hash forms (A/B, process-wide, read once): FHH_OT_SEND_HASH / FHH_OT_RECV_HASH = 0 (r03: 1024
-// threads, 4 waves per SIMD), 512 or 768 (the prefetching forms)
-static int ot_hash_form(bool send) {
-    static std::atomic<int> form[2] = {-1, -1};
-    int f = form[send].load(std::memory_order_relaxed);
-    if (f < 0) {
-        const char* e = std::getenv(send ? "FHH_OT_SEND_HASH" : "FHH_OT_RECV_HASH");
-        f = e ? std::atoi(e) : 0;
-        if (f != 512 && f != 768) f = 0;
-        form[send].store(f, std::memory_order_relaxed);
-    }
-    return f;
-}
-
-static int ot_rows_grid_waves(const OtArgs& a, int waves) {
-    const uint64_t tiles = (a.m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
-    const uint64_t need = (tiles + waves - 1) / waves, cap = (uint64_t)device_cus();
-    return (int)(need < cap ? (need ? need : 1) : cap);
-}
-
 hipError_t launch_ot_send_hash_rows(const OtArgs& a, hipStream_t stream) {
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // tiles of 16 words stay inside a row
-    switch (a.fe.n ? 0 : ot_hash_form(true)) {   // the prefetching forms read x0 / x1 only
-        case 512: hipLaunchKernelGGL(k_ot_send_hash_pf<512>, dim3(ot_rows_grid_waves(a, 8)), dim3(512), 0, stream, a); break;
-        case 768: hipLaunchKernelGGL(k_ot_send_hash_pf<768>, dim3(ot_rows_grid_waves(a, 12)), dim3(768), 0, stream, a); break;
-        default: hipLaunchKernelGGL(k_ot_send_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    const dim3 g(ot_rows_grid(a)), b(kOtRowsThreads);
+    switch (a.mode) {
+        case 0: hipLaunchKernelGGL(k_ot_send_hash_rows<0>, g, b, 0, stream, a); break;
+        case 1: hipLaunchKernelGGL(k_ot_send_hash_rows<1>, g, b, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL(k_ot_send_hash_rows<2>, g, b, 0, stream, a); break;
+        case 3: hipLaunchKernelGGL(k_ot_send_hash_rows<3>, g, b, 0, stream, a); break;
+        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_ot_recv_hash_rows(const OtArgs& a, hipStream_t stream) {
     if (a.mp % 8192 != 0) return hipErrorInvalidValue;
-    switch (ot_hash_form(false)) {
-        case 512: hipLaunchKernelGGL(k_ot_recv_hash_pf<512>, dim3(ot_rows_grid_waves(a, 8)), dim3(512), 0, stream, a); break;
-        case 768: hipLaunchKernelGGL(k_ot_recv_hash_pf<768>, dim3(ot_rows_grid_waves(a, 12)), dim3(768), 0, stream, a); break;
-        default: hipLaunchKernelGGL(k_ot_recv_hash_rows, dim3(ot_rows_grid(a)), dim3(kOtRowsThreads), 0, stream, a);
+    const dim3 g(ot_rows_grid(a)), b(kOtRowsThreads);
+    switch (a.mode) {
+        case 0: hipLaunchKernelGGL(k_ot_recv_hash_rows<0>, g, b, 0, stream, a); break;
+        case 1: hipLaunchKernelGGL(k_ot_recv_hash_rows<1>, g, b, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL(k_ot_recv_hash_rows<2>, g, b, 0, stream, a); break;
+        case 3: hipLaunchKernelGGL(k_ot_recv_hash_rows<3>, g, b, 0, stream, a); break;
+        default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_cot_fe255_finish(const OtArgs& a, hipStream_t stream) {
+    if (a.mode != 3 || a.m % 2) return hipErrorInvalidValue;
+    const uint64_t tests = a.m / 2;
+    const uint64_t need = (tests + 255) / 256, cap = (uint64_t)device_cus() * 8;
+    hipLaunchKernelGGL(k_cot_fe255_finish, dim3((int)(need < cap ? (need ? need : 1) : cap)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

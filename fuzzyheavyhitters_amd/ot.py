@@ -4,6 +4,7 @@ collect.rs:437-471), backed by fhh_ot.hip. Both parties run in one process; the 
 are ideal. See include/fhh.h (fhh_ot_batch) for the exact construction."""
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -46,3 +47,30 @@ def ot_extend(kc, choices, x0, x1=None, delta=None, base_seeds=None, base_choice
                                    ptr(seeds), ptr(s), tweak_base, ptr(out), ptr(u) if transcript else None,
                                    ptr(y0) if transcript else None, ptr(y1) if transcript else None), kc.handle)
     return (out, u, y0, y1) if transcript else out
+
+
+def cot_extend(kc, mode: int, choices, base_seeds, base_choice, delta=None, mask: int = 0, ctr_off: int = 0,
+               transcript: bool = False):
+    """Correlated OT extension on the GPU (fhh_cot_extend_host; the r05 protocol's two OTs, see
+    include/fhh.h FHH_COT_*): returns (sender_out, out) and, with transcript, (U, y).
+    mode 1 (labels): sender_out = x0 [m][16] (x1 = x0 ^ delta), out [m][16]; mode 2 (FE share):
+    sender values / out [m] u64 (the garbler's r1 = v + mask, the receiver's share); mode 3 (FieldElm,
+    OT pairs with one choice): sender values / out [m/2][32] BlockPairs."""
+    from ._lib import FHH_COT_FE, FHH_COT_FE255
+    ch = np.ascontiguousarray(np.asarray(choices).astype(np.uint8) & 1)
+    m = ch.size
+    seeds = np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16)
+    s = np.frombuffer(bytes(base_choice), np.uint8).copy()
+    d = np.frombuffer(bytes(delta), np.uint8).copy() if delta is not None else np.zeros(16, np.uint8)
+    if mode == FHH_COT_FE:
+        sx, out, y = np.zeros(m, np.uint64), np.zeros(m, np.uint64), np.zeros(m, np.uint64)
+    elif mode == FHH_COT_FE255:
+        sx, out, y = np.zeros((m // 2, 32), np.uint8), np.zeros((m // 2, 32), np.uint8), np.zeros((m, 16), np.uint8)
+    else:
+        sx, out, y = np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8)
+    u = np.zeros((128, (m + 127) // 128, 16), np.uint8) if transcript else None
+    u8 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    check(lib().fhh_cot_extend_host(kc.handle, m, mode, ptr(ch), ptr(d), int(mask) & 1, ptr(seeds), ptr(s), ctr_off,
+                                    u8(sx), u8(out), ptr(u) if transcript else None, u8(y) if transcript else None),
+          kc.handle)
+    return (sx, out, u, y) if transcript else (sx, out)

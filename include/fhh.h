@@ -271,9 +271,11 @@ typedef struct fhh_sim_config {
     /* mode 1, device loop: the per-(child, client) equality bit comes from the garbled-circuit
      * equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
      * evaluates), as tree_crawl does with gc_sender (collect.rs:419-482). 1 = the OTs (the
-     * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU OT
-     * extension (fhh_ot_*; base OTs ideal; a FieldElm share travels as a BlockPair = 2 OTs).
-     * Same sums as 0; fresh garbler key, Delta, mask and base OTs per level, from prf_seed. */
+     * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU correlated
+     * OT extension (fhh_cot_extend_host's modes; a FieldElm share travels as a BlockPair = 2 OTs).
+     * Same sums as 0. Material from prf_seed (a harness, not private): garbler key, Delta and mask
+     * fresh per chunk of children; one base-OT session per level and OT kind, each chunk on its own
+     * row-PRG counter range. */
     uint32_t gc;
     /* parity probe of the device loop (tests; probe_n_levels = 0 disables it): right after level
      * probe_levels[k]'s k_expand, the pending children's EvalStates (ibDCF.rs:24-30) of the
@@ -293,10 +295,11 @@ typedef struct fhh_sim_config {
     uint8_t* probe_ty;
     uint64_t* probe_children;
     /* gc = 2: 0 = ideal base OTs (seed pairs derived on the device per level); 1 = real base OTs:
-     * Chou–Orlandi (fhh_base_ot_co15), a fresh instance for each of the 2 OT extensions of every
-     * level (the evaluator's labels, then the FE / FieldElm share conversion), produced by a pool of
-     * host threads (OMP_NUM_THREADS) one level ahead of the GPU (busy time in
-     * fhh_stats.base_ot_ms) and uploaded as key schedules before the level's OT. */
+     * Chou–Orlandi (fhh_base_ot_co15), a fresh instance for each of the 2 OT kinds of every level
+     * (the evaluator's labels, then the FE / FieldElm share conversion), produced by a pool of host
+     * threads (OMP_NUM_THREADS) a few levels ahead of the GPU (fhh_stats.base_ot_ms: their compute
+     * time; base_ot_stall_ms: the time the loop waited for them) and uploaded as key schedules
+     * before the level's OTs. */
     uint32_t base_ot;
 } fhh_sim_config;
 
@@ -491,69 +494,112 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
                        const uint8_t delta[16], const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                        uint64_t tweak_base, uint8_t* out, uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out);
 
+/* ---- correlated OT extension (r05: the protocol's two OTs) ----------------------------------
+ * The reference moves the evaluator's input labels (equalitytest.rs:67-82) and the FE shares
+ * (collect.rs:437-471) with plain OTs of two chosen messages. Both pairs are correlated — labels
+ * (x, x ^ Delta), shares (r, r +- 1) — so the build runs them as ALSZ correlated OT (ocelot's
+ * AlszSender::send_correlated): the sender's first message is the hash itself, x0_j = H(q_j), and
+ * only y_j = f(x0_j) ^ H(q_j ^ s) crosses. That removes the garbler's evaluator-label blocks, the
+ * share PRF and half of each reply. Modes (oracle/fhh_oracle.c orc_cot_extend is the restatement):
+ *   FHH_COT_LABELS  x1 = x0 ^ delta; y 16 B; out = r ? y ^ H(t) : H(t); sender_out = x0 [m][16]
+ *   FHH_COT_FE      v = H(q_j) as a little-endian u128 mod p_FE; the garbler's pair is ordered by
+ *                   its mask as collect.rs:447-451 orders (r0, r1): pair[0] = v, pair[1] = mask ?
+ *                   v + 1 : v - 1, its node value r1 = v + mask (sender_out [m] u64); y = lo64(H(q_j
+ *                   ^ s)) ^ pair[1] (8 B); out [m] u64 = r ? lo64(y ^ H(t)) : H(t) mod p
+ *   FHH_COT_FE255   a test is the OT pair (2t, 2t + 1) with one choice (m even): V = the 32 big-endian
+ *                   bytes H(q_2t) || H(q_2t+1) mod p255, pair[1] = mask ? V + 1 : V - 1 as a BlockPair
+ *                   (field.rs:478-492); sender_out [m/2][32] = V + mask; y 16 B per OT; out [m/2][32]
+ *                   = r ? y ^ H(t) : H(t), the raw BlockPair FieldElm::try_from reads unreduced
+ *                   (field.rs:466-476)
+ * ctr_off: the row PRG's first block (a multiple of 256): batches that extend one set of base OTs
+ * must use disjoint counter ranges (the party ABI below keeps a running counter per session).
+ * Host buffers: choices [m] 0/1 bytes; u_out [128][ceil(m/128)][16]; y_out [m][8 or 16]. */
+#define FHH_COT_LABELS 1
+#define FHH_COT_FE 2
+#define FHH_COT_FE255 3
+int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
+                        uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                        uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out);
+/* The r05 labels step of one batch on host buffers: the labels C-OT (choice bits = the evaluator's
+ * bits at OT index j npad + i, npad = n rounded up to 64), garbling on the C-OT's zero labels (the
+ * garbler draws only its bits + 1 wires: label of (t, w) = AES_label_key(LE128(label_nonce + t S +
+ * w)), S the power of two >= bits + 1, min 4), evaluation on the OT'd active labels. Outputs AoS as
+ * fhh_gc_equality_host, plus ev_zero / ev_active [n][bits][16] (the C-OT's sender messages / the
+ * evaluator's labels); any output but `out` may be NULL. */
+int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                    uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
+                    uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                    uint64_t ctr_off, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_zero, uint8_t* ev_active,
+                    uint8_t* decode, uint8_t* out);
+
 /* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
  * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;
  * equalitytest.rs:25-106): each server runs only its own half on its own ctx, right after its
- * fhh_tree_crawl / fhh_tree_crawl_last, and keeps its secrets; what crosses is five byte buffers,
- * in this order:
- *   server 0 (garbler, OT sender)                         server 1 (evaluator, OT receiver)
- *   fhh_gb_garble        -> gc  ---------------------->   fhh_ev_ot_labels -> u1
- *   fhh_gb_ot_labels(u1) -> y1  ---------------------->   fhh_ev_evaluate(gc, y1) -> u2
- *   fhh_gb_ot_shares(u2) -> y2  ---------------------->   fhh_ev_ot_shares(y2)
- *   fhh_party_node_sums                                   fhh_party_node_sums
- * (the evaluator may call fhh_ev_ot_labels before receiving gc). Outputs are device buffers owned
- * by the producing ctx, valid until its next party call; inputs are device pointers on the
- * receiving ctx's GPU (the caller moves the bytes: a network in a deployment, a device copy in the
- * in-process tests). The circuit, labels and OTs are those of fhh_gc_batch / fhh_ot_batch;
- * gc = [tables (bits-1) x 2 | garbler labels bits + 1 | decode 1 B] per test, tests = C x n in
- * child-major order; u = the OT receiver's [128][m padded to 8192 / 128] blocks; y = Y0 | Y1
- * ([m] blocks each). OT 1 moves the evaluator's input labels (m = C x 2d x npad: its share planes
- * are the choice bits), OT 2 the FE share (m = C x n; a FieldElm at tree_crawl_last = a
- * BlockPair, 2 OTs per test, collect.rs:846-876). The garbler's node value is r1 = r0 + 1, the
- * evaluator's the OT output (collect.rs:439-472); fhh_party_node_sums sums them on the device:
- * non-last level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm
- * (the frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own
- * channel, as the reference runs a level's tests over several channels (collect.rs:423-430).
- * Chunks of children: a cfg with child_count > 0 runs the protocol for children [child_begin,
- * child_begin + child_count) only (C above = the chunk's children, tests child-major within it) —
- * one protocol instance per chunk, as the reference's channels each run a slice of the level's
- * tests (collect.rs:423-430); this bounds the level's buffers (~400 B per test for both parties at
- * d = 1) at 1M clients. Chunks run in order, each the full five-message sequence, and together
- * cover [0, C); fhh_party_node_sums follows the last one and sums the whole level. Both parties
- * must use the same window. child_count = 0: the whole level in one instance. */
-typedef struct fhh_gc_party_cfg {
-    /* garbler only (fresh per level: AesRng::new(), collect.rs:432) */
-    uint8_t label_key[16];               /* label PRG key                                          */
+ * fhh_tree_crawl / fhh_tree_crawl_last, with only its OWN secrets — the garbler's fhh_gb_cfg and the
+ * evaluator's fhh_ev_cfg share nothing (each server draws its material itself: AesRng::new() per
+ * channel, collect.rs:431; base OTs by fhh_co15_* over the channel, OtSender / OtReceiver::init,
+ * collect.rs:454,460). Five byte buffers cross per chunk, in this order:
+ *   server 0 (garbler, OT sender)                          server 1 (evaluator, OT receiver)
+ *                                      <--------------  fhh_ev_ot_labels(ev_cfg) -> u1
+ *   fhh_gb_ot_labels(gb_cfg, u1) -> y1 -------------->
+ *   fhh_gb_garble -> gc               -------------->   fhh_ev_evaluate(gc, y1) -> u2
+ *   fhh_gb_ot_shares(u2) -> y2        -------------->   fhh_ev_ot_shares(y2)
+ *   fhh_party_node_sums                                  fhh_party_node_sums
+ * Outputs are device buffers owned by the producing ctx, valid until its next party call; inputs are
+ * device pointers on the receiving ctx's GPU (the caller moves the bytes: a network in a deployment, a
+ * device copy in the in-process tests). Both OTs are correlated OTs (fhh_cot_extend_host's modes):
+ * OT 1 (FHH_COT_LABELS) delivers the evaluator's input labels (m = C x 2d x npad: its share planes are
+ * the choice bits), OT 2 (FHH_COT_FE, FHH_COT_FE255 at tree_crawl_last: 2 OTs per test) the share;
+ * the circuit is fhh_gc_cot_host's. gc = [tables (bits-1) x 2 | garbler labels bits + 1 | decode 1 B]
+ * per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
+ * y1 16 B per OT, y2 8 B per OT (FE) or 16 B per OT (FieldElm). Each server's node values (the garbler's
+ * r1 = v + mask, the evaluator's OT output) stay on its device; fhh_party_node_sums sums them: non-last
+ * level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm (the
+ * frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own channel,
+ * as the reference runs a level's tests over several channels (collect.rs:423-430).
+ * Chunks of children: child_count > 0 runs the protocol for children [child_begin, child_begin +
+ * child_count) only (C above = the chunk's children) — one protocol instance per chunk, as the
+ * reference's channels each run a slice of the level's tests (collect.rs:423-430); this bounds the
+ * level's buffers at 1M clients. Chunks run in order and together cover [0, C); fhh_party_node_sums
+ * follows the last one. Both parties must use the same windows. child_count = 0: the whole level.
+ * Freshness: the garbler's label key / Delta / mask should be fresh per chunk (labels and gate tweaks
+ * are indexed by the test's index in the whole level, so a key reused WITHIN a level never repeats a
+ * label, but Delta must not outlive the level). Base OTs may be reused across chunks and levels: each
+ * ctx keeps, per OT kind, the running row-PRG counter of the base material it last saw and continues
+ * it while the material is unchanged (a new set starts at 0), so pads never repeat. */
+typedef struct fhh_gb_cfg {
+    uint8_t label_key[16];               /* label PRG key (AesRng::new(), collect.rs:431)           */
     uint8_t delta[16];                   /* free-XOR offset (bit 0 forced to 1)                    */
-    uint32_t mask;                       /* the level's mask bit (equalitytest.rs:38-43)           */
+    uint32_t mask;                       /* the chunk's mask bit (equalitytest.rs:38-43)           */
     uint32_t pad_;
-    uint64_t share_seed;                 /* PRF key of the r0 values (T::random(), collect.rs:441) */
-    /* the base OTs of OT 1 (index 0) and OT 2 (index 1) (OtSender/OtReceiver::init,
-     * collect.rs:454-471): the OT-extension receiver holds both seeds of every base OT, the sender
-     * one seed per base OT and its choice bits (e.g. from fhh_co15_*) */
-    uint8_t base_pairs[2][128][2][16];   /* evaluator                                              */
-    uint8_t base_chosen[2][128][16];     /* garbler: base_pairs[t][i][s_i]                         */
-    uint8_t base_choice[2][16];          /* garbler: s (bit i % 8 of byte i / 8)                   */
-    /* both parties: the chunk of the level's children this instance covers (0 / 0 = all) */
+    uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares): k_i^{s_i} from the   */
+    uint8_t base_choice[2][16];          /* base OTs, and s (bit i % 8 of byte i / 8)              */
     uint64_t child_begin;
     uint64_t child_count;
-} fhh_gc_party_cfg;
-int fhh_gb_garble(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes);
-int fhh_gb_ot_labels(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);
-int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);
-int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_gc_party_cfg* cfg, const uint8_t** u_dev, uint64_t* u_bytes);
+} fhh_gb_cfg;
+typedef struct fhh_ev_cfg {
+    uint8_t base_pairs[2][128][2][16];   /* per OT kind: both base-OT keys of every base OT        */
+    uint64_t child_begin;
+    uint64_t child_count;
+} fhh_ev_cfg;
+int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev, uint64_t* u_bytes);
+int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev,
+                     uint64_t* y_bytes);
+int fhh_gb_garble(fhh_ctx* ctx, const uint8_t** gc_msg_dev, uint64_t* gc_msg_bytes);
 int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_msg_bytes, const uint8_t* y_dev,
                     uint64_t y_bytes, const uint8_t** u_dev, uint64_t* u_bytes);
+int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_bytes, const uint8_t** y_dev, uint64_t* y_bytes);
 int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_bytes);
 /* sums_a = uint64_t[C] (non-last level) or uint32_t[C][10] unreduced (last); sums_b = NULL or
  * uint32_t[C][8] canonical (last level) */
 int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b);
 /* bytes this ctx sent in the level so far (its outgoing messages) */
 int fhh_party_bytes_sent(const fhh_ctx* ctx, uint64_t* bytes);
-/* The in-process level loop's per-level material (fhh_sim_config.gc = 2, ideal base OTs) for
- * prf_seed and level, so a two-ctx run can reproduce fhh_sim_crawl's transcripts; a deployment
- * draws fresh randomness instead. */
-int fhh_gc_party_level_cfg(uint64_t prf_seed, uint32_t level, fhh_gc_party_cfg* out);
+/* TEST MODE ONLY: both parties' configs derived from one seed — the in-process level loop's material
+ * (fhh_sim_config.gc = 2, ideal base OTs) for prf_seed and level, so a two-ctx run can mirror
+ * fhh_sim_crawl. Not private (one seed knows both sides); a deployment draws each party's
+ * material on its own side. */
+int fhh_gc_party_test_cfgs(uint64_t prf_seed, uint32_t level, fhh_gb_cfg* gb, fhh_ev_cfg* ev);
 
 /* ---- base OTs (the OT extension's init, collect.rs:454-471) -------------------------------
  * Chou–Orlandi "simplest OT" over NIST P-256 (ocelot runs it over Ristretto; not vendored, so the
@@ -581,7 +627,8 @@ typedef struct fhh_stats {
     uint64_t levels;            /* crawled levels                                        */
     double keygen_ms;
     uint64_t expand_launches_timed; /* k_expand launches covered by expand_ms             */
-    double base_ot_ms;          /* host time of the real base OTs (fhh_sim_config.base_ot) */
+    double base_ot_ms;          /* real base OTs (fhh_sim_config.base_ot): summed per-instance host
+                                 * compute time (CO15 + key schedules) over the producer's threads */
     double allreduce_ms;        /* device loop, cfg->comm / allreduce: summed per-level cross-rank
                                  * all-reduce time (HIP events around it on the engine stream,
                                  * on the levels fhh_set_timing times)                      */
@@ -590,6 +637,9 @@ typedef struct fhh_stats {
                                  * planes, garble, OTs, evaluate, share sums; HIP events on the
                                  * engine stream, on the levels fhh_set_timing times)        */
     uint64_t gcot_timed;        /* levels covered by gcot_ms                                  */
+    double base_ot_stall_ms;    /* time the level loop's enqueueing thread waited for a base-OT
+                                 * instance it needed (the base OTs on the crawl's critical path) */
+    uint64_t base_ot_instances; /* base-OT instances (128 CO15 OTs each) computed              */
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);

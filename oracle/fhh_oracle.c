@@ -176,10 +176,39 @@ __attribute__((target("aes,sse4.1"))) void orc_aes128_zero_encrypt_ni(const uint
     __m128i x = _mm_loadu_si128((const __m128i*)in);
     _mm_storeu_si128((__m128i*)out, ni_aes0(x));
 }
+
+/* Keyed AES-NI block under an expanded key (the GC label PRG and the OT extension's row PRG:
+ * swanky's AesRng / scuttlebutt Aes128 run on AES-NI, as the reference builds with
+ * target-cpu=native, README.md:43). */
+__attribute__((target("aes,sse4.1"))) static void ni_aes_rk(const uint8_t rk[176], const uint8_t in[16],
+                                                            uint8_t out[16]) {
+    __m128i x = _mm_xor_si128(_mm_loadu_si128((const __m128i*)in), _mm_loadu_si128((const __m128i*)rk));
+    for (int r = 1; r < 10; r++) x = _mm_aesenc_si128(x, _mm_loadu_si128((const __m128i*)(rk + 16 * r)));
+    _mm_storeu_si128((__m128i*)out, _mm_aesenclast_si128(x, _mm_loadu_si128((const __m128i*)(rk + 160))));
+}
 #else
 int orc_aes_ni_available(void) { return 0; }
 void orc_aes128_zero_encrypt_ni(const uint8_t in[16], uint8_t out[16]) { orc_aes128_zero_encrypt(in, out); }
+static void ni_aes_rk(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) { aes128_encrypt_rk(rk, in, out); }
 #endif
+
+/* The GC / OT restatement (row f1) runs its AES on AES-NI when the CPU has it (-1: not yet
+ * decided), the byte-wise FIPS-197 path otherwise; orc_gc_set_ni(0) forces the byte-wise path (the
+ * tests compare both). */
+static int g_gc_ni = -1;
+void orc_gc_set_ni(int on) { g_gc_ni = on ? orc_aes_ni_available() : 0; }
+int orc_gc_get_ni(void) {
+    if (g_gc_ni < 0) g_gc_ni = orc_aes_ni_available();
+    return g_gc_ni;
+}
+static void gc_aes_rk(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) {
+    if (orc_gc_get_ni()) ni_aes_rk(rk, in, out);
+    else aes128_encrypt_rk(rk, in, out);
+}
+static void gc_aes0(const uint8_t in[16], uint8_t out[16]) {
+    if (orc_gc_get_ni()) orc_aes128_zero_encrypt_ni(in, out);
+    else orc_aes128_zero_encrypt(in, out);
+}
 
 /* ------------------------------------------------------------------ */
 /* Fixed-key PRG (src/prg.rs)                                          */
@@ -927,10 +956,10 @@ void orc_sketch_verify_fe255_batch(uint64_t n_keys, uint32_t n_nodes, const uint
 /* ------------------------------------------------------------------ */
 static void gc_tccr(const uint8_t x[16], uint64_t tweak, uint8_t out[16]) {
     uint8_t px[16], q[16], y[16];
-    orc_aes128_zero_encrypt(x, px);
+    gc_aes0(x, px);
     memcpy(q, px, 16);
     for (int k = 0; k < 8; k++) q[k] ^= (uint8_t)(tweak >> (8 * k));
-    orc_aes128_zero_encrypt(q, y);
+    gc_aes0(q, y);
     for (int k = 0; k < 16; k++) out[k] = y[k] ^ px[k];
 }
 
@@ -938,18 +967,25 @@ static void gc_xor(uint8_t* d, const uint8_t* a, const uint8_t* b) {
     for (int k = 0; k < 16; k++) d[k] = a[k] ^ b[k];
 }
 
-/* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits. The evaluator's
- * active labels (what OT delivers, gb_set_fancy_inputs :67-82) are output too. Layouts:
- * tables [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last), ev_labels [n][bits][16]. */
-void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits, uint32_t mask,
-                      const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
-                      uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels, uint8_t* decode) {
+/* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits. Layouts: tables
+ * [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last), ev_labels [n][bits][16].
+ * ev_zero == NULL (ideal OT): every zero label is AES_key(LE128(nonce + t S + w)), S = the power of
+ * two >= 2 bits + 1 (w < bits: the garbler's string, w = bits: the mask, w > bits: the evaluator's
+ * string), and the evaluator's ACTIVE labels (what an OT would deliver, gb_set_fancy_inputs :67-82)
+ * are written to ev_labels. ev_zero != NULL [n][bits][16] (r05: the labels OT is a correlated OT,
+ * orc_cot_extend mode 1): the evaluator's zero labels are the C-OT's sender messages, the garbler
+ * draws only its own wires and the mask (S = the power of two >= bits + 1, min 4) and ev_labels is
+ * not written. */
+static void gc_garble_impl(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                           const uint8_t* ev_zero, uint32_t mask, const uint8_t key[16], const uint8_t delta_in[16],
+                           uint64_t label_nonce, uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels,
+                           uint8_t* ev_labels, uint8_t* decode) {
     oracle_init();
     uint8_t rk[176], D[16];
     key_expand(key, rk);
     memcpy(D, delta_in, 16);
     D[0] |= 1;
-    const uint64_t W = 2 * (uint64_t)bits + 1;
+    const uint64_t W = ev_zero ? (uint64_t)bits + 1 : 2 * (uint64_t)bits + 1;
     uint64_t WS = 4;                                 /* label counter stride: the power of two >= W */
     while (WS < W) WS *= 2;
 #pragma omp parallel for schedule(static)
@@ -959,15 +995,19 @@ void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const u
             uint8_t ctr[16] = {0};
             const uint64_t c = label_nonce + (uint64_t)t * WS + w;
             for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
-            aes128_encrypt_rk(rk, ctr, L[w]);
+            gc_aes_rk(rk, ctr, L[w]);
         }
+        if (ev_zero)                                 /* the C-OT's sender messages */
+            for (uint32_t j = 0; j < bits; j++) memcpy(L[bits + 1 + j], ev_zero + ((uint64_t)t * bits + j) * 16, 16);
         for (uint32_t j = 0; j < bits; j++) {        /* active input labels */
             uint8_t* g = gb_labels + ((uint64_t)t * (bits + 1) + j) * 16;
-            uint8_t* e = ev_labels + ((uint64_t)t * bits + j) * 16;
             memcpy(g, L[j], 16);
-            memcpy(e, L[bits + 1 + j], 16);
             if (gb_bits[(uint64_t)t * bits + j] & 1) gc_xor(g, g, D);
-            if (ev_bits[(uint64_t)t * bits + j] & 1) gc_xor(e, e, D);
+            if (!ev_zero) {
+                uint8_t* e = ev_labels + ((uint64_t)t * bits + j) * 16;
+                memcpy(e, L[bits + 1 + j], 16);
+                if (ev_bits[(uint64_t)t * bits + j] & 1) gc_xor(e, e, D);
+            }
         }
         uint8_t* m = gb_labels + ((uint64_t)t * (bits + 1) + bits) * 16;
         memcpy(m, L[bits], 16);
@@ -1006,6 +1046,22 @@ void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const u
         }
         decode[t] = (uint8_t)((acc[0] ^ L[bits][0]) & 1);   /* colour of out's zero label */
     }
+}
+
+void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits, uint32_t mask,
+                      const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
+                      uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels, uint8_t* decode) {
+    gc_garble_impl(n, bits, gb_bits, ev_bits, NULL, mask, key, delta_in, label_nonce, gate_base, tables, gb_labels,
+                   ev_labels, decode);
+}
+
+/* The garbler of the r05 protocol: the evaluator's zero labels ev_zero [n][bits][16] come from the
+ * labels C-OT (orc_cot_extend mode 1), the garbler labels its own string and the mask. */
+void orc_gc_garble_eq_cot(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
+                          const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
+                          uint8_t* tables, uint8_t* gb_labels, uint8_t* decode) {
+    gc_garble_impl(n, bits, gb_bits, NULL, ev_zero, mask, key, delta_in, label_nonce, gate_base, tables, gb_labels,
+                   NULL, decode);
 }
 
 /* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */
@@ -1051,7 +1107,7 @@ void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint
 static void ot_prg_block(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
     uint8_t ctr[16] = {0};
     for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
-    aes128_encrypt_rk(rk, ctr, out);
+    gc_aes_rk(rk, ctr, out);
 }
 
 /* Correlation-robust hash of the OT extension: scuttlebutt AesHash::cr_hash(i, x) = pi(x) ^ x,
@@ -1059,7 +1115,7 @@ static void ot_prg_block(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
  * pi = AES-128 under the all-zero key (swanky's fixed AesHash key is not restatable). */
 static void ot_cr_hash(const uint8_t x[16], uint8_t out[16]) {
     uint8_t px[16];
-    orc_aes128_zero_encrypt(x, px);
+    gc_aes0(x, px);
     for (int k = 0; k < 16; k++) out[k] = px[k] ^ x[k];
 }
 
@@ -1129,4 +1185,168 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
     free(T);
     free(Q);
     free(U);
+}
+
+/* ------------------------------------------------------------------ */
+/* r05: the protocol's two OTs as CORRELATED OT extension (ALSZ13     */
+/* C-OT: the sender's first message of OT j is the hash H(q_j) itself */
+/* and only y_j = f(H(q_j)) ^ H(q_j ^ s) crosses; ocelot's AlszSender */
+/* offers the same as `send_correlated`). Fewer AES blocks per test   */
+/* than the reference's plain OTs (collect.rs:454-471,                */
+/* equalitytest.rs:67-82), same functionality:                        */
+/*  mode 1  labels (XOR correlation, the evaluator's input labels):   */
+/*          x0_j = H(q_j) = the evaluator's zero label, x1 = x0 ^ D;  */
+/*          y_j = x0_j ^ D ^ H(q_j ^ s) (16 B);                       */
+/*          receiver out_j = r_j ? y_j ^ H(t_j) : H(t_j).             */
+/*  mode 2  the FE share (collect.rs:437-452): v_j = H(q_j) as a      */
+/*          little-endian u128 mod p; the garbler's pair is           */
+/*          (r0, r1) = mask ? (v, v + 1) : (v - 1, v) ordered         */
+/*          (r0, r1) if mask else (r1, r0) — so pair[0] = v and       */
+/*          pair[1] = mask ? v + 1 : v - 1; its node value r1 =       */
+/*          v + mask; y_j = lo64(H(q_j ^ s)) ^ pair[1] (8 B); the     */
+/*          receiver's value = r_j ? lo64(y_j ^ H(t_j)) : v.          */
+/*  mode 3  the FieldElm share (collect.rs:846-876): a test is the    */
+/*          OT pair (2t, 2t + 1) with the same choice; V = the        */
+/*          32 big-endian bytes H(q_2t) || H(q_2t+1) mod p255, pair   */
+/*          [1] = mask ? V + 1 : V - 1 as a BlockPair (field.rs:      */
+/*          478-492), node value V + mask; y = H(q ^ s) ^ pair[1]     */
+/*          (16 B per OT); the receiver's BlockPair = r ? y ^ H(t) :  */
+/*          H(t), read unreduced as FieldElm::try_from(BlockPair)     */
+/*          does (field.rs:466-476).                                  */
+/* H = cr_hash (ot_cr_hash). ctr_off: the row PRG G starts at block   */
+/* ctr_off — the running counter of a base-OT session, so several     */
+/* batches can extend one set of base OTs without repeating pads (as  */
+/* ocelot's AlszSender keeps its PRG across `send` calls).            */
+/* Parity: functional (the tests check the OT identities); wire       */
+/* format unpinned like the rest of row f1.                           */
+/* ------------------------------------------------------------------ */
+static uint64_t cot_fe_of_block(const uint8_t b[16]) {
+    unsigned __int128 x = 0;
+    for (int k = 15; k >= 0; k--) x = (x << 8) | b[k];
+    return (uint64_t)(x % (unsigned __int128)FE_P);
+}
+
+/* 32 big-endian bytes <-> 8 little-endian u32 limbs */
+static void be32_to_limbs(const uint8_t* be, uint32_t v[8]) {
+    for (int k = 0; k < 8; k++) {
+        const uint8_t* q = be + 4 * (7 - k);
+        v[k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+}
+static void limbs_to_be32(const uint32_t v[8], uint8_t* be) {
+    for (int k = 0; k < 8; k++) {
+        uint8_t* q = be + 4 * (7 - k);
+        q[0] = (uint8_t)(v[k] >> 24);
+        q[1] = (uint8_t)(v[k] >> 16);
+        q[2] = (uint8_t)(v[k] >> 8);
+        q[3] = (uint8_t)v[k];
+    }
+}
+
+void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16], uint32_t mask,
+                    const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t ctr_off, uint8_t* sender_out,
+                    uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
+    oracle_init();
+    mask &= 1;
+    const uint64_t nblk = (m + 127) / 128;
+    uint8_t* T = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* Q = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* U = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* H0 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j) */
+    uint8_t* H1 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j ^ s) */
+    uint8_t* HT = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(t_j) */
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < 128; i++) {
+        uint8_t rk0[176], rk1[176], rks[176];
+        key_expand(seeds + (i * 2 + 0) * 16, rk0);
+        key_expand(seeds + (i * 2 + 1) * 16, rk1);
+        const int si = (s[i / 8] >> (i % 8)) & 1;
+        key_expand(seeds + (i * 2 + si) * 16, rks);
+        for (uint64_t c = 0; c < nblk; c++) {
+            uint8_t g0[16], g1[16], gs[16];
+            ot_prg_block(rk0, ctr_off + c, g0);
+            ot_prg_block(rk1, ctr_off + c, g1);
+            uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
+            uint8_t* u = U + ((uint64_t)i * nblk + c) * 16;
+            for (int k = 0; k < 16; k++) {
+                uint8_t r = 0;
+                for (int b = 0; b < 8; b++) {
+                    const uint64_t j = c * 128 + (uint64_t)k * 8 + b;
+                    if (j < m && ((choices[j / 8] >> (j % 8)) & 1)) r |= (uint8_t)(1u << b);
+                }
+                t[k] = g0[k];
+                u[k] = g0[k] ^ g1[k] ^ r;
+            }
+            ot_prg_block(rks, ctr_off + c, gs);
+            uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
+            for (int k = 0; k < 16; k++) q[k] = gs[k] ^ (si ? u[k] : 0);
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < (int64_t)m; j++) {
+        uint8_t qj[16] = {0}, tj[16] = {0}, qs[16];
+        const uint64_t c = (uint64_t)j / 128, bit = (uint64_t)j % 128;
+        for (int i = 0; i < 128; i++) {
+            const uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
+            const uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
+            if ((q[bit / 8] >> (bit % 8)) & 1) qj[i / 8] |= (uint8_t)(1u << (i % 8));
+            if ((t[bit / 8] >> (bit % 8)) & 1) tj[i / 8] |= (uint8_t)(1u << (i % 8));
+        }
+        for (int k = 0; k < 16; k++) qs[k] = qj[k] ^ s[k];
+        ot_cr_hash(qj, H0 + j * 16);
+        ot_cr_hash(qs, H1 + j * 16);
+        ot_cr_hash(tj, HT + j * 16);
+    }
+    if (mode == 1) {
+        for (uint64_t j = 0; j < m; j++) {
+            const int rj = (choices[j / 8] >> (j % 8)) & 1;
+            uint8_t y[16];
+            for (int k = 0; k < 16; k++) y[k] = H0[j * 16 + k] ^ delta[k] ^ H1[j * 16 + k];
+            if (sender_out) memcpy(sender_out + j * 16, H0 + j * 16, 16);
+            if (y_out) memcpy(y_out + j * 16, y, 16);
+            for (int k = 0; k < 16; k++) out[j * 16 + k] = (rj ? y[k] : 0) ^ HT[j * 16 + k];
+        }
+    } else if (mode == 2) {
+        for (uint64_t j = 0; j < m; j++) {
+            const int rj = (choices[j / 8] >> (j % 8)) & 1;
+            const uint64_t v = cot_fe_of_block(H0 + j * 16);
+            const uint64_t gv = mask ? (v + 1 == FE_P ? 0 : v + 1) : v;          /* r1 = v + mask */
+            const uint64_t p1 = mask ? gv : (v == 0 ? FE_P - 1 : v - 1);         /* pair[1] */
+            uint64_t h1, ht;
+            memcpy(&h1, H1 + j * 16, 8);
+            memcpy(&ht, HT + j * 16, 8);
+            const uint64_t y = h1 ^ p1;
+            if (sender_out) memcpy(sender_out + j * 8, &gv, 8);
+            if (y_out) memcpy(y_out + j * 8, &y, 8);
+            const uint64_t got = rj ? (y ^ ht) : cot_fe_of_block(HT + j * 16);
+            memcpy(out + j * 8, &got, 8);
+        }
+    } else if (mode == 3) {
+        for (uint64_t t = 0; 2 * t + 1 < m; t++) {
+            uint32_t V[8], one[8] = {1, 0, 0, 0, 0, 0, 0, 0}, gv[8], p1[8];
+            be32_to_limbs(H0 + 2 * t * 16, V);   /* H(q_2t) || H(q_2t+1): 32 big-endian bytes */
+            fe255_canon(V);
+            if (mask) {
+                orc_fe255_add(V, one, gv);
+                memcpy(p1, gv, 32);
+            } else {
+                memcpy(gv, V, 32);
+                orc_fe255_sub(V, one, p1);
+            }
+            uint8_t pb[32], y[32];
+            limbs_to_be32(p1, pb);
+            for (int k = 0; k < 32; k++) y[k] = H1[2 * t * 16 + k] ^ pb[k];
+            if (sender_out) limbs_to_be32(gv, sender_out + t * 32);
+            if (y_out) memcpy(y_out + t * 32, y, 32);
+            const int rj = (choices[(2 * t) / 8] >> ((2 * t) % 8)) & 1;
+            for (int k = 0; k < 32; k++) out[t * 32 + k] = (rj ? y[k] : 0) ^ HT[2 * t * 16 + k];
+        }
+    }
+    if (u_out) memcpy(u_out, U, 128 * nblk * 16);
+    free(T);
+    free(Q);
+    free(U);
+    free(H0);
+    free(H1);
+    free(HT);
 }

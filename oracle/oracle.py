@@ -713,3 +713,66 @@ def ot_extend(choices: np.ndarray, x0: np.ndarray, x1, delta: bytes, seeds: np.n
                         None if u is None else _p(u), None if y0 is None else _p(y0),
                         None if y1 is None else _p(y1))
     return (out, u, y0, y1) if transcript else out
+
+
+def gc_set_ni(on: bool) -> None:
+    """Row f1's AES (labels, TCCR, OT PRG and cr_hash) on AES-NI (the default where the CPU has it,
+    as swanky's fixed-key AES does) or on the byte-wise FIPS-197 path."""
+    lib().orc_gc_set_ni(ctypes.c_int(1 if on else 0))
+
+
+def gc_get_ni() -> bool:
+    return bool(lib().orc_gc_get_ni())
+
+
+def gc_garble_eq_cot(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, key: bytes, delta: bytes,
+                     label_nonce: int = 0, gate_base: int = 0):
+    """The r05 garbler: the evaluator's zero labels ev_zero [n][bits][16] come from the labels C-OT;
+    the garbler labels its own bits and the mask (stride pow2 >= bits + 1). Returns (tables, gb_labels,
+    decode) as gc_garble_eq."""
+    g = np.ascontiguousarray(gb_bits, np.uint8)
+    z = np.ascontiguousarray(ev_zero, np.uint8)
+    n, bits = g.shape
+    tables = np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8)
+    gbl = np.zeros((n, bits + 1, 16), np.uint8)
+    dec = np.zeros(n, np.uint8)
+    k = np.frombuffer(key, np.uint8).copy()
+    d = np.frombuffer(delta, np.uint8).copy()
+    lib().orc_gc_garble_eq_cot(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z), ctypes.c_uint32(mask & 1),
+                               _p(k), _p(d), ctypes.c_uint64(label_nonce), ctypes.c_uint64(gate_base), _p(tables),
+                               _p(gbl), _p(dec))
+    return tables, gbl, dec
+
+
+COT_LABELS, COT_FE, COT_FE255 = 1, 2, 3
+
+
+def cot_extend(mode: int, choices: np.ndarray, seeds: np.ndarray, s: bytes, delta: bytes | None = None,
+               mask: int = 0, ctr_off: int = 0):
+    """Correlated OT extension (fhh_oracle.c orc_cot_extend). Returns (sender_out, out, U, y):
+    mode 1: sender_out = x0 [m][16], out [m][16], y [m][16]; mode 2: sender values [m] u64, out [m]
+    u64, y [m] u64; mode 3 (m even, pairs with one choice): sender values / out [m/2][32] BlockPairs,
+    y [m][16]."""
+    ch = np.packbits(np.asarray(choices, np.uint8) & 1, bitorder="little")
+    m = len(choices)
+    sd = np.ascontiguousarray(seeds, np.uint8)
+    sv = np.frombuffer(s, np.uint8).copy()
+    dl = np.frombuffer(delta if delta is not None else bytes(16), np.uint8).copy()
+    nblk = (m + 127) // 128
+    u = np.zeros((128, nblk, 16), np.uint8)
+    if mode == COT_FE:
+        sx = np.zeros(m, np.uint64)
+        out = np.zeros(m, np.uint64)
+        y = np.zeros(m, np.uint64)
+    elif mode == COT_FE255:
+        sx = np.zeros((m // 2, 32), np.uint8)
+        out = np.zeros((m // 2, 32), np.uint8)
+        y = np.zeros((m, 16), np.uint8)
+    else:
+        sx = np.zeros((m, 16), np.uint8)
+        out = np.zeros((m, 16), np.uint8)
+        y = np.zeros((m, 16), np.uint8)
+    lib().orc_cot_extend(ctypes.c_uint64(m), ctypes.c_uint32(mode), _p(np.ascontiguousarray(ch)), _p(dl),
+                         ctypes.c_uint32(mask & 1), _p(sd), _p(sv), ctypes.c_uint64(ctr_off),
+                         sx.ctypes.data_as(u8p), out.ctypes.data_as(u8p), _p(u), y.ctypes.data_as(u8p))
+    return sx, out, u, y

@@ -43,7 +43,8 @@ def test_default_expand_variant_does_not_spill(tmp_path):
     assert int(k["LDS Size [bytes/block]"]) == 131072, k
 
 
-OT_HASH_ROWS = ("_ZN3fhh19k_ot_send_hash_rowsENS_6OtArgsE", "_ZN3fhh19k_ot_recv_hash_rowsENS_6OtArgsE")
+# every mode of both hashes (0 plain OT, 1 labels C-OT, 2 FE share C-OT, 3 FieldElm share C-OT)
+OT_HASH_ROWS = tuple(f"_ZN3fhh19k_ot_{k}_hash_rowsILi{m}EEEvNS_6OtArgsE" for k in ("send", "recv") for m in range(4))
 
 
 def test_ot_hash_rows_do_not_spill(tmp_path):
@@ -67,7 +68,8 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     if not shutil.which("hipcc"):
         pytest.skip("hipcc not available")
     u = _resource_usage("fhh_gc.hip", tmp_path)
-    names = [f"_ZN3fhh11k_gc_garbleILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
+    # both garbler forms: the ideal-OT one and the r05 one on the labels C-OT's zero labels
+    names = [f"_ZN3fhh11k_gc_garbleILi{b}ELb{e}EEEvNS_6GcArgsE" for b in range(1, 9) for e in (0, 1)]
     names += [f"_ZN3fhh9k_gc_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)

@@ -160,3 +160,106 @@ def test_co15_base_ot_functionality():
     bad[1:] ^= 0x5A                                                      # not on the curve
     assert lib().fhh_co15_receiver(1, bad.ctypes.data_as(u8p), ch.ctypes.data_as(u8p), sb.ctypes.data_as(u8p),
                                    B.ctypes.data_as(u8p), kr.ctypes.data_as(u8p)) != 0
+
+
+# ---- r05: correlated OT extension (the protocol's two OTs as ALSZ C-OT) ------------------------------
+FE_P = (1 << 62) - (1 << 30) - 1
+P255 = (1 << 255) - 19
+
+
+def _bp_int(b):
+    return int.from_bytes(bytes(b), "big")
+
+
+@pytest.mark.parametrize("m", [1, 128, 1000, 4099])
+@pytest.mark.parametrize("ctr_off", [0, 256, 1 << 20])
+def test_oracle_cot_functionality(oracle, m, ctr_off):
+    """The three C-OT modes deliver what the reference's plain OTs deliver (collect.rs:437-471,
+    equalitytest.rs:67-82): labels out = x0 ^ r Delta with x0 the sender's H(q_j); FE / FieldElm
+    shares with v_garbler - v_receiver = 1 iff the choice differs from the garbler's mask (eq = mask ^ o,
+    A.5), every value canonical (the receiver's FieldElm unreduced < 2^256, == mod p)."""
+    ch, _, _, seeds, s, delta = _inputs(m, m + ctr_off)
+    # labels
+    x0, out, u, y = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=ctr_off)
+    D = np.frombuffer(delta, np.uint8)
+    assert np.array_equal(out, np.where(ch[:, None] == 1, x0 ^ D, x0))
+    # FE share, both masks
+    for mask in (0, 1):
+        gv, ev, _, _ = oracle.cot_extend(oracle.COT_FE, ch, seeds, s, mask=mask, ctr_off=ctr_off)
+        assert int(gv.max()) < FE_P and int(ev.max()) < FE_P
+        diff = (gv.astype(object) - ev.astype(object)) % FE_P
+        assert np.array_equal(diff.astype(np.uint64), (ch != mask).astype(np.uint64))
+    # FieldElm share: pairs (2t, 2t + 1) with one choice
+    mm = 2 * ((m + 1) // 2)
+    ch2 = np.repeat(ch[: mm // 2], 2)
+    for mask in (0, 1):
+        gv, ev, _, y2 = oracle.cot_extend(oracle.COT_FE255, ch2, seeds, s, mask=mask, ctr_off=ctr_off)
+        for t in range(mm // 2):
+            g, e = _bp_int(gv[t]), _bp_int(ev[t])
+            assert g < P255 and e < (1 << 256)
+            assert (g - e) % P255 == (1 if ch2[2 * t] != mask else 0)
+
+
+def test_oracle_cot_counter_offset_gives_fresh_pads(oracle):
+    """Batches extending one set of base OTs at disjoint row-PRG counters (the party ABI's running
+    session counter) get unrelated pads: U and y differ, while each batch stays correct. The same
+    counter twice would repeat U ^ choices (the ADVICE r04 hazard)."""
+    m = 600
+    ch, _, _, seeds, s, delta = _inputs(m, 77)
+    a = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=0)
+    b = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=256)
+    c = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=0)
+    assert not np.array_equal(a[2], b[2]) and not np.array_equal(a[0], b[0])
+    assert np.array_equal(a[2], c[2])
+    # at ctr_off 0 the C-OT's row matrices equal the plain OT's (same base material, same counters)
+    _, u_plain, _, _ = oracle.ot_extend(ch, a[0], None, delta, seeds, s, transcript=True)
+    assert np.array_equal(a[2], u_plain)
+
+
+def test_oracle_gc_aes_ni_matches_bytewise(oracle):
+    """Row f1's restatement on AES-NI (the CPU baseline's path) equals the byte-wise FIPS-197 path."""
+    if not oracle.aes_ni_available():
+        pytest.skip("no AES-NI on this CPU")
+    m = 700
+    ch, x0, x1, seeds, s, delta = _inputs(m, 3)
+    try:
+        oracle.gc_set_ni(True)
+        a = oracle.ot_extend(ch, x0, x1, None, seeds, s, transcript=True)
+        ca = oracle.cot_extend(oracle.COT_FE, ch, seeds, s, mask=1, ctr_off=512)
+        oracle.gc_set_ni(False)
+        b = oracle.ot_extend(ch, x0, x1, None, seeds, s, transcript=True)
+        cb = oracle.cot_extend(oracle.COT_FE, ch, seeds, s, mask=1, ctr_off=512)
+    finally:
+        oracle.gc_set_ni(True)
+    for p, q in zip(a, b):
+        assert np.array_equal(p, q)
+    for p, q in zip(ca, cb):
+        assert np.array_equal(p, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [1, 127, 1000, 8193, 100_000])
+def test_gpu_cot_bit_exact(oracle, m):
+    """GPU correlated OT (every mode, at a nonzero session counter) = the oracle: both parties'
+    outputs and both protocol messages (U, y)."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import ot
+    ch, _, _, seeds, s, delta = _inputs(m, 5 * m + 1)
+    kc = fhh.KeyCollection(8, 1)
+    for ctr_off in (0, 512):
+        got = ot.cot_extend(kc, 1, ch, seeds, s, delta=delta, ctr_off=ctr_off, transcript=True)
+        exp = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=ctr_off)
+        for g, e in zip(got, exp):
+            assert np.array_equal(g, e)
+        for mask in (0, 1):
+            got = ot.cot_extend(kc, 2, ch, seeds, s, mask=mask, ctr_off=ctr_off, transcript=True)
+            exp = oracle.cot_extend(oracle.COT_FE, ch, seeds, s, mask=mask, ctr_off=ctr_off)
+            for g, e in zip(got, exp):
+                assert np.array_equal(g, e)
+        mm = 2 * ((m + 1) // 2)
+        ch2 = np.repeat(ch[: mm // 2], 2)
+        for mask in (0, 1):
+            got = ot.cot_extend(kc, 3, ch2, seeds, s, mask=mask, ctr_off=ctr_off, transcript=True)
+            exp = oracle.cot_extend(oracle.COT_FE255, ch2, seeds, s, mask=mask, ctr_off=ctr_off)
+            for g, e in zip(got, exp):
+                assert np.array_equal(g, e)

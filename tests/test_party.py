@@ -1,9 +1,10 @@
 """The two servers' halves of the GC equality test + OT, each on its own ctx (fhh_gb_* / fhh_ev_*;
 src/collect.rs:419-482 with gc_sender = true on server 0 and false on server 1,
-src/equalitytest.rs:25-106). Only the protocol's five messages per level cross (party.Channel
-copies them into memory the receiving server owns). With fhh_sim_crawl's per-level material the
-split run reproduces the in-process GC + OT crawl (fhh_sim_config.gc = 2) level by level, and its
-heavy hitters equal the plaintext recount."""
+src/equalitytest.rs:25-106). Only protocol messages cross (party.Channel copies them into memory the
+receiving server owns): the Chou–Orlandi base-OT messages of every level and the five messages per
+chunk. Each server draws its own material (material="fresh"), or both come from one test seed
+(material="test"); either way the leader's output equals the in-process GC + OT crawl
+(fhh_sim_config.gc = 2) level by level, and its heavy hitters equal the plaintext recount."""
 import ctypes
 
 import numpy as np
@@ -27,13 +28,15 @@ def _assert_same_crawl(a, b):
     assert [(r.path, r.value) for r in a.final] == [(r.path, r.value) for r in b.final]
 
 
+@pytest.mark.parametrize("material", ["fresh", "test"])
 @pytest.mark.parametrize("channel", ["copy", "inplace"])
 @pytest.mark.parametrize("d,n,L,thr", [(1, 300, 24, 0.02), (2, 200, 12, 0.05), (1, 64 * 3, 20, 0.03)],
                          ids=["d1", "d2", "whole-words"])
-def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel):
+def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     """Level by level: the leader's v0 - v1 per child and the final heavy hitters of the split run
-    equal fhh_sim_crawl(gc = "ot") (both parties in one device loop) on the same material, whether
-    each message is copied into the receiver's buffer or read where the sender produced it."""
+    equal fhh_sim_crawl(gc = "ot") (both parties in one device loop), whether each server drew its own
+    material and ran CO15 base OTs with the other ("fresh") or both sides come from one test seed, and
+    whether each message is copied into the receiver's buffer or read where the sender produced it."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
     wl = workload.zipf_workload(n, max(L, 32), d, num_sites=5, seed=3 + d)
@@ -41,9 +44,11 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel):
     c0, c1 = _keys(wl, L, d)
     ref = fhh.sim_crawl(c0, c1, thr, mode="fe", prf_seed=77, gc="ot")
     p0, p1 = _keys(wl, L, d)
-    got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77, channel=channel)
+    got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77, channel=channel, material=material)
     _assert_same_crawl(ref, got)
     assert len(got.final) > 0
+    if material == "fresh":   # two CO15 runs per level (labels, shares), A + 128 B points each
+        assert got.base_ot_runs == 2 * L and got.base_ot_bytes == 2 * L * 65 * 129
     t = max(1, int(thr * n))
     cnt, paths, vals = workload.plaintext_crawl(wl.left, wl.right, t, t)
     assert sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in got.final) == sorted(paths)
@@ -52,22 +57,27 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel):
     C0, bits = int(got.level_children[0]), 2 * d
     npad = (n + 63) // 64 * 64
     assert lb["gc"] == C0 * n * ((2 * (bits - 1) + bits + 1) * 16 + 1)
-    assert lb["y1"] == C0 * bits * npad * 32 and lb["y2"] == C0 * n * 32
+    # r05 correlated OTs: one 16-B y per labels OT, one 8-B y per FE share OT
+    assert lb["y1"] == C0 * bits * npad * 16 and lb["y2"] == C0 * n * 8
 
 
 def test_two_party_fresh_randomness_same_output():
-    """Independent per-level material (another label key, Delta, mask, r0 and base OTs per level)
-    changes every transcript but not the leader's output."""
+    """Independently drawn material (each party's own label keys, Deltas, masks and CO15 base OTs) in
+    two runs: every transcript differs, the leader's output does not, and equals the test-seed run's;
+    with one base-OT run per OT kind for the whole crawl (the library continues its counters) too."""
     import fuzzyheavyhitters_amd as fhh
-    from fuzzyheavyhitters_amd import party, workload
+    from fuzzyheavyhitters_amd import workload
     n, L = 250, 20
     wl = workload.zipf_workload(n, 32, 1, num_sites=4, seed=12)
     wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
-    a0, a1 = _keys(wl, L, 1)
-    b0, b1 = _keys(wl, L, 1)
-    ra = fhh.two_party_crawl(a0, a1, 0.02, prf_seed=1)
-    rb = fhh.two_party_crawl(b0, b1, 0.02, cfg_fn=lambda lv, k=0: party.level_cfg(0xABCDEF ^ (lv * 7919), lv + 1000))
-    _assert_same_crawl(ra, rb)
+    runs = []
+    for kw in (dict(material="test", prf_seed=1), dict(material="fresh"), dict(material="fresh"),
+               dict(material="fresh", base_ot_every="crawl")):
+        a0, a1 = _keys(wl, L, 1)
+        runs.append(fhh.two_party_crawl(a0, a1, 0.02, **kw))
+    for r in runs[1:]:
+        _assert_same_crawl(runs[0], r)
+    assert runs[3].base_ot_runs == 2 and runs[1].base_ot_runs == 2 * L
 
 
 @pytest.mark.parametrize("channel", ["copy", "inplace"])
@@ -83,38 +93,42 @@ def test_two_party_multi_device_shards(channel):
     c0, c1 = _keys(wl, L, 1)
     ref = fhh.sim_crawl(c0, c1, 0.02, mode="fe", prf_seed=5, gc="ot")
     g0, g1 = _keys(wl, L, 1, devices=[0, 0, 0])
-    got = fhh.two_party_crawl(g0, g1, 0.02, prf_seed=5, channel=channel)
+    got = fhh.two_party_crawl(g0, g1, 0.02, channel=channel)
     _assert_same_crawl(ref, got)
 
 
 def test_party_calls_out_of_order_refused():
     """Each half checks the protocol order and the message sizes (FHH_E_STATE / FHH_E_ARG)."""
-    import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import party, workload
     from fuzzyheavyhitters_amd._lib import lib
     wl = workload.zipf_workload(100, 32, 1, num_sites=3, seed=1)
     c0, c1 = _keys(wl, 32, 1)
     out, nb = ctypes.c_void_p(), ctypes.c_uint64()
-    cfg = party.level_cfg(1, 0)
-    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == -2   # no crawl
+    gb, ev = party.test_cfgs(1, 0)
+    assert lib().fhh_ev_ot_labels(c1.handle, ctypes.byref(ev), ctypes.byref(out), ctypes.byref(nb)) == -2   # no crawl
     c0.tree_init()
     c1.tree_init()
     c0.tree_crawl()
     c1.tree_crawl()
-    assert lib().fhh_gb_ot_labels(c0.handle, None, 0, ctypes.byref(out), ctypes.byref(nb)) == -2        # before garble
+    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(out), ctypes.byref(nb)) == -2        # before the labels OT
     assert lib().fhh_ev_evaluate(c1.handle, None, 0, None, 0, ctypes.byref(out), ctypes.byref(nb)) == -2
-    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == 0
-    assert lib().fhh_gb_ot_labels(c0.handle, out, 12345, ctypes.byref(out), ctypes.byref(nb)) == -1     # wrong size
+    assert lib().fhh_ev_ot_labels(c1.handle, ctypes.byref(ev), ctypes.byref(out), ctypes.byref(nb)) == 0
+    u, un = out.value, nb.value
+    assert lib().fhh_gb_ot_labels(c0.handle, ctypes.byref(gb), out, 12345, ctypes.byref(out), ctypes.byref(nb)) == -1
     assert b"expected" in lib().fhh_last_error(c0.handle)
+    assert lib().fhh_gb_ot_labels(c0.handle, ctypes.byref(gb), ctypes.c_void_p(u), un, ctypes.byref(out),
+                                  ctypes.byref(nb)) == 0
+    assert lib().fhh_gb_ot_shares(c0.handle, None, 0, ctypes.byref(out), ctypes.byref(nb)) == -2   # before garble
 
 
 @pytest.mark.parametrize("chunk", [None, 150], ids=["whole-levels", "chunks-of-150"])
 def test_two_party_configs1_full_size(chunk):
     """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): the split
-    GC + OT crawl equals the in-process GC + OT crawl level by level, and both equal the plaintext
-    recount (222 heavy hitters) — with each level's tests in one protocol instance, and (r04) in
-    chunks of 150 children, one instance per chunk (the 1M configuration's shape). Prints the bytes
-    that would cross the channel."""
+    GC + OT crawl — each server drawing its own material, and every level's two OT extensions on
+    Chou–Orlandi base OTs run between the servers over the channel (1 024 runs) — equals the
+    in-process GC + OT crawl level by level, and both equal the plaintext recount (222 heavy hitters);
+    with each level's tests in one protocol instance, and in chunks of 150 children, one instance per
+    chunk (the 1M configuration's shape). Prints the bytes that would cross the channel."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import workload
     n, L = 100_000, 512
@@ -123,10 +137,12 @@ def test_two_party_configs1_full_size(chunk):
     ref = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=7, gc="ot")
     del c0, c1
     p0, p1 = _keys(wl, L, 1)
-    got = fhh.two_party_crawl(p0, p1, 0.001, prf_seed=7, expect_counts=ref.counts,
+    got = fhh.two_party_crawl(p0, p1, 0.001, expect_counts=ref.counts, material="fresh",
                               chunk_children=chunk, channel="inplace" if chunk else "copy")
     _assert_same_crawl(ref, got)
     assert len(got.final) == 222
+    assert got.base_ot_runs == 2 * L
+    print(f"base OTs: {got.base_ot_runs} CO15 runs, {got.base_ot_bytes} B, crawl waited {got.base_ot_wait_s:.3f} s")
     if chunk:
         assert max(got.level_children) > chunk
     tot = {k: sum(lb[k] for lb in got.level_bytes) for k in got.level_bytes[0]}
@@ -149,14 +165,13 @@ def test_two_party_chunked_children(chunk, devices):
     c0, c1 = _keys(wl, L, 1)
     ref = fhh.sim_crawl(c0, c1, 0.02, mode="fe", prf_seed=9, gc="ot")
     p0, p1 = _keys(wl, L, 1, devices=devices)
-    got = fhh.two_party_crawl(p0, p1, 0.02, prf_seed=9, channel="inplace", chunk_children=chunk)
+    got = fhh.two_party_crawl(p0, p1, 0.02, prf_seed=9, channel="inplace", chunk_children=chunk, material="test")
     _assert_same_crawl(ref, got)
     assert max(ref.level_children) > chunk   # some level really ran in several chunks
 
 
 def test_party_chunks_out_of_order_refused():
     """Chunks run in order and cover the level before the node sums (FHH_E_STATE)."""
-    import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import party, workload
     from fuzzyheavyhitters_amd._lib import lib
     wl = workload.zipf_workload(100, 32, 1, num_sites=3, seed=1)
@@ -167,14 +182,16 @@ def test_party_chunks_out_of_order_refused():
     c1.tree_crawl()
     assert C == 2
     out, nb = ctypes.c_void_p(), ctypes.c_uint64()
-    cfg = party.level_cfg(1, 0)
-    cfg.child_begin, cfg.child_count = 1, 1       # the level's first chunk must start at child 0
-    assert lib().fhh_gb_garble(c0.handle, ctypes.byref(cfg), ctypes.byref(out), ctypes.byref(nb)) == -2
-    cfg.child_begin, cfg.child_count = 0, 1
+    gb, ev = party.test_cfgs(1, 0)
+    ev.child_begin, ev.child_count = 1, 1        # the level's first chunk must start at child 0
+    assert lib().fhh_ev_ot_labels(c1.handle, ctypes.byref(ev), ctypes.byref(out), ctypes.byref(nb)) == -2
+    for cfg in (gb, ev):
+        cfg.child_begin, cfg.child_count = 0, 1
     to_gb, to_ev = party.Channel(0, "inplace"), party.Channel(0, "inplace")
-    party.run_level(c0, c1, cfg, cfg, to_gb, to_ev)   # child 0 only
+    party.run_chunk(c0, c1, gb, ev, to_gb, to_ev)   # child 0 only
     sums = np.zeros(2, np.uint64)
     assert lib().fhh_party_node_sums(c0.handle, sums.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), None) == -2
-    cfg.child_begin = 1
-    party.run_level(c0, c1, cfg, cfg, to_gb, to_ev)   # child 1: the level is covered
+    for cfg in (gb, ev):
+        cfg.child_begin = 1
+    party.run_chunk(c0, c1, gb, ev, to_gb, to_ev)   # child 1: the level is covered
     assert lib().fhh_party_node_sums(c0.handle, sums.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), None) == 0

@@ -19,13 +19,51 @@ def test_chunk_windows_cover_the_level_in_order(C, chunk):
     assert w[-1][0] + w[-1][1] == C
 
 
-def test_party_cfg_layout_matches_header():
-    """fhh_gc_party_cfg (include/fhh.h): the r04 chunk fields follow the base-OT arrays; the ctypes
-    mirror must have the C layout (no padding on x86-64: every field is naturally aligned)."""
-    from fuzzyheavyhitters_amd._lib import FhhGcPartyCfg
-    size = 16 + 16 + 4 + 4 + 8 + 2 * 128 * 2 * 16 + 2 * 128 * 16 + 2 * 16 + 8 + 8
-    assert ctypes.sizeof(FhhGcPartyCfg) == size
-    assert FhhGcPartyCfg.child_begin.offset == size - 16
-    assert FhhGcPartyCfg.child_count.offset == size - 8
-    cfg = FhhGcPartyCfg()
-    assert cfg.child_begin == 0 and cfg.child_count == 0   # zero-initialised: the whole level
+def test_party_cfg_layouts_match_header():
+    """fhh_gb_cfg / fhh_ev_cfg (include/fhh.h): the ctypes mirrors have the C layout (no padding on
+    x86-64: every field is naturally aligned), the chunk window last."""
+    from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
+    gb = 16 + 16 + 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8
+    ev = 2 * 128 * 2 * 16 + 8 + 8
+    assert ctypes.sizeof(FhhGbCfg) == gb and ctypes.sizeof(FhhEvCfg) == ev
+    for T, size in ((FhhGbCfg, gb), (FhhEvCfg, ev)):
+        assert T.child_begin.offset == size - 16 and T.child_count.offset == size - 8
+        cfg = T()
+        assert cfg.child_begin == 0 and cfg.child_count == 0   # zero-initialised: the whole level
+
+
+def test_evaluator_cfg_carries_no_garbler_secret():
+    """the evaluator's half never receives the garbler's secrets. fhh_ev_cfg holds only
+    its base-OT key pairs and the chunk window; the label key, Delta, mask, the base-OT receiver's
+    choice bits and chosen keys exist only in fhh_gb_cfg, and the share PRF key is gone (the share
+    values come from the correlated OT itself)."""
+    from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
+    ev_fields = {f for f, _ in FhhEvCfg._fields_}
+    gb_fields = {f for f, _ in FhhGbCfg._fields_}
+    assert ev_fields == {"base_pairs", "child_begin", "child_count"}
+    for secret in ("label_key", "delta", "mask", "base_chosen", "base_choice"):
+        assert secret in gb_fields and secret not in ev_fields
+    assert not any("seed" in f for f in gb_fields | ev_fields)
+    # and the header agrees: the evaluator's entry points take only fhh_ev_cfg
+    import os
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "fhh.h")).read()
+    for fn in ("fhh_ev_ot_labels", "fhh_ev_evaluate", "fhh_ev_ot_shares"):
+        decl = hdr[hdr.index("int " + fn + "("):]
+        decl = decl[:decl.index(";")]
+        assert "fhh_gb_cfg" not in decl and "mask" not in decl and "delta" not in decl
+
+
+def test_party_python_sides_hold_their_own_material():
+    """party.GarblerParty / EvaluatorParty draw their material themselves (os.urandom): two chunk
+    configs of the garbler never repeat a label key, Delta or mask sequence, and the evaluator's config
+    is built from its own base-OT pairs only."""
+    import numpy as np
+    from fuzzyheavyhitters_amd.party import EvaluatorParty, GarblerParty
+    base_gb = [(np.zeros((128, 16), np.uint8), np.zeros(16, np.uint8))] * 2
+    a = GarblerParty(None).chunk_cfg(base_gb, 0, 3)
+    b = GarblerParty(None).chunk_cfg(base_gb, 3, 3)
+    assert bytes(a.label_key) != bytes(b.label_key) and bytes(a.delta) != bytes(b.delta)
+    pairs = [np.full((128, 2, 16), 7, np.uint8), np.full((128, 2, 16), 9, np.uint8)]
+    e = EvaluatorParty.chunk_cfg(pairs, 3, 3)
+    assert bytes(e.base_pairs)[:4] == b"\x07" * 4 and bytes(e.base_pairs)[-4:] == b"\x09" * 4
+    assert (e.child_begin, e.child_count) == (3, 3)

@@ -192,7 +192,6 @@ class FhhOtBatch(ctypes.Structure):
 class FhhGbCfg(ctypes.Structure):
     """fhh_gb_cfg: the garbler's (server 0's) own material for one chunk (include/fhh.h)."""
     _fields_ = [
-        ("label_key", ctypes.c_uint8 * 16),
         ("delta", ctypes.c_uint8 * 16),
         ("mask", ctypes.c_uint32),
         ("pad_", ctypes.c_uint32),
@@ -284,8 +283,7 @@ def lib():
         "fhh_party_bytes_sent": (i, [vp, u64p]),
         "fhh_gc_party_test_cfgs": (i, [u64, u32, P(FhhGbCfg), P(FhhEvCfg)]),
         "fhh_cot_extend_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
-        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p,
-                                u8p, u8p]),
+        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p]),
         "fhh_memcpy_device": (i, [i, vp, vp, u64]),
         "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),

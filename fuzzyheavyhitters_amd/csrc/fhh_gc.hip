@@ -90,10 +90,9 @@ __device__ __forceinline__ void ld_blk(const uint4* base, uint64_t row, uint64_t
     v[3] = q.w;
 }
 
-// EVIN (r05, the labels OT is a correlated OT): the evaluator's zero labels are inputs — the C-OT's
-// sender messages H(q_j), at OT index (g B + k) Npad + i of a.ev_labels — and the garbler draws only
-// its own B wires and the mask: W = B + 1 label blocks per test (3 instead of 5 at d = 1).
-template <int B, bool EVIN>
+// The ideal-OT garbler (fhh_gc_equality_*, fhh_sim_config.gc = 1): every label drawn by the garbler,
+// the evaluator's active ones written to ev_labels as an ideal OT would deliver them.
+template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
     // a workgroup without tests leaves before filling 128 KiB of tables (the level loop enqueues a
@@ -106,14 +105,13 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     uint32_t zrk[11][4];
     zero_rk(zrk);
     const uint64_t n = a.G * a.N;
-    const uint64_t Npad = (uint64_t)a.nw * 64;
     const uint32_t D[4] = {a.delta[0], a.delta[1], a.delta[2], a.delta[3]};
     uint32_t lrk[11][4];   // uniform: the label key schedule stays in SGPRs
 #pragma unroll
     for (int r = 0; r < 11; r++)
 #pragma unroll
         for (int c = 0; c < 4; c++) lrk[r][c] = a.rk_label[r][c];
-    constexpr int W = EVIN ? B + 1 : 2 * B + 1;
+    constexpr int W = 2 * B + 1;
     // label counter stride: the power of two >= W, so with label_nonce a multiple of it (the level
     // loop and the party ABI use 0) a test's W counters differ in byte 0 alone and a pass of its
     // label blocks shares AES rounds 1-2 (aes_rk_ctr: 133 instead of 160 lookups per extra block)
@@ -124,7 +122,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         const uint32_t i = (uint32_t)(t - g * a.N);
         const uint64_t tg = a.g_off * a.N + t;       // the test's index in the whole level
         // zero labels, generated per wire pair as the gates consume them (registers do not
-        // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B (EVIN: loaded)
+        // grow with B): garbler string 0..B-1, mask B, evaluator string B+1..2B
         const uint64_t ctr0 = a.label_nonce + tg * WS;
         // wave-uniform: no lane's counters ctr0 .. ctr0 + W - 1 carry out of byte 0 (always, for an
         // aligned label_nonce; otherwise the pass runs every round in full)
@@ -135,9 +133,9 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
             b[2] = 0u;
             b[3] = 0u;
         };
-        // W <= 5 (d = 1, and d = 2 with EVIN): all label blocks in one pass up front, sharing rounds 1-2
-        // with the first (692 instead of 719 lookups at d = 1 without EVIN; 5 / 3 independent blocks in
-        // flight per lane)
+        // B <= 2 (d = 1: the metric's configuration): all W <= 5 label blocks in one pass up front, 4
+        // sharing rounds 1-2 with the first, instead of a 2-block pass then a 3-block one (692 instead of
+        // 719 lookups, and 5 independent blocks in flight per lane)
         constexpr bool kOnePass = W <= 5;
         uint32_t L[kOnePass ? W : 1][4];
         if constexpr (kOnePass) {
@@ -151,34 +149,12 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
         for (int k = 0; k < B; k++) {
             // wires k (garbler) and B + 1 + k (evaluator); the last pair also takes the mask wire B
             uint32_t s[2][4];
-            if constexpr (EVIN) {   // the evaluator's zero label: the C-OT's sender message
-                ld_blk(a.ev_labels, g * B + k, Npad, i, s[1]);
-            }
             if constexpr (kOnePass) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     s[0][c] = L[k][c];
-                    if constexpr (!EVIN) s[1][c] = L[B + 1 + k][c];
+                    s[1][c] = L[B + 1 + k][c];
                     if (k == B - 1) m[0][c] = L[B][c];
-                }
-            } else if constexpr (EVIN) {
-                if (k == B - 1) {   // the garbler's last wire and the mask
-                    uint32_t s2[2][4];
-                    ctr_blk(s2[0], ctr0 + k);
-                    ctr_blk(s2[1], ctr0 + B);
-                    if (shared) aes_rk_ctr<GcTab, 2, 0, 0>(s2, tbl_gc, b0, b1, lrk);
-                    else aes_rk<GcTab, 2>(s2, tbl_gc, b0, b1, lrk);
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        s[0][c] = s2[0][c];
-                        m[0][c] = s2[1][c];
-                    }
-                } else {
-                    uint32_t s1[1][4];
-                    ctr_blk(s1[0], ctr0 + k);
-                    aes_rk<GcTab, 1>(s1, tbl_gc, b0, b1, lrk);
-#pragma unroll
-                    for (int c = 0; c < 4; c++) s[0][c] = s1[0][c];
                 }
             } else if (k == B - 1) {
                 uint32_t s3[3][4];
@@ -208,7 +184,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
                 bz[c] = s[0][c] ^ s[1][c] ^ D[c];   // z_k = NOT(x_k ^ y_k): free XOR, NOT = ^Delta
             }
             st_blk(a.gb_labels, k, n, t, x);
-            if constexpr (!EVIN) {   // ideal OT: the evaluator's active label (what an OT would deliver)
+            {   // ideal OT: the evaluator's active label (what an OT would deliver)
                 const uint32_t eb = plane_bit(a.ev_planes, a.g_off + g, B, k, a.nw, i);
                 uint32_t y[4];
 #pragma unroll
@@ -254,6 +230,74 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble(GcArgs a) {
     }
 }
 
+// The r05 garbler (ev_ot = 1): the evaluator's input labels arrive by correlated OT — its zero label
+// of share bit k is the C-OT's sender message E_k = H(q_j) at OT index (g B + k) Npad + i — and the
+// garbler's own string is folded into the circuit instead of being encoded as input wires: for the
+// input z_k = NOT(x_k ^ y_k) the garbler knows x_k, so it takes Z_k^0 = E_k ^ (x_k ? 0 : Delta), which
+// makes the evaluator's OT'd label E_k ^ y_k Delta exactly Z_k's active label (XOR with a constant
+// the garbler knows is free under free-XOR and hidden like any free gate). The mask folds into the
+// decoding bit the same way: d = colour(out^0) ^ mask, so out = colour(acc) ^ d = eq ^ mask. No label
+// is drawn at all (0 instead of 2 bits + 1 AES blocks per test) and no garbler label is sent: the gc
+// message is the tables and the decoding bit (33 B per test at d = 1 instead of 81).
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gc_garble_cot(GcArgs a) {
+    __shared__ uint32_t tbl_gc[GcTab::kWords];
+    if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;   // no tests: skip the table fill
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(threadIdx.x & 63, b0, b1);
+    uint32_t zrk[11][4];
+    zero_rk(zrk);
+    const uint64_t n = a.G * a.N;
+    const uint64_t Npad = (uint64_t)a.nw * 64;
+    const uint32_t D[4] = {a.delta[0], a.delta[1], a.delta[2], a.delta[3]};
+    const uint64_t n_act = gc_active(a);
+    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
+        const uint64_t g = t / a.N;                  // group within the chunk
+        const uint32_t i = (uint32_t)(t - g * a.N);
+        const uint64_t tg = a.g_off * a.N + t;       // the test's index in the whole level (gate tweaks)
+        uint32_t acc[4];
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            uint32_t bz[4];
+            ld_blk(a.ev_labels, g * B + k, Npad, i, bz);   // E_k, the C-OT's zero label
+            const uint32_t xb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
+#pragma unroll
+            for (int c = 0; c < 4; c++) bz[c] ^= xb ? 0u : D[c];   // Z_k^0 = E_k ^ (x_k ? 0 : Delta)
+            if (k == 0) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) acc[c] = bz[c];
+                continue;
+            }
+            // half-gates AND(acc, z_k), gate index gate_base + t (B - 1) + k - 1
+            uint32_t h[4][4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                h[0][c] = acc[c];
+                h[1][c] = acc[c] ^ D[c];
+                h[2][c] = bz[c];
+                h[3][c] = bz[c] ^ D[c];
+            }
+            const uint32_t pa = acc[0] & 1u, pb = bz[0] & 1u;
+            const uint64_t j = 2 * (a.gate_base + tg * (B - 1) + (k - 1));
+            const uint64_t tw[4] = {j, j, j + 1, j + 1};
+            tccr<4>(h, tw, tbl_gc, b0, b1, zrk);
+            uint32_t TG[4], TE[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                TG[c] = h[0][c] ^ h[1][c] ^ (pb ? D[c] : 0u);
+                TE[c] = h[2][c] ^ h[3][c] ^ acc[c];
+                const uint32_t wg = h[0][c] ^ (pa ? TG[c] : 0u);
+                const uint32_t we = h[2][c] ^ (pb ? (TE[c] ^ acc[c]) : 0u);
+                acc[c] = wg ^ we;
+            }
+            st_blk(a.tables, 2 * (k - 1), n, t, TG);
+            st_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
+        }
+        a.decode[t] = (uint8_t)((acc[0] ^ a.mask) & 1u);   // colour of eq's zero label, mask folded in
+    }
+}
+
 // spread 32 bits to 64: bit k -> bits 2k and 2k + 1 (the doubled choices of a BlockPair OT)
 __device__ __forceinline__ uint64_t spread2(uint32_t x) {
     uint64_t v = x;
@@ -268,7 +312,10 @@ __device__ __forceinline__ uint64_t spread2(uint32_t x) {
 // Waves step over aligned 64-test slices (t0 wave-uniform), so with out_packed set the wave's
 // ballot of its output bits is directly the OT choice words of tests t0 .. t0 + 63 (dup = 2:
 // each bit twice, collect.rs:868) — no separate byte-to-bit pass.
-template <int B>
+// FOLD (ev_ot, r05): the garbler's string and the mask are folded into the circuit (k_gc_garble_cot),
+// so the evaluator's OT'd label of bit k IS input z_k's active label, and the message has no garbler
+// labels; otherwise (ideal OT) z_k = garbler label ^ evaluator label and the mask is a wire.
+template <int B, bool FOLD>
 __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];   // static: a dynamic base costs an add per lookup
     if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;   // no tests: skip the table fill
@@ -288,18 +335,24 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
         if (t < n_act) {
             const uint64_t g = t / a.N;
             const uint32_t i = (uint32_t)(t - g * a.N);
-            uint32_t acc[4], x[4], y[4];
-            ld_blk(a.gb_labels, 0, n, t, x);
-            if (a.ev_ot) ld_blk(a.ev_labels, g * B, Npad, i, y);
-            else ld_blk(a.ev_labels, 0, n, t, y);
+            uint32_t acc[4], x[4] = {0, 0, 0, 0}, y[4];
+            if constexpr (FOLD) {
+                ld_blk(a.ev_labels, g * B, Npad, i, y);
+            } else {
+                ld_blk(a.gb_labels, 0, n, t, x);
+                ld_blk(a.ev_labels, 0, n, t, y);
+            }
 #pragma unroll
             for (int c = 0; c < 4; c++) acc[c] = x[c] ^ y[c];   // NOT is free for the evaluator
 #pragma unroll
             for (int k = 1; k < B; k++) {
                 uint32_t h[2][4], TG[4], TE[4];
-                ld_blk(a.gb_labels, k, n, t, x);
-                if (a.ev_ot) ld_blk(a.ev_labels, g * B + k, Npad, i, y);
-                else ld_blk(a.ev_labels, k, n, t, y);
+                if constexpr (FOLD) {
+                    ld_blk(a.ev_labels, g * B + k, Npad, i, y);
+                } else {
+                    ld_blk(a.gb_labels, k, n, t, x);
+                    ld_blk(a.ev_labels, k, n, t, y);
+                }
                 ld_blk(a.tables, 2 * (k - 1), n, t, TG);
                 ld_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
 #pragma unroll
@@ -318,7 +371,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
                     acc[c] = wg ^ we;
                 }
             }
-            ld_blk(a.gb_labels, B, n, t, x);   // mask wire
+            if constexpr (!FOLD) ld_blk(a.gb_labels, B, n, t, x);   // mask wire (FOLD: in the decoding bit)
             bit = ((acc[0] ^ x[0]) & 1u) ^ a.decode[t];
             a.out[t] = (uint8_t)bit;
         }
@@ -347,9 +400,10 @@ static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     // evaluate at configs[1] but +3.2 % for evaluate and +0.7 % for the whole GC + OT crawl at 1M
     // clients, alternated twice; r03)
     const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
-    if (garble && a.ev_ot) hipLaunchKernelGGL((k_gc_garble<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-    else if (garble) hipLaunchKernelGGL((k_gc_garble<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-    else hipLaunchKernelGGL(k_gc_eval<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    if (garble && a.ev_ot) hipLaunchKernelGGL(k_gc_garble_cot<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else if (garble) hipLaunchKernelGGL(k_gc_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else if (a.ev_ot) hipLaunchKernelGGL((k_gc_eval<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else hipLaunchKernelGGL((k_gc_eval<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
     return hipGetLastError();
 }
 

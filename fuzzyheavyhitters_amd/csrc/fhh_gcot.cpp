@@ -410,16 +410,15 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
 }
 
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                    uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
-                    uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
-                    uint64_t ctr_off, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_zero, uint8_t* ev_active,
-                    uint8_t* decode, uint8_t* out) {
+                    uint32_t mask, const uint8_t delta[16], uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
+                    uint8_t* ev_active, uint8_t* decode, uint8_t* out) {
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc_cot: bits must be in [1, 8]");
     if (n == 0) return FHH_OK;
-    if (!gb_bits || !ev_bits || !label_key || !delta || !base_seeds || !base_choice || !out)
+    if (!gb_bits || !ev_bits || !delta || !base_seeds || !base_choice || !out)
         return ctx->fail(FHH_E_ARG, "gc_cot: NULL argument");
     if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc_cot: n must fit 32 bits");
     const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad;
@@ -431,13 +430,13 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
             for (uint32_t j = 0; j < bits; j++)
                 if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
     }
-    DevBuf dp[2], dt, dg, de, da, dd, dout, dch;
+    DevBuf dp[2], dt, dg, de, da, dd, dout;
     for (int s = 0; s < 2; s++) {
         HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
         HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
     }
     HIP_TRY(ctx, dt.ensure((size_t)std::max(bits - 1, 1u) * 2 * n * 16));
-    HIP_TRY(ctx, dg.ensure((size_t)(bits + 1) * n * 16));
+    HIP_TRY(ctx, dg.ensure(16));   // no garbler labels in this protocol (gc_args wants a pointer)
     HIP_TRY(ctx, de.ensure(m * 16));
     HIP_TRY(ctx, da.ensure(m * 16));
     HIP_TRY(ctx, dd.ensure(n));
@@ -452,9 +451,7 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     gb.words = (uint32_t)nw;
     gb.bits = bits;
     gb.mask = mask;
-    std::memcpy(gb.label_key, label_key, 16);
-    std::memcpy(gb.delta, delta, 16);
-    gb.label_nonce = label_nonce;
+    std::memcpy(gb.delta, delta, 16);   // no label key: the garbler draws no labels
     gb.gate_base = gate_base;
     gb.gb_planes_dev = dp[0].as<uint64_t>();
     gb.ev_planes_dev = dp[1].as<uint64_t>();
@@ -477,7 +474,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     a.out = da.as<uint4>();
     rc = ot_run(ctx, a, m, nullptr);
     if (rc) return rc;
-    // 2. garble on the C-OT's zero labels, 3. evaluate on the OT'd active labels
+    // 2. garble on the C-OT's zero labels with the garbler's string and mask folded in, 3. evaluate on the
+    // OT'd active labels
     g.ev_ot = 1;
     HIP_TRY(ctx, launch_gc_garble(g, ctx->stream));
     g.ev_labels = da.as<uint4>();
@@ -496,7 +494,6 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
         return FHH_OK;
     };
     rc = soa_to_aos(dt, 2 * (bits - 1), n, tables);
-    if (!rc) rc = soa_to_aos(dg, bits + 1, n, gb_labels);
     if (!rc) rc = soa_to_aos(de, bits, npad, ev_zero);
     if (!rc) rc = soa_to_aos(da, bits, npad, ev_active);
     return rc;
@@ -512,7 +509,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
 // never the garbler's. Five buffers cross per chunk, in protocol order (r05: both OTs correlated):
 //   E -> G  u1      labels C-OT: U (the evaluator's share planes are its choice bits)
 //   G -> E  y1      labels C-OT: y = H(q) ^ Delta ^ H(q ^ s), 16 B per OT
-//   G -> E  gc      the garbled tables, the garbler's active labels (+ mask wire), decode bits
+//   G -> E  gc      the garbled tables and decoding bits (the garbler's string and mask are folded
+//                   into the circuit, k_gc_garble_cot: no garbler labels cross)
 //   E -> G  u2      share C-OT (collect.rs:437-471 / 846-876): U
 //   G -> E  y2      share C-OT: 8 B per OT (FE), 16 B per OT (FieldElm: 2 OTs per test)
 // Buffers are device memory owned by the producing ctx (valid until its next party call); the
@@ -520,7 +518,7 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
 // Counters: each OT kind's base-OT session (the cfg's base material) keeps a running row-PRG
 // counter per ctx, so chunks and levels that extend the same base OTs never repeat pads (ocelot's
 // AlszSender keeps its PRG across `send` calls the same way); a new set of base OTs starts at 0. The
-// garbler's labels and gate tweaks use the test's index in the whole level (child_begin x n + t).
+// gate tweaks use the test's index in the whole level (child_begin x n + t).
 // ================================================================================================
 namespace fhh {
 namespace eng {
@@ -675,7 +673,7 @@ int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver) {
 
 // message sizes
 uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
-uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)(2 * (P.bits - 1) + P.bits + 1) * 16 + 1); }
+uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1); }
 uint64_t y2_bytes(const PartyState& P) { return P.m2 * (P.last ? 16 : 8); }
 
 int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const char* what) {
@@ -686,21 +684,16 @@ int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const cha
     return FHH_OK;
 }
 
-// carve the gc message [tables | garbler labels | decode]
+// carve the gc message [tables | decode] (the garbler's string and mask are folded into the circuit:
+// no garbler labels cross, k_gc_garble_cot)
 void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
     const uint64_t t = P.tests;
     g.tables = reinterpret_cast<uint4*>(base);
-    g.gb_labels = reinterpret_cast<uint4*>(base + (uint64_t)2 * (P.bits - 1) * t * 16);
-    g.decode = base + (uint64_t)(2 * (P.bits - 1) + P.bits + 1) * t * 16;
+    g.gb_labels = nullptr;
+    g.decode = base + (uint64_t)2 * (P.bits - 1) * t * 16;
 }
 
-// the chunk's label nonce and gate tweaks: the test's index in the whole level (c_off n + t)
-uint64_t party_label_nonce(const PartyState& P) {
-    const uint64_t W = P.bits + 1;
-    uint64_t WS = 4;
-    while (WS < W) WS *= 2;
-    return P.c_off * P.n * WS;
-}
+// the chunk's gate tweaks: the test's index in the whole level (c_off n + t)
 uint64_t party_gate_base(const PartyState& P) { return P.c_off * P.n * (P.bits - 1); }
 
 }  // namespace
@@ -767,9 +760,7 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     gb.words = (uint32_t)P.nw;
     gb.bits = P.bits;
     gb.mask = P.mask;
-    std::memcpy(gb.label_key, cfg->label_key, 16);
     std::memcpy(gb.delta, cfg->delta, 16);
-    gb.label_nonce = party_label_nonce(P);
     gb.gate_base = party_gate_base(P);
     gb.gb_planes_dev = P.planes.as<uint64_t>();
     gb.ev_planes_dev = P.planes.as<uint64_t>();   // not read: the evaluator's labels go by OT
@@ -1001,7 +992,8 @@ int fhh_gc_party_test_cfgs(uint64_t prf_seed, uint32_t level, fhh_gb_cfg* gb, fh
     }
     std::memset(gb, 0, sizeof(*gb));
     std::memset(ev, 0, sizeof(*ev));
-    gc_level_material(prf_seed, level, gb->label_key, gb->delta, &gb->mask);
+    uint8_t label_key[16];   // the ideal-OT loop's label key; the r05 garbler draws no labels
+    gc_level_material(prf_seed, level, label_key, gb->delta, &gb->mask);
     for (uint32_t salt = 0; salt < 2; salt++) {
         uint32_t sw[4];
         ot_level_choice(prf_seed, level, salt, sw);

@@ -1290,7 +1290,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     }
                 }
                 HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
-                HIP_TRY(c0, B.gc_gbl.ensure((size_t)(bits + 1) * tests * 16));
+                // garbler labels: the ideal-OT garbler's only (the r05 garbler folds its string in)
+                HIP_TRY(c0, B.gc_gbl.ensure(real_ot ? 16 : (size_t)(bits + 1) * tests * 16));
                 // ideal OT: the evaluator's active labels [bits][tests]; OT mode: its zero labels (the
                 // labels C-OT's sender messages) at OT index (g bits + j) npad + i
                 HIP_TRY(c0, B.gc_evl.ensure(std::max<size_t>((size_t)bits * tests, real_ot ? m1 : 0) * 16));
@@ -1321,7 +1322,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1's choice bits are
                         // its share planes [C][bits][nw] from the chunk's first group on, as they stand
                         // (m1 a multiple of 128: npad of 64, bits even); server 0's sender messages
-                        // x0 = H(q_j) are the zero labels it garbles with, x1 = x0 ^ Delta
+                        // x0 = H(q_j) are the zero labels it garbles with, x1 = x0 ^ Delta; its own string
+                        // and mask fold into the circuit (k_gc_garble_cot: no label is drawn)
                         HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
                         OtArgs a1{};
                         a1.mode = 1;

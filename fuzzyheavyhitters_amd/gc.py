@@ -132,25 +132,23 @@ def planes_from_bits(bits_gn: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(packed).view(np.uint64).reshape(G, bits, nw)
 
 
-def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, label_key, delta, base_seeds, base_choice,
-                      label_nonce: int = 0, gate_base: int = 0, ctr_off: int = 0):
+def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, delta, base_seeds, base_choice, gate_base: int = 0,
+                      ctr_off: int = 0):
     """The r05 labels step on the GPU (fhh_gc_cot_host): the evaluator's input labels by correlated OT
-    (its bits are the choice bits), garbling on the C-OT's zero labels, evaluation. Returns (out [n],
-    dict of the transcript: tables, gb_labels, ev_zero, ev_active, decode)."""
+    (its bits are the choice bits), garbling with the garbler's string and mask folded into the circuit,
+    evaluation. Returns (out [n], dict of the transcript: tables, ev_zero, ev_active, decode)."""
     g = np.ascontiguousarray(np.asarray(gb_inputs).astype(np.uint8) & 1)
     e = np.ascontiguousarray(np.asarray(ev_inputs).astype(np.uint8) & 1)
     if g.ndim != 2 or g.shape != e.shape:
         raise ValueError("equality_test_cot: inputs must both be [n][bits]")
     n, bits = g.shape
-    key = np.frombuffer(_block(label_key), np.uint8).copy()
     dl = np.frombuffer(_block(delta), np.uint8).copy()
     seeds = np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16)
     s = np.frombuffer(bytes(base_choice), np.uint8).copy()
-    tr = {"tables": np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8), "gb_labels": np.zeros((n, bits + 1, 16), np.uint8),
-          "ev_zero": np.zeros((n, bits, 16), np.uint8), "ev_active": np.zeros((n, bits, 16), np.uint8),
-          "decode": np.zeros(n, np.uint8)}
+    tr = {"tables": np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8), "ev_zero": np.zeros((n, bits, 16), np.uint8),
+          "ev_active": np.zeros((n, bits, 16), np.uint8), "decode": np.zeros(n, np.uint8)}
     out = np.zeros(n, np.uint8)
-    check(lib().fhh_gc_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, ptr(key), ptr(dl), label_nonce,
-                                gate_base, ptr(seeds), ptr(s), ctr_off, ptr(tr["tables"]), ptr(tr["gb_labels"]),
-                                ptr(tr["ev_zero"]), ptr(tr["ev_active"]), ptr(tr["decode"]), ptr(out)), kc.handle)
+    check(lib().fhh_gc_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, ptr(dl), gate_base, ptr(seeds),
+                                ptr(s), ctr_off, ptr(tr["tables"]), ptr(tr["ev_zero"]), ptr(tr["ev_active"]),
+                                ptr(tr["decode"]), ptr(out)), kc.handle)
     return out, tr

@@ -6,7 +6,7 @@ Each server holds only its own secrets and draws them itself, as the reference's
 (`AesRng::new()` per channel, collect.rs:431; `OtSender::init` / `OtReceiver::init` per channel and
 level, collect.rs:454,460):
 
-  * the garbler (server 0): its label key, Delta and mask per chunk (os.urandom), and the base-OT
+  * the garbler (server 0): its Delta and mask per chunk (os.urandom), and the base-OT
     receiver's side of each level's Chou–Orlandi runs (its choice bits s, its seed);
   * the evaluator (server 1): the base-OT sender's side (its seed, hence both keys of every base OT).
 
@@ -98,7 +98,6 @@ class GarblerParty:
 
     def __init__(self, kc: KeyCollection):
         self.kc = kc
-        self.base = [None, None]   # per OT kind: (chosen [128][16], s [16]) of the current session
 
     # -- base OTs: the CO15 receiver with choice bits s (OtSender::init's base OTs, collect.rs:454)
     def co15_receive(self, A: bytes):
@@ -113,10 +112,10 @@ class GarblerParty:
         return B.tobytes(), (chosen, s)
 
     def chunk_cfg(self, base, child_begin: int, child_count: int) -> FhhGbCfg:
-        """The garbler's material for one chunk: a fresh label key, Delta and mask (AesRng::new() per
-        channel, collect.rs:431), and the level's base OTs (both kinds)."""
+        """The garbler's material for one chunk: a fresh Delta and mask (AesRng::new() per channel,
+        collect.rs:431; its string is folded into the circuit, so it draws no labels), and the level's
+        base OTs (both kinds)."""
         cfg = FhhGbCfg()
-        cfg.label_key[:] = list(os.urandom(16))
         cfg.delta[:] = list(os.urandom(16))
         cfg.mask = os.urandom(1)[0] & 1
         chosen = np.stack([b[0] for b in base])      # [2][128][16]
@@ -244,7 +243,7 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     (fhh_party_node_sums), keep_values on the leader, prune both.
 
     material "fresh" (the default, a deployment's behaviour): each party draws its own secrets —
-    the garbler a label key, Delta and mask per chunk — and every level's two OT extensions start
+    the garbler a Delta and mask per chunk — and every level's two OT extensions start
     from real Chou–Orlandi base OTs run between the parties over the channel (base_ot_every "level",
     as the reference inits per level, collect.rs:454,460; "crawl": one run per OT kind for the whole
     crawl, the library extending it from a running counter). The runs are computed `base_ot_ahead`

@@ -521,16 +521,18 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
                         uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                         uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out);
 /* The r05 labels step of one batch on host buffers: the labels C-OT (choice bits = the evaluator's
- * bits at OT index j npad + i, npad = n rounded up to 64), garbling on the C-OT's zero labels (the
- * garbler draws only its bits + 1 wires: label of (t, w) = AES_label_key(LE128(label_nonce + t S +
- * w)), S the power of two >= bits + 1, min 4), evaluation on the OT'd active labels. Outputs AoS as
- * fhh_gc_equality_host, plus ev_zero / ev_active [n][bits][16] (the C-OT's sender messages / the
- * evaluator's labels); any output but `out` may be NULL. */
+ * bits at OT index j npad + i, npad = n rounded up to 64; its sender messages are the evaluator's zero
+ * labels E_j), garbling with the garbler's string and mask FOLDED into the circuit — the garbler knows
+ * x_j, so input z_j = NOT(x_j ^ y_j) takes the zero label E_j ^ (x_j ? 0 : Delta) and the evaluator's
+ * OT'd label is z_j's active label; decode = colour(eq's zero label) ^ mask — and evaluation on the
+ * OT'd labels (out = colour ^ decode = eq ^ mask). No label PRG, no garbler labels on the wire; gate
+ * tweaks 2 g, 2 g + 1 with g = gate_base + t (bits - 1) + k as in fhh_gc_batch. Outputs AoS: tables
+ * [n][bits-1][2][16], ev_zero / ev_active [n][bits][16], decode [n], out [n]; any but `out` may be
+ * NULL. */
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                    uint32_t mask, const uint8_t label_key[16], const uint8_t delta[16], uint64_t label_nonce,
-                    uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
-                    uint64_t ctr_off, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_zero, uint8_t* ev_active,
-                    uint8_t* decode, uint8_t* out);
+                    uint32_t mask, const uint8_t delta[16], uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
+                    uint8_t* ev_active, uint8_t* decode, uint8_t* out);
 
 /* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
  * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;
@@ -550,8 +552,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * device copy in the in-process tests). Both OTs are correlated OTs (fhh_cot_extend_host's modes):
  * OT 1 (FHH_COT_LABELS) delivers the evaluator's input labels (m = C x 2d x npad: its share planes are
  * the choice bits), OT 2 (FHH_COT_FE, FHH_COT_FE255 at tree_crawl_last: 2 OTs per test) the share;
- * the circuit is fhh_gc_cot_host's. gc = [tables (bits-1) x 2 | garbler labels bits + 1 | decode 1 B]
- * per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
+ * the circuit is fhh_gc_cot_host's (the garbler's string and mask folded in). gc = [tables (bits-1) x 2
+ * | decode 1 B] per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
  * y1 16 B per OT, y2 8 B per OT (FE) or 16 B per OT (FieldElm). Each server's node values (the garbler's
  * r1 = v + mask, the evaluator's OT output) stay on its device; fhh_party_node_sums sums them: non-last
  * level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm (the
@@ -562,14 +564,13 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * reference's channels each run a slice of the level's tests (collect.rs:423-430); this bounds the
  * level's buffers at 1M clients. Chunks run in order and together cover [0, C); fhh_party_node_sums
  * follows the last one. Both parties must use the same windows. child_count = 0: the whole level.
- * Freshness: the garbler's label key / Delta / mask should be fresh per chunk (labels and gate tweaks
- * are indexed by the test's index in the whole level, so a key reused WITHIN a level never repeats a
- * label, but Delta must not outlive the level). Base OTs may be reused across chunks and levels: each
+ * Freshness: the garbler's Delta and mask should be fresh per chunk (gate tweaks are indexed by the
+ * test's index in the whole level; Delta must not outlive the level). Base OTs may be reused across chunks and levels: each
  * ctx keeps, per OT kind, the running row-PRG counter of the base material it last saw and continues
  * it while the material is unchanged (a new set starts at 0), so pads never repeat. */
 typedef struct fhh_gb_cfg {
-    uint8_t label_key[16];               /* label PRG key (AesRng::new(), collect.rs:431)           */
-    uint8_t delta[16];                   /* free-XOR offset (bit 0 forced to 1)                    */
+    uint8_t delta[16];                   /* free-XOR offset (bit 0 forced to 1; AesRng::new(),
+                                            collect.rs:431)                                        */
     uint32_t mask;                       /* the chunk's mask bit (equalitytest.rs:38-43)           */
     uint32_t pad_;
     uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares): k_i^{s_i} from the   */

@@ -967,25 +967,22 @@ static void gc_xor(uint8_t* d, const uint8_t* a, const uint8_t* b) {
     for (int k = 0; k < 16; k++) d[k] = a[k] ^ b[k];
 }
 
-/* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits. Layouts: tables
- * [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last), ev_labels [n][bits][16].
- * ev_zero == NULL (ideal OT): every zero label is AES_key(LE128(nonce + t S + w)), S = the power of
- * two >= 2 bits + 1 (w < bits: the garbler's string, w = bits: the mask, w > bits: the evaluator's
- * string), and the evaluator's ACTIVE labels (what an OT would deliver, gb_set_fancy_inputs :67-82)
- * are written to ev_labels. ev_zero != NULL [n][bits][16] (r05: the labels OT is a correlated OT,
- * orc_cot_extend mode 1): the evaluator's zero labels are the C-OT's sender messages, the garbler
- * draws only its own wires and the mask (S = the power of two >= bits + 1, min 4) and ev_labels is
- * not written. */
+/* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits with an ideal OT for the
+ * evaluator's labels. Layouts: tables [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last),
+ * ev_labels [n][bits][16]. Every zero label is AES_key(LE128(nonce + t S + w)), S = the power of two
+ * >= 2 bits + 1 (w < bits: the garbler's string, w = bits: the mask, w > bits: the evaluator's
+ * string); the evaluator's ACTIVE labels (what an OT would deliver, gb_set_fancy_inputs :67-82) are
+ * written to ev_labels. */
 static void gc_garble_impl(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                           const uint8_t* ev_zero, uint32_t mask, const uint8_t key[16], const uint8_t delta_in[16],
-                           uint64_t label_nonce, uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels,
-                           uint8_t* ev_labels, uint8_t* decode) {
+                           uint32_t mask, const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce,
+                           uint64_t gate_base, uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels,
+                           uint8_t* decode) {
     oracle_init();
     uint8_t rk[176], D[16];
     key_expand(key, rk);
     memcpy(D, delta_in, 16);
     D[0] |= 1;
-    const uint64_t W = ev_zero ? (uint64_t)bits + 1 : 2 * (uint64_t)bits + 1;
+    const uint64_t W = 2 * (uint64_t)bits + 1;
     uint64_t WS = 4;                                 /* label counter stride: the power of two >= W */
     while (WS < W) WS *= 2;
 #pragma omp parallel for schedule(static)
@@ -997,17 +994,13 @@ static void gc_garble_impl(uint64_t n, uint32_t bits, const uint8_t* gb_bits, co
             for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
             gc_aes_rk(rk, ctr, L[w]);
         }
-        if (ev_zero)                                 /* the C-OT's sender messages */
-            for (uint32_t j = 0; j < bits; j++) memcpy(L[bits + 1 + j], ev_zero + ((uint64_t)t * bits + j) * 16, 16);
         for (uint32_t j = 0; j < bits; j++) {        /* active input labels */
             uint8_t* g = gb_labels + ((uint64_t)t * (bits + 1) + j) * 16;
             memcpy(g, L[j], 16);
             if (gb_bits[(uint64_t)t * bits + j] & 1) gc_xor(g, g, D);
-            if (!ev_zero) {
-                uint8_t* e = ev_labels + ((uint64_t)t * bits + j) * 16;
-                memcpy(e, L[bits + 1 + j], 16);
-                if (ev_bits[(uint64_t)t * bits + j] & 1) gc_xor(e, e, D);
-            }
+            uint8_t* e = ev_labels + ((uint64_t)t * bits + j) * 16;
+            memcpy(e, L[bits + 1 + j], 16);
+            if (ev_bits[(uint64_t)t * bits + j] & 1) gc_xor(e, e, D);
         }
         uint8_t* m = gb_labels + ((uint64_t)t * (bits + 1) + bits) * 16;
         memcpy(m, L[bits], 16);
@@ -1051,17 +1044,92 @@ static void gc_garble_impl(uint64_t n, uint32_t bits, const uint8_t* gb_bits, co
 void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits, uint32_t mask,
                       const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
                       uint8_t* tables, uint8_t* gb_labels, uint8_t* ev_labels, uint8_t* decode) {
-    gc_garble_impl(n, bits, gb_bits, ev_bits, NULL, mask, key, delta_in, label_nonce, gate_base, tables, gb_labels,
+    gc_garble_impl(n, bits, gb_bits, ev_bits, mask, key, delta_in, label_nonce, gate_base, tables, gb_labels,
                    ev_labels, decode);
 }
 
-/* The garbler of the r05 protocol: the evaluator's zero labels ev_zero [n][bits][16] come from the
- * labels C-OT (orc_cot_extend mode 1), the garbler labels its own string and the mask. */
+/* The garbler of the r05 protocol (k_gc_garble_cot): the evaluator's zero labels ev_zero [n][bits][16]
+ * come from the labels C-OT (orc_cot_extend mode 1), and the garbler's own string and mask are FOLDED
+ * into the circuit instead of encoded as input wires — it knows x_j, so the input z_j = NOT(x_j ^ y_j)
+ * gets the zero label Z_j = E_j ^ (x_j ? 0 : D), which makes the evaluator's OT'd label E_j ^ y_j D
+ * exactly z_j's active label (XOR with a garbler-known constant is free under free-XOR), and the mask
+ * goes into the decoding bit: decode = colour(out^0) ^ mask. No label is drawn (no label key) and no
+ * garbler label is sent. Same circuit as bin_eq_bundles / and_many (:128-189). Layouts: tables
+ * [n][bits-1][2][16], decode [n]. */
 void orc_gc_garble_eq_cot(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
-                          const uint8_t key[16], const uint8_t delta_in[16], uint64_t label_nonce, uint64_t gate_base,
-                          uint8_t* tables, uint8_t* gb_labels, uint8_t* decode) {
-    gc_garble_impl(n, bits, gb_bits, NULL, ev_zero, mask, key, delta_in, label_nonce, gate_base, tables, gb_labels,
-                   NULL, decode);
+                          const uint8_t delta_in[16], uint64_t gate_base, uint8_t* tables, uint8_t* decode) {
+    oracle_init();
+    uint8_t D[16];
+    memcpy(D, delta_in, 16);
+    D[0] |= 1;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t acc[16];
+        for (uint32_t k = 0; k < bits; k++) {
+            uint8_t bz[16];
+            memcpy(bz, ev_zero + ((uint64_t)t * bits + k) * 16, 16);
+            if (!(gb_bits[(uint64_t)t * bits + k] & 1)) gc_xor(bz, bz, D);   /* Z_k = E_k ^ (x_k ? 0 : D) */
+            if (k == 0) {
+                memcpy(acc, bz, 16);
+                continue;
+            }
+            uint8_t a1[16], b1[16], hA0[16], hA1[16], hB0[16], hB1[16], TG[16], TE[16], WG[16], WE[16];
+            gc_xor(a1, acc, D);
+            gc_xor(b1, bz, D);
+            const int pa = acc[0] & 1, pb = bz[0] & 1;
+            const uint64_t j = 2 * (gate_base + (uint64_t)t * (bits - 1) + (k - 1));
+            gc_tccr(acc, j, hA0);
+            gc_tccr(a1, j, hA1);
+            gc_tccr(bz, j + 1, hB0);
+            gc_tccr(b1, j + 1, hB1);
+            gc_xor(TG, hA0, hA1);
+            if (pb) gc_xor(TG, TG, D);
+            memcpy(WG, hA0, 16);
+            if (pa) gc_xor(WG, WG, TG);
+            gc_xor(TE, hB0, hB1);
+            gc_xor(TE, TE, acc);
+            memcpy(WE, hB0, 16);
+            if (pb) {
+                uint8_t te_a[16];
+                gc_xor(te_a, TE, acc);
+                gc_xor(WE, WE, te_a);
+            }
+            uint8_t* tb = tables + ((uint64_t)t * (bits - 1) + (k - 1)) * 32;
+            memcpy(tb, TG, 16);
+            memcpy(tb + 16, TE, 16);
+            gc_xor(acc, WG, WE);
+        }
+        decode[t] = (uint8_t)((acc[0] ^ mask) & 1);   /* colour of eq's zero label, mask folded in */
+    }
+}
+
+/* The r05 evaluator: its OT'd labels ev_active [n][bits][16] are the inputs' active labels;
+ * out[t] = colour(acc) ^ decode[t] = eq ^ mask. */
+void orc_gc_eval_eq_cot(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* ev_active,
+                        const uint8_t* decode, uint64_t gate_base, uint8_t* out) {
+    oracle_init();
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t acc[16];
+        memcpy(acc, ev_active + (uint64_t)t * bits * 16, 16);
+        for (uint32_t k = 1; k < bits; k++) {
+            uint8_t b[16], hA[16], hB[16];
+            memcpy(b, ev_active + ((uint64_t)t * bits + k) * 16, 16);
+            const int sa = acc[0] & 1, sb = b[0] & 1;
+            const uint64_t j = 2 * (gate_base + (uint64_t)t * (bits - 1) + (k - 1));
+            const uint8_t* tb = tables + ((uint64_t)t * (bits - 1) + (k - 1)) * 32;
+            gc_tccr(acc, j, hA);
+            gc_tccr(b, j + 1, hB);
+            if (sa) gc_xor(hA, hA, tb);
+            if (sb) {
+                uint8_t te_a[16];
+                gc_xor(te_a, tb + 16, acc);
+                gc_xor(hB, hB, te_a);
+            }
+            gc_xor(acc, hA, hB);
+        }
+        out[t] = (uint8_t)((acc[0] & 1) ^ decode[t]);
+    }
 }
 
 /* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */

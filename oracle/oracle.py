@@ -725,23 +725,31 @@ def gc_get_ni() -> bool:
     return bool(lib().orc_gc_get_ni())
 
 
-def gc_garble_eq_cot(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, key: bytes, delta: bytes,
-                     label_nonce: int = 0, gate_base: int = 0):
-    """The r05 garbler: the evaluator's zero labels ev_zero [n][bits][16] come from the labels C-OT;
-    the garbler labels its own bits and the mask (stride pow2 >= bits + 1). Returns (tables, gb_labels,
-    decode) as gc_garble_eq."""
+def gc_garble_eq_cot(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, delta: bytes, gate_base: int = 0):
+    """The r05 garbler (fhh_oracle.c orc_gc_garble_eq_cot): the evaluator's zero labels ev_zero
+    [n][bits][16] come from the labels C-OT; the garbler's string and mask are folded into the circuit.
+    Returns (tables [n][bits-1][2][16], decode [n])."""
     g = np.ascontiguousarray(gb_bits, np.uint8)
     z = np.ascontiguousarray(ev_zero, np.uint8)
     n, bits = g.shape
     tables = np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8)
-    gbl = np.zeros((n, bits + 1, 16), np.uint8)
     dec = np.zeros(n, np.uint8)
-    k = np.frombuffer(key, np.uint8).copy()
     d = np.frombuffer(delta, np.uint8).copy()
     lib().orc_gc_garble_eq_cot(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z), ctypes.c_uint32(mask & 1),
-                               _p(k), _p(d), ctypes.c_uint64(label_nonce), ctypes.c_uint64(gate_base), _p(tables),
-                               _p(gbl), _p(dec))
-    return tables, gbl, dec
+                               _p(d), ctypes.c_uint64(gate_base), _p(tables), _p(dec))
+    return tables, dec
+
+
+def gc_eval_eq_cot(tables, ev_active, decode, gate_base: int = 0) -> np.ndarray:
+    """The r05 evaluator: out [n] = eq ^ mask from its OT'd labels ev_active [n][bits][16]."""
+    t = np.ascontiguousarray(tables, np.uint8)
+    e = np.ascontiguousarray(ev_active, np.uint8)
+    d = np.ascontiguousarray(decode, np.uint8)
+    n, bits = e.shape[0], e.shape[1]
+    out = np.zeros(n, np.uint8)
+    lib().orc_gc_eval_eq_cot(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(t), _p(e), _p(d),
+                             ctypes.c_uint64(gate_base), _p(out))
+    return out
 
 
 COT_LABELS, COT_FE, COT_FE255 = 1, 2, 3

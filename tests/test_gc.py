@@ -206,10 +206,11 @@ def test_gpu_crawl_gc_rejects_count_mode():
         sim_crawl(c0, c1, 0.01, mode="count", gc=True)
 
 
-# ---- r05: the evaluator's labels by correlated OT (oracle chain = GPU chain) -------------------------
-def _oracle_cot_chain(oracle, g, e, mask, seeds, s, nonce=0, gate_base=0, ctr_off=0):
+# ---- r05: the evaluator's labels by correlated OT, the garbler's string folded in --------------------
+def _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
     """The labels C-OT (choice bits: the evaluator's bits at OT index j npad + i), garbling on its
-    zero labels, evaluation on its active labels — all in the oracle."""
+    zero labels with the garbler's string and mask folded in, evaluation on the evaluator's OT'd
+    labels — all in the oracle."""
     n, bits = g.shape
     npad = (n + 63) // 64 * 64
     ch = np.zeros(bits * npad, np.uint8)
@@ -218,9 +219,9 @@ def _oracle_cot_chain(oracle, g, e, mask, seeds, s, nonce=0, gate_base=0, ctr_of
     x0, out, u, y = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=_delta1(), ctr_off=ctr_off)
     ev_zero = np.stack([x0[k * npad: k * npad + n] for k in range(bits)], axis=1)
     ev_act = np.stack([out[k * npad: k * npad + n] for k in range(bits)], axis=1)
-    t, gl, d = oracle.gc_garble_eq_cot(g, ev_zero, mask, KEY, DELTA, label_nonce=nonce, gate_base=gate_base)
-    res = oracle.gc_eval_eq(t, gl, ev_act, d, gate_base=gate_base)
-    return res, dict(tables=t, gb_labels=gl, ev_zero=ev_zero, ev_active=ev_act, decode=d)
+    t, d = oracle.gc_garble_eq_cot(g, ev_zero, mask, DELTA, gate_base=gate_base)
+    res = oracle.gc_eval_eq_cot(t, ev_act, d, gate_base=gate_base)
+    return res, dict(tables=t, ev_zero=ev_zero, ev_active=ev_act, decode=d)
 
 
 def _delta1():
@@ -232,24 +233,26 @@ def _delta1():
 @pytest.mark.parametrize("bits", [1, 2, 4, 8])
 def test_oracle_cot_labels_chain_functional(oracle, bits):
     """eq_gc's assertion (equalitytest.rs:258-265) through the r05 labels step: masks ^ results ==
-    (gb == ev), and the evaluator's active labels differ from the C-OT's zero labels by Delta exactly
-    on its set bits."""
+    (gb == ev), for both masks and for complemented evaluator strings; the evaluator's active labels
+    differ from the C-OT's zero labels by Delta exactly on its set bits."""
     rng = np.random.default_rng(40 + bits)
     g, e = _cases(rng, 300, bits)
     seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
     s = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
     for mask in (0, 1):
-        out, tr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, nonce=0, gate_base=5, ctr_off=256)
+        out, tr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=5, ctr_off=256)
         assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))
         D = np.frombuffer(_delta1(), np.uint8)
         assert np.array_equal(tr["ev_zero"] ^ tr["ev_active"], e[:, :, None] * D)
+        out2, _ = _oracle_cot_chain(oracle, g, 1 - e, mask, seeds, s, gate_base=5, ctr_off=256)
+        assert np.array_equal(out2 ^ mask, (g == 1 - e).all(axis=1).astype(np.uint8))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bits", [(1, 1), (63, 2), (65, 2), (1000, 2), (4097, 4), (300, 6), (130, 8)])
 def test_gpu_cot_labels_chain_bit_exact(oracle, n, bits):
     """fhh_gc_cot_host (the C-OT + garble + evaluate of one batch) = the oracle chain: zero labels,
-    active labels, tables, garbler labels, decoding bits, outputs."""
+    active labels, tables, decoding bits, outputs."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import gc
     rng = np.random.default_rng(n * 3 + bits)
@@ -257,11 +260,10 @@ def test_gpu_cot_labels_chain_bit_exact(oracle, n, bits):
     seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
     s = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
     kc = fhh.KeyCollection(8, 1)
-    for nonce, mask, ctr in ((0, 0, 0), (0, 1, 256), (123, 1, 512)):
-        out, tr = gc.equality_test_cot(kc, g, e, mask, KEY, DELTA, seeds, s, label_nonce=nonce, gate_base=7,
-                                       ctr_off=ctr)
-        exp, etr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, nonce=nonce, gate_base=7, ctr_off=ctr)
-        for k in ("ev_zero", "ev_active", "tables", "gb_labels", "decode"):
+    for mask, ctr in ((0, 0), (1, 256), (1, 512)):
+        out, tr = gc.equality_test_cot(kc, g, e, mask, DELTA, seeds, s, gate_base=7, ctr_off=ctr)
+        exp, etr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=7, ctr_off=ctr)
+        for k in ("ev_zero", "ev_active", "tables", "decode"):
             assert np.array_equal(tr[k], etr[k]), k
         assert np.array_equal(out, exp)
         assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))

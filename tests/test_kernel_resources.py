@@ -68,9 +68,11 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     if not shutil.which("hipcc"):
         pytest.skip("hipcc not available")
     u = _resource_usage("fhh_gc.hip", tmp_path)
-    # both garbler forms: the ideal-OT one and the r05 one on the labels C-OT's zero labels
-    names = [f"_ZN3fhh11k_gc_garbleILi{b}ELb{e}EEEvNS_6GcArgsE" for b in range(1, 9) for e in (0, 1)]
-    names += [f"_ZN3fhh9k_gc_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
+    # both garblers (the ideal-OT one, the r05 one on the labels C-OT's zero labels with the garbler's
+    # string folded in) and both evaluator forms
+    names = [f"_ZN3fhh11k_gc_garbleILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
+    names += [f"_ZN3fhh15k_gc_garble_cotILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
+    names += [f"_ZN3fhh9k_gc_evalILi{b}ELb{f}EEEvNS_6GcArgsE" for b in range(1, 9) for f in (0, 1)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
     names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE"]

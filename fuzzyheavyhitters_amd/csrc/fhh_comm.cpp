@@ -15,10 +15,12 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
-#include <vector>
 #include <string>
+#include <thread>
+#include <vector>
 
 struct fhh_comm {
     ncclComm_t comm = nullptr;
@@ -26,6 +28,9 @@ struct fhh_comm {
     // set once by comm_abort (ncclCommAbort freed the communicator; `comm` itself is left in place
     // so a peer thread inside comm_allreduce never sees it change)
     std::atomic<bool> aborted{false};
+    // threads between their `aborted` check and the return of their ncclAllReduce: comm_abort waits
+    // for them (briefly) so no thread can pass the check and then enqueue on a freed communicator
+    std::atomic<int> inflight{0};
     // hosted communicator (fhh_comm_create_hosted): the same cfg->comm code path of the level
     // loop, with the sum done by a host callback instead of RCCL (tests without RCCL ranks)
     fhh_allreduce_fn hosted = nullptr;
@@ -71,7 +76,9 @@ int load_locked(const char* path) {
     if (g_rccl.handle) return FHH_OK;
     void* h = nullptr;
     if (path && *path) {
-        h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+        // an explicit library (a chosen RCCL build, or tests/stubs/librccl_stub.so): resolved through
+        // its own handle only, so it never interposes on the process's other nccl* users
+        h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     } else {
         for (const char* name : {"librccl.so", "librccl.so.1"}) {
             h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);   // already in the process (e.g. torch's)
@@ -134,11 +141,16 @@ int comm_allreduce(fhh_comm* c, const uint64_t* send, uint64_t* recv, uint64_t c
         }
         return FHH_OK;
     }
+    // increment before the check, so an abort that set `aborted` after this thread's check sees it
+    // in flight and waits for the enqueue to return (check-then-use race)
+    c->inflight.fetch_add(1);
     if (c->aborted.load()) {
+        c->inflight.fetch_sub(1);
         if (err) *err = "ncclAllReduce: communicator aborted by a failing peer";
         return FHH_E_COMM;
     }
     const ncclResult_t r = g_rccl.all_reduce(send, recv, count, ncclUint64, ncclSum, c->comm, stream);
+    c->inflight.fetch_sub(1);
     if (r != ncclSuccess) {
         if (err) *err = std::string("ncclAllReduce: ") + g_rccl.error_string(r);
         return FHH_E_COMM;
@@ -206,6 +218,11 @@ int comm_group_allreduce(const std::vector<::fhh_comm*>& comms, const std::vecto
 void comm_abort(::fhh_comm* c) {
     if (!c || !c->comm || !g_rccl.comm_abort) return;
     if (c->aborted.exchange(true)) return;   // another thread got here first
+    // an enqueue that passed its check returns promptly; one still inside after 100 ms is blocked in
+    // the collective itself (a peer never arrived), which is what ncclCommAbort exists to release
+    const auto t0 = std::chrono::steady_clock::now();
+    while (c->inflight.load() > 0 && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(100))
+        std::this_thread::yield();
     (void)hipSetDevice(c->device);
     (void)g_rccl.comm_abort(c->comm);
 }

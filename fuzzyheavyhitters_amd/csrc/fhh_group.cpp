@@ -93,6 +93,8 @@ struct Group {
     uint64_t client_base = 0;                // fhh_set_client_base of the collection
     bool distinct = false;                   // every shard on its own GPU
     bool force_host = false;                 // FHH_GROUP_REDUCE=host
+    bool force_rccl = false;                 // FHH_GROUP_REDUCE=rccl: the RCCL branch on a repeated device
+                                             // (tests, with tests/stubs/librccl_stub.so loaded)
     std::vector<::fhh_comm*> comms;          // in-process RCCL communicators (distinct devices)
     std::string comm_err;
 
@@ -105,7 +107,7 @@ struct Group {
     // FHH_REDUCE_*: RCCL only when every shard holds clients (all ranks join each collective)
     int reduction() const {
         if (shards.size() == 1) return FHH_REDUCE_NONE;
-        if (!distinct || force_host) return FHH_REDUCE_HOST;
+        if ((!distinct && !force_rccl) || force_host) return FHH_REDUCE_HOST;
         for (size_t k = 0; k < shards.size(); k++)
             if (placed && !count[k]) return FHH_REDUCE_HOST;
         return FHH_REDUCE_RCCL;
@@ -579,6 +581,7 @@ int fhh_create_multi(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, const in
     G->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     const char* e = std::getenv("FHH_GROUP_REDUCE");
     G->force_host = e && std::string(e) == "host";
+    G->force_rccl = e && std::string(e) == "rccl";
     auto* g = new fhh_ctx();
     g->device = devices[0];
     g->L = data_len;

@@ -107,7 +107,8 @@ int fhh_gen_keys_pair(fhh_ctx* ctx0, fhh_ctx* ctx1, uint64_t n, const uint8_t* l
  * results of a one-GPU collection: share planes are gathered in client order, node sums are summed
  * over the shards as u64 32-bit-limb partials — an in-process RCCL all-reduce (ncclCommInitAll,
  * one grouped ncclAllReduce over the shards' streams) when the devices are distinct, on the host
- * otherwise (or with FHH_GROUP_REDUCE=host) — and reduced mod p once; prune applies the keep mask
+ * otherwise (or with FHH_GROUP_REDUCE=host; FHH_GROUP_REDUCE=rccl takes the RCCL branch even on a
+ * repeated device — for tests with a stand-in RCCL loaded by fhh_rccl_load) — and reduced mod p once; prune applies the keep mask
  * to every shard; fhh_sim_crawl runs the device level loop per shard pair with the per-level
  * all-reduce over the same communicators. The reference server holds one such collection behind
  * its Mutex (src/bin/server.rs:44-52, 332-335). */

@@ -484,6 +484,7 @@ int group_sim_crawl(fhh_ctx* g0, fhh_ctx* g1, const fhh_sim_config* cfg) {
     // the first failing shard releases its peers waiting in a collective, once for the whole call
     // (two shards failing together must not both abort the same communicators)
     std::once_flag abort_once;
+    int root = -1;   // the shard whose failure started the abort (its peers then fail with "aborted")
     for (size_t k : act)
         th.emplace_back([&, k] {
             fhh_sim_config c = *cfg;
@@ -496,6 +497,7 @@ int group_sim_crawl(fhh_ctx* g0, fhh_ctx* g1, const fhh_sim_config* cfg) {
             rcs[k] = fhh_sim_crawl(G0.shards[k], G1.shards[k], &c);
             if (rcs[k])
                 std::call_once(abort_once, [&] {
+                    root = (int)k;
                     tr.abort();
                     if (red == FHH_REDUCE_RCCL)
                         for (auto* cm : comms) comm_abort(cm);
@@ -503,7 +505,7 @@ int group_sim_crawl(fhh_ctx* g0, fhh_ctx* g1, const fhh_sim_config* cfg) {
         });
     for (auto& t : th) t.join();
     for (auto* c : hosted) fhh_comm_destroy(c);
-    int first = -1;
+    int first = root;
     for (size_t k : act)
         if (rcs[k] && first < 0) first = (int)k;
     if (first >= 0) {

@@ -106,7 +106,8 @@ def test_failing_shard_aborts_its_peers_and_the_collection_recovers(tmp_path):
                        timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["err"] is not None and "injected" in out["err"], out
+    # the error names the root cause: the shard whose all-reduce failed, not a peer it aborted
+    assert out["err"] is not None and "shard 1 " in out["err"] and "injected" in out["err"], out
     init_all, _, _, _, _, aborts, _, _, _, failed = out["after_fail"]
     assert failed == 1 and aborts >= 2 and init_all >= 1, out   # every rank's communicator aborted once
     assert out["final"][0] == init_all + 1, out                  # rebuilt on the next use

@@ -79,10 +79,13 @@ def cpu_baseline(args):
     wl = workload.zipf_workload(n_cpu, L, 1, num_sites=10_000, zipf_s=1.03, ball_size=1, seed=args.seed)
     k0, k1 = O.gen_keys(wl.left, wl.right, wl.root_seeds)
     threads, why = host_threads()
+    sample_levels = list(range(1, L, 64))   # the protocol sample's levels (states kept for these)
     t0 = time.perf_counter()
-    res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds)
+    res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds,
+                  keep_levels=sample_levels)
     dt = time.perf_counter() - t0
     done = len(res.n_children)
+    protocol = cpu_protocol_baseline(args, O, res, n_cpu, threads)
     return {
         "value": res.aes_blocks / dt,
         "unit": "AES blocks/s",
@@ -98,6 +101,87 @@ def cpu_baseline(args):
                    f"children, {res.aes_blocks} AES blocks in {dt:.2f} s, {len(res.final_paths)} heavy hitters "
                    f"(oracle/fhh_oracle.c: AES-NI single block per eval_bit, reference child order, OpenMP "
                    f"{threads} threads on {cpu_model()})"),
+        "protocol": protocol,
+    }
+
+
+def res_levels(res):
+    return 512   # configs[0]'s data_len
+
+
+def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int):
+    """The reference's dominant per-level cost on the host cores: tree_crawl's GC equality test + OTs
+    (collect.rs:419-482, equalitytest.rs:25-106) in the REFERENCE's protocol form — the garbler labels
+    every wire (2 bits + 1 AES-CTR labels), the evaluator's labels and the FE shares go by plain OT
+    extension (ocelot AlszSender::send with both messages: 6 AES per OT) — on the oracle restatement
+    with AES-NI (swanky's fixed-key AES runs on AES-NI), OpenMP over the host threads. Bounded sample:
+    the share strings of configs[0]'s levels 1, 65, 129, ... (states from the crawl above) until
+    ~cpu_baseline_seconds / 6 of protocol time; tests/s extrapolated to the configs[0] crawl's tests.
+    Every sampled level's v0 - v1 equals the plaintext count (checked)."""
+    import numpy as np
+    budget = max(5.0, args.cpu_baseline_seconds / 6)
+    rng = np.random.default_rng(args.seed)
+    FE_P = O.FE_P
+    tests = 0
+    spent = 0.0
+    levels = []
+    for lv in sorted(res.level_states):
+        s0, s1 = res.level_states[lv]
+        g = O.share_bits(s0)   # [C][n][bits]
+        e = O.share_bits(s1)
+        C, n, bits = g.shape
+        if C == 0:
+            continue
+        T = C * n
+        gb = g.reshape(T, bits)
+        ev = e.reshape(T, bits)
+        key = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        delta = bytearray(rng.integers(0, 256, 16, dtype=np.uint8).tobytes())
+        delta[0] |= 1
+        delta = bytes(delta)
+        D = np.frombuffer(delta, np.uint8)
+        mask = int(rng.integers(0, 2))
+        seeds = [rng.integers(0, 256, (128, 2, 16), dtype=np.uint8) for _ in range(2)]
+        sch = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(2)]
+        r0 = rng.integers(0, FE_P, T, dtype=np.uint64)
+        r1 = (r0 + np.uint64(1)) % np.uint64(FE_P)
+        t0 = time.perf_counter()
+        # garbler: labels + half-gates (the evaluator's active labels come out for the OT's check only)
+        tables, gbl, evl, dec = O.gc_garble_eq(gb, ev, mask, key, delta)
+        zero = evl ^ (ev[:, :, None] * D)          # the OT sender's x0: the evaluator's zero labels
+        # the labels OT (plain OT of (x0, x0 ^ Delta), gb_set_fancy_inputs, equalitytest.rs:67-82)
+        lab = O.ot_extend(ev.reshape(-1), zero.reshape(-1, 16), None, delta, seeds[0], sch[0])
+        out = O.gc_eval_eq(tables, gbl, lab.reshape(T, bits, 16), dec)
+        # the share OT (collect.rs:439-471): (r0, r1) if mask else (r1, r0), choice = the GC output
+        blk = lambda v: np.concatenate([v.view(np.uint8).reshape(T, 8), np.zeros((T, 8), np.uint8)], axis=1)
+        m0, m1 = (r0, r1) if mask else (r1, r0)
+        got = O.ot_extend(out, blk(m0), blk(m1), None, seeds[1], sch[1])
+        dt = time.perf_counter() - t0
+        v1 = np.ascontiguousarray(got[:, :8]).view(np.uint64).reshape(C, n)
+        diff = (r1.reshape(C, n).astype(object).sum(axis=1) - v1.astype(object).sum(axis=1)) % FE_P
+        assert [int(x) for x in diff] == [int(x) for x in res.counts[lv]], f"CPU protocol level {lv} != plaintext"
+        spent += dt
+        tests += T
+        levels.append(lv)
+        if spent >= budget:
+            break
+    if not tests:
+        return None
+    rate = tests / spent
+    full = len(res.n_children) == res_levels(res)
+    crawl_tests = int(sum(res.n_children)) * n_cpu
+    aes = (2 * bits + 1) + 8 * (bits - 1) + 4 * (bits - 1) + 6 * bits + 6
+    return {
+        "value": rate, "unit": "GC equality tests + OTs per s", "cores": threads, "kind": "port",
+        "aes_blocks_per_test": aes,
+        "configs0_crawl_tests": crawl_tests if full else None,
+        "configs0_crawl_s_extrapolated": crawl_tests / rate if full else None,
+        "tests_in_levels_crawled": crawl_tests, "levels_crawled": len(res.n_children),
+        "sample": (f"configs[0] levels {levels} ({tests} tests, {spent:.2f} s): the reference's protocol form "
+                   f"(garbler labels all {2 * bits + 1} wires, half-gates + TCCR, plain ALSZ OT for the labels and "
+                   f"the FE share; {aes} AES per test) on oracle/fhh_oracle.c with AES-NI, OpenMP {threads} "
+                   f"threads; v0 - v1 per child = the plaintext count at every sampled level; extrapolated to the "
+                   f"crawl's {crawl_tests} tests"),
     }
 
 

@@ -85,7 +85,7 @@ def cpu_baseline(args):
                   keep_levels=sample_levels)
     dt = time.perf_counter() - t0
     done = len(res.n_children)
-    protocol = cpu_protocol_baseline(args, O, res, n_cpu, threads)
+    protocol = cpu_protocol_baseline(args, O, res, n_cpu, threads, L)
     return {
         "value": res.aes_blocks / dt,
         "unit": "AES blocks/s",
@@ -105,11 +105,7 @@ def cpu_baseline(args):
     }
 
 
-def res_levels(res):
-    return 512   # configs[0]'s data_len
-
-
-def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int):
+def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int):
     """The reference's dominant per-level cost on the host cores: tree_crawl's GC equality test + OTs
     (collect.rs:419-482, equalitytest.rs:25-106) in the REFERENCE's protocol form — the garbler labels
     every wire (2 bits + 1 AES-CTR labels), the evaluator's labels and the FE shares go by plain OT
@@ -168,7 +164,7 @@ def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int):
     if not tests:
         return None
     rate = tests / spent
-    full = len(res.n_children) == res_levels(res)
+    full = len(res.n_children) == L   # the crawl above finished inside its time bound
     crawl_tests = int(sum(res.n_children)) * n_cpu
     aes = (2 * bits + 1) + 8 * (bits - 1) + 4 * (bits - 1) + 6 * bits + 6
     return {

@@ -541,7 +541,7 @@ def gc_bench(args, world, rank, local_rank, dist):
             reps += 1
         cpu_t = time.perf_counter() - t1
         cpu = {"value": m * reps / cpu_t, "unit": "equality tests/s", "cores": host_threads()[0],
-               "kind": "port", "sample": f"{m} tests x {reps} reps, oracle garble+eval (byte AES, OpenMP)"}
+               "kind": "port", "sample": f"{m} tests x {reps} reps, oracle garble+eval (AES-NI as swanky, OpenMP), ni={O.gc_get_ni()}"}
     if rank == 0:
         lds_bytes = tests * aes_per_test * LDS_BYTES_PER_BLOCK
         print(json.dumps({

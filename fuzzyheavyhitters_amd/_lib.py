@@ -222,6 +222,8 @@ def build(verbose: bool = False) -> str:
     objdir = os.path.join(_HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+    if os.environ.get("FHH_AB_VARIANTS"):   # A/B builds: the measured-negative k_expand variants too
+        flags.append("-DFHH_AB_VARIANTS")
 
     def compile_one(f):
         obj = os.path.join(objdir, f + ".o")

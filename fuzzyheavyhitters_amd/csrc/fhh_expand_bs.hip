@@ -15,6 +15,7 @@
 // upper u64 lane for dir 1 (prg.rs:273-276, a bitsliced ripple carry), AES-128 with the zero
 // key (aes_bs_gen.h, generated), feed-forward + correction word (reloaded from L2), store.
 #include "fhh_internal.h"
+#ifdef FHH_AB_VARIANTS   // A/B builds only (fhh_kernels.hip's variant table); the default build has stubs below
 #include "aes_bs_gen.h"
 #include "aes_tables.h"
 #include "bitslice.h"
@@ -725,3 +726,14 @@ namespace fhh {
 int expand_bs_threads(int which) { return bs_pair_mode(which) ? 128 : kBsThreads; }
 
 }  // namespace fhh
+
+#else   // !FHH_AB_VARIANTS: no bitsliced variant in this build (set_variant refuses 14..26)
+namespace fhh {
+hipError_t launch_expand_bs(const ExpandLaunch&, int, int, uint32_t*, hipStream_t) { return hipErrorInvalidValue; }
+const void* expand_bs_fn(int) { return nullptr; }
+int expand_bs_count() { return 0; }
+int expand_bs_threads(int) { return 0; }
+size_t expand_bs_dyn_lds(int) { return 0; }
+hipError_t launch_bitslice(const uint4*, uint4*, uint64_t, uint32_t, int, hipStream_t) { return hipErrorInvalidValue; }
+}  // namespace fhh
+#endif

@@ -2295,6 +2295,9 @@ int fhh_set_variant(fhh_ctx* ctx, int variant) {
     CTX_CHECK(ctx);
     if (ctx->group) return group_each(ctx, fhh_set_variant, variant);
     if (variant < 0 || variant >= expand_variant_count()) return ctx->fail(FHH_E_ARG, "set_variant: no such variant");
+    if (!expand_threads(variant))
+        return ctx->fail(FHH_E_ARG, "set_variant: variant " + std::to_string(variant) +
+                                        " is not in this build (the A/B variants build with FHH_AB_VARIANTS=1)");
     // 43 / 44 store no / only the dir-0 child seeds (HBM-write A/B): their states are incomplete,
     // so they are refused unless the caller asks for diagnostics explicitly
     if ((variant == 43 || variant == 44) && !std::getenv("FHH_DIAGNOSTIC_VARIANTS"))
@@ -2306,8 +2309,8 @@ int fhh_set_variant(fhh_ctx* ctx, int variant) {
 }
 
 int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* grid_per_device) {
-    if (variant < 0 || variant >= expand_variant_count()) {
-        g_err = "variant_info: no such variant";
+    if (variant < 0 || variant >= expand_variant_count() || !expand_threads(variant)) {
+        g_err = "variant_info: no such variant in this build";
         return FHH_E_ARG;
     }
     if (name && cap) std::snprintf(name, cap, "%s", expand_variant_name(variant));

@@ -13,8 +13,19 @@
 //   k_keys_from_aos add_key wire layout -> SoA device layout
 #include "fhh_internal.h"
 #include "expand_kernel.h"
-#include "expand_ps.h"
 #include "../../include/fhh.h"
+// The measured-negative k_expand variants (hybrid T-table + pair-sliced VALU waves 45-49, the bitsliced
+// 14-26 in fhh_expand_bs.hip, the r01-r02 T-table forms) and their generated AES programs
+// (aes_ps_gen.h, aes_bs_gen.h) build only with -DFHH_AB_VARIANTS (FHH_AB_VARIANTS=1 for
+// _lib.build(): A/B builds, tools/ab_builds.sh); the default build holds the product variant 52 and the
+// generic-AES variant 33 the parity suite compares it with.
+#ifdef FHH_AB_VARIANTS
+#include "expand_ps.h"
+#else
+namespace fhh {
+__device__ __forceinline__ void expand_item_ps(const ExpandJob&, uint64_t, uint32_t) {}   // no hybrid variant built
+}  // namespace fhh
+#endif
 
 namespace fhh {
 
@@ -365,6 +376,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
 
 // test hook: AES_0 of 1024 blocks through the hybrid's pair-sliced data path (k_debug_aes_ps);
 // in / out are host arrays of 1024 x 16 bytes
+#ifdef FHH_AB_VARIANTS
 extern "C" int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out) {
     if (!in || !out) return FHH_E_ARG;
     if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
@@ -384,6 +396,9 @@ extern "C" int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out) {
     (void)hipFree(dout);
     return e == hipSuccess ? FHH_OK : FHH_E_HIP;
 }
+#else
+extern "C" int fhh_debug_aes_ps(int, const uint8_t*, uint8_t*) { return FHH_E_ARG; }   // FHH_AB_VARIANTS only
+#endif
 
 // arm the wave timeline: buf = device buffer of cap launches x grid waves x 3 u64 (NULL disarms)
 extern "C" int fhh_wave_profile_arm(int device, uint64_t* buf, uint32_t cap) {
@@ -401,7 +416,14 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     return hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_wprof_launch), sizeof *launches) == hipSuccess ? FHH_OK : FHH_E_HIP;
 }
 
-// Variant table (fhh_set_variant). Order matters: index = variant id.
+// Variant table (fhh_set_variant): id, table layout, blocks per lane, threads, min waves, dynamic
+// items, [prefetch, FLAGS]. The default build holds 33 and 52 (the product default); the rest are
+// the A/B forms of r01-r03, built with -DFHH_AB_VARIANTS.
+#ifndef FHH_AB_VARIANTS
+#define FHH_EXPAND_VARIANTS(X)                                   \
+    X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)            \
+    X(52, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096 | 8192)
+#else
 #define FHH_EXPAND_VARIANTS(X)                          \
     X(0, TabT0R64<DevOpsX>, 4, 512, 1, false)           \
     X(1, TabT0R64<DevOpsX>, 4, 512, 1, true)            \
@@ -443,6 +465,7 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
     X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)      \
     X(51, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096) \
     X(52, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096 | 8192)
+#endif
 
 struct VariantInfo {
     const void* fn;
@@ -461,7 +484,7 @@ static VariantInfo variant_info(int v) {
                                       "bitsliced pair2/rolled/carry4 (slow-path test)",
                                       "bitsliced pair2/rolled/3 waves", "bitsliced pair2/unrolled/3 waves"};
         const int w = v - kBsVariant;
-        if (w >= expand_bs_count()) return VariantInfo{nullptr, 0, false, ""};
+        if (w >= expand_bs_count()) return VariantInfo{nullptr, 0, false, ""};   // 0 without FHH_AB_VARIANTS
         return VariantInfo{expand_bs_fn(w), expand_bs_threads(w), true, names[w]};
     }
     switch (v) {

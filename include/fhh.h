@@ -646,10 +646,12 @@ typedef struct fhh_stats {
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);
 /* Select the k_expand variant (LDS table layout / blocks per lane / workgroup size / work
- * distribution). All variants are bit-identical; they differ in speed. */
+ * distribution). All variants are bit-identical; they differ in speed. The default
+ * build holds the product variant 52 and the generic-AES variant 33; the measured-negative A/B
+ * variants (0-51) build only with FHH_AB_VARIANTS=1 — FHH_E_ARG for a variant not in this build. */
 int fhh_set_variant(fhh_ctx* ctx, int variant);
 /* Describe variant: layout name, workgroup size, persistent grid on the current device.
- * Returns FHH_E_ARG past the last variant. */
+ * Returns FHH_E_ARG for an id not in this build. */
 int fhh_variant_info(int variant, char* name, size_t cap, int* threads, int* grid_per_device);
 int fhh_reset_stats(fhh_ctx* ctx);
 /* 1 to time every k_expand launch with HIP events (default 1); K > 1 times every K-th launch

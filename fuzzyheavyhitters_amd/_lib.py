@@ -224,6 +224,8 @@ def build(verbose: bool = False) -> str:
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall"]
     if os.environ.get("FHH_AB_VARIANTS"):   # A/B builds: the measured-negative k_expand variants too
         flags.append("-DFHH_AB_VARIANTS")
+    if os.environ.get("FHH_EXTRA_DEFINES"):   # A/B builds only (tools/ab_builds.sh)
+        flags += ["-D" + d for d in os.environ["FHH_EXTRA_DEFINES"].split()]
 
     def compile_one(f):
         obj = os.path.join(objdir, f + ".o")

@@ -115,6 +115,7 @@ struct fhh_ctx {
     int grid = 0;
     uint32_t loop_cap_hint = 0;   // device loop: capacity the previous crawl grew to
     DevBuf work_counter;          // dynamic item distribution
+    uint32_t expand_seq = 0;      // k_expand launches on work_counter (its counter slot alternates)
 
     // host-staged keys (add_key); uploaded at tree_init
     std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;

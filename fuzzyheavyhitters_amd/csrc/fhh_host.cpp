@@ -405,7 +405,7 @@ int crawl_one(fhh_ctx* ctx, bool last) {
     finalize_launch(La, ctx->grid, ctx->variant);
     size_t slot = 0;
     if (ctx->timing) HIP_TRY(ctx, timing_begin(ctx, &slot));
-    HIP_TRY(ctx, launch_expand(La, ctx->variant, ctx->grid, ctx->work_counter.as<uint32_t>(), ctx->stream));
+    HIP_TRY(ctx, launch_expand(La, ctx->variant, ctx->grid, ctx->work_counter.as<uint32_t>(), &ctx->expand_seq, ctx->stream));
     if (ctx->timing) HIP_TRY(ctx, timing_end(ctx, slot, launch_blocks(ctx)));
     ctx->stats.expand_launches++;
     return post_expand(ctx, last);
@@ -437,7 +437,7 @@ int crawl_pair(fhh_ctx* c0, fhh_ctx* c1, bool last) {
     size_t slot = 0;
     const uint64_t blocks = launch_blocks(c0) + launch_blocks(c1);
     if (c0->timing) HIP_TRY(c0, timing_begin(c0, &slot));
-    HIP_TRY(c0, launch_expand(La, c0->variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
+    HIP_TRY(c0, launch_expand(La, c0->variant, c0->grid, c0->work_counter.as<uint32_t>(), &c0->expand_seq, c0->stream));
     if (c0->timing) HIP_TRY(c0, timing_end(c0, slot, blocks));
     c0->stats.expand_launches++;
     rc = post_expand(c0, last);
@@ -1194,7 +1194,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
             const bool timed = c0->timing && lv % c0->timing_every == 0;
             if (timed) HIP_TRY(c0, timing_begin(c0, &slot));
             La.total_items = 1;   // non-zero: the real count comes from LoopCtl
-            HIP_TRY(c0, launch_expand(La, variant, c0->grid, c0->work_counter.as<uint32_t>(), c0->stream));
+            HIP_TRY(c0, launch_expand(La, variant, c0->grid, c0->work_counter.as<uint32_t>(), &c0->expand_seq, c0->stream));
             if (timed) HIP_TRY(c0, timing_end(c0, slot, 0));
             c0->stats.expand_launches++;
             for (uint32_t k = 0; k < cfg->probe_n_levels; k++) {
@@ -1695,7 +1695,8 @@ int fhh_create(fhh_ctx** out, uint32_t data_len, uint32_t n_dims, int device) {
     }
     ctx->variant = kDefaultVariant;
     ctx->grid = expand_grid(device, ctx->variant);
-    if (ctx->work_counter.ensure(256) != hipSuccess || hipMemset(ctx->work_counter.p, 0, 256) != hipSuccess) {
+    if (ctx->work_counter.ensure(kWorkCounterBytes) != hipSuccess ||
+        hipMemset(ctx->work_counter.p, 0, kWorkCounterBytes) != hipSuccess) {
         g_err = "work counter allocation failed";
         (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;

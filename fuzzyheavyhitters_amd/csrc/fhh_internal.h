@@ -92,8 +92,12 @@ struct LoopCtl {
 // small for the single counter — configs[3] at 1M clients made 62 500 items of ~2.5 entries per
 // level and k_expand ran at the counter's 88 items/µs (25 G blocks/s). A bulk item then spans
 // wpi = max_group / (entries per group) consecutive words (64-client units), lowered until the
-// launch still has 2 items per wave; wide levels (groups of ≥ max_group / 2 entries) keep wpi = 1.
+// launch still has kMwItemsPerWave items per wave; wide levels (groups of ≥ max_group / 2 entries)
+// keep wpi = 1.
 constexpr uint32_t kTailGroup = 8;
+// r05: 4 (was 2) since k_expand draws from 8 per-XCD heads on narrow levels: configs[3] k_expand
+// 0.44 -> 0.47 of the VALU roofline, the d = 1 headline unchanged (profiles/r05/expand_heads/)
+constexpr uint64_t kMwItemsPerWave = 4;
 struct ItemLayout {
     uint32_t g, g_b, wpi;
     uint64_t items_a, total;
@@ -119,7 +123,7 @@ __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njo
             const uint64_t e_eff = entries / groups;   // >= 1: every group holds an entry
             wpi = e_eff >= max_group ? 1 : max_group / e_eff;
             if (wpi > max_wpi) wpi = max_wpi;
-            while (wpi > 1 && groups * ((unit + wpi - 1) / wpi) < 2 * grid_waves) wpi--;
+            while (wpi > 1 && groups * ((unit + wpi - 1) / wpi) < kMwItemsPerWave * grid_waves) wpi--;
         }
     }
     L.wpi = (uint32_t)wpi;
@@ -147,6 +151,15 @@ __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njo
     L.total = begin;
 }
 
+// k_expand's dynamic work heads inside fhh_ctx::work_counter (kWorkCounterBytes): two sets of
+// kExpandHeads per-XCD heads (one 64-B line each) by launch parity (the kernel zeroes the next
+// launch's set), then the wave-timeline exit count of the profiling variant; words 0-1 belong to the
+// A/B bitsliced kernels' re-armed counter (FHH_AB_VARIANTS)
+constexpr uint32_t kExpandHeads = 8, kExpandSlot0 = 16, kExpandSlotStride = 16;
+constexpr uint32_t kExpandProfSlot = kExpandSlot0 + 2 * kExpandHeads * kExpandSlotStride;
+constexpr size_t kWorkCounterBytes = 2048;
+static_assert((kExpandProfSlot + 1) * 4 <= kWorkCounterBytes, "work counter layout");
+
 struct ExpandLaunch {
     ExpandJob job[kMaxJobs];
     uint32_t njobs;
@@ -154,7 +167,7 @@ struct ExpandLaunch {
     uint64_t total_items;
     uint64_t items_a;           // host-driven launches: bulk items (== total_items without a tail phase)
     uint32_t wpi;               // host-driven launches: words per bulk item (item_layout)
-    uint32_t pad_;
+    uint32_t seq;               // the counter's launch number (fhh_ctx::expand_seq): k_expand counter slot
     const LoopCtl* ctl;         // non-null: n_live / group / item_begin / total_items from here
 };
 
@@ -274,7 +287,9 @@ struct KeygenArgs {
 };
 
 // ---- launch wrappers (fhh_kernels.hip); all asynchronous on `stream` ----
-hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream);
+// seq: the counter's launch count (fhh_ctx::expand_seq), advanced per k_expand launch
+hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, uint32_t* seq,
+                         hipStream_t stream);
 int expand_variant_count();
 const char* expand_variant_name(int variant);
 int expand_threads(int variant);

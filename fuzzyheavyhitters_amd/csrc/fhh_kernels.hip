@@ -272,7 +272,9 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     static_assert(!(MW && (AHEAD || TAIL || NBS > 0 || PF)), "MW: plain dynamic items only");
     static_assert(NBS <= THR / 64, "hybrid: NBS VALU waves out of THR / 64");
     __shared__ uint32_t tbl[Tab::kWords];
+    __shared__ uint32_t s_drained;   // bit h: a wave of this workgroup found head h dry
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
+    if (threadIdx.x == 0) s_drained = 0;
     __syncthreads();
     uint64_t prof_t0 = 0, prof_items = 0;
     if constexpr (PROF) prof_t0 = wall_clock64();
@@ -286,15 +288,42 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     // sizes: kernel arguments (host-driven crawl) or LoopCtl (device-resident loop)
     const LoopCtl* ctl = a.ctl;
     const uint64_t total = ctl ? (ctl->abort ? 0 : ctl->total_items) : a.total_items;
-    uint64_t item = work_counter ? 0 : (uint64_t)blockIdx.x * wpb + wave_id_uniform();
-    const uint64_t draw_base = MW ? nwaves : 0;   // counter value v -> item v + draw_base
-    if (MW) {
-        item = (uint64_t)blockIdx.x * wpb + wave_id_uniform();
-    } else if (work_counter) {
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(work_counter, 1u);
-        item = __builtin_amdgcn_readfirstlane(v);
-    }
+    // Dynamic items come from H heads, one per XCD (blocks b and b + 8 share an XCD: one word
+    // saturates at ≈88 dequeues/µs, 8 per-XCD heads do not), head h handing out items
+    // draw_base + h + H·v. A block draws from its own head first, then from the others once they
+    // run dry. The heads of a launch alternate between two sets by launch number: the first block
+    // zeroes the other set for the next launch on the stream (the previous launch, done, used it),
+    // so there is no exit count (4 096 same-address exit atomics alone cost ≈46 µs per launch).
+    constexpr uint32_t H = AHEAD ? 1u : kExpandHeads;
+    uint32_t* heads = work_counter ? work_counter + kExpandSlot0 + (a.seq & 1) * kExpandHeads * kExpandSlotStride : nullptr;
+    if (work_counter && blockIdx.x == 0 && threadIdx.x < kExpandHeads)
+        atomicExch(work_counter + kExpandSlot0 + ((a.seq + 1) & 1) * kExpandHeads * kExpandSlotStride +
+                       threadIdx.x * kExpandSlotStride, 0u);
+    // (MW: wide levels, one-word items, keep one head — the per-XCD split measured ≈1 % slower there)
+    const uint32_t nh = MW ? (__builtin_amdgcn_readfirstlane(ctl ? ctl->wpi : a.wpi) > 1 ? H : 1u) : H;
+    const uint32_t home = blockIdx.x & (nh - 1);
+    const uint64_t draw_base = MW ? nwaves : 0;   // the first nwaves items are dealt statically (MW)
+    // lane 0 draws; bit h of s_drained: a wave of this block found head h dry (its siblings skip it)
+    auto draw = [&]() -> uint64_t {
+        uint64_t it = total;
+        if (lane == 0) {
+            for (uint32_t k = 0; k < nh; k++) {
+                const uint32_t h = (home + k) & (nh - 1);
+                if ((*(volatile uint32_t*)&s_drained >> h) & 1u) continue;
+                const uint32_t v = atomicAdd(heads + h * kExpandSlotStride, 1u);
+                const uint64_t cand = draw_base + h + (uint64_t)nh * v;
+                if (cand < total) {
+                    it = cand;
+                    break;
+                }
+                atomicOr(&s_drained, 1u << h);
+            }
+        }
+        return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(it >> 32)) << 32) |
+               __builtin_amdgcn_readfirstlane((uint32_t)it);
+    };
+    uint64_t item = (uint64_t)blockIdx.x * wpb + wave_id_uniform();   // static, MW
+    if (heads && !MW) item = draw();
     const uint64_t items_a = TAIL ? (ctl ? ctl->items_a : a.items_a) : total;
     while (item < total) {
         // bulk items [0, items_a), then the end phase (item_layout): same job order in each
@@ -342,18 +371,15 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
                 expand_item_wg<Tab, NB, NT, PAIR, STORE, NTL>(J, w, grp, tbl, lane, b0, b1);
         } else if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
         else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
-        else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, work_counter, &nxt);
+        else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, heads, &nxt);
         else expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1);
-        if (work_counter) {
-            uint32_t v = nxt;
-            if (!AHEAD && lane == 0) v = atomicAdd(work_counter, 1u);
-            item = (uint64_t)__builtin_amdgcn_readfirstlane(v) + draw_base;
+        if (heads) {
+            if constexpr (AHEAD) item = (uint64_t)__builtin_amdgcn_readfirstlane(nxt) + draw_base;   // H = 1
+            else item = draw();
         } else {
             item += nwaves;
         }
     }
-    // dynamic mode: every wave drew exactly one item past the end; the last wave to leave
-    // re-arms the counter for the next launch (no memset between launches)
     if constexpr (PROF) {
         const uint64_t t1 = wall_clock64();
         const uint32_t L = g_wprof_launch;
@@ -364,12 +390,13 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             r[2] = prof_items;
         }
     }
-    if (work_counter && lane == 0) {
-        const uint32_t done = atomicAdd(work_counter + 1, 1u);
-        if (done + 1 == (uint32_t)nwaves) {
-            if constexpr (PROF) atomicAdd(&g_wprof_launch, 1u);
-            atomicExch(work_counter, 0u);
-            atomicExch(work_counter + 1, 0u);
+    if constexpr (PROF) {   // the wave timeline's launch index: the last wave out bumps it
+        if (work_counter && lane == 0) {
+            const uint32_t done = atomicAdd(work_counter + kExpandProfSlot, 1u);
+            if (done + 1 == (uint32_t)nwaves) {
+                atomicAdd(&g_wprof_launch, 1u);
+                atomicExch(work_counter + kExpandProfSlot, 0u);
+            }
         }
     }
 }
@@ -500,16 +527,20 @@ int expand_variant_count() { return kBsVariant + kBsCount + 26; }
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
-hipError_t launch_expand(const ExpandLaunch& a, int variant, int grid, uint32_t* work_counter, hipStream_t stream) {
-    if (a.total_items == 0) return hipSuccess;
-    if (variant_is_bs(variant)) return launch_expand_bs(a, variant - kBsVariant, grid, work_counter, stream);
+hipError_t launch_expand(const ExpandLaunch& a0, int variant, int grid, uint32_t* work_counter, uint32_t* seq,
+                         hipStream_t stream) {
+    if (a0.total_items == 0) return hipSuccess;
+    if (variant_is_bs(variant)) return launch_expand_bs(a0, variant - kBsVariant, grid, work_counter, stream);
+    ExpandLaunch a = a0;
+    a.seq = (*seq)++;
     const VariantInfo vi = variant_info(variant);
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;
     const uint64_t blocks_needed = (a.total_items + wpb - 1) / wpb;
     // device-resident loop: the item count is only known on the device -> full persistent grid
     const int g = a.ctl ? grid : (int)(blocks_needed < (uint64_t)grid ? blocks_needed : (uint64_t)grid);
-    // dynamic mode: work_counter[0..1] must be zero at launch; the kernel re-arms it on exit
+    // dynamic mode: the counter slot of launch a.seq must be zero at launch (the previous
+    // k_expand on this counter zeroed it; fhh_create zeroes both)
     uint32_t* ctr = vi.dynamic ? work_counter : nullptr;
     switch (variant) {
 #define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \

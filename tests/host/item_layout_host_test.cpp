@@ -2,7 +2,7 @@
 // kernel's item -> (job, entry range, word range) decode (fhh_kernels.hip k_expand, including
 // the multi-word bulk items of variant 51): for random job sizes, every (job, entry, word) is
 // covered exactly once, no item reaches past n_live or nw, and a multi-word layout still gives
-// every wave at least two items.
+// every wave at least kMwItemsPerWave items.
 // Built with hipcc (host code only) by tests/test_host_aes.py; prints "OK" on success.
 #include "../../fuzzyheavyhitters_amd/csrc/fhh_internal.h"
 #include <cstdio>
@@ -27,7 +27,7 @@ int main() {
         for (uint32_t k = 0; k < njobs; k++) seen[k].assign((size_t)n_live[k] * unit, 0);
         if (L.items_a > L.total) fails++;
         if (L.wpi < 1 || L.wpi > max_wpi || (tail && L.wpi != 1)) fails++;
-        if (L.wpi > 1 && L.total < 2 * waves) fails++;
+        if (L.wpi > 1 && L.total < fhh::kMwItemsPerWave * waves) fails++;
         const uint32_t nwi = (unit + L.wpi - 1) / L.wpi;   // bulk items per entry group
         for (uint64_t item = 0; item < L.total; item++) {
             const bool tl = item >= L.items_a;
@@ -58,7 +58,7 @@ int main() {
         const uint32_t narrow[4] = {1, 1, 1, 1};   // configs[3]: ~1 entry per (server, dim)
         fhh::ItemLayout L;
         fhh::item_layout(narrow, 4, 15625, 16, 4096, false, L, 16);
-        if (L.wpi != 7 || L.total != 4 * 2233) fails++;   // lowered until 2 items per wave
+        if (L.wpi != 3 || L.total != 4 * 5209) fails++;   // lowered until 4 items per wave
         const uint32_t wide[2] = {200, 200};                // a deep d = 1 level
         fhh::item_layout(wide, 2, 15625, 16, 4096, false, L, 16);
         if (L.g != 16) fails++;

@@ -346,12 +346,14 @@ def dropin_bench(args, world, rank, local_rank, dist):
         fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
         return c0, c1
 
+    runs = {}
+
     def timed(fn, reps, warm=1):
         for _ in range(warm):
             t0 = time.perf_counter()
             fn()
             print(f"dropin:   warm-up run {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
-        best, out = None, None
+        times, out = [], None
         for _ in range(reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -359,8 +361,9 @@ def dropin_bench(args, world, rank, local_rank, dist):
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             print(f"dropin:   timed run {dt:.2f} s", file=sys.stderr, flush=True)
-            best = dt if best is None else min(best, dt)
-        return best, out
+            times.append(dt)
+        runs[id(fn)] = times
+        return float(np.median(times)), out   # the median run: a typical crawl, not the best one
 
     reps = max(1, args.steps)
     warm = max(0, args.warmup)
@@ -376,11 +379,14 @@ def dropin_bench(args, world, rank, local_rank, dist):
                                "base OTs", "parallelism": "single GPU"},
     }
     c0, c1 = pair()
-    t_fused, res = timed(lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False),
-                         reps, warm)
+    fused_fn = lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False)  # noqa: E731
+    t_fused, res = timed(fused_fn, reps, warm)
+    fused_runs = runs[id(fused_fn)]
     hh = len(res.final)
     del c0, c1
     print(f"dropin: fused protocol crawl {t_fused:.2f} s, {hh} heavy hitters", file=sys.stderr, flush=True)
+
+    leg_runs = {}
 
     def dropin_leg(devices=None, channel="inplace"):
         p0, p1 = pair(devices)
@@ -394,6 +400,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
             last["r"] = r
             return r
         t, r = timed(run, reps, warm)
+        leg_runs[(tuple(devices) if devices else None, channel)] = runs[id(run)]
         assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
         tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
         tot["base_ot"] = r.base_ot_bytes
@@ -405,24 +412,29 @@ def dropin_bench(args, world, rank, local_rank, dist):
     out.update({
         "value": t_d, "ms_per_step": t_d * 1e3,
         "fused_protocol_crawl_s": t_fused, "dropin_crawl_s": t_d, "dropin_over_fused": t_d / t_fused,
+        "timing_stat": "median of the timed runs per leg (every run listed in *_runs_s)",
+        "fused_runs_s": fused_runs, "dropin_runs_s": leg_runs[(None, "inplace")],
         "dropin_ms_per_level": per_d,
         "dropin_overhead_ms_per_level": (t_d - t_fused) / L * 1e3,
         "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",
         "channel_bytes_per_crawl": bytes_d, "channel_bytes_total": sum(bytes_d.values()),
         "heavy_hitters": hh,
-        "dropin_material": "each server its own (os.urandom: label key, Delta, mask per chunk); every level's two OT "
-                           "extensions on Chou-Orlandi base OTs between the servers over the channel",
+        "dropin_material": "each server its own (os.urandom: Delta and mask per chunk, CO15 seeds and s); every "
+                           "level's two correlated-OT extensions on Chou-Orlandi base OTs between the servers over "
+                           "the channel (2 CO15 runs per level)",
         "dropin_base_ot_runs": r_d.base_ot_runs, "dropin_base_ot_wait_s": r_d.base_ot_wait_s,
     })
     if not args.no_party:
         t_2, per_2, _, _ = dropin_leg(devices=[local_rank, local_rank])
         out.update({"dropin_2shard_crawl_s": t_2, "dropin_2shard_over_fused": t_2 / t_fused,
+                    "dropin_2shard_runs_s": leg_runs[((local_rank, local_rank), "inplace")],
                     "dropin_2shard_ms_per_level": per_2,
                     "dropin_2shard_note": "fhh_create_multi over [this GPU, this GPU]: host reduction of the shards' "
                                           "device-resident sums, one protocol instance per shard"})
     if args.dropin_copy:
         t_c, per_c, _, _ = dropin_leg(channel="copy")
         out.update({"dropin_copy_crawl_s": t_c, "dropin_copy_over_fused": t_c / t_fused,
+                    "dropin_copy_runs_s": leg_runs[(None, "copy")],
                     "dropin_copy_ms_per_level": per_c})
     if args.dropin_host_values:
         c0, c1 = pair()

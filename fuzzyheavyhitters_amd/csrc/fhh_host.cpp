@@ -949,8 +949,8 @@ size_t table_entry_bytes(const fhh_ctx* c) { return 2 * c->npad * 16 + 2 * 2 * c
 // loop_cap_hint all follow from it, and their free memory differs. So each rank's "does candidate k
 // fit here" flags are summed over the ranks through the loop's own reduction and the first candidate
 // that fits on every rank is taken. FHH_TEST_TABLE_BYTES="a0,a1,..." replaces the available bytes of
-// comm rank r by a_r (the last entry for higher ranks; entry 0 without a communicator): tests force
-// different free memory per rank with it.
+// rank r by a_r (the last entry for higher ranks): r = the communicator's rank, or FHH_TEST_RANK on the
+// cfg->allreduce callback path (0 if unset): tests force different free memory per rank with it.
 int loop_entry_cap(fhh_ctx* const (&cs)[2], const fhh_sim_config* cfg, LoopBuffers& B, uint32_t d, uint32_t E_cap,
                    uint32_t need, uint32_t la, uint32_t& out) {
     size_t free_b = 0, total_b = 0;
@@ -969,7 +969,8 @@ int loop_entry_cap(fhh_ctx* const (&cs)[2], const fhh_sim_config* cfg, LoopBuffe
     const size_t margin = (size_t)2 << 30;
     size_t avail = free_b + held > margin ? free_b + held - margin : 0;
     if (const char* e = std::getenv("FHH_TEST_TABLE_BYTES")) {
-        const int r = cfg->comm ? comm_rank(cfg->comm) : 0;
+        const char* tr = std::getenv("FHH_TEST_RANK");
+        const int r = cfg->comm ? comm_rank(cfg->comm) : (tr ? std::atoi(tr) : 0);
         std::string s(e);
         size_t pos = 0;
         for (int k = 0;; k++) {

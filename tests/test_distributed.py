@@ -130,9 +130,14 @@ def test_sharded_crawl_equals_single_process(oracle, mode):
 
 
 def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_capacity=0, gc=False,
-                hosted_comm=False):
+                hosted_comm=False, tight_rank1=False):
     import sys
     sys.path.insert(0, ROOT)
+    if tight_rank1:
+        # rank 0 sees ample memory, rank 1 none: the growth choice must be agreed over the callback
+        # all-reduce (loop_entry_cap), or the ranks' collectives would stop pairing up
+        os.environ["FHH_TEST_TABLE_BYTES"] = f"{1 << 40},0"
+        os.environ["FHH_TEST_RANK"] = str(rank)
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -166,22 +171,26 @@ def _gpu_worker(rank, world, port, wl_args, thr, mode, q, host_loop=False, init_
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,loop", [("count", "device_grow"), ("count", "host"), ("fe", "device_grow"),
                                        ("fe", "host"), ("fe", "device_gc_ot"), ("count", "comm_grow"),
-                                       ("fe", "comm_grow"), ("fe", "comm_host")])
+                                       ("fe", "comm_grow"), ("fe", "comm_host"), ("count", "device_grow_tight"),
+                                       ("fe", "comm_grow_tight")])
 def test_gpu_two_ranks_allreduce_hook(oracle, mode, loop):
     """Two ranks share one GPU over the host all-reduce hook. device_grow starts the device
     loop at capacity 2 so it aborts and resumes several times: the cross-rank sum of an
     aborted level must not be applied twice (out-of-place reduction). comm_* drive the level
     loop's native-communicator path (cfg.comm, the path bench.py takes at N > 1) with a hosted
     communicator (fhh_comm_create_hosted: the sum over gloo instead of RCCL, which cannot put two
-    ranks on one GPU)."""
+    ranks on one GPU). *_tight: rank 1 has no memory for table growth (FHH_TEST_TABLE_BYTES /
+    FHH_TEST_RANK), so the growth capacity must be agreed over the reduction — the callback hook's
+    (device_grow_tight) as well as the communicator's (comm_grow_tight)."""
     from fuzzyheavyhitters_amd import workload
     wl_args = {"n": 256, "L": 48, "d": 1, "sites": 6, "seed": 77}
     thr = 0.02
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    kw = {"host_loop": loop in ("host", "comm_host"), "init_capacity": 2 if loop.endswith("grow") else 0,
-          "gc": "ot" if loop == "device_gc_ot" else False, "hosted_comm": loop.startswith("comm")}
+    kw = {"host_loop": loop in ("host", "comm_host"), "init_capacity": 2 if "grow" in loop else 0,
+          "gc": "ot" if loop == "device_gc_ot" else False, "hosted_comm": loop.startswith("comm"),
+          "tight_rank1": loop.endswith("_tight")}
     procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, wl_args, thr, mode, q), kwargs=kw) for r in range(2)]
     for p in procs:
         p.start()

@@ -661,7 +661,9 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
         "base_ot_stall_ms": s0["base_ot_stall_ms"],
         "base_ot_note": "compute = summed per-instance CO15 + key-schedule time over the host threads; stall = time "
                         "the level loop waited for an instance it needed (the base OTs on the critical path)",
-        "protocol": "GC (half-gates, TCCR) + ALSZ correlated OT for the evaluator's labels and the FE share",
+        "protocol": "GC (half-gates, TCCR; the garbler's string and mask folded in) + the evaluator's labels as "
+                    "the IKNP correlation (Delta = the labels OT's s, no reply) + the FE share by ALSZ correlated OT "
+                    "(24 AES blocks per d=1 test)",
         "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
         "expand_gpu_ms": s0["expand_ms"],
         "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,

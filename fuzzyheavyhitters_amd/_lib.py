@@ -192,7 +192,6 @@ class FhhOtBatch(ctypes.Structure):
 class FhhGbCfg(ctypes.Structure):
     """fhh_gb_cfg: the garbler's (server 0's) own material for one chunk (include/fhh.h)."""
     _fields_ = [
-        ("delta", ctypes.c_uint8 * 16),
         ("mask", ctypes.c_uint32),
         ("pad_", ctypes.c_uint32),
         ("base_chosen", ctypes.c_uint8 * (2 * 128 * 16)),
@@ -212,7 +211,7 @@ class FhhEvCfg(ctypes.Structure):
 
 
 # fhh_cot_extend_host modes (include/fhh.h)
-FHH_COT_LABELS, FHH_COT_FE, FHH_COT_FE255 = 1, 2, 3
+FHH_COT_LABELS, FHH_COT_FE, FHH_COT_FE255, FHH_COT_RAW = 1, 2, 3, 4
 
 
 def build(verbose: bool = False) -> str:
@@ -287,7 +286,7 @@ def lib():
         "fhh_party_bytes_sent": (i, [vp, u64p]),
         "fhh_gc_party_test_cfgs": (i, [u64, u32, P(FhhGbCfg), P(FhhEvCfg)]),
         "fhh_cot_extend_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
-        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p]),
+        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p]),
         "fhh_memcpy_device": (i, [i, vp, vp, u64]),
         "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),

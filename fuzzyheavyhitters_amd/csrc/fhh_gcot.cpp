@@ -117,6 +117,7 @@ void ot_level_choice(uint64_t prf, uint32_t level, uint32_t salt, uint32_t s[4])
     s[1] = (uint32_t)(z0 >> 32);
     s[2] = (uint32_t)z1;
     s[3] = (uint32_t)(z1 >> 32);
+    if (salt == 0) s[0] |= 1u;   // the labels session's s is the circuit's free-XOR Delta: colour bit 1
 }
 
 // padded choice-bit buffer of the ctx's OT scratch (mp / 32 words, zero past m)
@@ -152,27 +153,33 @@ int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t 
 // `a` (mode, choices from ot_choices_buffer or a padded buffer of its own, x0 / x1 / delta, mask, sx,
 // out, rk, s, ctr_off, ctl / per_group / g_off); ot_run sets the sizes and the scratch matrices and
 // messages, then launches receiver expand -> sender expand -> send hash (-> the FieldElm finish) ->
-// receive hash. Mode 0 keeps Y0 | Y1 in ot_buf[5 / 6]; the C-OT modes one y buffer in ot_buf[5].
+// receive hash (mode 4: the two row transposes instead). Mode 0 keeps Y0 | Y1 in ot_buf[5 / 6]; modes
+// 1-3 one y buffer in ot_buf[5]; mode 4 has no y.
 int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
     if (m == 0) return FHH_OK;
     if (a.ctr_off % 256) return ctx->fail(FHH_E_ARG, "ot: the row PRG offset must be a multiple of 256 blocks");
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
     for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
-    HIP_TRY(ctx, ctx->ot_buf[5].ensure(m * 16));
+    if (a.mode != 4) HIP_TRY(ctx, ctx->ot_buf[5].ensure(m * 16));
     if (a.mode == 0) HIP_TRY(ctx, ctx->ot_buf[6].ensure(m * 16));
     a.m = m;
     a.mp = mp;
     a.T = ctx->ot_buf[0].as<uint4>();
     a.U = ctx->ot_buf[1].as<uint4>();
     a.Q = ctx->ot_buf[2].as<uint4>();
-    a.Y0 = ctx->ot_buf[5].as<uint4>();
+    a.Y0 = a.mode != 4 ? ctx->ot_buf[5].as<uint4>() : nullptr;
     a.Y1 = a.mode == 0 ? ctx->ot_buf[6].as<uint4>() : nullptr;
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
-    HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: y (Y0 | Y1)
-    if (a.mode == 3) HIP_TRY(ctx, launch_cot_fe255_finish(a, ctx->stream));
-    HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
+    if (a.mode == 4) {   // the correlation itself: q_j, t_j (no hash, no y)
+        HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));
+        HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));
+    } else {
+        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));  // sender -> receiver: y (Y0 | Y1)
+        if (a.mode == 3) HIP_TRY(ctx, launch_cot_fe255_finish(a, ctx->stream));
+        HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
+    }
     if (tr) {
         tr->U = a.U;
         tr->Y0 = a.Y0;
@@ -361,7 +368,7 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
-    if (mode < FHH_COT_LABELS || mode > FHH_COT_FE255) return ctx->fail(FHH_E_ARG, "cot_extend: mode must be 1, 2 or 3");
+    if (mode < FHH_COT_LABELS || mode > FHH_COT_RAW) return ctx->fail(FHH_E_ARG, "cot_extend: mode must be 1..4");
     if (m == 0) return FHH_OK;
     if (!choices || !out || !base_seeds || !base_choice || (mode == FHH_COT_LABELS && !delta))
         return ctx->fail(FHH_E_ARG, "cot_extend: NULL argument");
@@ -401,7 +408,7 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(out, dout.p, m * per, hipMemcpyDeviceToHost));
     if (sender_out) HIP_TRY(ctx, hipMemcpy(sender_out, dsx.p, m * per, hipMemcpyDeviceToHost));
-    if (y_out) HIP_TRY(ctx, hipMemcpy(y_out, tr.Y0, m * per, hipMemcpyDeviceToHost));
+    if (y_out && mode != FHH_COT_RAW) HIP_TRY(ctx, hipMemcpy(y_out, tr.Y0, m * per, hipMemcpyDeviceToHost));
     if (u_out) {
         const uint64_t nb = (m + 127) / 128;
         HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
@@ -410,7 +417,7 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
 }
 
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                    uint32_t mask, const uint8_t delta[16], uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
                     uint8_t* ev_active, uint8_t* decode, uint8_t* out) {
     CTX_CHECK(ctx);
@@ -418,8 +425,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     if (rc) return rc;
     if (bits < 1 || bits > (uint32_t)kGcMaxBits) return ctx->fail(FHH_E_ARG, "gc_cot: bits must be in [1, 8]");
     if (n == 0) return FHH_OK;
-    if (!gb_bits || !ev_bits || !delta || !base_seeds || !base_choice || !out)
-        return ctx->fail(FHH_E_ARG, "gc_cot: NULL argument");
+    if (!gb_bits || !ev_bits || !base_seeds || !base_choice || !out) return ctx->fail(FHH_E_ARG, "gc_cot: NULL argument");
+    if (!(base_choice[0] & 1)) return ctx->fail(FHH_E_ARG, "gc_cot: s is the free-XOR Delta: its bit 0 must be 1");
     if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc_cot: n must fit 32 bits");
     const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad;
     std::vector<uint64_t> planes[2];
@@ -441,7 +448,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     HIP_TRY(ctx, da.ensure(m * 16));
     HIP_TRY(ctx, dd.ensure(n));
     HIP_TRY(ctx, dout.ensure(n));
-    // 1. the labels C-OT (OtArgs mode 1): choice bits = the evaluator's planes at OT index j npad + i
+    // 1. the labels OT (OtArgs mode 4): choice bits = the evaluator's planes at OT index j npad + i;
+    // the garbler's zero labels q_j, the evaluator's active labels t_j = q_j ^ r_j s
     const uint32_t* rk = nullptr;
     rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
     if (rc) return rc;
@@ -451,7 +459,7 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     gb.words = (uint32_t)nw;
     gb.bits = bits;
     gb.mask = mask;
-    std::memcpy(gb.delta, delta, 16);   // no label key: the garbler draws no labels
+    std::memcpy(gb.delta, base_choice, 16);   // Delta = s; no label key: the garbler draws no labels
     gb.gate_base = gate_base;
     gb.gb_planes_dev = dp[0].as<uint64_t>();
     gb.ev_planes_dev = dp[1].as<uint64_t>();
@@ -464,11 +472,10 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     rc = gc_args(ctx, &gb, g);
     if (rc) return rc;
     OtArgs a{};
-    a.mode = 1;
+    a.mode = 4;
     a.rk = rk;
     words_from_bytes(base_choice, a.s);
     a.choices = dp[1].as<uint32_t>();
-    for (int c = 0; c < 4; c++) a.delta[c] = g.delta[c];   // the colour-forced Delta
     a.ctr_off = ctr_off;
     a.sx = de.p;
     a.out = da.as<uint4>();
@@ -506,9 +513,11 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
 // server 0 and false on server 1; equalitytest.rs:25-106). Each server's ctx runs only its own half
 // and holds only its own secrets: the garbler's fhh_gb_cfg (label key, Delta, mask, its base-OT
 // outputs) never reaches the evaluator's ctx, the evaluator's fhh_ev_cfg (its base-OT key pairs)
-// never the garbler's. Five buffers cross per chunk, in protocol order (r05: both OTs correlated):
-//   E -> G  u1      labels C-OT: U (the evaluator's share planes are its choice bits)
-//   G -> E  y1      labels C-OT: y = H(q) ^ Delta ^ H(q ^ s), 16 B per OT
+// never the garbler's. Four buffers cross per chunk, in protocol order (r05: both OTs correlated; y1
+// is empty since r05b):
+//   E -> G  u1      labels OT: U (the evaluator's share planes are its choice bits); the IKNP
+//                   correlation itself is the label pair: zero label q_j, active label t_j = q_j ^ r_j s,
+//                   with the garbler's labels-kind s as the circuit's Delta — no reply
 //   G -> E  gc      the garbled tables and decoding bits (the garbler's string and mask are folded
 //                   into the circuit, k_gc_garble_cot: no garbler labels cross)
 //   E -> G  u2      share C-OT (collect.rs:437-471 / 846-876): U
@@ -663,11 +672,11 @@ OtArgs party_ot(PartyState& P, int w, uint64_t m) {
     return a;
 }
 
-int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver) {
+int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver, bool reply = true) {
     const uint64_t rows = 16 * ot_padded(m);   // [128][mp / 128] blocks
     HIP_TRY(ctx, (receiver ? P.T : P.Q).ensure(rows));
     if (receiver) HIP_TRY(ctx, P.U.ensure(rows));
-    else HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 16));
+    else if (reply) HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 16));
     return FHH_OK;
 }
 
@@ -693,8 +702,9 @@ void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
     g.decode = base + (uint64_t)2 * (P.bits - 1) * t * 16;
 }
 
-// the chunk's gate tweaks: the test's index in the whole level (c_off n + t)
-uint64_t party_gate_base(const PartyState& P) { return P.c_off * P.n * (P.bits - 1); }
+// the chunk's gate tweaks: the level in bits 40+ (Delta = the labels session's s may serve several levels
+// when base OTs are reused), then the test's index in the whole level (c_off n + t)
+uint64_t party_gate_base(const PartyState& P) { return ((uint64_t)P.level_id << 40) + P.c_off * P.n * (P.bits - 1); }
 
 }  // namespace
 }  // namespace eng
@@ -716,10 +726,14 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
     if (rc) return rc;
     rc = party_ot_buffers(ctx, P, P.m1, true);
     if (rc) return rc;
+    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
     if (P.m1) {   // OT 1's receiver: choice bits = this server's share planes as they stand
         OtArgs a = party_ot(P, 0, P.m1);
+        a.mode = 4;
         a.choices = P.planes.as<uint32_t>();
-        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));   // T, U
+        a.out = P.labels.as<uint4>();
+        HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));        // T, U
+        HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));    // its active labels t_j
     }
     rc = ctx_sync(ctx);
     if (rc) return rc;
@@ -740,6 +754,8 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     rc = check_in(ctx, u_dev, u_len, P.m1 ? u_bytes(P.m1) : 0, "U (labels OT)");
     if (rc) return rc;
     P.mask = cfg->mask & 1u;
+    if (!(cfg->base_choice[0][0] & 1))
+        return ctx->fail(FHH_E_ARG, "gb_ot_labels: the labels base OTs' s is the free-XOR Delta: its bit 0 must be 1");
     // both OT kinds' sender schedules and session counters (OtSender::init, collect.rs:454)
     for (int w = 0; w < 2; w++) {
         std::vector<uint8_t> mat((size_t)128 * 16 + 16);
@@ -760,7 +776,7 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     gb.words = (uint32_t)P.nw;
     gb.bits = P.bits;
     gb.mask = P.mask;
-    std::memcpy(gb.delta, cfg->delta, 16);
+    std::memcpy(gb.delta, cfg->base_choice[0], 16);   // Delta = the labels session's s
     gb.gate_base = party_gate_base(P);
     gb.gb_planes_dev = P.planes.as<uint64_t>();
     gb.ev_planes_dev = P.planes.as<uint64_t>();   // not read: the evaluator's labels go by OT
@@ -774,27 +790,24 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     gc_layout(P, P.gc.as<uint8_t>(), P.g);
     P.g.ev_ot = 1;
     P.g.out = nullptr;
-    // OT 1 as a correlated OT (gb_set_fancy_inputs, equalitytest.rs:67-82): x0 = H(q_j) becomes the
-    // evaluator's zero label of its share bit j, x1 = x0 ^ Delta; y = x0 ^ Delta ^ H(q_j ^ s)
-    rc = party_ot_buffers(ctx, P, P.m1, false);
+    // OT 1 as the IKNP correlation (gb_set_fancy_inputs, equalitytest.rs:67-82): q_j is the evaluator's
+    // zero label of its share bit j, q_j ^ s its one label, and s = Delta: nothing to send back
+    rc = party_ot_buffers(ctx, P, P.m1, false, false);
     if (rc) return rc;
     if (P.m1) {
         OtArgs a = party_ot(P, 0, P.m1);
-        a.mode = 1;
+        a.mode = 4;
         a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
         for (int c = 0; c < 4; c++) a.s[c] = P.s[0][c];
-        for (int c = 0; c < 4; c++) a.delta[c] = P.g.delta[c];
         a.sx = P.labels.p;
-        a.Y0 = P.Y.as<uint4>();
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
-        HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));   // zero labels, y
+        HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));   // the zero labels q_j
     }
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 1;
-    *y_dev = P.Y.as<uint8_t>();
-    *y_len = P.m1 * 16;
-    P.bytes_sent += *y_len;
+    *y_dev = nullptr;
+    *y_len = 0;   // the labels OT has no reply
     return FHH_OK;
 }
 
@@ -827,18 +840,10 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     PartyState& P = *Pp;
     rc = check_in(ctx, gc_msg_dev, gc_len, gc_bytes(P), "gc message");
     if (rc) return rc;
-    rc = check_in(ctx, y_dev, y_len, P.m1 * 16, "y (labels OT)");
+    rc = check_in(ctx, y_dev, y_len, 0, "y (labels OT: empty since r05b)");
     if (rc) return rc;
-    // 1. OT 1 output: the evaluator's active input labels (ev_set_fancy_inputs, equalitytest.rs:108-119)
-    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
-    if (P.m1) {
-        OtArgs a = party_ot(P, 0, P.m1);
-        a.mode = 1;
-        a.choices = P.planes.as<uint32_t>();
-        a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
-        a.out = P.labels.as<uint4>();
-        HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
-    }
+    // 1. OT 1's output, the evaluator's active input labels t_j (ev_set_fancy_inputs,
+    // equalitytest.rs:108-119), is in P.labels since fhh_ev_ot_labels
     // 2. evaluate (multiple_ev_equality_test); the outputs are packed as OT 2's choice words
     const uint64_t mp2 = ot_padded(std::max<uint64_t>(P.m2, 1));
     HIP_TRY(ctx, P.choices2.ensure(mp2 / 8 + 64));
@@ -992,8 +997,8 @@ int fhh_gc_party_test_cfgs(uint64_t prf_seed, uint32_t level, fhh_gb_cfg* gb, fh
     }
     std::memset(gb, 0, sizeof(*gb));
     std::memset(ev, 0, sizeof(*ev));
-    uint8_t label_key[16];   // the ideal-OT loop's label key; the r05 garbler draws no labels
-    gc_level_material(prf_seed, level, label_key, gb->delta, &gb->mask);
+    uint8_t label_key[16], delta[16];   // the ideal-OT loop's; the r05 garbler draws no labels, Delta = s
+    gc_level_material(prf_seed, level, label_key, delta, &gb->mask);
     for (uint32_t salt = 0; salt < 2; salt++) {
         uint32_t sw[4];
         ot_level_choice(prf_seed, level, salt, sw);

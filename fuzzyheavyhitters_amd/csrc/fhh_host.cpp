@@ -1306,6 +1306,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     gb.words = (uint32_t)c0->nw;
                     gb.bits = bits;
                     gc_chunk_material(cfg->prf_seed, lv, k, gb.label_key, gb.delta, &gb.mask);
+                    gb.gate_base = (uint64_t)lv << 40;   // the level in the gate tweaks (party_gate_base)
                     gb.gb_planes_dev = B.gc_planes[0].as<uint64_t>();
                     gb.ev_planes_dev = B.gc_planes[1].as<uint64_t>();
                     gb.tables_dev = B.gc_tables.as<uint8_t>();
@@ -1322,16 +1323,18 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         // 1. the evaluator's input labels by correlated OT (gb_set_fancy_inputs /
                         // ev_set_fancy_inputs, equalitytest.rs:67-82,108-119): server 1's choice bits are
                         // its share planes [C][bits][nw] from the chunk's first group on, as they stand
-                        // (m1 a multiple of 128: npad of 64, bits even); server 0's sender messages
-                        // x0 = H(q_j) are the zero labels it garbles with, x1 = x0 ^ Delta; its own string
-                        // and mask fold into the circuit (k_gc_garble_cot: no label is drawn)
+                        // (m1 a multiple of 128: npad of 64, bits even). The IKNP correlation is the label
+                        // pair (r05b, OtArgs mode 4): server 0's q_j is the zero label, server 1's t_j =
+                        // q_j ^ r_j s the active one, with the labels session's s (colour bit set) as the
+                        // circuit's Delta; server 0's string and mask fold into the circuit
+                        // (k_gc_garble_cot: no label is drawn, no reply is sent)
                         HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
+                        for (int c = 0; c < 4; c++) g.delta[c] = sw_ot[0][c];
                         OtArgs a1{};
-                        a1.mode = 1;
+                        a1.mode = 4;
                         a1.rk = rk_ot[0];
                         for (int c = 0; c < 4; c++) a1.s[c] = sw_ot[0][c];
                         a1.choices = B.gc_planes[1].as<uint32_t>() + g_off * bits * c0->nw * 2;
-                        for (int c = 0; c < 4; c++) a1.delta[c] = g.delta[c];
                         a1.ctr_off = k * ot_session_blocks(m1);
                         a1.sx = B.gc_evl.p;
                         a1.out = B.gc_evact.as<uint4>();

@@ -342,6 +342,9 @@ hipError_t launch_prune(const PruneArgs& a, hipStream_t stream);
 //      H(t_j)) : H(t_j) mod p
 //   3  correlated OT, FieldElm share, raw pass: sx[j] = H(q_j), Y0[j] = H(q_j ^ s); k_cot_fe255_finish
 //      turns OT pairs (2t, 2t + 1) into the sender's node values and y; out = r_j ? Y0[j] ^ H(t_j) : H(t_j)
+//   4  (r05b) the IKNP correlation itself, the labels OT: no hash, no y — sx[j] = q_j, out[j] = t_j =
+//      q_j ^ r_j s (k_ot_rows_out transposes Q / T); with s as the free-XOR Delta, q_j is the zero label
+//      of the evaluator's input wire j and t_j its active label
 struct OtArgs {
     uint64_t m;                  // OTs (capacity)
     uint64_t mp;                 // m padded to a multiple of 8192 (whole waves per row)
@@ -356,11 +359,11 @@ struct OtArgs {
     const LoopCtl* ctl;
     uint64_t per_group;
     uint64_t g_off;              // level loop chunk: OTs of groups [g_off, ctl->C) only
-    uint32_t mode;               // 0..3 above
+    uint32_t mode;               // 0..4 above
     uint32_t mask;               // modes 2, 3: the garbler's mask bit
     uint64_t ctr_off;            // the row PRG's first block (a multiple of 256): a base-OT session's
                                  // running counter, so batches extending one session never repeat pads
-    void* sx;                    // modes 1, 3: uint4 [m]; mode 2: u64 [m] (the sender's node values)
+    void* sx;                    // modes 1, 3, 4: uint4 [m]; mode 2: u64 [m] (the sender's node values)
 };
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
@@ -378,6 +381,8 @@ hipError_t launch_ot_level_keys(uint64_t prf, uint32_t level, uint32_t salt, con
 // big-endian bytes, sx) mod p255 -> sx pair = V + mask (its node value, a canonical BlockPair), Y0 pair
 // ^= (mask ? V + 1 : V - 1); tests = the active OT pairs (ctl-aware as the hashes)
 hipError_t launch_cot_fe255_finish(const OtArgs& a, hipStream_t stream);
+// mode 4: the tile-major Q (sender: -> sx) or T (receiver: -> out) as one 16-B row per OT
+hipError_t launch_ot_rows_out(const OtArgs& a, bool sender, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,

@@ -435,6 +435,37 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
     }
 }
 
+// Mode 4 (r05b): the labels OT as the IKNP correlation itself. With the sender's s as the free-XOR
+// offset, q_j (sender) and t_j = q_j ^ r_j s (receiver) already are the zero label and the active label
+// of the evaluator's input wire j — the random correlated OT that free-XOR garbling consumes — so no
+// hash and no message y is needed: this kernel only transposes the tile-major matrix into one 16-B row
+// per OT (the hashes' load + in-register transpose + LDS exchange, without their T-tables: 8 KiB of
+// stage per 256-thread workgroup).
+constexpr int kOtOutThreads = 256;
+__global__ __launch_bounds__(kOtOutThreads) void k_ot_rows_out(OtArgs a, int sender) {
+    __shared__ uint32_t stage[kOtOutThreads / 64][512];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t m = ot_active(a);
+    const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtOutThreads / 64);
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(sender ? a.Q : a.T);
+    uint4* out = sender ? static_cast<uint4*>(a.sx) : a.out;
+    for (uint64_t t = (uint64_t)blockIdx.x * (kOtOutThreads / 64) + wv; t < tiles; t += nwaves) {
+        uint32_t x[32];
+        ot_tile_load(rows, t, lane, x);
+#pragma unroll 1
+        for (int r = 0; r < 4; r++) {
+            uint4 v[2];
+            ot_tile_round(stage[wv], x, lane, v);
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint64_t j = ot_tile_ot(t, lane, r, u);
+                if (j < m) out[j] = v[u];
+            }
+        }
+    }
+}
+
 // mode 3's second pass (the garbler's FieldElm share, collect.rs:846-876): test t = OT pair (2t, 2t + 1).
 // V = H(q_2t) || H(q_2t+1) read as 32 big-endian bytes (the BlockPair convention, field.rs:466-492),
 // reduced mod p255; the garbler's node value r1 = V + mask replaces the H(q) pair in sx (canonical
@@ -633,6 +664,15 @@ hipError_t launch_ot_recv_hash_rows(const OtArgs& a, hipStream_t stream) {
         case 3: hipLaunchKernelGGL(k_ot_recv_hash_rows<3>, g, b, 0, stream, a); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_ot_rows_out(const OtArgs& a, bool sender, hipStream_t stream) {
+    if (a.mp % 8192 != 0) return hipErrorInvalidValue;   // tiles of 16 words stay inside a row
+    const uint64_t tiles = (a.m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
+    const uint64_t wpb = kOtOutThreads / 64, need = (tiles + wpb - 1) / wpb, cap = (uint64_t)device_cus() * 8;
+    hipLaunchKernelGGL(k_ot_rows_out, dim3((int)(need < cap ? (need ? need : 1) : cap)), dim3(kOtOutThreads), 0, stream,
+                       a, sender ? 1 : 0);
     return hipGetLastError();
 }
 

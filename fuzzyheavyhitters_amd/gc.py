@@ -132,23 +132,24 @@ def planes_from_bits(bits_gn: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(packed).view(np.uint64).reshape(G, bits, nw)
 
 
-def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, delta, base_seeds, base_choice, gate_base: int = 0,
+def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate_base: int = 0,
                       ctr_off: int = 0):
-    """The r05 labels step on the GPU (fhh_gc_cot_host): the evaluator's input labels by correlated OT
-    (its bits are the choice bits), garbling with the garbler's string and mask folded into the circuit,
-    evaluation. Returns (out [n], dict of the transcript: tables, ev_zero, ev_active, decode)."""
+    """The labels step on the GPU (fhh_gc_cot_host): the evaluator's input labels by the labels OT (its
+    bits are the choice bits; since r05b the IKNP correlation itself: zero label q_j, active label t_j,
+    Delta = base_choice, whose bit 0 must be 1), garbling with the garbler's string and mask folded into
+    the circuit, evaluation. Returns (out [n], dict of the transcript: tables, ev_zero, ev_active,
+    decode)."""
     g = np.ascontiguousarray(np.asarray(gb_inputs).astype(np.uint8) & 1)
     e = np.ascontiguousarray(np.asarray(ev_inputs).astype(np.uint8) & 1)
     if g.ndim != 2 or g.shape != e.shape:
         raise ValueError("equality_test_cot: inputs must both be [n][bits]")
     n, bits = g.shape
-    dl = np.frombuffer(_block(delta), np.uint8).copy()
     seeds = np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16)
     s = np.frombuffer(bytes(base_choice), np.uint8).copy()
     tr = {"tables": np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8), "ev_zero": np.zeros((n, bits, 16), np.uint8),
           "ev_active": np.zeros((n, bits, 16), np.uint8), "decode": np.zeros(n, np.uint8)}
     out = np.zeros(n, np.uint8)
-    check(lib().fhh_gc_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, ptr(dl), gate_base, ptr(seeds),
+    check(lib().fhh_gc_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, gate_base, ptr(seeds),
                                 ptr(s), ctr_off, ptr(tr["tables"]), ptr(tr["ev_zero"]), ptr(tr["ev_active"]),
                                 ptr(tr["decode"]), ptr(out)), kc.handle)
     return out, tr

@@ -55,7 +55,8 @@ def cot_extend(kc, mode: int, choices, base_seeds, base_choice, delta=None, mask
     include/fhh.h FHH_COT_*): returns (sender_out, out) and, with transcript, (U, y).
     mode 1 (labels): sender_out = x0 [m][16] (x1 = x0 ^ delta), out [m][16]; mode 2 (FE share):
     sender values / out [m] u64 (the garbler's r1 = v + mask, the receiver's share); mode 3 (FieldElm,
-    OT pairs with one choice): sender values / out [m/2][32] BlockPairs."""
+    OT pairs with one choice): sender values / out [m/2][32] BlockPairs; mode 4 (FHH_COT_RAW, the labels
+    OT since r05b): sender_out = q [m][16], out = t [m][16] = q ^ r s, no y (zeros)."""
     from ._lib import FHH_COT_FE, FHH_COT_FE255
     ch = np.ascontiguousarray(np.asarray(choices).astype(np.uint8) & 1)
     m = ch.size

@@ -6,12 +6,12 @@ Each server holds only its own secrets and draws them itself, as the reference's
 (`AesRng::new()` per channel, collect.rs:431; `OtSender::init` / `OtReceiver::init` per channel and
 level, collect.rs:454,460):
 
-  * the garbler (server 0): its Delta and mask per chunk (os.urandom), and the base-OT
-    receiver's side of each level's Chou–Orlandi runs (its choice bits s, its seed);
+  * the garbler (server 0): its mask per chunk (os.urandom), and the base-OT receiver's side of each
+    level's Chou–Orlandi runs (its choice bits s, its seed; the labels run's s is its free-XOR Delta);
   * the evaluator (server 1): the base-OT sender's side (its seed, hence both keys of every base OT).
 
 Only protocol messages cross between them: the CO15 messages A and B of each base-OT run, then per
-chunk u1, y1, gc, u2, y2. In a deployment they go over the servers' channel; here `Channel` copies
+chunk u1, y1 (empty since r05b: the labels OT needs no reply), gc, u2, y2. In a deployment they go over the servers' channel; here `Channel` copies
 each one into a buffer the receiving party owns (`fhh_memcpy_device`, or a bytes copy for the host
 messages) and counts the bytes. `GarblerParty` and `EvaluatorParty` keep the two sides' state apart;
 nothing of one is handed to the other except through a Channel.
@@ -99,9 +99,12 @@ class GarblerParty:
     def __init__(self, kc: KeyCollection):
         self.kc = kc
 
-    # -- base OTs: the CO15 receiver with choice bits s (OtSender::init's base OTs, collect.rs:454)
-    def co15_receive(self, A: bytes):
+    # -- base OTs: the CO15 receiver with choice bits s (OtSender::init's base OTs, collect.rs:454).
+    # The labels kind's s is the circuit's free-XOR Delta (its bit 0, the colour bit, is 1)
+    def co15_receive(self, A: bytes, colour: bool = False):
         s = _rand(16)
+        if colour:
+            s[0] |= 1
         seed = _rand(32)
         Av = np.frombuffer(A, np.uint8).copy()
         B = np.zeros((128, 65), np.uint8)
@@ -112,11 +115,10 @@ class GarblerParty:
         return B.tobytes(), (chosen, s)
 
     def chunk_cfg(self, base, child_begin: int, child_count: int) -> FhhGbCfg:
-        """The garbler's material for one chunk: a fresh Delta and mask (AesRng::new() per channel,
-        collect.rs:431; its string is folded into the circuit, so it draws no labels), and the level's
-        base OTs (both kinds)."""
+        """The garbler's material for one chunk: a fresh mask (AesRng::new() per channel, collect.rs:431;
+        its string is folded into the circuit, so it draws no labels) and the level's base OTs (both
+        kinds; the labels kind's s is the circuit's Delta)."""
         cfg = FhhGbCfg()
-        cfg.delta[:] = list(os.urandom(16))
         cfg.mask = os.urandom(1)[0] & 1
         chosen = np.stack([b[0] for b in base])      # [2][128][16]
         choice = np.stack([b[1] for b in base])      # [2][16]
@@ -155,12 +157,13 @@ class EvaluatorParty:
         return cfg
 
 
-def base_ot_run(gb: GarblerParty, ev: EvaluatorParty, to_gb: Channel, to_ev: Channel):
+def base_ot_run(gb: GarblerParty, ev: EvaluatorParty, to_gb: Channel, to_ev: Channel, colour: bool = False):
     """One Chou–Orlandi run of 128 OTs between the parties (the OT extension's init,
-    collect.rs:454,460): A from the evaluator, B back from the garbler. Returns (the garbler's
-    (chosen, s), the evaluator's pairs) — each side's own result."""
+    collect.rs:454,460): A from the evaluator, B back from the garbler (colour: the labels kind, whose s
+    is the free-XOR Delta). Returns (the garbler's (chosen, s), the evaluator's pairs) — each side's
+    own result."""
     A, seed_e = ev.co15_start()
-    B, gb_side = gb.co15_receive(to_gb.send_host(A))
+    B, gb_side = gb.co15_receive(to_gb.send_host(A), colour=colour)
     ev_side = ev.co15_finish(seed_e, to_ev.send_host(B))
     return gb_side, ev_side
 
@@ -285,7 +288,7 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
         def runs(k):
             gbp, evp = parties[k]
             to_gb, to_ev = chans[k]
-            return [base_ot_run(gbp, evp, to_gb, to_ev) for _ in range(2)]   # kind 0 labels, kind 1 shares
+            return [base_ot_run(gbp, evp, to_gb, to_ev, colour=(w == 0)) for w in range(2)]   # kind 0 labels, 1 shares
 
         def submit(lv):
             key = 0 if base_ot_every == "crawl" else lv

@@ -512,26 +512,33 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
  *                   (field.rs:478-492); sender_out [m/2][32] = V + mask; y 16 B per OT; out [m/2][32]
  *                   = r ? y ^ H(t) : H(t), the raw BlockPair FieldElm::try_from reads unreduced
  *                   (field.rs:466-476)
+ *   FHH_COT_RAW     (r05b, the labels OT since) the IKNP correlation itself: sender_out [m][16] = q_j,
+ *                   out [m][16] = t_j = q_j ^ r_j s, no hash and no y (y_out unused). With the
+ *                   sender's s as the free-XOR Delta (bit 0 of byte 0 set), q_j is the zero label of
+ *                   the evaluator's input wire j and t_j its active label: the random correlated OT
+ *                   that free-XOR garbling consumes (delta, mask unused).
  * ctr_off: the row PRG's first block (a multiple of 256): batches that extend one set of base OTs
  * must use disjoint counter ranges (the party ABI below keeps a running counter per session).
  * Host buffers: choices [m] 0/1 bytes; u_out [128][ceil(m/128)][16]; y_out [m][8 or 16]. */
 #define FHH_COT_LABELS 1
 #define FHH_COT_FE 2
 #define FHH_COT_FE255 3
+#define FHH_COT_RAW 4
 int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
                         uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                         uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out);
-/* The r05 labels step of one batch on host buffers: the labels C-OT (choice bits = the evaluator's
- * bits at OT index j npad + i, npad = n rounded up to 64; its sender messages are the evaluator's zero
- * labels E_j), garbling with the garbler's string and mask FOLDED into the circuit — the garbler knows
- * x_j, so input z_j = NOT(x_j ^ y_j) takes the zero label E_j ^ (x_j ? 0 : Delta) and the evaluator's
- * OT'd label is z_j's active label; decode = colour(eq's zero label) ^ mask — and evaluation on the
- * OT'd labels (out = colour ^ decode = eq ^ mask). No label PRG, no garbler labels on the wire; gate
- * tweaks 2 g, 2 g + 1 with g = gate_base + t (bits - 1) + k as in fhh_gc_batch. Outputs AoS: tables
+/* The labels step of one batch on host buffers: the labels OT (FHH_COT_RAW since r05b: choice bits =
+ * the evaluator's bits at OT index j npad + i, npad = n rounded up to 64; the evaluator's zero labels
+ * E_j = q_j, its active labels t_j, Delta = the sender's s, whose bit 0 must be 1), garbling with the
+ * garbler's string and mask FOLDED into the circuit — the garbler knows x_j, so input z_j = NOT(x_j ^
+ * y_j) takes the zero label E_j ^ (x_j ? 0 : Delta) and the evaluator's OT'd label is z_j's active
+ * label; decode = colour(eq's zero label) ^ mask — and evaluation on the OT'd labels (out = colour ^
+ * decode = eq ^ mask). No label PRG, no garbler labels and no labels-OT reply on the wire; gate tweaks
+ * 2 g, 2 g + 1 with g = gate_base + t (bits - 1) + k as in fhh_gc_batch. Outputs AoS: tables
  * [n][bits-1][2][16], ev_zero / ev_active [n][bits][16], decode [n], out [n]; any but `out` may be
  * NULL. */
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                    uint32_t mask, const uint8_t delta[16], uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
                     uint8_t* ev_active, uint8_t* decode, uint8_t* out);
 
@@ -541,21 +548,22 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * fhh_tree_crawl / fhh_tree_crawl_last, with only its OWN secrets — the garbler's fhh_gb_cfg and the
  * evaluator's fhh_ev_cfg share nothing (each server draws its material itself: AesRng::new() per
  * channel, collect.rs:431; base OTs by fhh_co15_* over the channel, OtSender / OtReceiver::init,
- * collect.rs:454,460). Five byte buffers cross per chunk, in this order:
+ * collect.rs:454,460). Four byte buffers cross per chunk, in this order (y1 has 0 bytes since r05b):
  *   server 0 (garbler, OT sender)                          server 1 (evaluator, OT receiver)
  *                                      <--------------  fhh_ev_ot_labels(ev_cfg) -> u1
- *   fhh_gb_ot_labels(gb_cfg, u1) -> y1 -------------->
+ *   fhh_gb_ot_labels(gb_cfg, u1) -> y1 (empty)
  *   fhh_gb_garble -> gc               -------------->   fhh_ev_evaluate(gc, y1) -> u2
  *   fhh_gb_ot_shares(u2) -> y2        -------------->   fhh_ev_ot_shares(y2)
  *   fhh_party_node_sums                                  fhh_party_node_sums
  * Outputs are device buffers owned by the producing ctx, valid until its next party call; inputs are
  * device pointers on the receiving ctx's GPU (the caller moves the bytes: a network in a deployment, a
  * device copy in the in-process tests). Both OTs are correlated OTs (fhh_cot_extend_host's modes):
- * OT 1 (FHH_COT_LABELS) delivers the evaluator's input labels (m = C x 2d x npad: its share planes are
- * the choice bits), OT 2 (FHH_COT_FE, FHH_COT_FE255 at tree_crawl_last: 2 OTs per test) the share;
- * the circuit is fhh_gc_cot_host's (the garbler's string and mask folded in). gc = [tables (bits-1) x 2
- * | decode 1 B] per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
- * y1 16 B per OT, y2 8 B per OT (FE) or 16 B per OT (FieldElm). Each server's node values (the garbler's
+ * OT 1 (FHH_COT_RAW) delivers the evaluator's input labels (m = C x 2d x npad: its share planes are
+ * the choice bits; the garbler's labels-kind s is the circuit's Delta, so no reply crosses), OT 2
+ * (FHH_COT_FE, FHH_COT_FE255 at tree_crawl_last: 2 OTs per test) the share; the circuit is
+ * fhh_gc_cot_host's (the garbler's string and mask folded in). gc = [tables (bits-1) x 2 | decode 1 B]
+ * per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
+ * y1 0 B, y2 8 B per OT (FE) or 16 B per OT (FieldElm). Each server's node values (the garbler's
  * r1 = v + mask, the evaluator's OT output) stay on its device; fhh_party_node_sums sums them: non-last
  * level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm (the
  * frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own channel,
@@ -565,17 +573,17 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * reference's channels each run a slice of the level's tests (collect.rs:423-430); this bounds the
  * level's buffers at 1M clients. Chunks run in order and together cover [0, C); fhh_party_node_sums
  * follows the last one. Both parties must use the same windows. child_count = 0: the whole level.
- * Freshness: the garbler's Delta and mask should be fresh per chunk (gate tweaks are indexed by the
- * test's index in the whole level; Delta must not outlive the level). Base OTs may be reused across chunks and levels: each
+ * Freshness: Delta is the labels session's s (fresh with each base-OT run: run the base OTs per level,
+ * as the reference's init per channel does); the mask should be fresh per chunk (gate tweaks are indexed
+ * by the test's index in the whole level). Base OTs may be reused across chunks: each
  * ctx keeps, per OT kind, the running row-PRG counter of the base material it last saw and continues
  * it while the material is unchanged (a new set starts at 0), so pads never repeat. */
 typedef struct fhh_gb_cfg {
-    uint8_t delta[16];                   /* free-XOR offset (bit 0 forced to 1; AesRng::new(),
-                                            collect.rs:431)                                        */
     uint32_t mask;                       /* the chunk's mask bit (equalitytest.rs:38-43)           */
     uint32_t pad_;
     uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares): k_i^{s_i} from the   */
-    uint8_t base_choice[2][16];          /* base OTs, and s (bit i % 8 of byte i / 8)              */
+    uint8_t base_choice[2][16];          /* base OTs, and s (bit i % 8 of byte i / 8); the labels
+                                            kind's s is the free-XOR Delta: its bit 0 must be 1   */
     uint64_t child_begin;
     uint64_t child_count;
 } fhh_gb_cfg;

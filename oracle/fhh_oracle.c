@@ -1281,6 +1281,13 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
 /*          (16 B per OT); the receiver's BlockPair = r ? y ^ H(t) :  */
 /*          H(t), read unreduced as FieldElm::try_from(BlockPair)     */
 /*          does (field.rs:466-476).                                  */
+/*  mode 4  r05b, labels as the IKNP correlation itself (random COT   */
+/*          with the global offset s): no hash and no message after   */
+/*          U — sender_out_j = q_j, out_j = t_j = q_j ^ r_j s. Used   */
+/*          with s as the free-XOR Delta (bit 0 of byte 0 set by the  */
+/*          garbler), q_j is the zero label of input wire j and t_j   */
+/*          the evaluator's active label: the correlated OT free-XOR  */
+/*          garbling consumes. y_out is not written.                  */
 /* H = cr_hash (ot_cr_hash). ctr_off: the row PRG G starts at block   */
 /* ctr_off — the running counter of a base-OT session, so several     */
 /* batches can extend one set of base OTs without repeating pads (as  */
@@ -1359,6 +1366,11 @@ void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uin
             const uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
             if ((q[bit / 8] >> (bit % 8)) & 1) qj[i / 8] |= (uint8_t)(1u << (i % 8));
             if ((t[bit / 8] >> (bit % 8)) & 1) tj[i / 8] |= (uint8_t)(1u << (i % 8));
+        }
+        if (mode == 4) {   /* the correlation itself, unhashed */
+            if (sender_out) memcpy(sender_out + j * 16, qj, 16);
+            memcpy(out + j * 16, tj, 16);
+            continue;
         }
         for (int k = 0; k < 16; k++) qs[k] = qj[k] ^ s[k];
         ot_cr_hash(qj, H0 + j * 16);

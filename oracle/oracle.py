@@ -752,7 +752,7 @@ def gc_eval_eq_cot(tables, ev_active, decode, gate_base: int = 0) -> np.ndarray:
     return out
 
 
-COT_LABELS, COT_FE, COT_FE255 = 1, 2, 3
+COT_LABELS, COT_FE, COT_FE255, COT_RAW = 1, 2, 3, 4
 
 
 def cot_extend(mode: int, choices: np.ndarray, seeds: np.ndarray, s: bytes, delta: bytes | None = None,
@@ -760,7 +760,8 @@ def cot_extend(mode: int, choices: np.ndarray, seeds: np.ndarray, s: bytes, delt
     """Correlated OT extension (fhh_oracle.c orc_cot_extend). Returns (sender_out, out, U, y):
     mode 1: sender_out = x0 [m][16], out [m][16], y [m][16]; mode 2: sender values [m] u64, out [m]
     u64, y [m] u64; mode 3 (m even, pairs with one choice): sender values / out [m/2][32] BlockPairs,
-    y [m][16]."""
+    y [m][16]; mode 4 (the IKNP correlation, unhashed): sender_out = q [m][16], out = t [m][16] =
+    q ^ r s, y unused (zeros)."""
     ch = np.packbits(np.asarray(choices, np.uint8) & 1, bitorder="little")
     m = len(choices)
     sd = np.ascontiguousarray(seeds, np.uint8)

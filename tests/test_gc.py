@@ -208,41 +208,42 @@ def test_gpu_crawl_gc_rejects_count_mode():
 
 # ---- r05: the evaluator's labels by correlated OT, the garbler's string folded in --------------------
 def _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
-    """The labels C-OT (choice bits: the evaluator's bits at OT index j npad + i), garbling on its
-    zero labels with the garbler's string and mask folded in, evaluation on the evaluator's OT'd
-    labels — all in the oracle."""
+    """The labels OT (r05b: the IKNP correlation itself; choice bits: the evaluator's bits at OT index
+    j npad + i), garbling on its zero labels q_j with Delta = s and the garbler's string and mask folded
+    in, evaluation on the evaluator's t_j — all in the oracle."""
     n, bits = g.shape
     npad = (n + 63) // 64 * 64
     ch = np.zeros(bits * npad, np.uint8)
     for k in range(bits):
         ch[k * npad: k * npad + n] = e[:, k]
-    x0, out, u, y = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=_delta1(), ctr_off=ctr_off)
-    ev_zero = np.stack([x0[k * npad: k * npad + n] for k in range(bits)], axis=1)
-    ev_act = np.stack([out[k * npad: k * npad + n] for k in range(bits)], axis=1)
-    t, d = oracle.gc_garble_eq_cot(g, ev_zero, mask, DELTA, gate_base=gate_base)
+    q, t_rows, u, _ = oracle.cot_extend(oracle.COT_RAW, ch, seeds, s, ctr_off=ctr_off)
+    ev_zero = np.stack([q[k * npad: k * npad + n] for k in range(bits)], axis=1)
+    ev_act = np.stack([t_rows[k * npad: k * npad + n] for k in range(bits)], axis=1)
+    t, d = oracle.gc_garble_eq_cot(g, ev_zero, mask, s, gate_base=gate_base)
     res = oracle.gc_eval_eq_cot(t, ev_act, d, gate_base=gate_base)
     return res, dict(tables=t, ev_zero=ev_zero, ev_active=ev_act, decode=d)
 
 
-def _delta1():
-    D = np.frombuffer(DELTA, np.uint8).copy()
-    D[0] |= 1   # the colour-forced Delta the garbler uses (and the C-OT's correlation)
-    return D.tobytes()
+def _colour_s(rng):
+    """The garbler's labels-kind s: the circuit's free-XOR Delta, so its colour bit (bit 0) is 1."""
+    s = rng.integers(0, 256, 16, dtype=np.uint8)
+    s[0] |= 1
+    return s.tobytes()
 
 
 @pytest.mark.parametrize("bits", [1, 2, 4, 8])
 def test_oracle_cot_labels_chain_functional(oracle, bits):
     """eq_gc's assertion (equalitytest.rs:258-265) through the r05 labels step: masks ^ results ==
     (gb == ev), for both masks and for complemented evaluator strings; the evaluator's active labels
-    differ from the C-OT's zero labels by Delta exactly on its set bits."""
+    differ from the labels OT's zero labels by Delta = s exactly on its set bits."""
     rng = np.random.default_rng(40 + bits)
     g, e = _cases(rng, 300, bits)
     seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
-    s = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    s = _colour_s(rng)
     for mask in (0, 1):
         out, tr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=5, ctr_off=256)
         assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))
-        D = np.frombuffer(_delta1(), np.uint8)
+        D = np.frombuffer(s, np.uint8)   # Delta = s
         assert np.array_equal(tr["ev_zero"] ^ tr["ev_active"], e[:, :, None] * D)
         out2, _ = _oracle_cot_chain(oracle, g, 1 - e, mask, seeds, s, gate_base=5, ctr_off=256)
         assert np.array_equal(out2 ^ mask, (g == 1 - e).all(axis=1).astype(np.uint8))
@@ -251,17 +252,19 @@ def test_oracle_cot_labels_chain_functional(oracle, bits):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bits", [(1, 1), (63, 2), (65, 2), (1000, 2), (4097, 4), (300, 6), (130, 8)])
 def test_gpu_cot_labels_chain_bit_exact(oracle, n, bits):
-    """fhh_gc_cot_host (the C-OT + garble + evaluate of one batch) = the oracle chain: zero labels,
-    active labels, tables, decoding bits, outputs."""
+    """fhh_gc_cot_host (the labels OT + garble + evaluate of one batch) = the oracle chain: zero labels,
+    active labels, tables, decoding bits, outputs; an s without the colour bit is refused."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import gc
     rng = np.random.default_rng(n * 3 + bits)
     g, e = _cases(rng, n, bits)
     seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
-    s = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+    s = _colour_s(rng)
     kc = fhh.KeyCollection(8, 1)
+    with pytest.raises(fhh.FhhError):   # Delta = s needs the colour bit
+        gc.equality_test_cot(kc, g, e, 0, seeds, bytes([s[0] & 0xFE]) + s[1:])
     for mask, ctr in ((0, 0), (1, 256), (1, 512)):
-        out, tr = gc.equality_test_cot(kc, g, e, mask, DELTA, seeds, s, gate_base=7, ctr_off=ctr)
+        out, tr = gc.equality_test_cot(kc, g, e, mask, seeds, s, gate_base=7, ctr_off=ctr)
         exp, etr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=7, ctr_off=ctr)
         for k in ("ev_zero", "ev_active", "tables", "decode"):
             assert np.array_equal(tr[k], etr[k]), k

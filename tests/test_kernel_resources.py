@@ -76,7 +76,8 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     names += [f"_ZN3fhh9k_gc_evalILi{b}ELb{f}EEEvNS_6GcArgsE" for b in range(1, 9) for f in (0, 1)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
-    names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE"]
+    names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE",
+              "_ZN3fhh13k_ot_rows_outENS_6OtArgsEi"]   # r05b: the labels OT's row transpose (mode 4)
     for name in names:
         assert name in u, f"{name} not found"
         k = u[name]

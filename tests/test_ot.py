@@ -183,6 +183,12 @@ def test_oracle_cot_functionality(oracle, m, ctr_off):
     x0, out, u, y = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=ctr_off)
     D = np.frombuffer(delta, np.uint8)
     assert np.array_equal(out, np.where(ch[:, None] == 1, x0 ^ D, x0))
+    # labels as the IKNP correlation (r05b): t_j = q_j ^ r_j s, no reply; the pads are the plain /
+    # hashed C-OT's pre-images (the same rows, unhashed)
+    q, t, u4, _ = oracle.cot_extend(oracle.COT_RAW, ch, seeds, s, ctr_off=ctr_off)
+    S = np.frombuffer(s, np.uint8)
+    assert np.array_equal(t, np.where(ch[:, None] == 1, q ^ S, q))
+    assert np.array_equal(u4, u)
     # FE share, both masks
     for mask in (0, 1):
         gv, ev, _, _ = oracle.cot_extend(oracle.COT_FE, ch, seeds, s, mask=mask, ctr_off=ctr_off)
@@ -241,7 +247,7 @@ def test_oracle_gc_aes_ni_matches_bytewise(oracle):
 @pytest.mark.parametrize("m", [1, 127, 1000, 8193, 100_000])
 def test_gpu_cot_bit_exact(oracle, m):
     """GPU correlated OT (every mode, at a nonzero session counter) = the oracle: both parties'
-    outputs and both protocol messages (U, y)."""
+    outputs and both protocol messages (U, y; mode 4 has no y)."""
     import fuzzyheavyhitters_amd as fhh
     from fuzzyheavyhitters_amd import ot
     ch, _, _, seeds, s, delta = _inputs(m, 5 * m + 1)
@@ -250,6 +256,10 @@ def test_gpu_cot_bit_exact(oracle, m):
         got = ot.cot_extend(kc, 1, ch, seeds, s, delta=delta, ctr_off=ctr_off, transcript=True)
         exp = oracle.cot_extend(oracle.COT_LABELS, ch, seeds, s, delta=delta, ctr_off=ctr_off)
         for g, e in zip(got, exp):
+            assert np.array_equal(g, e)
+        got = ot.cot_extend(kc, 4, ch, seeds, s, ctr_off=ctr_off, transcript=True)
+        exp = oracle.cot_extend(oracle.COT_RAW, ch, seeds, s, ctr_off=ctr_off)
+        for g, e in zip(got[:3], exp[:3]):   # q, t, U (no y)
             assert np.array_equal(g, e)
         for mask in (0, 1):
             got = ot.cot_extend(kc, 2, ch, seeds, s, mask=mask, ctr_off=ctr_off, transcript=True)

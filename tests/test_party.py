@@ -57,8 +57,9 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     C0, bits = int(got.level_children[0]), 2 * d
     npad = (n + 63) // 64 * 64
     assert lb["gc"] == C0 * n * (2 * (bits - 1) * 16 + 1)   # tables + decoding bit (garbler string folded in)
-    # r05 correlated OTs: one 16-B y per labels OT, one 8-B y per FE share OT
-    assert lb["y1"] == C0 * bits * npad * 16 and lb["y2"] == C0 * n * 8
+    # r05b: the labels OT is the IKNP correlation itself (no reply); one 8-B y per FE share OT
+    assert lb["u1"] == 16 * ((C0 * bits * npad + 8191) // 8192 * 8192)
+    assert lb["y1"] == 0 and lb["y2"] == C0 * n * 8
 
 
 def test_two_party_fresh_randomness_same_output():

@@ -1,6 +1,6 @@
 """Host-side pieces of the two-party GC + OT driver (no GPU): the chunk windows a level's tests run
 in (fhh_gc_party_cfg child_begin / child_count; the reference splits a level's tests over its
-channels, collect.rs:423-430) and the ctypes layout of fhh_gc_party_cfg against include/fhh.h."""
+channels, collect.rs:423-430) and the ctypes layouts of fhh_gb_cfg / fhh_ev_cfg against include/fhh.h."""
 import ctypes
 
 import pytest
@@ -23,7 +23,7 @@ def test_party_cfg_layouts_match_header():
     """fhh_gb_cfg / fhh_ev_cfg (include/fhh.h): the ctypes mirrors have the C layout (no padding on
     x86-64: every field is naturally aligned), the chunk window last."""
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
-    gb = 16 + 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8
+    gb = 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8
     ev = 2 * 128 * 2 * 16 + 8 + 8
     assert ctypes.sizeof(FhhGbCfg) == gb and ctypes.sizeof(FhhEvCfg) == ev
     for T, size in ((FhhGbCfg, gb), (FhhEvCfg, ev)):
@@ -34,15 +34,17 @@ def test_party_cfg_layouts_match_header():
 
 def test_evaluator_cfg_carries_no_garbler_secret():
     """the evaluator's half never receives the garbler's secrets. fhh_ev_cfg holds only
-    its base-OT key pairs and the chunk window; Delta, the mask, the base-OT receiver's choice bits
-    and chosen keys exist only in fhh_gb_cfg, and the share PRF key is gone (the share values come from
-    the correlated OT itself), as is the label key (the r05 garbler draws no labels)."""
+    its base-OT key pairs and the chunk window; the mask, the base-OT receiver's choice bits (the labels
+    kind's s is the circuit's Delta since r05b) and chosen keys exist only in fhh_gb_cfg, and the share
+    PRF key is gone (the share values come from the correlated OT itself), as is the label key (the r05
+    garbler draws no labels)."""
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
     ev_fields = {f for f, _ in FhhEvCfg._fields_}
     gb_fields = {f for f, _ in FhhGbCfg._fields_}
     assert ev_fields == {"base_pairs", "child_begin", "child_count"}
-    for secret in ("delta", "mask", "base_chosen", "base_choice"):
+    for secret in ("mask", "base_chosen", "base_choice"):
         assert secret in gb_fields and secret not in ev_fields
+    assert "delta" not in gb_fields | ev_fields
     assert not any("seed" in f for f in gb_fields | ev_fields)
     # and the header agrees: the evaluator's entry points take only fhh_ev_cfg
     import os
@@ -54,15 +56,24 @@ def test_evaluator_cfg_carries_no_garbler_secret():
 
 
 def test_party_python_sides_hold_their_own_material():
-    """party.GarblerParty / EvaluatorParty draw their material themselves (os.urandom): two chunk
-    configs of the garbler never repeat a Delta, and the evaluator's config is built from its own
-    base-OT pairs only."""
+    """party.GarblerParty / EvaluatorParty draw their material themselves (os.urandom): the garbler's
+    choice bits s of two base-OT runs differ and the labels run's s (the circuit's Delta) has its colour
+    bit set, a chunk config carries the garbler's own s and chosen keys, and the evaluator's config is
+    built from its own base-OT pairs only."""
     import numpy as np
     from fuzzyheavyhitters_amd.party import EvaluatorParty, GarblerParty
-    base_gb = [(np.zeros((128, 16), np.uint8), np.zeros(16, np.uint8))] * 2
+    gp, ep = GarblerParty(None), EvaluatorParty(None)
+    sides = []
+    for colour in (True, True, False):
+        A, seed = ep.co15_start()
+        B, (chosen, s) = gp.co15_receive(A, colour=colour)
+        pairs = ep.co15_finish(seed, B)
+        assert np.array_equal(chosen, pairs[np.arange(128), (np.unpackbits(s, bitorder="little"))])
+        sides.append(s)
+    assert sides[0][0] & 1 and sides[1][0] & 1 and bytes(sides[0]) != bytes(sides[1])
+    base_gb = [(np.full((128, 16), 3, np.uint8), sides[0]), (np.full((128, 16), 5, np.uint8), sides[2])]
     a = GarblerParty(None).chunk_cfg(base_gb, 0, 3)
-    b = GarblerParty(None).chunk_cfg(base_gb, 3, 3)
-    assert bytes(a.delta) != bytes(b.delta)
+    assert bytes(a.base_choice)[:16] == bytes(sides[0]) and bytes(a.base_chosen)[:1] == b"\x03"
     pairs = [np.full((128, 2, 16), 7, np.uint8), np.full((128, 2, 16), 9, np.uint8)]
     e = EvaluatorParty.chunk_cfg(pairs, 3, 3)
     assert bytes(e.base_pairs)[:4] == b"\x07" * 4 and bytes(e.base_pairs)[-4:] == b"\x09" * 4

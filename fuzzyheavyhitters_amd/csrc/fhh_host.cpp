@@ -1273,8 +1273,10 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 if (real_ot) {
                     HIP_TRY(c0, c0->ot_rk.ensure((size_t)2 * 3 * 128 * 44 * 4));
                     if (B.base_ot) {
-                        // keep the producer a few levels ahead of the enqueueing
-                        constexpr uint32_t kAhead = 4;
+                        // keep the producer well ahead of the enqueueing: the first levels take ~1 ms of
+                        // GPU time against ~9 ms per CO15 instance, so at 4 levels ahead the loop waited
+                        // 0.56-0.59 s per 1M crawl (base_ot_stall_ms); 32 levels = 64 instances, 4.3 MB
+                        constexpr uint32_t kAhead = 32;
                         for (uint32_t l = lv; l < std::min(levels, lv + kAhead); l++)
                             for (uint32_t w = 0; w < 2; w++) (void)B.bot->request(l, w);
                     }

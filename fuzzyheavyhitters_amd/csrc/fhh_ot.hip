@@ -439,30 +439,36 @@ __global__ __launch_bounds__(kOtRowsThreads) void k_ot_recv_hash_rows(OtArgs a) 
 // offset, q_j (sender) and t_j = q_j ^ r_j s (receiver) already are the zero label and the active label
 // of the evaluator's input wire j — the random correlated OT that free-XOR garbling consumes — so no
 // hash and no message y is needed: this kernel only transposes the tile-major matrix into one 16-B row
-// per OT (the hashes' load + in-register transpose + LDS exchange, without their T-tables: 8 KiB of
-// stage per 256-thread workgroup).
+// per OT. One wave per 512-OT tile: the hashes' row loads + in-register 32 x 32 transposes, then the
+// whole tile goes through LDS once so that every store writes 64 consecutive OTs (1 KiB): lane (q, g)
+// writes word g of OTs 32 q + k at 132 q + 4 k + g (banks 4 q + g + 4 k: conflict-free), lane l reads
+// OT 64 r + l as one ds_read_b128. No T-tables: 8.25 KiB of stage per wave.
 constexpr int kOtOutThreads = 256;
+constexpr int kOtOutStride = 132;   // words per 32-OT group in the stage (128 + 4: bank spread)
 __global__ __launch_bounds__(kOtOutThreads) void k_ot_rows_out(OtArgs a, int sender) {
-    __shared__ uint32_t stage[kOtOutThreads / 64][512];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kOtOutThreads / 64][kOtTileWords * kOtOutStride];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t m = ot_active(a);
     const uint64_t tiles = (m + 32 * kOtTileWords - 1) / (32 * kOtTileWords);
     const uint64_t nwaves = (uint64_t)gridDim.x * (kOtOutThreads / 64);
     const uint32_t* rows = reinterpret_cast<const uint32_t*>(sender ? a.Q : a.T);
     uint4* out = sender ? static_cast<uint4*>(a.sx) : a.out;
+    uint32_t* st = stage[wv];
+    const uint32_t q = lane >> 2, g = lane & 3;
     for (uint64_t t = (uint64_t)blockIdx.x * (kOtOutThreads / 64) + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
-        ot_tile_load(rows, t, lane, x);
-#pragma unroll 1
-        for (int r = 0; r < 4; r++) {
-            uint4 v[2];
-            ot_tile_round(stage[wv], x, lane, v);
+        ot_tile_load(rows, t, lane, x);   // x[k] = word g of OT 32 (16 t + q) + k
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const uint64_t j = ot_tile_ot(t, lane, r, u);
-                if (j < m) out[j] = v[u];
-            }
+        for (int k = 0; k < 32; k++) st[kOtOutStride * q + 4 * k + g] = x[k];
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t j0 = 512 * t;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const uint32_t o = 64 * r + lane;
+            const uint4 v = *reinterpret_cast<const uint4*>(st + kOtOutStride * (o >> 5) + 4 * (o & 31));
+            if (j0 + o < m) out[j0 + o] = v;
         }
+        __builtin_amdgcn_wave_barrier();   // the reads precede the next tile's stage writes
     }
 }
 

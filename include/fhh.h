@@ -273,10 +273,11 @@ typedef struct fhh_sim_config {
      * equality test on the GPU (fhh_gc_*: server 0 garbles its share planes, server 1
      * evaluates), as tree_crawl does with gc_sender (collect.rs:419-482). 1 = the OTs (the
      * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU correlated
-     * OT extension (fhh_cot_extend_host's modes; a FieldElm share travels as a BlockPair = 2 OTs).
-     * Same sums as 0. Material from prf_seed (a harness, not private): garbler key, Delta and mask
-     * fresh per chunk of children; one base-OT session per level and OT kind, each chunk on its own
-     * row-PRG counter range. */
+     * OT extension (fhh_cot_extend_host's modes: the labels as FHH_COT_RAW with the labels session's
+     * s as Delta, the share as FHH_COT_FE / FHH_COT_FE255, a FieldElm share as a BlockPair = 2 OTs).
+     * Same sums as 0. Material from prf_seed (a harness, not private): the mask fresh per chunk of
+     * children; one base-OT session per level and OT kind, each chunk on its own row-PRG counter
+     * range; gate tweaks carry the level (bits 40+). */
     uint32_t gc;
     /* parity probe of the device loop (tests; probe_n_levels = 0 disables it): right after level
      * probe_levels[k]'s k_expand, the pending children's EvalStates (ibDCF.rs:24-30) of the

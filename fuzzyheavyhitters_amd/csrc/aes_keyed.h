@@ -162,6 +162,87 @@ __device__ __forceinline__ void aes_ctr_shared(uint32_t (&s)[NB][4], const uint3
         }
 }
 
+// r05: the per-key constant part of rounds 1-2 for AES-CTR blocks that ALL differ from s0 only in
+// the byte at row R of column C (the sketch keystream: big-endian counters b < 256 differ in byte 15
+// alone, for every block of the key). aes_ctr_shared pays block 0's rounds 1-2 in full on every
+// call; here they are paid once per key: pre[0] = round 1's column-D terms other than T_R, with
+// rk1[D]; pre[1 + c] = round 2's column-c terms other than the one fed by column D, with rk2[c];
+// pre[5] = rk0[C]. Every block then costs 1 + 4 lookups in rounds 1-2 (133 per block, aes_ctr_pre).
+template <class Tab, int R, int C, class Rk>
+__device__ __forceinline__ void aes_ctr_pre_init(const uint32_t (&s0)[4], const uint32_t* tbl, uint32_t b0,
+                                                 uint32_t b1, const Rk& src, uint32_t (&pre)[6]) {
+    constexpr int D = (C - R + 4) & 3;
+    uint32_t rk[4], a[4], y[4];
+    src.get(0, rk);
+    pre[5] = rk[C];
+#pragma unroll
+    for (int c = 0; c < 4; c++) a[c] = s0[c] ^ rk[c];
+    src.get(1, rk);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k] = term_k<Tab>(k, tbl, b0, b1, a[(c + k) & 3]);
+        y[c] = DevOpsX::xor3(DevOpsX::xor3(t[0], t[1], t[2]), t[3], rk[c]);
+        if (c == D) pre[0] = DevOpsX::xor3(t[(R + 1) & 3], t[(R + 2) & 3], t[(R + 3) & 3]) ^ rk[c];
+    }
+    src.get(2, rk);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int k = (D - c + 4) & 3;   // the row of column D that output column c takes
+        uint32_t t[4];
+#pragma unroll
+        for (int j = 1; j < 4; j++) t[j] = term_k<Tab>((k + j) & 3, tbl, b0, b1, y[(c + ((k + j) & 3)) & 3]);
+        pre[1 + c] = DevOpsX::xor3(t[1], t[2], t[3]) ^ rk[c];
+    }
+}
+
+template <class Tab, int NB, int R, int C, class Rk>
+__device__ __forceinline__ void aes_ctr_pre(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
+                                            const Rk& src, const uint32_t (&pre)[6]) {
+    constexpr int D = (C - R + 4) & 3;
+    uint32_t x[NB][4];
+#pragma unroll
+    for (int q = 0; q < NB; q++) {
+        const uint32_t yd = pre[0] ^ term_k<Tab>(R, tbl, b0, b1, s[q][C] ^ pre[5]);   // round 1, column D
+#pragma unroll
+        for (int c = 0; c < 4; c++) x[q][c] = pre[1 + c] ^ term_k<Tab>((D - c + 4) & 3, tbl, b0, b1, yd);   // round 2
+    }
+    uint32_t rk[4];
+#pragma unroll
+    for (int r = 3; r < 10; r++) {
+        src.get(r, rk);
+        uint32_t z[NB][4];
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t t0 = Tab::template term<0>(tbl, b0, b1, x[q][c]);
+                const uint32_t t1 = Tab::template term<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+                const uint32_t t2 = Tab::template term<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+                const uint32_t t3 = Tab::template term<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+                z[q][c] = DevOpsX::xor3(DevOpsX::xor3(t0, t1, t2), t3, rk[c]);
+            }
+#pragma unroll
+        for (int q = 0; q < NB; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[q][c] = z[q][c];
+    }
+    src.get(10, rk);
+    constexpr uint32_t sel_lo = 0x0C0C0000u | ((uint32_t)(4 + Tab::spos(1)) << 8) | (uint32_t)Tab::spos(0);
+    constexpr uint32_t sel_hi = ((uint32_t)(4 + Tab::spos(3)) << 24) | ((uint32_t)Tab::spos(2) << 16) | 0x0C0Cu;
+#pragma unroll
+    for (int q = 0; q < NB; q++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t a0 = Tab::template last<0>(tbl, b0, b1, x[q][c]);
+            const uint32_t a1 = Tab::template last<1>(tbl, b0, b1, x[q][(c + 1) & 3]);
+            const uint32_t a2 = Tab::template last<2>(tbl, b0, b1, x[q][(c + 2) & 3]);
+            const uint32_t a3 = Tab::template last<3>(tbl, b0, b1, x[q][(c + 3) & 3]);
+            s[q][c] = DevOpsX::xor3(DevOpsX::perm(a1, a0, sel_lo), DevOpsX::perm(a3, a2, sel_hi), rk[c]);
+        }
+}
+
 template <class Tab, int NB, int R, int C>
 __device__ __forceinline__ void aes_rk_ctr(uint32_t (&s)[NB][4], const uint32_t* tbl, uint32_t b0, uint32_t b1,
                                            const uint32_t (&rk)[11][4]) {

@@ -304,6 +304,18 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
+        // r05: when every block of the key's stream (and the passes' overrun) has a counter below 256,
+        // all of them differ only in byte 15, so rounds 1-2 keep a per-key constant part: paid here once
+        // (aes_ctr_pre_init), then 5 instead of 32 lookups per block in rounds 1-2 (aes_ctr_pre: 133
+        // lookups per block against 146.5 for aes_ctr_shared's pairs)
+        const bool pre_ok = SCHED == 2 && nb + (uint64_t)NBP * LPK <= 256;   // wave-uniform
+        uint32_t pre[6] = {0, 0, 0, 0, 0, 0};
+        if constexpr (SCHED == 2) {
+            if (pre_ok) {
+                const uint32_t z[4] = {0u, 0u, 0u, 0u};   // counter 0: BE128(0)
+                aes_ctr_pre_init<Tab, 3, 3>(z, tbl, b0, b1, RkLds{rkl}, pre);
+            }
+        }
         const uint64_t* x = a.x + kk * F;
         const uint64_t* kx = a.kx + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
@@ -341,7 +353,8 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
                 // block index) unless a lane's blocks straddle a multiple of 256: then rounds 1-2
                 // of the second block reuse the first's terms (aes_ctr_shared, 293 vs 320 lookups)
                 const bool same_hi = (bb >> 8) == ((bb + LPK * (NB - 1)) >> 8);
-                if (NB == 1 || __ballot(!same_hi) == 0) aes_lds_rk_ctr<Tab, NB, 3, 3>(st, tbl, b0, b1, rkl);
+                if (pre_ok) aes_ctr_pre<Tab, NB, 3, 3>(st, tbl, b0, b1, RkLds{rkl}, pre);
+                else if (NB == 1 || __ballot(!same_hi) == 0) aes_lds_rk_ctr<Tab, NB, 3, 3>(st, tbl, b0, b1, rkl);
                 else aes_lds_rk<Tab, NB>(st, tbl, b0, b1, rkl);
             } else if constexpr (OTF) aes_otf<Tab, NB>(st, tbl, b0, b1, seed);
             else aes_rk<Tab, NB>(st, tbl, b0, b1, rk);

@@ -2525,11 +2525,16 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
     }();
     const bool overlap = nl > 1 && kOverlapEnv;
     uint64_t* alt[2] = {nullptr, nullptr};
+    // r05: when the batch's sketches fit (12 GiB), every level but the last writes a slot of its own, so
+    // the main stream never waits for a verify: the two-slot scheme's wait put a barrier between every
+    // two levels' main launches (11.5 us median gap, 1023 per configs[4] step)
+    const size_t level_words = (size_t)2 * b->n_keys * 6;
+    const bool own_slots = overlap && (size_t)(nl - 1) * level_words * 8 <= ((size_t)12 << 30);
     if (overlap) {
         if (!ctx->side_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
         for (hipEvent_t& e : ctx->side_ev)
             if (!e) HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_TRY(ctx, ctx->sketch_alt.ensure((size_t)2 * b->n_keys * 6 * 8));
+        HIP_TRY(ctx, ctx->sketch_alt.ensure((own_slots ? (size_t)(nl - 1) : 1) * level_words * 8));
         for (int s = 0; s < 2; s++) alt[s] = ctx->sketch_alt.as<uint64_t>() + (size_t)s * b->n_keys * 6;
         // the side stream starts after everything already on the main stream (triples, uploads)
         HIP_TRY(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
@@ -2548,16 +2553,22 @@ int fhh_sim_sketch_verify_fe(fhh_ctx* ctx, const fhh_sketch_batch* b) {
     } drain{overlap ? ctx->side_stream : nullptr, overlap};
     for (uint32_t k = 0; k < nl; k++) {
         const uint32_t lv = b->level + k;
-        const int slot = overlap ? (int)((nl - 1 - k) & 1) : 0;
+        const int slot = own_slots ? 0 : overlap ? (int)((nl - 1 - k) & 1) : 0;
         uint64_t* out[2] = {slot ? alt[0] : b->sketch_dev[0], slot ? alt[1] : b->sketch_dev[1]};
-        if (overlap && k >= 2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev_ver[slot], 0));
-        for (int s = 0; s < 2; s++) {
+        if (own_slots && k + 1 < nl)
+            for (int s = 0; s < 2; s++) out[s] = alt[s] + (size_t)k * level_words;
+        if (overlap && !own_slots && k >= 2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev_ver[slot], 0));
+        {   // both servers' sketches in one main launch (r05: one launch transition per level, not two)
             SketchArgs a{};
             a.seeds = b->seeds_dev;
-            a.x = b->x_dev[s] + (size_t)k * b->x_level_stride;
-            a.kx = b->kx_dev[s] + (size_t)k * b->x_level_stride;
-            a.out = out[s];
-            a.n_keys = b->n_keys;
+            a.x = b->x_dev[0] + (size_t)k * b->x_level_stride;
+            a.kx = b->kx_dev[0] + (size_t)k * b->x_level_stride;
+            a.out = out[0];
+            a.x1 = b->x_dev[1] + (size_t)k * b->x_level_stride;
+            a.kx1 = b->kx_dev[1] + (size_t)k * b->x_level_stride;
+            a.out1 = out[1];
+            a.n_srv = b->n_keys;
+            a.n_keys = 2 * b->n_keys;
             a.n_nodes = b->n_nodes;
             a.force_sequential = b->force_sequential;
             a.level = lv;

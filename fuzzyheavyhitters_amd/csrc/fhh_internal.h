@@ -418,6 +418,12 @@ struct SketchArgs {
     uint32_t n_nodes;
     uint32_t force_sequential;   // 1: every key takes the sequential-stream path (tests)
     uint32_t level;              // the level's stream seed = seed with bytes 12..15 ^= level
+    // r05: both servers in one k_sketch_fe launch (the level batch): keys [n_srv, n_keys) are server
+    // 1's keys k - n_srv (same seeds, its own x1 / kx1 / out1); n_srv = 0: one server
+    uint64_t n_srv;
+    const uint64_t* x1;
+    const uint64_t* kx1;
+    uint64_t* out1;
 };
 // k_sketch_fe launch plan: keys [0, n_main) at lpk_main lanes per key, the rest at lpk_tail
 struct SketchPlan {

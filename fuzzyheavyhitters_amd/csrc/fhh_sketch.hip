@@ -282,9 +282,15 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
     const uint64_t nb = (F + 3 + 1) / 2;   // draws 0..F+2
     const uint64_t wave = (uint64_t)blockIdx.x * (THR / 64) + (threadIdx.x >> 6);
     for (uint64_t kbase = wave * KPW; kbase < a.n_keys; kbase += nwaves * KPW) {
-        const uint64_t k = kbase + seg;
-        const bool kact = k < a.n_keys;
-        const uint64_t kk = kact ? k : kbase;
+        const uint64_t k_all = kbase + seg;
+        const bool kact = k_all < a.n_keys;
+        // the two-server form: keys past n_srv are server 1's (same seeds, its own vectors and outputs)
+        const bool srv1 = a.n_srv && (kact ? k_all : kbase) >= a.n_srv;
+        const uint64_t k = srv1 ? k_all - a.n_srv : k_all;
+        const uint64_t kk = kact ? k : (srv1 ? kbase - a.n_srv : kbase);
+        const uint64_t* const xs = srv1 ? a.x1 : a.x;
+        const uint64_t* const kxs = srv1 ? a.kx1 : a.kx;
+        uint64_t* const outs = srv1 ? a.out1 : a.out;
         uint32_t seed[4];
 #pragma unroll
         for (int c = 0; c < 4; c++) seed[c] = reinterpret_cast<const uint32_t*>(a.seeds)[4 * kk + c];
@@ -316,8 +322,8 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
                 aes_ctr_pre_init<Tab, 3, 3>(z, tbl, b0, b1, RkLds{rkl}, pre);
             }
         }
-        const uint64_t* x = a.x + kk * F;
-        const uint64_t* kx = a.kx + kk * F;
+        const uint64_t* x = xs + kk * F;
+        const uint64_t* kx = kxs + kk * F;
         uint64_t rx = 0, r2x = 0, rkx = 0, rnd0 = 0, rnd1 = 0;
         bool rej = false;
         // one pass: NB keystream blocks per lane (bb, bb + LPK, ...) and their draws' products
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
         const uint64_t rand2 = __shfl(rnd1, seg * LPK, 64);
         const uint64_t rand3 = __shfl(rnd0, seg * LPK + 1, 64);
         if (kact && !key_rej && sl == 0) {
-            uint64_t* o = a.out + 6 * k;
+            uint64_t* o = outs + 6 * k;
             o[0] = rx;
             o[1] = r2x;
             o[2] = rkx;
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
             o[4] = rand2;
             o[5] = rand3;
         } else if (kact && key_rej && sl == 0 && OTF) {
-            sketch_sequential_otf<Tab>(tbl, b0, b1, seed, x, kx, F, a.out + 6 * k);
+            sketch_sequential_otf<Tab>(tbl, b0, b1, seed, x, kx, F, outs + 6 * k);
         } else if (kact && key_rej && sl == 0) {
             // sequential PrgStream with FE::from_rng redraws (field.rs:252-264) for this key
             uint64_t pos = 0, cur_b = ~0ull, d[2] = {0, 0};
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(THR) void k_sketch_fe(SketchArgs a) {
                 s2x = fe_addc(s2x, fe_mulc(xv, r2));
                 skx = fe_addc(skx, fe_mulc(kxv, r));
             }
-            uint64_t* o = a.out + 6 * k;
+            uint64_t* o = outs + 6 * k;
             o[0] = sx;
             o[1] = s2x;
             o[2] = skx;
@@ -811,6 +817,21 @@ hipError_t launch_sketch_fe(const SketchArgs& a, hipStream_t stream) { return la
 // on `tail_stream`: a caller with a second stream lets the tail fill the main launch's ragged end
 hipError_t launch_sketch_fe2(const SketchArgs& a, hipStream_t stream, hipStream_t tail_stream) {
     if (a.n_keys == 0) return hipSuccess;
+    if (g_sketch_impl == 4 && a.n_srv) {   // the producer / consumer kernel takes one server at a time
+        for (int srv = 0; srv < 2; srv++) {
+            SketchArgs o = a;
+            o.n_srv = 0;
+            o.n_keys = srv ? a.n_keys - a.n_srv : a.n_srv;
+            if (srv) {
+                o.x = a.x1;
+                o.kx = a.kx1;
+                o.out = a.out1;
+            }
+            const hipError_t e = launch_sketch_pc(o, stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     if (g_sketch_impl == 4) return launch_sketch_pc(a, stream);
     if (g_sketch_impl == 1)
         return launch_sketch_kernel(k_sketch_fe<kSketchKeysPerWave>, kSketchThreads, kSketchKeysPerWave, a, stream);
@@ -823,15 +844,27 @@ hipError_t launch_sketch_fe2(const SketchArgs& a, hipStream_t stream, hipStream_
     m.n_keys = p.n_main;
     hipError_t e = launch_sketch_lpk(p.lpk_main, m, stream);
     if (e != hipSuccess || p.n_main == a.n_keys) return e;
-    SketchArgs t = a;   // the tail: the keys past n_main, in one round of the producer / consumer form
-    t.seeds = a.seeds + 16 * p.n_main;
-    t.x = a.x ? a.x + p.n_main * a.n_nodes : nullptr;
-    t.kx = a.kx ? a.kx + p.n_main * a.n_nodes : nullptr;
-    t.out = a.out + 6 * p.n_main;
-    t.n_keys = a.n_keys - p.n_main;
-    // (r03, configs[4]: its 3 blocks per lane cover a 130-block key at LPK 64 in one pass where the
-    // fused form takes two: 16.2 vs 28.8 us; the main launch stays fused, 227 vs 236 us)
-    return launch_sketch_pc_lpk(p.lpk_tail, t, sketch_cus(), tail_stream);
+    // the tail: the keys past n_main, in one round of the producer / consumer form (r03, configs[4]: its
+    // 3 blocks per lane cover a 130-block key at LPK 64 in one pass where the fused form takes two: 16.2
+    // vs 28.8 us; the main launch stays fused, 227 vs 236 us); one launch per server the tail touches
+    const uint64_t ns = a.n_srv ? a.n_srv : a.n_keys;
+    for (int srv = 0; srv < (a.n_srv ? 2 : 1); srv++) {
+        const uint64_t lo = std::max<uint64_t>(p.n_main, srv * ns), hi = srv ? a.n_keys : std::min(a.n_keys, ns);
+        if (lo >= hi) continue;
+        const uint64_t off = lo - srv * ns;   // the server's first tail key
+        SketchArgs t = a;
+        t.n_srv = 0;
+        t.seeds = a.seeds + 16 * off;
+        const uint64_t* xs = srv ? a.x1 : a.x;
+        const uint64_t* kxs = srv ? a.kx1 : a.kx;
+        t.x = xs ? xs + off * a.n_nodes : nullptr;
+        t.kx = kxs ? kxs + off * a.n_nodes : nullptr;
+        t.out = (srv ? a.out1 : a.out) + 6 * off;
+        t.n_keys = hi - lo;
+        e = launch_sketch_pc_lpk(p.lpk_tail, t, sketch_cus(), tail_stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // ---- MulState (mpc.rs:83-220), FE, one lane per key ---------------------------------------

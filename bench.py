@@ -654,16 +654,17 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
         "wall_s": wall,
         "heavy_hitters": hh,
         "heavy_hitters_equal_headline": hh == headline_hh,
-        "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per OT kind per level; chunks on "
-                   "disjoint row-PRG counters)",
+        "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per level for the labels OT and one "
+                   "for the FieldElm level's share OT; chunks on disjoint row-PRG counters)",
         "base_ot_instances": s0["base_ot_instances"],
         "base_ot_compute_ms": s0["base_ot_ms"],
         "base_ot_stall_ms": s0["base_ot_stall_ms"],
         "base_ot_note": "compute = summed per-instance CO15 + key-schedule time over the host threads; stall = time "
                         "the level loop waited for an instance it needed (the base OTs on the critical path)",
         "protocol": "GC (half-gates, TCCR; the garbler's string and mask folded in) + the evaluator's labels as "
-                    "the IKNP correlation (Delta = the labels OT's s, no reply) + the FE share by ALSZ correlated OT "
-                    "(24 AES blocks per d=1 test)",
+                    "the IKNP correlation (Delta = the labels OT's s, no reply) + the FE share from the circuit's "
+                    "output labels (cr_hash of W_0, W_0 ^ Delta; the FieldElm level by ALSZ correlated OT) "
+                    "(21 AES blocks per d=1 test: garble 8 + 2, evaluate 4 + 1, labels OT expands 2 x 3)",
         "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
         "expand_gpu_ms": s0["expand_ms"],
         "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,

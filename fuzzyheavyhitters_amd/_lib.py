@@ -286,7 +286,8 @@ def lib():
         "fhh_party_bytes_sent": (i, [vp, u64p]),
         "fhh_gc_party_test_cfgs": (i, [u64, u32, P(FhhGbCfg), P(FhhEvCfg)]),
         "fhh_cot_extend_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
-        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p]),
+        "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
+                                u64p]),
         "fhh_memcpy_device": (i, [i, vp, vp, u64]),
         "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),

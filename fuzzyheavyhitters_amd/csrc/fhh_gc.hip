@@ -19,6 +19,7 @@
 // a wave's 64 lanes read and write 64 consecutive 16-B blocks.
 #include "fhh_internal.h"
 #include "aes_keyed.h"
+#include "cot_fe.h"
 
 namespace fhh {
 
@@ -295,6 +296,24 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_garble_cot(GcArgs a) {
             st_blk(a.tables, 2 * (k - 1) + 1, n, t, TE);
         }
         a.decode[t] = (uint8_t)((acc[0] ^ a.mask) & 1u);   // colour of eq's zero label, mask folded in
+        if (a.sh_gb) {
+            // r05c: the FE share from the output labels (oracle gc_share_garbler). W_0 = the label of
+            // o = eq ^ mask = 0, W_1 = W_0 ^ Delta; (W_0, Delta) play the share C-OT's (q_j, s):
+            // v = H(W_0) mod p, pair[1] = mask ? v + 1 : v - 1, node value r1 = v + mask,
+            // y = lo64(H(W_1)) ^ pair[1]; H = cr_hash (2 AES blocks per test instead of the C-OT's 6)
+            uint32_t h[2][4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                h[0][c] = acc[c] ^ (a.mask ? D[c] : 0u);
+                h[1][c] = h[0][c] ^ D[c];
+            }
+            aes0_mmo_tab<DevOpsX, GcTab, 2>(h, tbl_gc, b0, b1);
+            const uint64_t v = ot_fe_of_u128((uint64_t)h[0][0] | ((uint64_t)h[0][1] << 32),
+                                             (uint64_t)h[0][2] | ((uint64_t)h[0][3] << 32));
+            const uint64_t vp = v + 1 == kOtFeP ? 0 : v + 1, vm = v ? v - 1 : kOtFeP - 1;
+            a.sh_gb[t] = a.mask ? vp : v;
+            a.sh_y[t] = ((uint64_t)h[1][0] | ((uint64_t)h[1][1] << 32)) ^ (a.mask ? vp : vm);
+        }
     }
 }
 
@@ -373,7 +392,15 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
             }
             if constexpr (!FOLD) ld_blk(a.gb_labels, B, n, t, x);   // mask wire (FOLD: in the decoding bit)
             bit = ((acc[0] ^ x[0]) & 1u) ^ a.decode[t];
-            a.out[t] = (uint8_t)bit;
+            if (a.out) a.out[t] = (uint8_t)bit;
+            if (FOLD && a.sh_ev) {
+                // r05c: acc is W_o, o = bit (oracle gc_share_evaluator): o = 0 -> H(W_0) mod p = pair[0],
+                // o = 1 -> lo64(H(W_1)) ^ y = pair[1]
+                uint32_t h[1][4] = {{acc[0], acc[1], acc[2], acc[3]}};
+                aes0_mmo_tab<DevOpsX, GcTab, 1>(h, tbl_gc, b0, b1);
+                const uint64_t hl = (uint64_t)h[0][0] | ((uint64_t)h[0][1] << 32);
+                a.sh_ev[t] = bit ? (hl ^ a.sh_y[t]) : ot_fe_of_u128(hl, (uint64_t)h[0][2] | ((uint64_t)h[0][3] << 32));
+            }
         }
         if (a.out_packed) {
             const uint64_t v = __ballot(bit);

@@ -419,7 +419,8 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
                     uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
-                    uint8_t* ev_active, uint8_t* decode, uint8_t* out) {
+                    uint8_t* ev_active, uint8_t* decode, uint8_t* out, uint64_t* gb_share, uint64_t* ev_share,
+                    uint64_t* share_y) {
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
@@ -428,6 +429,9 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     if (!gb_bits || !ev_bits || !base_seeds || !base_choice || !out) return ctx->fail(FHH_E_ARG, "gc_cot: NULL argument");
     if (!(base_choice[0] & 1)) return ctx->fail(FHH_E_ARG, "gc_cot: s is the free-XOR Delta: its bit 0 must be 1");
     if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gc_cot: n must fit 32 bits");
+    const bool share = gb_share || ev_share || share_y;
+    if (share && !(gb_share && ev_share && share_y))
+        return ctx->fail(FHH_E_ARG, "gc_cot: gb_share, ev_share and share_y go together");
     const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad;
     std::vector<uint64_t> planes[2];
     const uint8_t* src[2] = {gb_bits, ev_bits};
@@ -437,7 +441,7 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
             for (uint32_t j = 0; j < bits; j++)
                 if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
     }
-    DevBuf dp[2], dt, dg, de, da, dd, dout;
+    DevBuf dp[2], dt, dg, de, da, dd, dout, dsh;
     for (int s = 0; s < 2; s++) {
         HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
         HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -448,6 +452,7 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     HIP_TRY(ctx, da.ensure(m * 16));
     HIP_TRY(ctx, dd.ensure(n));
     HIP_TRY(ctx, dout.ensure(n));
+    if (share) HIP_TRY(ctx, dsh.ensure(3 * n * 8));   // [gb | y | ev]
     // 1. the labels OT (OtArgs mode 4): choice bits = the evaluator's planes at OT index j npad + i;
     // the garbler's zero labels q_j, the evaluator's active labels t_j = q_j ^ r_j s
     const uint32_t* rk = nullptr;
@@ -484,12 +489,23 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     // 2. garble on the C-OT's zero labels with the garbler's string and mask folded in, 3. evaluate on the
     // OT'd active labels
     g.ev_ot = 1;
+    if (share) {
+        g.sh_gb = dsh.as<uint64_t>();
+        g.sh_y = g.sh_gb + n;
+    }
     HIP_TRY(ctx, launch_gc_garble(g, ctx->stream));
     g.ev_labels = da.as<uint4>();
+    g.sh_gb = nullptr;
+    if (share) g.sh_ev = dsh.as<uint64_t>() + 2 * n;
     HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
     rc = ctx_sync(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(out, dout.p, n, hipMemcpyDeviceToHost));
+    if (share) {
+        HIP_TRY(ctx, hipMemcpy(gb_share, dsh.p, n * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(share_y, dsh.as<uint64_t>() + n, n * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipMemcpy(ev_share, dsh.as<uint64_t>() + 2 * n, n * 8, hipMemcpyDeviceToHost));
+    }
     if (decode) HIP_TRY(ctx, hipMemcpy(decode, dd.p, n, hipMemcpyDeviceToHost));
     auto soa_to_aos = [&](const DevBuf& d, uint32_t rows_, uint64_t stride, uint8_t* dst) -> int {
         if (!dst || rows_ == 0) return FHH_OK;
@@ -536,6 +552,7 @@ struct PartyState {
     int role = -1;              // 0 garbler / OT sender (server 0), 1 evaluator / OT receiver (server 1)
     int step = 0;               // protocol position (calls must come in order)
     bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
+    bool lshare = false;        // r05c (FE levels): the share from the GC output labels, no OT 2
     // C = this instance's children: the chunk [c_off, c_off + C) of the level's level_C children
     // (child_begin / child_count); covered = children whose OTs are finished
     uint64_t c_off = 0, level_C = 0, covered = 0;
@@ -607,8 +624,9 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
     P.bits = 2 * ctx->d;
     P.tests = P.C * P.n;
     P.per2 = P.last ? 2 : 1;
+    P.lshare = !P.last;
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
-    P.m2 = P.tests * P.per2;
+    P.m2 = P.lshare ? 0 : P.tests * P.per2;   // OT 2 (the share OT) at the FieldElm level only
     if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
     // this server's share planes [C][bits][nw] of the chunk (collect.rs:393-418), zero-padded to the
     // OT's whole choice words (ot_padded(m1) bits)
@@ -682,7 +700,7 @@ int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver, boo
 
 // message sizes
 uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
-uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1); }
+uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1 + (P.lshare ? 8 : 0)); }
 uint64_t y2_bytes(const PartyState& P) { return P.m2 * (P.last ? 16 : 8); }
 
 int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const char* what) {
@@ -693,14 +711,18 @@ int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const cha
     return FHH_OK;
 }
 
-// carve the gc message [tables | decode] (the garbler's string and mask are folded into the circuit:
-// no garbler labels cross, k_gc_garble_cot)
+// carve the gc message [tables | y | decode] (the garbler's string and mask are folded into the circuit:
+// no garbler labels cross, k_gc_garble_cot; y = the FE share's 8 B per test at the FE levels, r05c)
 void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
-    const uint64_t t = P.tests;
+    const uint64_t t = P.tests, tb = (uint64_t)2 * (P.bits - 1) * t * 16;
     g.tables = reinterpret_cast<uint4*>(base);
     g.gb_labels = nullptr;
-    g.decode = base + (uint64_t)2 * (P.bits - 1) * t * 16;
+    g.sh_y = P.lshare ? reinterpret_cast<uint64_t*>(base + tb) : nullptr;
+    g.decode = base + tb + (P.lshare ? 8 * t : 0);
 }
+
+// this chunk's rows of the level's node values (u64 FE, or a BlockPair at the last level)
+uint8_t* party_vals(PartyState& P) { return P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * (P.last ? 16 : 8); }
 
 // the chunk's gate tweaks: the level in bits 40+ (Delta = the labels session's s may serve several levels
 // when base OTs are reused), then the test's index in the whole level (c_off n + t)
@@ -719,10 +741,13 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
     if (rc) return rc;
     PartyState& P = *ctx->party;
     // both OT kinds' receiver schedules and session counters (OtReceiver::init, collect.rs:460)
+    // (kind 1, the share OT, at the FieldElm level only: the FE levels' share rides on the GC, r05c)
     party_session(P, 0, &cfg->base_pairs[0][0][0][0], 128 * 32, P.m1);
-    party_session(P, 1, &cfg->base_pairs[1][0][0][0], 128 * 32, P.m2);
     rc = party_keys(ctx, P, 0, &cfg->base_pairs[0][0][0][0], nullptr);
-    if (!rc) rc = party_keys(ctx, P, 1, &cfg->base_pairs[1][0][0][0], nullptr);
+    if (!rc && !P.lshare) {
+        party_session(P, 1, &cfg->base_pairs[1][0][0][0], 128 * 32, P.m2);
+        rc = party_keys(ctx, P, 1, &cfg->base_pairs[1][0][0][0], nullptr);
+    }
     if (rc) return rc;
     rc = party_ot_buffers(ctx, P, P.m1, true);
     if (rc) return rc;
@@ -756,8 +781,9 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     P.mask = cfg->mask & 1u;
     if (!(cfg->base_choice[0][0] & 1))
         return ctx->fail(FHH_E_ARG, "gb_ot_labels: the labels base OTs' s is the free-XOR Delta: its bit 0 must be 1");
-    // both OT kinds' sender schedules and session counters (OtSender::init, collect.rs:454)
-    for (int w = 0; w < 2; w++) {
+    // the OT kinds' sender schedules and session counters (OtSender::init, collect.rs:454): kind 1 (the
+    // share OT) at the FieldElm level only (r05c)
+    for (int w = 0; w < (P.lshare ? 1 : 2); w++) {
         std::vector<uint8_t> mat((size_t)128 * 16 + 16);
         std::memcpy(mat.data(), &cfg->base_chosen[w][0][0], 128 * 16);
         std::memcpy(mat.data() + 128 * 16, cfg->base_choice[w], 16);
@@ -790,6 +816,8 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     gc_layout(P, P.gc.as<uint8_t>(), P.g);
     P.g.ev_ot = 1;
     P.g.out = nullptr;
+    // r05c: the garbler's node values r1 straight into the level's rows (the y it forms travels in gc)
+    P.g.sh_gb = P.lshare ? reinterpret_cast<uint64_t*>(party_vals(P)) : nullptr;
     // OT 1 as the IKNP correlation (gb_set_fancy_inputs, equalitytest.rs:67-82): q_j is the evaluator's
     // zero label of its share bit j, q_j ^ s its one label, and s = Delta: nothing to send back
     rc = party_ot_buffers(ctx, P, P.m1, false, false);
@@ -859,8 +887,13 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     g.ev_labels = P.labels.as<uint4>();
     g.ev_ot = 1;
     g.out = P.out.as<uint8_t>();
-    g.out_packed = P.choices2.as<uint32_t>();
-    g.out_dup = P.per2;
+    if (P.lshare) {
+        // r05c: its node value from its output label and the gc message's y, straight into the rows
+        g.sh_ev = reinterpret_cast<uint64_t*>(party_vals(P));
+    } else {
+        g.out_packed = P.choices2.as<uint32_t>();
+        g.out_dup = P.per2;
+    }
     if (P.tests) HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
     // 3. OT 2's receiver: choice = the GC output (collect.rs:461-471); T and U reused
     rc = party_ot_buffers(ctx, P, P.m2, true);
@@ -900,7 +933,7 @@ int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const u
         a.mask = P.mask;
         a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
         for (int c = 0; c < 4; c++) a.s[c] = P.s[1][c];
-        a.sx = P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * (P.last ? 16 : 8);
+        a.sx = party_vals(P);
         a.Y0 = P.Y.as<uint4>();
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));
         HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));
@@ -930,7 +963,7 @@ int fhh_ev_ot_shares(fhh_ctx* ctx, const uint8_t* y_dev, uint64_t y_len) {
         a.mode = P.last ? 3 : 2;
         a.choices = P.choices2.as<uint32_t>();
         a.Y0 = const_cast<uint4*>(reinterpret_cast<const uint4*>(y_dev));
-        a.out = reinterpret_cast<uint4*>(P.vals.as<uint8_t>() + P.c_off * P.n * P.per2 * (P.last ? 16 : 8));
+        a.out = reinterpret_cast<uint4*>(party_vals(P));
         HIP_TRY(ctx, launch_ot_recv_hash_rows(a, ctx->stream));
     }
     P.covered = P.c_off + P.C;

@@ -854,7 +854,7 @@ struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
     DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
     DevBuf gc_planes[2], gc_tables, gc_gbl, gc_evl, gc_decode, gc_out;   // cfg->gc (row f1)
-    DevBuf gc_evact, gc_val[2];                                           // cfg->gc = 2: OT buffers
+    DevBuf gc_evact, gc_val[2], gc_y;                                     // cfg->gc = 2: OT / share buffers
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
@@ -1276,11 +1276,13 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         // keep the producer well ahead of the enqueueing: the first levels take ~1 ms of
                         // GPU time against ~9 ms per CO15 instance, so at 4 levels ahead the loop waited
                         // 0.56-0.59 s per 1M crawl (base_ot_stall_ms); 32 levels = 64 instances, 4.3 MB
+                        // (kind 1, the share OT, runs at the FieldElm level only: the FE levels take their
+                        // share from the circuit's output labels, r05c)
                         constexpr uint32_t kAhead = 32;
                         for (uint32_t l = lv; l < std::min(levels, lv + kAhead); l++)
-                            for (uint32_t w = 0; w < 2; w++) (void)B.bot->request(l, w);
+                            for (uint32_t w = 0; w < (l + 1 == levels ? 2u : 1u); w++) (void)B.bot->request(l, w);
                     }
-                    for (uint32_t w = 0; w < 2; w++) {
+                    for (uint32_t w = 0; w < (pmode == 2 ? 2u : 1u); w++) {
                         ot_level_choice(cfg->prf_seed, lv, w, sw_ot[w]);
                         if (B.base_ot) {
                             rc = upload_base_ot(c0, B, lv, w, &rk_ot[w]);
@@ -1347,14 +1349,29 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         if (rc) return rc;
                         g.ev_ot = 1;
                     }
+                    // r05c: at the FE levels the share comes from the circuit's output labels (W_0 and
+                    // W_0 ^ Delta of o = eq ^ mask in the share C-OT's roles): server 0's node value r1 and
+                    // the 8-B y from k_gc_garble_cot, server 1's value from k_gc_eval — no second OT
+                    const bool lshare = real_ot && pmode == 1;
+                    if (lshare) {
+                        for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
+                        HIP_TRY(c0, B.gc_y.ensure(tests * 8));
+                        g.sh_gb = B.gc_val[0].as<uint64_t>();
+                        g.sh_y = B.gc_y.as<uint64_t>();
+                    }
                     HIP_TRY(c0, launch_gc_garble(g, c0->stream));
                     if (real_ot) {
                         g.ev_labels = B.gc_evact.as<uint4>();
-                        // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
-                        uint32_t* och = nullptr;
-                        HIP_TRY(c0, ot_choices_buffer(c0, m2, &och));
-                        g.out_packed = och;
-                        g.out_dup = per2;
+                        g.sh_gb = nullptr;
+                        if (lshare) {
+                            g.sh_ev = B.gc_val[1].as<uint64_t>();
+                        } else {
+                            // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
+                            uint32_t* och = nullptr;
+                            HIP_TRY(c0, ot_choices_buffer(c0, m2, &och));
+                            g.out_packed = och;
+                            g.out_dup = per2;
+                        }
                     }
                     HIP_TRY(c0, launch_gc_eval(g, c0->stream));
                     ChildArgs ca = a;   // this chunk's children
@@ -1363,9 +1380,12 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     ca.gc_out = g.out;
                     ca.gc_N = g.N;
                     ca.gc_mask = g.mask;
-                    if (real_ot) {
-                        // 2. the share conversion by correlated OT (collect.rs:437-471; 846-876 at the
-                        // last level, where a FieldElm travels as a BlockPair = 2 OTs): server 0's pair is
+                    if (lshare) {
+                        ca.ot_val[0] = B.gc_val[0].p;
+                        ca.ot_val[1] = B.gc_val[1].p;
+                    } else if (real_ot) {
+                        // 2. the share conversion by correlated OT (collect.rs:846-876 at the last level,
+                        // where a FieldElm travels as a BlockPair = 2 OTs): server 0's pair is
                         // (H(q_j), H(q_j) +- 1) ordered by its mask, its node value r1 = H(q_j) + mask;
                         // server 1 chooses with its GC output bit
                         const size_t vb = pmode == 1 ? 8 : 16;

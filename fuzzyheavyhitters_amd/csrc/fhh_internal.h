@@ -240,6 +240,13 @@ struct GcArgs {
                                  // (tests t0.. of a 64-aligned wave slice; the FE-share OT choices)
     uint64_t g_off;              // chunk: groups [g_off, g_off + G) of the planes; tests, labels and
                                  // gate tweaks keep their whole-level index (g_off N + t)
+    // r05c (ev_ot, FE levels): the FE share from the output labels instead of a second OT, [G N] each
+    // (oracle gc_share_garbler / gc_share_evaluator): k_gc_garble_cot writes the garbler's node value
+    // r1 = v + mask to sh_gb and the 8-B message y to sh_y; k_gc_eval reads sh_y and writes the
+    // evaluator's node value to sh_ev. Null: no share.
+    uint64_t* sh_gb;
+    uint64_t* sh_y;
+    uint64_t* sh_ev;
 };
 
 struct PruneArgs {

@@ -22,6 +22,7 @@
 
 #include "aes_keyed.h"
 #include "bitslice.h"
+#include "cot_fe.h"
 
 
 namespace fhh {
@@ -255,18 +256,6 @@ __device__ __forceinline__ uint64_t ot_mix64(uint64_t z) {   // SplitMix64's fin
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
-}
-
-constexpr uint64_t kOtFeP = (1ull << 62) - (1ull << 30) - 1;
-
-// a 16-B hash output as a little-endian u128, mod p_FE (p = 2^62 - 2^30 - 1: 2^64 = 2^32 + 4 and
-// 2^62 = 2^30 + 1 mod p); the C-OT's FE value (statistically 2^-66 from uniform)
-__device__ __forceinline__ uint64_t ot_fe_of_u128(uint64_t lo, uint64_t hi) {
-    constexpr uint64_t M62 = (1ull << 62) - 1;
-    const unsigned __int128 x = (unsigned __int128)hi * ((1ull << 32) + 4) + lo;     // < 2^98
-    const unsigned __int128 y = (unsigned __int128)(uint64_t)(x >> 62) * ((1ull << 30) + 1) + ((uint64_t)x & M62);
-    uint64_t z = ((uint64_t)y & M62) + (uint64_t)(y >> 62) * ((1ull << 30) + 1);       // < 2^62 + 2^36
-    return z >= kOtFeP ? z - kOtFeP : z;
 }
 
 // The send hash: one wave per 512-OT tile (transposed in registers + LDS), one OT (2 blocks: q, q ^ s)

@@ -15,7 +15,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import FhhGcBatch, check, lib, ptr
+from ._lib import FhhGcBatch, check, lib, ptr, u64p
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 
@@ -133,12 +133,12 @@ def planes_from_bits(bits_gn: np.ndarray) -> np.ndarray:
 
 
 def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate_base: int = 0,
-                      ctr_off: int = 0):
+                      ctr_off: int = 0, share: bool = False):
     """The labels step on the GPU (fhh_gc_cot_host): the evaluator's input labels by the labels OT (its
     bits are the choice bits; since r05b the IKNP correlation itself: zero label q_j, active label t_j,
     Delta = base_choice, whose bit 0 must be 1), garbling with the garbler's string and mask folded into
     the circuit, evaluation. Returns (out [n], dict of the transcript: tables, ev_zero, ev_active,
-    decode)."""
+    decode; share (r05c): also gb_share, ev_share, share_y — the FE share from the output labels)."""
     g = np.ascontiguousarray(np.asarray(gb_inputs).astype(np.uint8) & 1)
     e = np.ascontiguousarray(np.asarray(ev_inputs).astype(np.uint8) & 1)
     if g.ndim != 2 or g.shape != e.shape:
@@ -149,7 +149,11 @@ def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choi
     tr = {"tables": np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8), "ev_zero": np.zeros((n, bits, 16), np.uint8),
           "ev_active": np.zeros((n, bits, 16), np.uint8), "decode": np.zeros(n, np.uint8)}
     out = np.zeros(n, np.uint8)
+    sh = [np.zeros(n, np.uint64) for _ in range(3)] if share else [None] * 3
     check(lib().fhh_gc_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, gate_base, ptr(seeds),
                                 ptr(s), ctr_off, ptr(tr["tables"]), ptr(tr["ev_zero"]), ptr(tr["ev_active"]),
-                                ptr(tr["decode"]), ptr(out)), kc.handle)
+                                ptr(tr["decode"]), ptr(out), *(None if a is None else ptr(a, u64p) for a in sh)),
+          kc.handle)
+    if share:
+        tr["gb_share"], tr["ev_share"], tr["share_y"] = sh
     return out, tr

@@ -11,7 +11,9 @@ level, collect.rs:454,460):
   * the evaluator (server 1): the base-OT sender's side (its seed, hence both keys of every base OT).
 
 Only protocol messages cross between them: the CO15 messages A and B of each base-OT run, then per
-chunk u1, y1 (empty since r05b: the labels OT needs no reply), gc, u2, y2. In a deployment they go over the servers' channel; here `Channel` copies
+chunk u1, y1 (empty since r05b: the labels OT needs no reply), gc, u2, y2 (both empty at the FE levels
+since r05c: the share rides in gc, taken from the circuit's output labels; the share OT and its base-OT
+run remain at the FieldElm level). In a deployment they go over the servers' channel; here `Channel` copies
 each one into a buffer the receiving party owns (`fhh_memcpy_device`, or a bytes copy for the host
 messages) and counts the bytes. `GarblerParty` and `EvaluatorParty` keep the two sides' state apart;
 nothing of one is handed to the other except through a Channel.
@@ -120,8 +122,10 @@ class GarblerParty:
         kinds; the labels kind's s is the circuit's Delta)."""
         cfg = FhhGbCfg()
         cfg.mask = os.urandom(1)[0] & 1
-        chosen = np.stack([b[0] for b in base])      # [2][128][16]
-        choice = np.stack([b[1] for b in base])      # [2][16]
+        chosen = np.zeros((2, 128, 16), np.uint8)    # [kind][128][16]; kind 1 only at the FieldElm level
+        choice = np.zeros((2, 16), np.uint8)
+        for w, b in enumerate(base):
+            chosen[w], choice[w] = b[0], b[1]
         ctypes.memmove(cfg.base_chosen, chosen.tobytes(), chosen.nbytes)
         ctypes.memmove(cfg.base_choice, choice.tobytes(), choice.nbytes)
         cfg.child_begin, cfg.child_count = child_begin, child_count
@@ -151,7 +155,9 @@ class EvaluatorParty:
     @staticmethod
     def chunk_cfg(base, child_begin: int, child_count: int) -> FhhEvCfg:
         cfg = FhhEvCfg()
-        pairs = np.stack(base)                       # [2][128][2][16]
+        pairs = np.zeros((2, 128, 2, 16), np.uint8)  # [kind][128][2][16]; kind 1 only at the FieldElm level
+        for w, b in enumerate(base):
+            pairs[w] = b
         ctypes.memmove(cfg.base_pairs, pairs.tobytes(), pairs.nbytes)
         cfg.child_begin, cfg.child_count = child_begin, child_count
         return cfg
@@ -285,16 +291,18 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
         nworkers = base_ot_workers or min(16, os.cpu_count() or 4)
         pool = ThreadPoolExecutor(max_workers=nworkers)
 
-        def runs(k):
+        def runs(k, kinds):
             gbp, evp = parties[k]
             to_gb, to_ev = chans[k]
-            return [base_ot_run(gbp, evp, to_gb, to_ev, colour=(w == 0)) for w in range(2)]   # kind 0 labels, 1 shares
+            # kind 0 labels (s = Delta: colour bit), kind 1 the share OT — at the FieldElm level only (r05c)
+            return [base_ot_run(gbp, evp, to_gb, to_ev, colour=(w == 0)) for w in range(kinds)]
 
         def submit(lv):
             key = 0 if base_ot_every == "crawl" else lv
+            kinds = 2 if (base_ot_every == "crawl" or lv == L - 1) else 1
             for k in range(len(shards)):
                 if shard_clients[k] and (key, k) not in pending:
-                    pending[(key, k)] = pool.submit(runs, k)
+                    pending[(key, k)] = pool.submit(runs, k, kinds)
 
         for lv in range(min(L, base_ot_ahead)):
             submit(lv)

@@ -537,11 +537,18 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
  * decode = eq ^ mask). No label PRG, no garbler labels and no labels-OT reply on the wire; gate tweaks
  * 2 g, 2 g + 1 with g = gate_base + t (bits - 1) + k as in fhh_gc_batch. Outputs AoS: tables
  * [n][bits-1][2][16], ev_zero / ev_active [n][bits][16], decode [n], out [n]; any but `out` may be
- * NULL. */
+ * NULL. r05c, the FE share from the output labels (the party ABI's FE levels): with gb_share, ev_share
+ * and share_y (uint64_t[n] each, all three or none) the garbler also forms the share pair from the
+ * labels of o = eq ^ mask — W_0 (o = 0) and W_1 = W_0 ^ Delta in the roles of the share C-OT's q_j and
+ * q_j ^ s: v = H(W_0) as a LE u128 mod p, node value r1 = v + mask (gb_share), y = lo64(H(W_1)) ^
+ * (mask ? v + 1 : v - 1) (share_y, 8 B per test) — and the evaluator its node value from W_o: o ?
+ * lo64(H(W_o)) ^ y : H(W_o) mod p (ev_share). H = cr_hash; gb_share - ev_share = eq ^ ... = the
+ * test's equality bit mod p, as FHH_COT_FE gives it. */
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
                     uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* tables, uint8_t* ev_zero,
-                    uint8_t* ev_active, uint8_t* decode, uint8_t* out);
+                    uint8_t* ev_active, uint8_t* decode, uint8_t* out, uint64_t* gb_share, uint64_t* ev_share,
+                    uint64_t* share_y);
 
 /* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
  * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;
@@ -549,7 +556,8 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * fhh_tree_crawl / fhh_tree_crawl_last, with only its OWN secrets — the garbler's fhh_gb_cfg and the
  * evaluator's fhh_ev_cfg share nothing (each server draws its material itself: AesRng::new() per
  * channel, collect.rs:431; base OTs by fhh_co15_* over the channel, OtSender / OtReceiver::init,
- * collect.rs:454,460). Four byte buffers cross per chunk, in this order (y1 has 0 bytes since r05b):
+ * collect.rs:454,460). Four byte buffers cross per chunk, in this order (y1 has 0 bytes since r05b; at
+ * the FE levels u2 and y2 have 0 bytes too since r05c — the share rides in gc — so two carry data):
  *   server 0 (garbler, OT sender)                          server 1 (evaluator, OT receiver)
  *                                      <--------------  fhh_ev_ot_labels(ev_cfg) -> u1
  *   fhh_gb_ot_labels(gb_cfg, u1) -> y1 (empty)
@@ -558,14 +566,16 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  *   fhh_party_node_sums                                  fhh_party_node_sums
  * Outputs are device buffers owned by the producing ctx, valid until its next party call; inputs are
  * device pointers on the receiving ctx's GPU (the caller moves the bytes: a network in a deployment, a
- * device copy in the in-process tests). Both OTs are correlated OTs (fhh_cot_extend_host's modes):
- * OT 1 (FHH_COT_RAW) delivers the evaluator's input labels (m = C x 2d x npad: its share planes are
- * the choice bits; the garbler's labels-kind s is the circuit's Delta, so no reply crosses), OT 2
- * (FHH_COT_FE, FHH_COT_FE255 at tree_crawl_last: 2 OTs per test) the share; the circuit is
- * fhh_gc_cot_host's (the garbler's string and mask folded in). gc = [tables (bits-1) x 2 | decode 1 B]
+ * device copy in the in-process tests). OT 1 (FHH_COT_RAW) delivers the evaluator's input labels
+ * (m = C x 2d x npad: its share planes are the choice bits; the garbler's labels-kind s is the
+ * circuit's Delta, so no reply crosses). The share: at the FE levels (r05c) from the circuit's output
+ * labels (fhh_gc_cot_host's share outputs: the garbler's r1 and y from W_0, W_0 ^ Delta, the evaluator's
+ * value from its W_o), so no second OT runs and the OT kind 1 base material is not read; at
+ * tree_crawl_last by OT 2 (FHH_COT_FE255: 2 OTs per test). The circuit is fhh_gc_cot_host's (the
+ * garbler's string and mask folded in). gc = [tables (bits-1) x 2 | y 8 B (FE levels) | decode 1 B]
  * per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
- * y1 0 B, y2 8 B per OT (FE) or 16 B per OT (FieldElm). Each server's node values (the garbler's
- * r1 = v + mask, the evaluator's OT output) stay on its device; fhh_party_node_sums sums them: non-last
+ * y1 0 B; u2 / y2: 0 B at the FE levels, FieldElm level: U and 16 B per OT. Each server's node values
+ * (the garbler's r1 = v + mask, the evaluator's share output) stay on its device; fhh_party_node_sums sums them: non-last
  * level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm (the
  * frontier_last values). For a multi-device ctx run each shard (fhh_shard_ctx) with its own channel,
  * as the reference runs a level's tests over several channels (collect.rs:423-430).
@@ -582,14 +592,16 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
 typedef struct fhh_gb_cfg {
     uint32_t mask;                       /* the chunk's mask bit (equalitytest.rs:38-43)           */
     uint32_t pad_;
-    uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares): k_i^{s_i} from the   */
+    uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares — read at tree_crawl_last
+                                            only since r05c): k_i^{s_i} from the                    */
     uint8_t base_choice[2][16];          /* base OTs, and s (bit i % 8 of byte i / 8); the labels
                                             kind's s is the free-XOR Delta: its bit 0 must be 1   */
     uint64_t child_begin;
     uint64_t child_count;
 } fhh_gb_cfg;
 typedef struct fhh_ev_cfg {
-    uint8_t base_pairs[2][128][2][16];   /* per OT kind: both base-OT keys of every base OT        */
+    uint8_t base_pairs[2][128][2][16];   /* per OT kind: both base-OT keys of every base OT (kind 1
+                                            read at tree_crawl_last only, r05c)                    */
     uint64_t child_begin;
     uint64_t child_count;
 } fhh_ev_cfg;

@@ -967,6 +967,41 @@ static void gc_xor(uint8_t* d, const uint8_t* a, const uint8_t* b) {
     for (int k = 0; k < 16; k++) d[k] = a[k] ^ b[k];
 }
 
+static void ot_cr_hash(const uint8_t x[16], uint8_t out[16]);
+static uint64_t cot_fe_of_block(const uint8_t b[16]);
+
+/* r05c: the FE share from the circuit's output labels instead of a second OT. The output wire
+ * o = eq ^ mask has the labels W_0 (o = 0) and W_1 = W_0 ^ D; the evaluator holds W_o and knows o.
+ * That is the correlated-OT situation of orc_cot_extend mode 2 with (q_j, s) = (W_0, D) and the
+ * evaluator's GC output as its choice, so the same pair is formed from the same hash: v = H(W_0) as a
+ * little-endian u128 mod p, pair[0] = v, pair[1] = mask ? v + 1 : v - 1, the garbler's node value
+ * r1 = v + mask, y = lo64(H(W_1)) ^ pair[1] (8 B); the evaluator's value = o ? lo64(H(W_o)) ^ y : H(W_o)
+ * mod p. H = cr_hash (pi(x) ^ x), as the OT's. collect.rs:437-452 (the pair and its order). */
+static void gc_share_garbler(const uint8_t eq0[16], const uint8_t D[16], uint32_t mask, uint64_t* gv_out,
+                             uint64_t* y_out) {
+    uint8_t w0[16], w1[16], h0[16], h1[16];
+    memcpy(w0, eq0, 16);
+    if (mask & 1) gc_xor(w0, w0, D);          /* o = 0 <=> eq = mask */
+    gc_xor(w1, w0, D);
+    ot_cr_hash(w0, h0);
+    ot_cr_hash(w1, h1);
+    const uint64_t v = cot_fe_of_block(h0);
+    const uint64_t gv = (mask & 1) ? (v + 1 == FE_P ? 0 : v + 1) : v;     /* r1 = v + mask */
+    const uint64_t p1 = (mask & 1) ? gv : (v == 0 ? FE_P - 1 : v - 1);     /* pair[1] */
+    uint64_t hl;
+    memcpy(&hl, h1, 8);
+    *gv_out = gv;
+    *y_out = hl ^ p1;
+}
+
+static uint64_t gc_share_evaluator(const uint8_t w[16], int o, uint64_t y) {
+    uint8_t h[16];
+    ot_cr_hash(w, h);
+    uint64_t hl;
+    memcpy(&hl, h, 8);
+    return o ? (hl ^ y) : cot_fe_of_block(h);
+}
+
 /* Garbler (multiple_gb_equality_test, :25-64) for n tests of `bits` bits with an ideal OT for the
  * evaluator's labels. Layouts: tables [n][bits-1][2][16], gb_labels [n][bits+1][16] (mask last),
  * ev_labels [n][bits][16]. Every zero label is AES_key(LE128(nonce + t S + w)), S = the power of two
@@ -1056,8 +1091,11 @@ void orc_gc_garble_eq(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const u
  * goes into the decoding bit: decode = colour(out^0) ^ mask. No label is drawn (no label key) and no
  * garbler label is sent. Same circuit as bin_eq_bundles / and_many (:128-189). Layouts: tables
  * [n][bits-1][2][16], decode [n]. */
-void orc_gc_garble_eq_cot(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
-                          const uint8_t delta_in[16], uint64_t gate_base, uint8_t* tables, uint8_t* decode) {
+/* gb_share / share_y (r05c, both or neither): the garbler's node value and the 8-B message per test
+ * (gc_share_garbler). */
+void orc_gc_garble_eq_cot_share(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero,
+                                uint32_t mask, const uint8_t delta_in[16], uint64_t gate_base, uint8_t* tables,
+                                uint8_t* decode, uint64_t* gb_share, uint64_t* share_y) {
     oracle_init();
     uint8_t D[16];
     memcpy(D, delta_in, 16);
@@ -1100,13 +1138,22 @@ void orc_gc_garble_eq_cot(uint64_t n, uint32_t bits, const uint8_t* gb_bits, con
             gc_xor(acc, WG, WE);
         }
         decode[t] = (uint8_t)((acc[0] ^ mask) & 1);   /* colour of eq's zero label, mask folded in */
+        if (gb_share) gc_share_garbler(acc, D, mask, gb_share + t, share_y + t);
     }
+}
+
+void orc_gc_garble_eq_cot(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
+                          const uint8_t delta_in[16], uint64_t gate_base, uint8_t* tables, uint8_t* decode) {
+    orc_gc_garble_eq_cot_share(n, bits, gb_bits, ev_zero, mask, delta_in, gate_base, tables, decode, NULL, NULL);
 }
 
 /* The r05 evaluator: its OT'd labels ev_active [n][bits][16] are the inputs' active labels;
  * out[t] = colour(acc) ^ decode[t] = eq ^ mask. */
-void orc_gc_eval_eq_cot(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* ev_active,
-                        const uint8_t* decode, uint64_t gate_base, uint8_t* out) {
+/* share_y / ev_share (r05c, both or neither): the evaluator's node value from its output label
+ * (gc_share_evaluator). */
+void orc_gc_eval_eq_cot_share(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* ev_active,
+                              const uint8_t* decode, uint64_t gate_base, uint8_t* out, const uint64_t* share_y,
+                              uint64_t* ev_share) {
     oracle_init();
 #pragma omp parallel for schedule(static)
     for (int64_t t = 0; t < (int64_t)n; t++) {
@@ -1129,7 +1176,13 @@ void orc_gc_eval_eq_cot(uint64_t n, uint32_t bits, const uint8_t* tables, const 
             gc_xor(acc, hA, hB);
         }
         out[t] = (uint8_t)((acc[0] & 1) ^ decode[t]);
+        if (ev_share) ev_share[t] = gc_share_evaluator(acc, out[t], share_y[t]);
     }
+}
+
+void orc_gc_eval_eq_cot(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* ev_active,
+                        const uint8_t* decode, uint64_t gate_base, uint8_t* out) {
+    orc_gc_eval_eq_cot_share(n, bits, tables, ev_active, decode, gate_base, out, NULL, NULL);
 }
 
 /* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */

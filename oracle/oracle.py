@@ -725,31 +725,40 @@ def gc_get_ni() -> bool:
     return bool(lib().orc_gc_get_ni())
 
 
-def gc_garble_eq_cot(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, delta: bytes, gate_base: int = 0):
+def gc_garble_eq_cot(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, delta: bytes, gate_base: int = 0,
+                     share: bool = False):
     """The r05 garbler (fhh_oracle.c orc_gc_garble_eq_cot): the evaluator's zero labels ev_zero
     [n][bits][16] come from the labels C-OT; the garbler's string and mask are folded into the circuit.
-    Returns (tables [n][bits-1][2][16], decode [n])."""
+    Returns (tables [n][bits-1][2][16], decode [n]); share (r05c, orc_gc_garble_eq_cot_share): also
+    the garbler's FE node values [n] and the 8-B share message y [n] from the output labels."""
     g = np.ascontiguousarray(gb_bits, np.uint8)
     z = np.ascontiguousarray(ev_zero, np.uint8)
     n, bits = g.shape
     tables = np.zeros((n, max(bits - 1, 0), 2, 16), np.uint8)
     dec = np.zeros(n, np.uint8)
     d = np.frombuffer(delta, np.uint8).copy()
-    lib().orc_gc_garble_eq_cot(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z), ctypes.c_uint32(mask & 1),
-                               _p(d), ctypes.c_uint64(gate_base), _p(tables), _p(dec))
-    return tables, dec
+    gv = np.zeros(n, np.uint64) if share else None
+    y = np.zeros(n, np.uint64) if share else None
+    lib().orc_gc_garble_eq_cot_share(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z),
+                                     ctypes.c_uint32(mask & 1), _p(d), ctypes.c_uint64(gate_base), _p(tables),
+                                     _p(dec), None if gv is None else _p(gv), None if y is None else _p(y))
+    return (tables, dec, gv, y) if share else (tables, dec)
 
 
-def gc_eval_eq_cot(tables, ev_active, decode, gate_base: int = 0) -> np.ndarray:
-    """The r05 evaluator: out [n] = eq ^ mask from its OT'd labels ev_active [n][bits][16]."""
+def gc_eval_eq_cot(tables, ev_active, decode, gate_base: int = 0, share_y=None):
+    """The r05 evaluator: out [n] = eq ^ mask from its OT'd labels ev_active [n][bits][16]; with share_y
+    (r05c) also its FE node values [n] from its output label: returns (out, values)."""
     t = np.ascontiguousarray(tables, np.uint8)
     e = np.ascontiguousarray(ev_active, np.uint8)
     d = np.ascontiguousarray(decode, np.uint8)
     n, bits = e.shape[0], e.shape[1]
     out = np.zeros(n, np.uint8)
-    lib().orc_gc_eval_eq_cot(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(t), _p(e), _p(d),
-                             ctypes.c_uint64(gate_base), _p(out))
-    return out
+    y = None if share_y is None else np.ascontiguousarray(share_y, np.uint64)
+    ev = np.zeros(n, np.uint64) if y is not None else None
+    lib().orc_gc_eval_eq_cot_share(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(t), _p(e), _p(d),
+                                   ctypes.c_uint64(gate_base), _p(out), None if y is None else _p(y),
+                                   None if ev is None else _p(ev))
+    return (out, ev) if y is not None else out
 
 
 COT_LABELS, COT_FE, COT_FE255, COT_RAW = 1, 2, 3, 4

@@ -207,7 +207,7 @@ def test_gpu_crawl_gc_rejects_count_mode():
 
 
 # ---- r05: the evaluator's labels by correlated OT, the garbler's string folded in --------------------
-def _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
+def _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0, share=False):
     """The labels OT (r05b: the IKNP correlation itself; choice bits: the evaluator's bits at OT index
     j npad + i), garbling on its zero labels q_j with Delta = s and the garbler's string and mask folded
     in, evaluation on the evaluator's t_j — all in the oracle."""
@@ -219,6 +219,11 @@ def _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
     q, t_rows, u, _ = oracle.cot_extend(oracle.COT_RAW, ch, seeds, s, ctr_off=ctr_off)
     ev_zero = np.stack([q[k * npad: k * npad + n] for k in range(bits)], axis=1)
     ev_act = np.stack([t_rows[k * npad: k * npad + n] for k in range(bits)], axis=1)
+    if share:   # r05c: the FE share from the output labels
+        t, d, gv, y = oracle.gc_garble_eq_cot(g, ev_zero, mask, s, gate_base=gate_base, share=True)
+        res, ev = oracle.gc_eval_eq_cot(t, ev_act, d, gate_base=gate_base, share_y=y)
+        return res, dict(tables=t, ev_zero=ev_zero, ev_active=ev_act, decode=d, gb_share=gv, ev_share=ev,
+                         share_y=y)
     t, d = oracle.gc_garble_eq_cot(g, ev_zero, mask, s, gate_base=gate_base)
     res = oracle.gc_eval_eq_cot(t, ev_act, d, gate_base=gate_base)
     return res, dict(tables=t, ev_zero=ev_zero, ev_active=ev_act, decode=d)
@@ -270,3 +275,53 @@ def test_gpu_cot_labels_chain_bit_exact(oracle, n, bits):
             assert np.array_equal(tr[k], etr[k]), k
         assert np.array_equal(out, exp)
         assert np.array_equal(out ^ mask, (g == e).all(axis=1).astype(np.uint8))
+
+
+# ---- r05c: the FE share from the circuit's output labels (no second OT at the FE levels) -----------
+FE_P = (1 << 62) - (1 << 30) - 1
+
+
+@pytest.mark.parametrize("bits", [2, 4])
+def test_oracle_output_label_share_functional(oracle, bits):
+    """The share pair of collect.rs:437-452 from the output labels: gb_share - ev_share = eq (mod p) for
+    every test and both masks (so the level sums reconstruct the plaintext counts): the evaluator's value
+    is pair[o] of the garbler's (v, mask ? v + 1 : v - 1) and gb_share = v + mask; values are canonical
+    FE (< p); y depends on Delta."""
+    rng = np.random.default_rng(70 + bits)
+    g, e = _cases(rng, 500, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    for mask in (0, 1):
+        out, tr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=3, share=True)
+        eq = (g == e).all(axis=1)
+        assert np.array_equal(out ^ mask, eq.astype(np.uint8))
+        gv, ev = tr["gb_share"].astype(object), tr["ev_share"].astype(object)
+        assert all(int(x) < FE_P for x in tr["gb_share"]) and all(int(x) < FE_P for x in tr["ev_share"])
+        assert np.array_equal(((gv - ev) % FE_P).astype(np.uint64), eq.astype(np.uint64))
+        # y hides pair[1] behind H(W_1): a different Delta gives different messages
+        s2 = bytes([s[0]]) + bytes((b ^ 0x5A) for b in s[1:])
+        _, tr2 = _oracle_cot_chain(oracle, g, e, mask, seeds, s2, gate_base=3, share=True)
+        assert not np.array_equal(tr2["share_y"], tr["share_y"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bits", [(1, 2), (65, 2), (1000, 2), (4097, 4), (130, 8)])
+def test_gpu_output_label_share_bit_exact(oracle, n, bits):
+    """fhh_gc_cot_host's share outputs (k_gc_garble_cot's node values and y, k_gc_eval's node values)
+    = the oracle's, bit for bit, with the rest of the transcript unchanged; gb - ev = eq mod p."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    rng = np.random.default_rng(n * 5 + bits)
+    g, e = _cases(rng, n, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    kc = fhh.KeyCollection(8, 1)
+    for mask, ctr in ((0, 0), (1, 256)):
+        out, tr = gc.equality_test_cot(kc, g, e, mask, seeds, s, gate_base=9, ctr_off=ctr, share=True)
+        exp, etr = _oracle_cot_chain(oracle, g, e, mask, seeds, s, gate_base=9, ctr_off=ctr, share=True)
+        for k in ("ev_zero", "ev_active", "tables", "decode", "gb_share", "share_y", "ev_share"):
+            assert np.array_equal(tr[k], etr[k]), k
+        assert np.array_equal(out, exp)
+        eq = (g == e).all(axis=1).astype(np.uint64)
+        assert np.array_equal(((tr["gb_share"].astype(object) - tr["ev_share"].astype(object)) % FE_P)
+                              .astype(np.uint64), eq)

@@ -47,8 +47,8 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     got = fhh.two_party_crawl(p0, p1, thr, prf_seed=77, channel=channel, material=material)
     _assert_same_crawl(ref, got)
     assert len(got.final) > 0
-    if material == "fresh":   # two CO15 runs per level (labels, shares), A + 128 B points each
-        assert got.base_ot_runs == 2 * L and got.base_ot_bytes == 2 * L * 65 * 129
+    if material == "fresh":   # one CO15 run per level (labels) + the FieldElm level's share OT, A + 128 B each
+        assert got.base_ot_runs == L + 1 and got.base_ot_bytes == (L + 1) * 65 * 129
     t = max(1, int(thr * n))
     cnt, paths, vals = workload.plaintext_crawl(wl.left, wl.right, t, t)
     assert sorted(tuple(tuple(int(b) for b in p) for p in r.path) for r in got.final) == sorted(paths)
@@ -56,10 +56,14 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     lb = got.level_bytes[0]
     C0, bits = int(got.level_children[0]), 2 * d
     npad = (n + 63) // 64 * 64
-    assert lb["gc"] == C0 * n * (2 * (bits - 1) * 16 + 1)   # tables + decoding bit (garbler string folded in)
-    # r05b: the labels OT is the IKNP correlation itself (no reply); one 8-B y per FE share OT
+    # tables + the FE share's 8-B y (r05c: from the output labels) + decoding bit (garbler string folded in)
+    assert lb["gc"] == C0 * n * (2 * (bits - 1) * 16 + 8 + 1)
+    # r05b: the labels OT is the IKNP correlation itself (no reply); r05c: no share OT at the FE levels
     assert lb["u1"] == 16 * ((C0 * bits * npad + 8191) // 8192 * 8192)
-    assert lb["y1"] == 0 and lb["y2"] == C0 * n * 8
+    assert lb["y1"] == 0 and lb["u2"] == 0 and lb["y2"] == 0
+    # the FieldElm level keeps its share OT: U and 16 B per OT, 2 OTs per test
+    lbl, Cl = got.level_bytes[-1], int(got.level_children[-1])
+    assert lbl["gc"] == Cl * n * (2 * (bits - 1) * 16 + 1) and lbl["y2"] == Cl * n * 2 * 16
 
 
 def test_two_party_fresh_randomness_same_output():
@@ -78,7 +82,7 @@ def test_two_party_fresh_randomness_same_output():
         runs.append(fhh.two_party_crawl(a0, a1, 0.02, **kw))
     for r in runs[1:]:
         _assert_same_crawl(runs[0], r)
-    assert runs[3].base_ot_runs == 2 and runs[1].base_ot_runs == 2 * L
+    assert runs[3].base_ot_runs == 2 and runs[1].base_ot_runs == L + 1
 
 
 @pytest.mark.parametrize("channel", ["copy", "inplace"])
@@ -125,8 +129,9 @@ def test_party_calls_out_of_order_refused():
 @pytest.mark.parametrize("chunk", [None, 150], ids=["whole-levels", "chunks-of-150"])
 def test_two_party_configs1_full_size(chunk):
     """configs[1] at full size (100 000 Zipf clients, data_len 512, threshold 0.001): the split
-    GC + OT crawl — each server drawing its own material, and every level's two OT extensions on
-    Chou–Orlandi base OTs run between the servers over the channel (1 024 runs) — equals the
+    GC + OT crawl — each server drawing its own material, and every level's OT extension on
+    Chou–Orlandi base OTs run between the servers over the channel (513 runs: the share OT at the
+    FieldElm level only) — equals the
     in-process GC + OT crawl level by level, and both equal the plaintext recount (222 heavy hitters);
     with each level's tests in one protocol instance, and in chunks of 150 children, one instance per
     chunk (the 1M configuration's shape). Prints the bytes that would cross the channel."""
@@ -142,7 +147,7 @@ def test_two_party_configs1_full_size(chunk):
                               chunk_children=chunk, channel="inplace" if chunk else "copy")
     _assert_same_crawl(ref, got)
     assert len(got.final) == 222
-    assert got.base_ot_runs == 2 * L
+    assert got.base_ot_runs == L + 1
     print(f"base OTs: {got.base_ot_runs} CO15 runs, {got.base_ot_bytes} B, crawl waited {got.base_ot_wait_s:.3f} s")
     if chunk:
         assert max(got.level_children) > chunk

@@ -662,10 +662,12 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
         "base_ot_stall_ms": s0["base_ot_stall_ms"],
         "base_ot_note": "compute = summed per-instance CO15 + key-schedule time over the host threads; stall = time "
                         "the level loop waited for an instance it needed (the base OTs on the critical path)",
-        "protocol": "GC (half-gates, TCCR; the garbler's string and mask folded in) + the evaluator's labels as "
-                    "the IKNP correlation (Delta = the labels OT's s, no reply) + the FE share from the circuit's "
-                    "output labels (cr_hash of W_0, W_0 ^ Delta; the FieldElm level by ALSZ correlated OT) "
-                    "(21 AES blocks per d=1 test: garble 8 + 2, evaluate 4 + 1, labels OT expands 2 x 3)",
+        "protocol": "the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); FE "
+                    "levels: equality + share as one garbled table per test (Yao's garbled gate with "
+                    "point-and-permute over the 2d input labels, rows keyed by cr_hash, 8 B per row; the "
+                    "garbler's string and mask folded in); the FieldElm level: half-gates GC (TCCR) + ALSZ "
+                    "correlated OT for the share (11 AES blocks per d=1 FE-level test: table 4 + 1, labels OT "
+                    "expands 2 x 3)",
         "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
         "expand_gpu_ms": s0["expand_ms"],
         "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,

@@ -414,6 +414,184 @@ __global__ __launch_bounds__(kGcThreads) void k_gc_eval(GcArgs a) {
     }
 }
 
+// ---- r05d: the FE levels' equality test + share as one garbled table ----------------------------
+// Yao's garbled gate with point-and-permute for the b-input gate "the share of eq ^ mask" (oracle
+// orc_gt_garble / orc_gt_eval): the inputs are the folded garbler's Z_k (as
+// k_gc_garble_cot), the evaluator's OT'd t_k is z_k's active label and its colours name its row r.
+// Row r's key H(K_r), K_r = XOR_k sigma^k(label of z_k in row r) ^ tweak (sigma = doubling in
+// GF(2^128)), H = cr_hash; row 0 carries no message (its value is H(K_0) mod p), rows 1 .. 2^b - 1
+// send lo64(H(K_r)) ^ pair[o_r]. Garbler 2^b AES per test (4 at d = 1, against 8 + 2 for half-gates +
+// the output-label share), evaluator 1 (against 4 + 1).
+__device__ __forceinline__ void gf_dbl(uint32_t (&x)[4]) {
+    const uint32_t carry = x[3] >> 31;
+    x[3] = (x[3] << 1) | (x[2] >> 31);
+    x[2] = (x[2] << 1) | (x[1] >> 31);
+    x[1] = (x[1] << 1) | (x[0] >> 31);
+    x[0] = (x[0] << 1) ^ (carry ? 0x87u : 0u);
+}
+
+__device__ __forceinline__ uint64_t fe_inc(uint64_t v) { return v + 1 == kOtFeP ? 0 : v + 1; }
+__device__ __forceinline__ uint64_t fe_dec(uint64_t v) { return v ? v - 1 : kOtFeP - 1; }
+
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
+    __shared__ uint32_t tbl_gc[GcTab::kWords];
+    if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;   // no tests: skip the table fill
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(threadIdx.x & 63, b0, b1);
+    constexpr uint32_t R = 1u << B;
+    constexpr int NB = R < 4 ? (int)R : 4;   // rows per AES pass
+    const uint64_t n = a.G * a.N;
+    const uint64_t Npad = (uint64_t)a.nw * 64;
+    uint32_t Dk[B][4];   // sigma^k(Delta)
+#pragma unroll
+    for (int c = 0; c < 4; c++) Dk[0][c] = a.delta[c];
+#pragma unroll
+    for (int k = 1; k < B; k++) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) Dk[k][c] = Dk[k - 1][c];
+        gf_dbl(Dk[k]);
+    }
+    const uint64_t n_act = gc_active(a);
+    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
+        const uint64_t g = t / a.N;
+        const uint32_t i = (uint32_t)(t - g * a.N);
+        const uint64_t tw = a.gate_base + a.g_off * a.N + t;   // the test's index in the whole level
+        uint32_t S[4] = {0u, 0u, 0u, 0u}, col = 0;
+#pragma unroll
+        for (int k = B - 1; k >= 0; k--) {   // Horner: S = sigma(S) ^ Z_k
+            uint32_t z[4];
+            ld_blk(a.ev_labels, g * B + k, Npad, i, z);   // E_k, the labels OT's q
+            const uint32_t xb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
+            gf_dbl(S);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                z[c] ^= xb ? 0u : a.delta[c];   // Z_k = E_k ^ (x_k ? 0 : Delta)
+                S[c] ^= z[c];
+            }
+            col |= (z[0] & 1u) << k;
+        }
+        S[0] ^= (uint32_t)tw;
+        S[1] ^= (uint32_t)(tw >> 32);
+        const uint32_t rstar = ~col & (R - 1);   // the row whose z are all 1 (eq = 1)
+        uint64_t p0 = 0, p1 = 0;
+#pragma unroll
+        for (uint32_t pass = 0; pass < R / NB; pass++) {
+            uint32_t h[NB][4];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const uint32_t flip = (pass * NB + j) ^ col;   // z_k of the row = bit k of r ^ col
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    uint32_t w = S[c];
+#pragma unroll
+                    for (int k = 0; k < B; k++) w ^= ((flip >> k) & 1u) ? Dk[k][c] : 0u;
+                    h[j][c] = w;
+                }
+            }
+            aes0_mmo_tab<DevOpsX, GcTab, NB>(h, tbl_gc, b0, b1);   // cr_hash: pi(K) ^ K
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const uint32_t r = pass * NB + j;
+                const uint32_t o = (uint32_t)(r == rstar) ^ a.mask;
+                const uint64_t hl = (uint64_t)h[j][0] | ((uint64_t)h[j][1] << 32);
+                if (r == 0) {   // row 0's value pair[o_0] is H(K_0) mod p: it fixes v
+                    const uint64_t hv = ot_fe_of_u128(hl, (uint64_t)h[j][2] | ((uint64_t)h[j][3] << 32));
+                    const uint64_t v = o == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
+                    p0 = v;
+                    p1 = a.mask ? fe_inc(v) : fe_dec(v);
+                    a.sh_gb[t] = a.mask ? fe_inc(v) : v;   // r1 = v + mask
+                } else {
+                    a.gt_msgs[(uint64_t)(r - 1) * n + t] = hl ^ (o ? p1 : p0);
+                }
+            }
+        }
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gt_eval(GcArgs a) {
+    __shared__ uint32_t tbl_gc[GcTab::kWords];
+    if ((uint64_t)blockIdx.x * kGcThreads >= gc_active(a)) return;
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(threadIdx.x & 63, b0, b1);
+    const uint64_t n = a.G * a.N;
+    const uint64_t Npad = (uint64_t)a.nw * 64;
+    const uint64_t n_act = gc_active(a);
+    // two tests per lane per pass (2 AES blocks in flight)
+    const uint64_t stride = (uint64_t)gridDim.x * kGcThreads;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t0 < n_act; t0 += 2 * stride) {
+        uint32_t h[2][4], row[2];
+        uint64_t tt[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t t = t0 + u * stride;
+            tt[u] = t;
+            const uint64_t tc = t < n_act ? t : t0;   // a valid test for the padding block
+            const uint64_t g = tc / a.N;
+            const uint32_t i = (uint32_t)(tc - g * a.N);
+            const uint64_t tw = a.gate_base + a.g_off * a.N + tc;
+            uint32_t S[4] = {0u, 0u, 0u, 0u}, r = 0;
+#pragma unroll
+            for (int k = B - 1; k >= 0; k--) {
+                uint32_t z[4];
+                ld_blk(a.ev_labels, g * B + k, Npad, i, z);   // t_k, z_k's active label
+                gf_dbl(S);
+#pragma unroll
+                for (int c = 0; c < 4; c++) S[c] ^= z[c];
+                r |= (z[0] & 1u) << k;
+            }
+            S[0] ^= (uint32_t)tw;
+            S[1] ^= (uint32_t)(tw >> 32);
+#pragma unroll
+            for (int c = 0; c < 4; c++) h[u][c] = S[c];
+            row[u] = r;
+        }
+        aes0_mmo_tab<DevOpsX, GcTab, 2>(h, tbl_gc, b0, b1);
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t t = tt[u];
+            if (t >= n_act) continue;
+            const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
+            a.sh_ev[t] = row[u] ? (hl ^ a.gt_msgs[(uint64_t)(row[u] - 1) * n + t])
+                                : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
+        }
+    }
+}
+
+template <int B>
+static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const uint64_t n = a.G * a.N;
+    const uint64_t need = (n + kGcThreads - 1) / kGcThreads;
+    const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
+    if (garble) hipLaunchKernelGGL(k_gt_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    else hipLaunchKernelGGL(k_gt_eval<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+static hipError_t gt_dispatch(const GcArgs& a, bool garble, hipStream_t stream) {
+    if (a.G * a.N == 0) return hipSuccess;
+    if (!a.gt_msgs || !(garble ? a.sh_gb : a.sh_ev) || !a.ev_labels) return hipErrorInvalidValue;
+    switch (a.bits) {
+        case 1: return gt_launch<1>(a, garble, stream);
+        case 2: return gt_launch<2>(a, garble, stream);
+        case 3: return gt_launch<3>(a, garble, stream);
+        case 4: return gt_launch<4>(a, garble, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_gt_garble(const GcArgs& a, hipStream_t stream) { return gt_dispatch(a, true, stream); }
+
+hipError_t launch_gt_eval(const GcArgs& a, hipStream_t stream) { return gt_dispatch(a, false, stream); }
+
 template <int B>
 static hipError_t gc_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     int dev = 0, cus = 0;

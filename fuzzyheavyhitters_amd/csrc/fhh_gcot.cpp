@@ -522,6 +522,95 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     return rc;
 }
 
+int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                    uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share) {
+    CTX_CHECK(ctx);
+    int rc = ctx_set_device(ctx);
+    if (rc) return rc;
+    if (bits < 1 || bits > (uint32_t)kGtMaxBits) return ctx->fail(FHH_E_ARG, "gt_cot: bits must be in [1, 4]");
+    if (n == 0) return FHH_OK;
+    if (!gb_bits || !ev_bits || !base_seeds || !base_choice || !gb_share || !ev_share)
+        return ctx->fail(FHH_E_ARG, "gt_cot: NULL argument");
+    if (!(base_choice[0] & 1)) return ctx->fail(FHH_E_ARG, "gt_cot: s is the free-XOR Delta: its bit 0 must be 1");
+    if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gt_cot: n must fit 32 bits");
+    const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad, R = 1ull << bits;
+    std::vector<uint64_t> planes[2];
+    const uint8_t* src[2] = {gb_bits, ev_bits};
+    for (int s = 0; s < 2; s++) {
+        planes[s].assign((size_t)bits * nw + ot_padded(m) / 64, 0);
+        for (uint64_t t = 0; t < n; t++)
+            for (uint32_t j = 0; j < bits; j++)
+                if (src[s][t * bits + j] & 1) planes[s][(size_t)j * nw + t / 64] |= 1ull << (t % 64);
+    }
+    DevBuf dp[2], de, da, dm, dsh;
+    for (int s = 0; s < 2; s++) {
+        HIP_TRY(ctx, dp[s].ensure(planes[s].size() * 8));
+        HIP_TRY(ctx, hipMemcpyAsync(dp[s].p, planes[s].data(), planes[s].size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, de.ensure(m * 16));
+    HIP_TRY(ctx, da.ensure(m * 16));
+    HIP_TRY(ctx, dm.ensure(std::max<uint64_t>(R - 1, 1) * n * 8));
+    HIP_TRY(ctx, dsh.ensure(2 * n * 8));
+    const uint32_t* rk = nullptr;
+    rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
+    if (rc) return rc;
+    // 1. the labels OT (mode 4), as fhh_gc_cot_host
+    OtArgs a{};
+    a.mode = 4;
+    a.rk = rk;
+    words_from_bytes(base_choice, a.s);
+    a.choices = dp[1].as<uint32_t>();
+    a.ctr_off = ctr_off;
+    a.sx = de.p;
+    a.out = da.as<uint4>();
+    rc = ot_run(ctx, a, m, nullptr);
+    if (rc) return rc;
+    // 2. the garbled table on the zero labels, 3. its row on the OT'd labels
+    GcArgs g{};
+    g.gb_planes = dp[0].as<uint64_t>();
+    g.ev_planes = dp[1].as<uint64_t>();
+    g.G = 1;
+    g.N = (uint32_t)n;
+    g.nw = (uint32_t)nw;
+    g.bits = bits;
+    g.mask = mask & 1u;
+    words_from_bytes(base_choice, g.delta);
+    g.gate_base = gate_base;
+    g.ev_labels = de.as<uint4>();
+    g.ev_ot = 1;
+    g.gt_msgs = dm.as<uint64_t>();
+    g.sh_gb = dsh.as<uint64_t>();
+    HIP_TRY(ctx, launch_gt_garble(g, ctx->stream));
+    g.ev_labels = da.as<uint4>();
+    g.sh_gb = nullptr;
+    g.sh_ev = dsh.as<uint64_t>() + n;
+    HIP_TRY(ctx, launch_gt_eval(g, ctx->stream));
+    rc = ctx_sync(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy(gb_share, dsh.p, n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipMemcpy(ev_share, dsh.as<uint64_t>() + n, n * 8, hipMemcpyDeviceToHost));
+    if (msgs && R > 1) {   // SoA [R-1][n] on the device -> [n][R-1]
+        std::vector<uint64_t> h((R - 1) * n);
+        HIP_TRY(ctx, hipMemcpy(h.data(), dm.p, h.size() * 8, hipMemcpyDeviceToHost));
+        for (uint64_t r = 0; r + 1 < R; r++)
+            for (uint64_t t = 0; t < n; t++) msgs[t * (R - 1) + r] = h[r * n + t];
+    }
+    auto soa_to_aos = [&](const DevBuf& d, uint8_t* dst) -> int {
+        if (!dst) return FHH_OK;
+        std::vector<uint8_t> h((size_t)bits * npad * 16);
+        HIP_TRY(ctx, hipMemcpy(h.data(), d.p, h.size(), hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < bits; r++)
+            for (uint64_t t = 0; t < n; t++)
+                std::memcpy(dst + (t * bits + r) * 16, h.data() + ((size_t)r * npad + t) * 16, 16);
+        return FHH_OK;
+    };
+    rc = soa_to_aos(de, ev_zero);
+    if (!rc) rc = soa_to_aos(da, ev_active);
+    return rc;
+}
+
 }  // extern "C"
 
 // ================================================================================================
@@ -553,6 +642,7 @@ struct PartyState {
     int step = 0;               // protocol position (calls must come in order)
     bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
     bool lshare = false;        // r05c (FE levels): the share from the GC output labels, no OT 2
+    bool ltable = false;        // r05d (FE levels, bits <= kGtMaxBits): one garbled table per test
     // C = this instance's children: the chunk [c_off, c_off + C) of the level's level_C children
     // (child_begin / child_count); covered = children whose OTs are finished
     uint64_t c_off = 0, level_C = 0, covered = 0;
@@ -625,6 +715,7 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
     P.tests = P.C * P.n;
     P.per2 = P.last ? 2 : 1;
     P.lshare = !P.last;
+    P.ltable = P.lshare && P.bits <= (uint32_t)kGtMaxBits;
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
     P.m2 = P.lshare ? 0 : P.tests * P.per2;   // OT 2 (the share OT) at the FieldElm level only
     if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
@@ -700,7 +791,10 @@ int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver, boo
 
 // message sizes
 uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
-uint64_t gc_bytes(const PartyState& P) { return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1 + (P.lshare ? 8 : 0)); }
+uint64_t gc_bytes(const PartyState& P) {
+    if (P.ltable) return P.tests * (((uint64_t)1 << P.bits) - 1) * 8;   // rows 1 .. 2^bits - 1, 8 B each
+    return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1 + (P.lshare ? 8 : 0));
+}
 uint64_t y2_bytes(const PartyState& P) { return P.m2 * (P.last ? 16 : 8); }
 
 int check_in(fhh_ctx* ctx, const void* p, uint64_t got, uint64_t want, const char* what) {
@@ -719,6 +813,12 @@ void gc_layout(const PartyState& P, uint8_t* base, GcArgs& g) {
     g.gb_labels = nullptr;
     g.sh_y = P.lshare ? reinterpret_cast<uint64_t*>(base + tb) : nullptr;
     g.decode = base + tb + (P.lshare ? 8 * t : 0);
+    if (P.ltable) {   // r05d: the gc message is the garbled table's rows 1 .. 2^bits - 1 (SoA, u64)
+        g.tables = nullptr;
+        g.sh_y = nullptr;
+        g.decode = nullptr;
+        g.gt_msgs = reinterpret_cast<uint64_t*>(base);
+    }
 }
 
 // this chunk's rows of the level's node values (u64 FE, or a BlockPair at the last level)
@@ -847,7 +947,7 @@ int fhh_gb_garble(fhh_ctx* ctx, const uint8_t** gc_msg_dev, uint64_t* gc_msg_byt
     PartyState* Pp = ctx->party;
     if (!Pp || Pp->role != 0 || Pp->step != 1) return ctx->fail(FHH_E_STATE, "gb_garble: call after fhh_gb_ot_labels");
     PartyState& P = *Pp;
-    if (P.tests) HIP_TRY(ctx, launch_gc_garble(P.g, ctx->stream));
+    if (P.tests) HIP_TRY(ctx, P.ltable ? launch_gt_garble(P.g, ctx->stream) : launch_gc_garble(P.g, ctx->stream));
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 2;
@@ -894,7 +994,7 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
         g.out_packed = P.choices2.as<uint32_t>();
         g.out_dup = P.per2;
     }
-    if (P.tests) HIP_TRY(ctx, launch_gc_eval(g, ctx->stream));
+    if (P.tests) HIP_TRY(ctx, P.ltable ? launch_gt_eval(g, ctx->stream) : launch_gc_eval(g, ctx->stream));
     // 3. OT 2's receiver: choice = the GC output (collect.rs:461-471); T and U reused
     rc = party_ot_buffers(ctx, P, P.m2, true);
     if (rc) return rc;

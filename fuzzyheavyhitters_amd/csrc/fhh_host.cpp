@@ -854,7 +854,7 @@ struct LoopBuffers {
     DevBuf ctl, live[2], pos[2], mark, partials, sizes, final_vals;
     DevBuf hist_rows, hist_packed;               // end-of-crawl readback (k_gather_hist)
     DevBuf gc_planes[2], gc_tables, gc_gbl, gc_evl, gc_decode, gc_out;   // cfg->gc (row f1)
-    DevBuf gc_evact, gc_val[2], gc_y;                                     // cfg->gc = 2: OT / share buffers
+    DevBuf gc_evact, gc_val[2], gc_y, gc_msgs;                            // cfg->gc = 2: OT / share / table buffers
     // multi-rank: kernels write this rank's partials, k_prune reads the cross-rank sum in
     // `reduced` (out of place, so re-reducing an aborted level's stale partials is idempotent)
     DevBuf reduced;
@@ -1353,27 +1353,42 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     // W_0 ^ Delta of o = eq ^ mask in the share C-OT's roles): server 0's node value r1 and
                     // the 8-B y from k_gc_garble_cot, server 1's value from k_gc_eval — no second OT
                     const bool lshare = real_ot && pmode == 1;
-                    if (lshare) {
+                    // r05d: tests of <= kGtMaxBits bits (d <= 2) take the share from ONE garbled table per
+                    // test (k_gt_garble / k_gt_eval: 2^bits + 1 AES instead of the half-gates chain's)
+                    const bool ltable = lshare && bits <= (uint32_t)kGtMaxBits;
+                    if (ltable) {
+                        for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
+                        HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
+                        g.gt_msgs = B.gc_msgs.as<uint64_t>();
+                        g.sh_gb = B.gc_val[0].as<uint64_t>();
+                        HIP_TRY(c0, launch_gt_garble(g, c0->stream));
+                        g.ev_labels = B.gc_evact.as<uint4>();
+                        g.sh_gb = nullptr;
+                        g.sh_ev = B.gc_val[1].as<uint64_t>();
+                        HIP_TRY(c0, launch_gt_eval(g, c0->stream));
+                    } else if (lshare) {
                         for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
                         HIP_TRY(c0, B.gc_y.ensure(tests * 8));
                         g.sh_gb = B.gc_val[0].as<uint64_t>();
                         g.sh_y = B.gc_y.as<uint64_t>();
                     }
-                    HIP_TRY(c0, launch_gc_garble(g, c0->stream));
-                    if (real_ot) {
-                        g.ev_labels = B.gc_evact.as<uint4>();
-                        g.sh_gb = nullptr;
-                        if (lshare) {
-                            g.sh_ev = B.gc_val[1].as<uint64_t>();
-                        } else {
-                            // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
-                            uint32_t* och = nullptr;
-                            HIP_TRY(c0, ot_choices_buffer(c0, m2, &och));
-                            g.out_packed = och;
-                            g.out_dup = per2;
+                    if (!ltable) {
+                        HIP_TRY(c0, launch_gc_garble(g, c0->stream));
+                        if (real_ot) {
+                            g.ev_labels = B.gc_evact.as<uint4>();
+                            g.sh_gb = nullptr;
+                            if (lshare) {
+                                g.sh_ev = B.gc_val[1].as<uint64_t>();
+                            } else {
+                                // k_gc_eval ballot-packs its outputs as the share-conversion OT's choice words
+                                uint32_t* och = nullptr;
+                                HIP_TRY(c0, ot_choices_buffer(c0, m2, &och));
+                                g.out_packed = och;
+                                g.out_dup = per2;
+                            }
                         }
+                        HIP_TRY(c0, launch_gc_eval(g, c0->stream));
                     }
-                    HIP_TRY(c0, launch_gc_eval(g, c0->stream));
                     ChildArgs ca = a;   // this chunk's children
                     ca.c_off = g_off;
                     ca.c_cnt = Gc;

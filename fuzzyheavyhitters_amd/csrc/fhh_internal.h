@@ -247,7 +247,12 @@ struct GcArgs {
     uint64_t* sh_gb;
     uint64_t* sh_y;
     uint64_t* sh_ev;
+    // r05d (FE levels, bits <= kGtMaxBits): the garbled table (oracle orc_gt_garble / orc_gt_eval):
+    // k_gt_garble writes rows 1 .. 2^bits - 1's messages SoA [2^bits - 1][G N] and the garbler's node
+    // values to sh_gb, k_gt_eval reads them and writes the evaluator's to sh_ev
+    uint64_t* gt_msgs;
 };
+constexpr int kGtMaxBits = 4;   // 16 rows (d = 2); wider tests keep the half-gates chain
 
 struct PruneArgs {
     LoopCtl* ctl;
@@ -392,6 +397,8 @@ hipError_t launch_cot_fe255_finish(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_rows_out(const OtArgs& a, bool sender, hipStream_t stream);
 hipError_t launch_gc_garble(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gc_eval(const GcArgs& a, hipStream_t stream);
+hipError_t launch_gt_garble(const GcArgs& a, hipStream_t stream);   // r05d garbled table
+hipError_t launch_gt_eval(const GcArgs& a, hipStream_t stream);
 hipError_t launch_gather_hist(const uint32_t* sizes, uint32_t stride, const uint32_t* const* rows, uint32_t levels,
                               uint32_t* out, uint64_t cap, hipStream_t stream);
 // parity probe of the device loop (fhh_sim_config.probe_*): the pending children's states of a

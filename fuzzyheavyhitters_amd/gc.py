@@ -157,3 +157,24 @@ def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choi
     if share:
         tr["gb_share"], tr["ev_share"], tr["share_y"] = sh
     return out, tr
+
+
+def table_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate_base: int = 0, ctr_off: int = 0):
+    """r05d, the FE levels' form (fhh_gt_cot_host, bits <= 4): the labels OT, then one garbled table
+    of 2^bits rows for "the share of eq ^ mask" (Yao's garbled gate, point-and-permute) instead of the
+    half-gates chain. Returns dict: msgs [n][2^bits - 1] u64, gb_share / ev_share [n] (gb - ev = eq mod
+    p), ev_zero / ev_active [n][bits][16]."""
+    g = np.ascontiguousarray(np.asarray(gb_inputs).astype(np.uint8) & 1)
+    e = np.ascontiguousarray(np.asarray(ev_inputs).astype(np.uint8) & 1)
+    if g.ndim != 2 or g.shape != e.shape:
+        raise ValueError("table_cot: inputs must both be [n][bits]")
+    n, bits = g.shape
+    seeds = np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16)
+    s = np.frombuffer(bytes(base_choice), np.uint8).copy()
+    tr = {"ev_zero": np.zeros((n, bits, 16), np.uint8), "ev_active": np.zeros((n, bits, 16), np.uint8),
+          "msgs": np.zeros((n, (1 << bits) - 1), np.uint64), "gb_share": np.zeros(n, np.uint64),
+          "ev_share": np.zeros(n, np.uint64)}
+    check(lib().fhh_gt_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, gate_base, ptr(seeds), ptr(s),
+                                ctr_off, ptr(tr["ev_zero"]), ptr(tr["ev_active"]), ptr(tr["msgs"], u64p),
+                                ptr(tr["gb_share"], u64p), ptr(tr["ev_share"], u64p)), kc.handle)
+    return tr

@@ -550,6 +550,22 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
                     uint8_t* ev_active, uint8_t* decode, uint8_t* out, uint64_t* gb_share, uint64_t* ev_share,
                     uint64_t* share_y);
 
+/* r05d: the FE levels' garbled TABLE on host buffers (bits <= 4): the labels OT as in fhh_gc_cot_host,
+ * then one garbled b-input gate instead of the half-gates chain + output-label share — Yao's garbled
+ * gate with point-and-permute for "the share of eq ^ mask": the inputs are the folded garbler's zero
+ * labels Z_k = q_k ^ (x_k ? 0 : Delta); the evaluator's OT'd t_k is z_k's active label and the colours
+ * lsb(t_k) name its row r; row r's key is cr_hash(K_r), K_r = XOR_k sigma^k(z_k's label in row r) ^
+ * (gate_base + t) (sigma = doubling in GF(2^128), x^128 + x^7 + x^2 + x + 1, block as LE u128); the
+ * values are the share C-OT's pair (pair[0] = v, pair[1] = mask ? v + 1 : v - 1; the garbler's node
+ * value r1 = v + mask) with pair[o_r], o_r = eq_r ^ mask; row 0's value is its hash mod p (no
+ * message), rows 1 .. 2^b - 1 send lo64(hash) ^ pair[o_r]. Outputs: msgs [n][2^bits - 1] u64 (may be
+ * NULL), gb_share / ev_share [n] (r1 and the evaluator's value: gb - ev = eq mod p), ev_zero /
+ * ev_active [n][bits][16] (may be NULL). Garbler 2^b AES per test, evaluator 1. */
+int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                    uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share);
+
 /* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
  * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;
  * equalitytest.rs:25-106): each server runs only its own half on its own ctx, right after its

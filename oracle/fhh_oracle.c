@@ -1185,6 +1185,101 @@ void orc_gc_eval_eq_cot(uint64_t n, uint32_t bits, const uint8_t* tables, const 
     orc_gc_eval_eq_cot_share(n, bits, tables, ev_active, decode, gate_base, out, NULL, NULL);
 }
 
+/* r05d: the FE levels' equality test + share as ONE garbled table (Yao's garbled gate with
+ * point-and-permute, generalised to the b-input gate "share of eq ^ mask") instead of the half-gates
+ * chain + the output-label share. Inputs are the folded-garbler zero labels Z_k = E_k ^ (x_k ? 0 : D)
+ * (E_k the labels OT's q, as orc_gc_garble_eq_cot), so the evaluator's OT'd label t_k is z_k's active
+ * label and its colour p_k = lsb(t_k) = lsb(Z_k) ^ z_k names its row r = sum p_k 2^k. Row r's key is
+ * H(K_r), K_r = XOR_k sigma^k(label of z_k in row r) ^ tweak, sigma = doubling in GF(2^128) (x^128 +
+ * x^7 + x^2 + x + 1 on the block as a little-endian u128), tweak = gate_base + t in the low 64 bits,
+ * H = cr_hash. Any other row's K differs from the evaluator's by (sum_{k in S} x^k) D for a nonempty
+ * S — a nonzero field element times the unknown D — so its key is hidden as H(q ^ s) hides the
+ * unchosen message in the correlated OT. eq = 1 in exactly the row r* whose z are all 1; o_r =
+ * eq_r ^ mask; the values are the C-OT share pair (collect.rs:447-451): pair[0] = v, pair[1] = mask ?
+ * v + 1 : v - 1, node value r1 = v + mask. Row 0 carries no message: its value pair[o_0] IS H(K_0) mod
+ * p (which fixes v); rows 1 .. 2^b - 1 send m_r = lo64(H(K_r)) ^ pair[o_r] (8 B each). The evaluator:
+ * value = r ? lo64(H(K)) ^ m_r : H(K) mod p. msgs [n][2^b - 1] u64, gb_share / ev_share [n]. */
+static void gf128_dbl(uint8_t b[16]) {
+    const int carry = b[15] >> 7;
+    for (int k = 15; k > 0; k--) b[k] = (uint8_t)((b[k] << 1) | (b[k - 1] >> 7));
+    b[0] = (uint8_t)(b[0] << 1);
+    if (carry) b[0] ^= 0x87;
+}
+
+/* XOR_k sigma^k(L_k) ^ tweak */
+static void gt_key(const uint8_t* labels /* [bits][16] */, uint32_t bits, uint64_t tweak, uint8_t K[16]) {
+    uint8_t acc[16] = {0};
+    for (int k = (int)bits - 1; k >= 0; k--) {   /* Horner: acc = sigma(acc) ^ L_k */
+        gf128_dbl(acc);
+        gc_xor(acc, acc, labels + (uint64_t)k * 16);
+    }
+    for (int k = 0; k < 8; k++) acc[k] ^= (uint8_t)(tweak >> (8 * k));
+    memcpy(K, acc, 16);
+}
+
+static uint64_t fe_add1(uint64_t v) { return v + 1 == FE_P ? 0 : v + 1; }
+static uint64_t fe_sub1(uint64_t v) { return v == 0 ? FE_P - 1 : v - 1; }
+
+void orc_gt_garble(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
+                   const uint8_t delta_in[16], uint64_t gate_base, uint64_t* msgs, uint64_t* gb_share) {
+    oracle_init();
+    uint8_t D[16];
+    memcpy(D, delta_in, 16);
+    D[0] |= 1;
+    mask &= 1;
+    const uint32_t R = 1u << bits;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t Z[8][16], L[8][16], K[16], H[16];
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < bits; k++) {
+            memcpy(Z[k], ev_zero + ((uint64_t)t * bits + k) * 16, 16);
+            if (!(gb_bits[(uint64_t)t * bits + k] & 1)) gc_xor(Z[k], Z[k], D);   /* Z_k = E_k ^ (x_k ? 0 : D) */
+            c |= (uint32_t)(Z[k][0] & 1) << k;
+        }
+        const uint32_t rstar = (~c) & (R - 1);   /* the row whose z are all 1 */
+        uint64_t v = 0, p0 = 0, p1 = 0;
+        for (uint32_t r = 0; r < R; r++) {
+            for (uint32_t k = 0; k < bits; k++) {   /* label of z_k = ((r >> k) ^ c_k) & 1 */
+                memcpy(L[k], Z[k], 16);
+                if ((((r ^ c) >> k) & 1)) gc_xor(L[k], L[k], D);
+            }
+            gt_key(&L[0][0], bits, gate_base + (uint64_t)t, K);
+            ot_cr_hash(K, H);
+            const uint32_t o = (uint32_t)(r == rstar) ^ mask;
+            if (r == 0) {
+                const uint64_t h = cot_fe_of_block(H);   /* = pair[o_0] */
+                v = o == 0 ? h : (mask ? fe_sub1(h) : fe_add1(h));
+                p0 = v;
+                p1 = mask ? fe_add1(v) : fe_sub1(v);
+                gb_share[t] = mask ? fe_add1(v) : v;     /* r1 = v + mask */
+            } else {
+                uint64_t hl;
+                memcpy(&hl, H, 8);
+                msgs[(uint64_t)t * (R - 1) + (r - 1)] = hl ^ (o ? p1 : p0);
+            }
+        }
+    }
+}
+
+void orc_gt_eval(uint64_t n, uint32_t bits, const uint8_t* ev_active, const uint64_t* msgs, uint64_t gate_base,
+                 uint64_t* ev_share) {
+    oracle_init();
+    const uint32_t R = 1u << bits;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        const uint8_t* Lt = ev_active + (uint64_t)t * bits * 16;
+        uint8_t K[16], H[16];
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < bits; k++) r |= (uint32_t)(Lt[k * 16] & 1) << k;   /* colours name the row */
+        gt_key(Lt, bits, gate_base + (uint64_t)t, K);
+        ot_cr_hash(K, H);
+        uint64_t hl;
+        memcpy(&hl, H, 8);
+        ev_share[t] = r ? (hl ^ msgs[(uint64_t)t * (R - 1) + (r - 1)]) : cot_fe_of_block(H);
+    }
+}
+
 /* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */
 void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* gb_labels,
                     const uint8_t* ev_labels, const uint8_t* decode, uint64_t gate_base, uint8_t* out) {

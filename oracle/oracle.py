@@ -761,6 +761,31 @@ def gc_eval_eq_cot(tables, ev_active, decode, gate_base: int = 0, share_y=None):
     return (out, ev) if y is not None else out
 
 
+def gt_garble(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, delta: bytes, gate_base: int = 0):
+    """r05d, the FE levels' garbled table (fhh_oracle.c orc_gt_garble): from the labels OT's zero labels
+    ev_zero [n][bits][16] and the garbler's bits, its messages [n][2^bits - 1] u64 (row 0 carries none)
+    and its node values [n] (r1 = v + mask)."""
+    g = np.ascontiguousarray(gb_bits, np.uint8)
+    z = np.ascontiguousarray(ev_zero, np.uint8)
+    n, bits = g.shape
+    msgs = np.zeros((n, (1 << bits) - 1), np.uint64)
+    gv = np.zeros(n, np.uint64)
+    d = np.frombuffer(delta, np.uint8).copy()
+    lib().orc_gt_garble(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z), ctypes.c_uint32(mask & 1), _p(d),
+                        ctypes.c_uint64(gate_base), _p(msgs), _p(gv))
+    return msgs, gv
+
+
+def gt_eval(ev_active: np.ndarray, msgs: np.ndarray, gate_base: int = 0) -> np.ndarray:
+    """r05d: the evaluator's node values [n] from its OT'd labels [n][bits][16] and the table's messages."""
+    e = np.ascontiguousarray(ev_active, np.uint8)
+    m = np.ascontiguousarray(msgs, np.uint64)
+    n, bits = e.shape[0], e.shape[1]
+    ev = np.zeros(n, np.uint64)
+    lib().orc_gt_eval(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(e), _p(m), ctypes.c_uint64(gate_base), _p(ev))
+    return ev
+
+
 COT_LABELS, COT_FE, COT_FE255, COT_RAW = 1, 2, 3, 4
 
 

@@ -325,3 +325,63 @@ def test_gpu_output_label_share_bit_exact(oracle, n, bits):
         eq = (g == e).all(axis=1).astype(np.uint64)
         assert np.array_equal(((tr["gb_share"].astype(object) - tr["ev_share"].astype(object)) % FE_P)
                               .astype(np.uint64), eq)
+
+
+# ---- r05d: the FE levels' garbled table (one b-input garbled gate per test) ------------------------
+def _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
+    """The labels OT (the IKNP correlation), then the garbled table on its zero labels and the
+    evaluator's row on its t_j — all in the oracle."""
+    n, bits = g.shape
+    npad = (n + 63) // 64 * 64
+    ch = np.zeros(bits * npad, np.uint8)
+    for k in range(bits):
+        ch[k * npad: k * npad + n] = e[:, k]
+    q, t_rows, _, _ = oracle.cot_extend(oracle.COT_RAW, ch, seeds, s, ctr_off=ctr_off)
+    ev_zero = np.stack([q[k * npad: k * npad + n] for k in range(bits)], axis=1)
+    ev_act = np.stack([t_rows[k * npad: k * npad + n] for k in range(bits)], axis=1)
+    msgs, gv = oracle.gt_garble(g, ev_zero, mask, s, gate_base=gate_base)
+    ev = oracle.gt_eval(ev_act, msgs, gate_base=gate_base)
+    return dict(ev_zero=ev_zero, ev_active=ev_act, msgs=msgs, gb_share=gv, ev_share=ev)
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3, 4])
+def test_oracle_garbled_table_functional(oracle, bits):
+    """The garbled table's share: gb_share - ev_share = eq (mod p) for every test and both masks; values
+    canonical; the evaluator's row is named by its labels' colours (each row is reached); messages depend
+    on Delta and on the tweak."""
+    rng = np.random.default_rng(90 + bits)
+    g, e = _cases(rng, 600, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    for mask in (0, 1):
+        tr = _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=21)
+        eq = (g == e).all(axis=1).astype(np.uint64)
+        assert all(int(x) < FE_P for x in tr["gb_share"]) and all(int(x) < FE_P for x in tr["ev_share"])
+        diff = (tr["gb_share"].astype(object) - tr["ev_share"].astype(object)) % FE_P
+        assert np.array_equal(diff.astype(np.uint64), eq)
+        rows = sum(((tr["ev_active"][:, k, 0] & 1).astype(int) << k) for k in range(bits))
+        assert len(set(rows.tolist())) == 1 << bits
+        tr2 = _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=22)
+        assert not np.array_equal(tr2["msgs"], tr["msgs"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bits", [(1, 2), (65, 1), (1000, 2), (777, 3), (4097, 4)])
+def test_gpu_garbled_table_bit_exact(oracle, n, bits):
+    """fhh_gt_cot_host (labels OT + k_gt_garble + k_gt_eval) = the oracle chain bit for bit: zero and
+    active labels, every row's message, both parties' node values; gb - ev = eq mod p."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    rng = np.random.default_rng(n * 7 + bits)
+    g, e = _cases(rng, n, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    kc = fhh.KeyCollection(8, 1)
+    for mask, ctr in ((0, 0), (1, 256)):
+        tr = gc.table_cot(kc, g, e, mask, seeds, s, gate_base=13, ctr_off=ctr)
+        etr = _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=13, ctr_off=ctr)
+        for k in ("ev_zero", "ev_active", "msgs", "gb_share", "ev_share"):
+            assert np.array_equal(tr[k], etr[k]), k
+        eq = (g == e).all(axis=1).astype(np.uint64)
+        assert np.array_equal(((tr["gb_share"].astype(object) - tr["ev_share"].astype(object)) % FE_P)
+                              .astype(np.uint64), eq)

@@ -74,6 +74,9 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     names = [f"_ZN3fhh11k_gc_garbleILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
     names += [f"_ZN3fhh15k_gc_garble_cotILi{b}EEEvNS_6GcArgsE" for b in range(1, 9)]
     names += [f"_ZN3fhh9k_gc_evalILi{b}ELb{f}EEEvNS_6GcArgsE" for b in range(1, 9) for f in (0, 1)]
+    # r05d: the FE levels' garbled table, b = 1..4
+    names += [f"_ZN3fhh11k_gt_garbleILi{b}EEEvNS_6GcArgsE" for b in range(1, 5)]
+    names += [f"_ZN3fhh9k_gt_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 5)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
     names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE",

@@ -56,8 +56,8 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     lb = got.level_bytes[0]
     C0, bits = int(got.level_children[0]), 2 * d
     npad = (n + 63) // 64 * 64
-    # tables + the FE share's 8-B y (r05c: from the output labels) + decoding bit (garbler string folded in)
-    assert lb["gc"] == C0 * n * (2 * (bits - 1) * 16 + 8 + 1)
+    # r05d: the FE levels' gc message is the garbled table's rows 1 .. 2^bits - 1, 8 B each
+    assert lb["gc"] == C0 * n * ((1 << bits) - 1) * 8
     # r05b: the labels OT is the IKNP correlation itself (no reply); r05c: no share OT at the FE levels
     assert lb["u1"] == 16 * ((C0 * bits * npad + 8191) // 8192 * 8192)
     assert lb["y1"] == 0 and lb["u2"] == 0 and lb["y2"] == 0

@@ -422,7 +422,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "dropin_material": "each server its own (os.urandom: Delta and mask per chunk, CO15 seeds and s); every "
                            "level's labels OT extension on Chou-Orlandi base OTs between the servers over the "
                            "channel (1 CO15 run per level, 2 at the FieldElm level: its share OT; the FE levels' "
-                           "shares ride on the GC output labels)",
+                           "shares come from one garbled table per test)",
         "dropin_base_ot_runs": r_d.base_ot_runs, "dropin_base_ot_wait_s": r_d.base_ot_wait_s,
     })
     if not args.no_party:

@@ -586,10 +586,12 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * (m = C x 2d x npad: its share planes are the choice bits; the garbler's labels-kind s is the
  * circuit's Delta, so no reply crosses). The share: at the FE levels (r05c) from the circuit's output
  * labels (fhh_gc_cot_host's share outputs: the garbler's r1 and y from W_0, W_0 ^ Delta, the evaluator's
- * value from its W_o), so no second OT runs and the OT kind 1 base material is not read; at
- * tree_crawl_last by OT 2 (FHH_COT_FE255: 2 OTs per test). The circuit is fhh_gc_cot_host's (the
- * garbler's string and mask folded in). gc = [tables (bits-1) x 2 | y 8 B (FE levels) | decode 1 B]
- * per test, tests = C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
+ * value from its W_o) — and since r05d, for 2d <= 4, from one garbled table per test (fhh_gt_cot_host)
+ * — so no second OT runs and the OT kind 1 base material is not read; at tree_crawl_last by OT 2
+ * (FHH_COT_FE255: 2 OTs per test). The circuit is fhh_gc_cot_host's (the garbler's string and mask
+ * folded in). gc at the FE levels, 2d <= 4: the table's rows 1 .. 2^(2d) - 1, 8 B each, SoA
+ * [row][tests]; otherwise [tables (bits-1) x 2 | y 8 B (FE levels) | decode 1 B] per test; tests =
+ * C x n child-major; u = the OT receiver's [128][m padded to 8192 / 128] blocks;
  * y1 0 B; u2 / y2: 0 B at the FE levels, FieldElm level: U and 16 B per OT. Each server's node values
  * (the garbler's r1 = v + mask, the evaluator's share output) stay on its device; fhh_party_node_sums sums them: non-last
  * level sums [C] canonical FE, last level [C][10] unreduced + [C][8] canonical FieldElm (the

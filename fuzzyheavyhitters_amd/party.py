@@ -284,7 +284,7 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     parties = [(GarblerParty(a), EvaluatorParty(b)) for a, b in shards]
     res = TwoPartyResult()
     shard_clients = [a.num_clients() for a, _ in shards]
-    # base OTs: a pool computing each (level, shard)'s two CO15 runs ahead of the crawl
+    # base OTs: a pool computing each (level, shard)'s CO15 runs (labels; + the share OT's at the last level) ahead
     pool = None
     pending: dict = {}
     if material == "fresh":

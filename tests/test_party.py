@@ -1,8 +1,8 @@
 """The two servers' halves of the GC equality test + OT, each on its own ctx (fhh_gb_* / fhh_ev_*;
 src/collect.rs:419-482 with gc_sender = true on server 0 and false on server 1,
 src/equalitytest.rs:25-106). Only protocol messages cross (party.Channel copies them into memory the
-receiving server owns): the Chou–Orlandi base-OT messages of every level and the five messages per
-chunk. Each server draws its own material (material="fresh"), or both come from one test seed
+receiving server owns): the Chou–Orlandi base-OT messages of every level and the four messages per
+chunk (two of them empty at the FE levels since r05c/r05d). Each server draws its own material (material="fresh"), or both come from one test seed
 (material="test"); either way the leader's output equals the in-process GC + OT crawl
 (fhh_sim_config.gc = 2) level by level, and its heavy hitters equal the plaintext recount."""
 import ctypes

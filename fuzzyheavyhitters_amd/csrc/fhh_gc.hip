@@ -433,6 +433,13 @@ __device__ __forceinline__ void gf_dbl(uint32_t (&x)[4]) {
 __device__ __forceinline__ uint64_t fe_inc(uint64_t v) { return v + 1 == kOtFeP ? 0 : v + 1; }
 __device__ __forceinline__ uint64_t fe_dec(uint64_t v) { return v ? v - 1 : kOtFeP - 1; }
 
+#ifndef FHH_GT_GARBLE_U
+#define FHH_GT_GARBLE_U 1   // tests per lane per pass (A/B knob)
+#endif
+#ifndef FHH_GT_EVAL_U
+#define FHH_GT_EVAL_U 2
+#endif
+
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];
@@ -441,7 +448,8 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
     uint32_t b0, b1;
     GcTab::bases(threadIdx.x & 63, b0, b1);
     constexpr uint32_t R = 1u << B;
-    constexpr int NB = R < 4 ? (int)R : 4;   // rows per AES pass
+    constexpr int NB = R < 4 ? (int)R : 4;   // rows per AES pass and test
+    constexpr int U = FHH_GT_GARBLE_U;       // tests per lane per pass
     const uint64_t n = a.G * a.N;
     const uint64_t Npad = (uint64_t)a.nw * 64;
     uint32_t Dk[B][4];   // sigma^k(Delta)
@@ -454,56 +462,74 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
         gf_dbl(Dk[k]);
     }
     const uint64_t n_act = gc_active(a);
-    for (uint64_t t = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t < n_act; t += (uint64_t)gridDim.x * kGcThreads) {
-        const uint64_t g = t / a.N;
-        const uint32_t i = (uint32_t)(t - g * a.N);
-        const uint64_t tw = a.gate_base + a.g_off * a.N + t;   // the test's index in the whole level
-        uint32_t S[4] = {0u, 0u, 0u, 0u}, col = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kGcThreads;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t0 < n_act; t0 += U * stride) {
+        uint32_t S[U][4], col[U];
+        uint64_t tt[U];
 #pragma unroll
-        for (int k = B - 1; k >= 0; k--) {   // Horner: S = sigma(S) ^ Z_k
-            uint32_t z[4];
-            ld_blk(a.ev_labels, g * B + k, Npad, i, z);   // E_k, the labels OT's q
-            const uint32_t xb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
-            gf_dbl(S);
+        for (int u = 0; u < U; u++) {
+            const uint64_t t = t0 + u * stride;
+            tt[u] = t;
+            const uint64_t tc = t < n_act ? t : t0;   // a valid test for the padding lanes
+            const uint64_t g = tc / a.N;
+            const uint32_t i = (uint32_t)(tc - g * a.N);
+            const uint64_t tw = a.gate_base + a.g_off * a.N + tc;   // the test's index in the whole level
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                z[c] ^= xb ? 0u : a.delta[c];   // Z_k = E_k ^ (x_k ? 0 : Delta)
-                S[c] ^= z[c];
-            }
-            col |= (z[0] & 1u) << k;
-        }
-        S[0] ^= (uint32_t)tw;
-        S[1] ^= (uint32_t)(tw >> 32);
-        const uint32_t rstar = ~col & (R - 1);   // the row whose z are all 1 (eq = 1)
-        uint64_t p0 = 0, p1 = 0;
+            for (int c = 0; c < 4; c++) S[u][c] = 0u;
+            col[u] = 0;
 #pragma unroll
-        for (uint32_t pass = 0; pass < R / NB; pass++) {
-            uint32_t h[NB][4];
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const uint32_t flip = (pass * NB + j) ^ col;   // z_k of the row = bit k of r ^ col
+            for (int k = B - 1; k >= 0; k--) {   // Horner: S = sigma(S) ^ Z_k
+                uint32_t z[4];
+                ld_blk(a.ev_labels, g * B + k, Npad, i, z);   // E_k, the labels OT's q
+                const uint32_t xb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
+                gf_dbl(S[u]);
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-                    uint32_t w = S[c];
-#pragma unroll
-                    for (int k = 0; k < B; k++) w ^= ((flip >> k) & 1u) ? Dk[k][c] : 0u;
-                    h[j][c] = w;
+                    z[c] ^= xb ? 0u : a.delta[c];   // Z_k = E_k ^ (x_k ? 0 : Delta)
+                    S[u][c] ^= z[c];
                 }
+                col[u] |= (z[0] & 1u) << k;
             }
-            aes0_mmo_tab<DevOpsX, GcTab, NB>(h, tbl_gc, b0, b1);   // cr_hash: pi(K) ^ K
+            S[u][0] ^= (uint32_t)tw;
+            S[u][1] ^= (uint32_t)(tw >> 32);
+        }
+        uint64_t p0[U], p1[U];
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const uint32_t r = pass * NB + j;
-                const uint32_t o = (uint32_t)(r == rstar) ^ a.mask;
-                const uint64_t hl = (uint64_t)h[j][0] | ((uint64_t)h[j][1] << 32);
-                if (r == 0) {   // row 0's value pair[o_0] is H(K_0) mod p: it fixes v
-                    const uint64_t hv = ot_fe_of_u128(hl, (uint64_t)h[j][2] | ((uint64_t)h[j][3] << 32));
-                    const uint64_t v = o == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
-                    p0 = v;
-                    p1 = a.mask ? fe_inc(v) : fe_dec(v);
-                    a.sh_gb[t] = a.mask ? fe_inc(v) : v;   // r1 = v + mask
-                } else {
-                    a.gt_msgs[(uint64_t)(r - 1) * n + t] = hl ^ (o ? p1 : p0);
+        for (uint32_t pass = 0; pass < R / NB; pass++) {
+            uint32_t h[U * NB][4];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int j = 0; j < NB; j++) {
+                    const uint32_t flip = (pass * NB + j) ^ col[u];   // z_k of the row = bit k of r ^ col
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        uint32_t w = S[u][c];
+#pragma unroll
+                        for (int k = 0; k < B; k++) w ^= ((flip >> k) & 1u) ? Dk[k][c] : 0u;
+                        h[u * NB + j][c] = w;
+                    }
+                }
+            aes0_mmo_tab<DevOpsX, GcTab, U * NB>(h, tbl_gc, b0, b1);   // cr_hash: pi(K) ^ K
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t t = tt[u];
+                const uint32_t rstar = ~col[u] & (R - 1);   // the row whose z are all 1 (eq = 1)
+#pragma unroll
+                for (int j = 0; j < NB; j++) {
+                    const uint32_t r = pass * NB + j;
+                    const uint32_t o = (uint32_t)(r == rstar) ^ a.mask;
+                    const uint32_t* hj = h[u * NB + j];
+                    const uint64_t hl = (uint64_t)hj[0] | ((uint64_t)hj[1] << 32);
+                    if (r == 0) {   // row 0's value pair[o_0] is H(K_0) mod p: it fixes v
+                        const uint64_t hv = ot_fe_of_u128(hl, (uint64_t)hj[2] | ((uint64_t)hj[3] << 32));
+                        const uint64_t v = o == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
+                        p0[u] = v;
+                        p1[u] = a.mask ? fe_inc(v) : fe_dec(v);
+                        if (t < n_act) a.sh_gb[t] = a.mask ? fe_inc(v) : v;   // r1 = v + mask
+                    } else if (t < n_act) {
+                        a.gt_msgs[(uint64_t)(r - 1) * n + t] = hl ^ (o ? p1[u] : p0[u]);
+                    }
                 }
             }
         }
@@ -520,13 +546,14 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval(GcArgs a) {
     const uint64_t n = a.G * a.N;
     const uint64_t Npad = (uint64_t)a.nw * 64;
     const uint64_t n_act = gc_active(a);
-    // two tests per lane per pass (2 AES blocks in flight)
+    // U tests per lane per pass (U AES blocks in flight)
+    constexpr int U = FHH_GT_EVAL_U;
     const uint64_t stride = (uint64_t)gridDim.x * kGcThreads;
-    for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t0 < n_act; t0 += 2 * stride) {
-        uint32_t h[2][4], row[2];
-        uint64_t tt[2];
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t0 < n_act; t0 += U * stride) {
+        uint32_t h[U][4], row[U];
+        uint64_t tt[U];
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < U; u++) {
             const uint64_t t = t0 + u * stride;
             tt[u] = t;
             const uint64_t tc = t < n_act ? t : t0;   // a valid test for the padding block
@@ -549,9 +576,9 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval(GcArgs a) {
             for (int c = 0; c < 4; c++) h[u][c] = S[c];
             row[u] = r;
         }
-        aes0_mmo_tab<DevOpsX, GcTab, 2>(h, tbl_gc, b0, b1);
+        aes0_mmo_tab<DevOpsX, GcTab, U>(h, tbl_gc, b0, b1);
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < U; u++) {
             const uint64_t t = tt[u];
             if (t >= n_act) continue;
             const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);

@@ -618,7 +618,7 @@ def collective_after_init(errs, rehearse_rccl: bool):
     return ("hosted" if rehearse_rccl else "fail"), err
 
 
-def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
+def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot"):
     """The real protocol's crawl on the headline's keys (tree_crawl with gc_sender per level,
     collect.rs:419-482, with OtSender/OtReceiver::init per channel and level, :454-471; the leader's
     loop leader.rs:422-440): the GPU garbled-circuit equality test and both OT extensions in every
@@ -630,7 +630,7 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
 
     def run(levels=None):
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=False,
-                             comm=comm, gc="ot", base_ot=True, levels=levels)
+                             comm=comm, gc=gc, base_ot=True, levels=levels)
 
     def barrier():
         if dist is not None:
@@ -662,7 +662,12 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh):
         "base_ot_stall_ms": s0["base_ot_stall_ms"],
         "base_ot_note": "compute = summed per-instance CO15 + key-schedule time over the host threads; stall = time "
                         "the level loop waited for an instance it needed (the base OTs on the critical path)",
-        "protocol": "the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); FE "
+        "protocol": ("the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); every "
+                     "level: half-gates GC (TCCR; the garbler's string and mask folded in); FE levels: the share "
+                     "from the circuit's output labels (cr_hash of W_0, W_0 ^ Delta); the FieldElm level: ALSZ "
+                     "correlated OT for the share (21 AES blocks per d=1 FE-level test: garble 8 + 2, evaluate "
+                     "4 + 1, labels OT expands 2 x 3)") if gc == "ot-circuit" else
+                    "the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); FE "
                     "levels: equality + share as one garbled table per test (Yao's garbled gate with "
                     "point-and-permute over the 2d input labels, rows keyed by cr_hash, 8 B per row; the "
                     "garbler's string and mask folded in); the FieldElm level: half-gates GC (TCCR) + ALSZ "
@@ -747,6 +752,8 @@ def main():
                          "exercises the init-failure fallback to the hosted communicator. Never a measurement.")
     ap.add_argument("--timing-every", type=int, default=1,
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
+    ap.add_argument("--no-protocol-circuit", action="store_true",
+                    help="skip the second protocol crawl with the half-gates circuit at every level")
     ap.add_argument("--no-protocol-crawl", action="store_true",
                     help="skip the real protocol's crawl (GC + OT + real base OTs every level) that follows the "
                          "headline's timed region on the zipf workload")
@@ -906,6 +913,12 @@ def main():
     proto = None
     if args.workload == "zipf" and args.gc == "none" and not args.no_protocol_crawl:
         proto = protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh)
+        if not args.no_protocol_circuit:
+            # the same crawl with the half-gates circuit at every level (the reference's construction,
+            # r05c form) beside the default garbled table: what the table buys, on the same box
+            circ = protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot-circuit")
+            proto["circuit_form"] = {k: circ[k] for k in ("wall_s", "heavy_hitters", "heavy_hitters_equal_headline",
+                                                          "gcot_gpu_ms", "expand_gpu_ms", "protocol")}
 
     if rank == 0:
         launches = max(1, s0["expand_launches_timed"])

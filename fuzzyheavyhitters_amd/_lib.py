@@ -193,7 +193,7 @@ class FhhGbCfg(ctypes.Structure):
     """fhh_gb_cfg: the garbler's (server 0's) own material for one chunk (include/fhh.h)."""
     _fields_ = [
         ("mask", ctypes.c_uint32),
-        ("pad_", ctypes.c_uint32),
+        ("form", ctypes.c_uint32),   # FE levels: 0 garbled table (2d <= 4), 1 half-gates circuit
         ("base_chosen", ctypes.c_uint8 * (2 * 128 * 16)),
         ("base_choice", ctypes.c_uint8 * (2 * 16)),
         ("child_begin", ctypes.c_uint64),
@@ -205,6 +205,8 @@ class FhhEvCfg(ctypes.Structure):
     """fhh_ev_cfg: the evaluator's (server 1's) own material: its base-OT key pairs, nothing else."""
     _fields_ = [
         ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
+        ("form", ctypes.c_uint32),   # as FhhGbCfg.form (public)
+        ("pad_", ctypes.c_uint32),
         ("child_begin", ctypes.c_uint64),
         ("child_count", ctypes.c_uint64),
     ]

@@ -680,7 +680,7 @@ PartyState& party_of(fhh_ctx* ctx) {
     return *ctx->party;
 }
 
-int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_count) {
+int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_count, uint32_t form) {
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     if (ctx->group) return ctx->fail(FHH_E_ARG, "party: run the GC + OT per shard (fhh_shard_ctx)");
@@ -715,7 +715,7 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
     P.tests = P.C * P.n;
     P.per2 = P.last ? 2 : 1;
     P.lshare = !P.last;
-    P.ltable = P.lshare && P.bits <= (uint32_t)kGtMaxBits;
+    P.ltable = P.lshare && P.bits <= (uint32_t)kGtMaxBits && form == 0;   // form 1: the circuit (r05c)
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
     P.m2 = P.lshare ? 0 : P.tests * P.per2;   // OT 2 (the share OT) at the FieldElm level only
     if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
@@ -837,7 +837,8 @@ extern "C" {
 int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev, uint64_t* u_len) {
     CTX_CHECK(ctx);
     if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
-    int rc = party_begin(ctx, 1, cfg->child_begin, cfg->child_count);
+    if (cfg->form > 1) return ctx->fail(FHH_E_ARG, "ev_ot_labels: form must be 0 (table) or 1 (circuit)");
+    int rc = party_begin(ctx, 1, cfg->child_begin, cfg->child_count, cfg->form);
     if (rc) return rc;
     PartyState& P = *ctx->party;
     // both OT kinds' receiver schedules and session counters (OtReceiver::init, collect.rs:460)
@@ -873,7 +874,8 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
                      uint64_t* y_len) {
     CTX_CHECK(ctx);
     if (!cfg || !y_dev || !y_len) return ctx->fail(FHH_E_ARG, "gb_ot_labels: NULL argument");
-    int rc = party_begin(ctx, 0, cfg->child_begin, cfg->child_count);
+    if (cfg->form > 1) return ctx->fail(FHH_E_ARG, "gb_ot_labels: form must be 0 (table) or 1 (circuit)");
+    int rc = party_begin(ctx, 0, cfg->child_begin, cfg->child_count, cfg->form);
     if (rc) return rc;
     PartyState& P = *ctx->party;
     rc = check_in(ctx, u_dev, u_len, P.m1 ? u_bytes(P.m1) : 0, "U (labels OT)");

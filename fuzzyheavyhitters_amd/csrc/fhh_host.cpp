@@ -1120,7 +1120,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     HIP_TRY(c0, B.ctl_host.ensure(sizeof(LoopCtl)));
     rc = loop_resize(c0, B, cap0, cap0, levels, 0, false, 0, 0, 1);
     if (rc) return rc;
-    if (cfg->gc == 2 && cfg->base_ot) {
+    if (cfg->gc >= 2 && cfg->base_ot) {
         // the OT extensions of every level and chunk each start with 128 Chou–Orlandi base OTs
         // (AlszSender/AlszReceiver::init, collect.rs:454-471): host threads produce them a few levels
         // ahead of this thread's enqueueing, which waits only for the chunk it is about to enqueue
@@ -1355,7 +1355,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     const bool lshare = real_ot && pmode == 1;
                     // r05d: tests of <= kGtMaxBits bits (d <= 2) take the share from ONE garbled table per
                     // test (k_gt_garble / k_gt_eval: 2^bits + 1 AES instead of the half-gates chain's)
-                    const bool ltable = lshare && bits <= (uint32_t)kGtMaxBits;
+                    const bool ltable = lshare && bits <= (uint32_t)kGtMaxBits && cfg->gc == 2;   // gc 3: the circuit
                     if (ltable) {
                         for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
                         HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
@@ -2236,7 +2236,8 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     const uint32_t levels = cfg->levels ? cfg->levels : c0->L;
     if (levels > c0->L) return c0->fail(FHH_E_ARG, "sim_crawl: levels > data_len");
     if (cfg->mode > 1) return c0->fail(FHH_E_ARG, "sim_crawl: bad mode");
-    if (cfg->gc > 2) return c0->fail(FHH_E_ARG, "sim_crawl: gc must be 0, 1 (ideal OT) or 2 (OT extension)");
+    if (cfg->gc > 3)
+        return c0->fail(FHH_E_ARG, "sim_crawl: gc must be 0, 1 (ideal OT), 2 (OT extension) or 3 (2 with the circuit at every level)");
     if (cfg->gc && (cfg->mode != 1 || cfg->host_loop))
         return c0->fail(FHH_E_ARG, "sim_crawl: gc needs mode 1 (OT share values) and the device loop");
     if (cfg->gc && 2 * c0->d > (uint32_t)kGcMaxBits) return c0->fail(FHH_E_ARG, "sim_crawl: gc supports d <= 4");

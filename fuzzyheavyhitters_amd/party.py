@@ -116,7 +116,7 @@ class GarblerParty:
                                             chosen.ctypes.data_as(u8p)))
         return B.tobytes(), (chosen, s)
 
-    def chunk_cfg(self, base, child_begin: int, child_count: int) -> FhhGbCfg:
+    def chunk_cfg(self, base, child_begin: int, child_count: int, form: int = 0) -> FhhGbCfg:
         """The garbler's material for one chunk: a fresh mask (AesRng::new() per channel, collect.rs:431;
         its string is folded into the circuit, so it draws no labels) and the level's base OTs (both
         kinds; the labels kind's s is the circuit's Delta)."""
@@ -129,6 +129,7 @@ class GarblerParty:
         ctypes.memmove(cfg.base_chosen, chosen.tobytes(), chosen.nbytes)
         ctypes.memmove(cfg.base_choice, choice.tobytes(), choice.nbytes)
         cfg.child_begin, cfg.child_count = child_begin, child_count
+        cfg.form = form
         return cfg
 
 
@@ -153,13 +154,14 @@ class EvaluatorParty:
         return pairs
 
     @staticmethod
-    def chunk_cfg(base, child_begin: int, child_count: int) -> FhhEvCfg:
+    def chunk_cfg(base, child_begin: int, child_count: int, form: int = 0) -> FhhEvCfg:
         cfg = FhhEvCfg()
         pairs = np.zeros((2, 128, 2, 16), np.uint8)  # [kind][128][2][16]; kind 1 only at the FieldElm level
         for w, b in enumerate(base):
             pairs[w] = b
         ctypes.memmove(cfg.base_pairs, pairs.tobytes(), pairs.nbytes)
         cfg.child_begin, cfg.child_count = child_begin, child_count
+        cfg.form = form
         return cfg
 
 
@@ -245,7 +247,8 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
                     channel: str = "copy", timing: dict | None = None, record: bool = True,
                     chunk_children: int | None = None, chunk_bytes: int = 64 << 30,
                     level_log: list | None = None, base_ot_every: str = "level",
-                    base_ot_workers: int | None = None, base_ot_ahead: int = 8) -> TwoPartyResult:
+                    base_ot_workers: int | None = None, base_ot_ahead: int = 8,
+                    form: str = "table") -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between the
     two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both, run the
     level's protocol through the channel, take each server's node sums from its own device
@@ -267,9 +270,14 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     phase: crawl, gcot, node_sums, keep, prune. A level's tests run in chunks of `chunk_children`
     children (None: as many as `chunk_bytes` of both parties' buffers hold at ~512 B per test; 0: the
     whole level), one protocol instance per chunk. `level_log` (a list) receives one (level, children,
-    crawl_s, gcot_s, node_sums_s) tuple per level."""
+    crawl_s, gcot_s, node_sums_s) tuple per level. `form`: "table" (the FE levels' test as one garbled
+    table where 2d <= 4, r05d) or "circuit" (the half-gates circuit at every level, r05c) — a public
+    protocol choice both parties make alike."""
     if material not in ("fresh", "test"):
         raise ValueError(f"two_party_crawl: material {material!r}")
+    if form not in ("table", "circuit"):
+        raise ValueError(f"two_party_crawl: form {form!r}")
+    form_id = 0 if form == "table" else 1
     if base_ot_every not in ("level", "crawl"):
         raise ValueError(f"two_party_crawl: base_ot_every {base_ot_every!r}")
     L = levels or c0.depth
@@ -344,12 +352,13 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
                     gb_base, ev_base = level_base(lv, k)
                 for j, (cb, cc) in enumerate(chunk_windows(C0, chunk_children)):
                     if material == "fresh":
-                        cfg_gb = gbp.chunk_cfg(gb_base, cb, cc)
-                        cfg_ev = evp.chunk_cfg(ev_base, cb, cc)
+                        cfg_gb = gbp.chunk_cfg(gb_base, cb, cc, form_id)
+                        cfg_ev = evp.chunk_cfg(ev_base, cb, cc, form_id)
                     else:
                         cfg_gb, cfg_ev = test_cfgs(prf_seed ^ (k << 40) ^ (j << 48), lv)
                         cfg_gb.child_begin, cfg_gb.child_count = cb, cc
                         cfg_ev.child_begin, cfg_ev.child_count = cb, cc
+                        cfg_gb.form = cfg_ev.form = form_id
                     for name, v in run_chunk(a, b, cfg_gb, cfg_ev, to_gb, to_ev).items():
                         sizes[name] = sizes.get(name, 0) + v
             res.level_bytes.append(sizes)

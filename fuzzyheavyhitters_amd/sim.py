@@ -70,7 +70,8 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     device loop) takes each (child, client) equality bit from the GPU garbled-circuit equality
     test (server 0 garbles, server 1 evaluates) instead of comparing shares: `True` / "ot" with
     the evaluator's labels and the FE shares moved by the GPU OT extension (base OTs ideal),
-    "ideal" with both OTs ideal.
+    "ideal" with both OTs ideal; "ot-circuit" as "ot" but the half-gates circuit (+ the output-label
+    share) at every level instead of the FE levels' garbled table.
 
     `probe` (parity tests) = {"levels": [...], "clients": [...], "capacity": C_max}: the device
     loop gathers those clients' EvalStates of every pending child right after each listed
@@ -85,7 +86,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.prf_seed = prf_seed
     cfg.host_loop = 1 if host_loop else 0
     cfg.init_capacity = init_capacity
-    cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2}[gc]
+    cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2, "ot-circuit": 3}[gc]
     cfg.base_ot = 1 if base_ot else 0   # gc = "ot": Chou–Orlandi base OTs on the host (else ideal)
     ar = None
     if comm is not None:

@@ -275,7 +275,9 @@ typedef struct fhh_sim_config {
      * evaluator's input labels, the FE share conversion) are ideal; 2 = both run as GPU correlated
      * OT extension (fhh_cot_extend_host's modes: the labels as FHH_COT_RAW with the labels session's
      * s as Delta, the share as FHH_COT_FE / FHH_COT_FE255, a FieldElm share as a BlockPair = 2 OTs).
-     * Same sums as 0. Material from prf_seed (a harness, not private): the mask fresh per chunk of
+     * 2 takes the FE levels' test (2d <= 4) as one garbled table (fhh_gt_cot_host, r05d); 3 = 2 with
+     * the half-gates circuit + output-label share (fhh_gc_cot_host's share outputs, r05c) at every FE
+     * level instead. Same sums as 0. Material from prf_seed (a harness, not private): the mask fresh per chunk of
      * children; one base-OT session per level and OT kind, each chunk on its own row-PRG counter
      * range; gate tweaks carry the level (bits 40+). */
     uint32_t gc;
@@ -609,7 +611,8 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * it while the material is unchanged (a new set starts at 0), so pads never repeat. */
 typedef struct fhh_gb_cfg {
     uint32_t mask;                       /* the chunk's mask bit (equalitytest.rs:38-43)           */
-    uint32_t pad_;
+    uint32_t form;                       /* FE levels: 0 = the garbled table where 2d <= 4 (r05d),
+                                            1 = the half-gates circuit (r05c); both parties alike  */
     uint8_t base_chosen[2][128][16];     /* per OT kind (0 labels, 1 shares — read at tree_crawl_last
                                             only since r05c): k_i^{s_i} from the                    */
     uint8_t base_choice[2][16];          /* base OTs, and s (bit i % 8 of byte i / 8); the labels
@@ -620,6 +623,8 @@ typedef struct fhh_gb_cfg {
 typedef struct fhh_ev_cfg {
     uint8_t base_pairs[2][128][2][16];   /* per OT kind: both base-OT keys of every base OT (kind 1
                                             read at tree_crawl_last only, r05c)                    */
+    uint32_t form;                       /* as fhh_gb_cfg.form (the public protocol choice)       */
+    uint32_t pad_;
     uint64_t child_begin;
     uint64_t child_count;
 } fhh_ev_cfg;

@@ -148,7 +148,7 @@ def _sig(res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15"])
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15", "ot-circuit", "ot-circuit+co15"])
 @pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
 def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
     """tree_crawl with the GC equality test (collect.rs:419-482) gives the same FE sums, keep
@@ -172,7 +172,7 @@ def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15"])
+@pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15", "ot-circuit"])
 def test_gpu_crawl_with_gc_in_chunks(monkeypatch, gc_mode):
     """A level's GC + OT split into chunks of children, each a fresh protocol instance (the
     reference spreads a level's tests over its channels, collect.rs:423-430; the device loop

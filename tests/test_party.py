@@ -66,6 +66,26 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     assert lbl["gc"] == Cl * n * (2 * (bits - 1) * 16 + 1) and lbl["y2"] == Cl * n * 2 * 16
 
 
+@pytest.mark.parametrize("d,n,L,thr", [(1, 300, 20, 0.02), (2, 200, 12, 0.05)], ids=["d1", "d2"])
+def test_two_party_circuit_form(d, n, L, thr):
+    """form="circuit" (both parties: the half-gates circuit + output-label share at every FE level,
+    r05c) equals fhh_sim_crawl(gc="ot-circuit") and the table form level by level; its gc message is the
+    tables, the 8-B share y and the decoding bit per test."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(n, 32, d, num_sites=5, seed=40 + d)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    c0, c1 = _keys(wl, L, d)
+    ref = fhh.sim_crawl(c0, c1, thr, mode="fe", prf_seed=5, gc="ot-circuit")
+    p0, p1 = _keys(wl, L, d)
+    got = fhh.two_party_crawl(p0, p1, thr, form="circuit")
+    _assert_same_crawl(ref, got)
+    t0, t1 = _keys(wl, L, d)
+    _assert_same_crawl(got, fhh.two_party_crawl(t0, t1, thr, form="table"))
+    lb, C0, bits = got.level_bytes[0], int(got.level_children[0]), 2 * d
+    assert lb["gc"] == C0 * n * (2 * (bits - 1) * 16 + 8 + 1) and lb["u2"] == 0 and lb["y2"] == 0
+
+
 def test_two_party_fresh_randomness_same_output():
     """Independently drawn material (each party's own label keys, Deltas, masks and CO15 base OTs) in
     two runs: every transcript differs, the leader's output does not, and equals the test-seed run's;

@@ -24,7 +24,7 @@ def test_party_cfg_layouts_match_header():
     x86-64: every field is naturally aligned), the chunk window last."""
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
     gb = 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8
-    ev = 2 * 128 * 2 * 16 + 8 + 8
+    ev = 2 * 128 * 2 * 16 + 4 + 4 + 8 + 8
     assert ctypes.sizeof(FhhGbCfg) == gb and ctypes.sizeof(FhhEvCfg) == ev
     for T, size in ((FhhGbCfg, gb), (FhhEvCfg, ev)):
         assert T.child_begin.offset == size - 16 and T.child_count.offset == size - 8
@@ -41,7 +41,7 @@ def test_evaluator_cfg_carries_no_garbler_secret():
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
     ev_fields = {f for f, _ in FhhEvCfg._fields_}
     gb_fields = {f for f, _ in FhhGbCfg._fields_}
-    assert ev_fields == {"base_pairs", "child_begin", "child_count"}
+    assert ev_fields == {"base_pairs", "form", "pad_", "child_begin", "child_count"}   # form: public
     for secret in ("mask", "base_chosen", "base_choice"):
         assert secret in gb_fields and secret not in ev_fields
     assert "delta" not in gb_fields | ev_fields

@@ -446,7 +446,13 @@ __global__ __launch_bounds__(kOtOutThreads) void k_ot_rows_out(OtArgs a, int sen
     const uint32_t q = lane >> 2, g = lane & 3;
     for (uint64_t t = (uint64_t)blockIdx.x * (kOtOutThreads / 64) + wv; t < tiles; t += nwaves) {
         uint32_t x[32];
-        ot_tile_load(rows, t, lane, x);   // x[k] = word g of OT 32 (16 t + q) + k
+        {   // the tile as ot_tile_load reads it, by cached loads: rows r, r + 1 share a 128-B line (the
+            // non-temporal form measured 2.40-2.48 s per 1M crawl against 2.29-2.33 s, profiles/r05/table/)
+            const uint32_t* p = rows + t * (128 * kOtTileWords) + (32 * g) * kOtTileWords + q;
+#pragma unroll
+            for (int i = 0; i < 32; i++) x[i] = p[i * kOtTileWords];
+            transpose32(x);   // x[k] = word g of OT 32 (16 t + q) + k
+        }
 #pragma unroll
         for (int k = 0; k < 32; k++) st[kOtOutStride * q + 4 * k + g] = x[k];
         __builtin_amdgcn_wave_barrier();

@@ -440,6 +440,7 @@ __device__ __forceinline__ uint64_t fe_dec(uint64_t v) { return v ? v - 1 : kOtF
 #define FHH_GT_EVAL_U 2
 #endif
 
+
 template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
     __shared__ uint32_t tbl_gc[GcTab::kWords];
@@ -463,32 +464,48 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble(GcArgs a) {
     }
     const uint64_t n_act = gc_active(a);
     const uint64_t stride = (uint64_t)gridDim.x * kGcThreads;
+    // the raw inputs of a lane's U tests (labels E_k, the garbler's bits x_k as a mask)
+    auto fetch = [&](uint64_t t0f, uint32_t (&zr)[U][B][4], uint32_t (&xr)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t t = t0f + u * stride;
+            const uint64_t tc = t < n_act ? t : (t0f < n_act ? t0f : 0);   // a valid test for padding lanes
+            const uint64_t g = tc / a.N;
+            const uint32_t i = (uint32_t)(tc - g * a.N);
+            xr[u] = 0;
+#pragma unroll
+            for (int k = 0; k < B; k++) {
+                ld_blk(a.ev_labels, g * B + k, Npad, i, zr[u][k]);   // E_k, the labels OT's q
+                xr[u] |= plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i) << k;
+            }
+        }
+    };
+    // (fetching the next pass's inputs during this pass's AES measured +1 %: the kernel waits on LDS
+    // issue, not on these loads; profiles/r05/table/ab_gt_prefetch.json)
     for (uint64_t t0 = (uint64_t)blockIdx.x * kGcThreads + threadIdx.x; t0 < n_act; t0 += U * stride) {
+        uint32_t zc[U][B][4], xc[U];
+        fetch(t0, zc, xc);
         uint32_t S[U][4], col[U];
         uint64_t tt[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t t = t0 + u * stride;
             tt[u] = t;
-            const uint64_t tc = t < n_act ? t : t0;   // a valid test for the padding lanes
-            const uint64_t g = tc / a.N;
-            const uint32_t i = (uint32_t)(tc - g * a.N);
+            const uint64_t tc = t < n_act ? t : t0;
             const uint64_t tw = a.gate_base + a.g_off * a.N + tc;   // the test's index in the whole level
 #pragma unroll
             for (int c = 0; c < 4; c++) S[u][c] = 0u;
             col[u] = 0;
 #pragma unroll
             for (int k = B - 1; k >= 0; k--) {   // Horner: S = sigma(S) ^ Z_k
-                uint32_t z[4];
-                ld_blk(a.ev_labels, g * B + k, Npad, i, z);   // E_k, the labels OT's q
-                const uint32_t xb = plane_bit(a.gb_planes, a.g_off + g, B, k, a.nw, i);
                 gf_dbl(S[u]);
+                const uint32_t xb = (xc[u] >> k) & 1u;
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-                    z[c] ^= xb ? 0u : a.delta[c];   // Z_k = E_k ^ (x_k ? 0 : Delta)
-                    S[u][c] ^= z[c];
+                    const uint32_t z = zc[u][k][c] ^ (xb ? 0u : a.delta[c]);   // Z_k = E_k ^ (x_k ? 0 : Delta)
+                    S[u][c] ^= z;
+                    if (c == 0) col[u] |= (z & 1u) << k;
                 }
-                col[u] |= (z[0] & 1u) << k;
             }
             S[u][0] ^= (uint32_t)tw;
             S[u][1] ^= (uint32_t)(tw >> 32);

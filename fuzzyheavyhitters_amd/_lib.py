@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,7 +40,7 @@ EXPORTS = [
     "fhh_node_sums_fe255", "fhh_tree_prune", "fhh_tree_prune_last", "fhh_frontier_size",
     "fhh_final_shares", "fhh_export_states", "fhh_keep_values", "fhh_keep_values_last",
     "fhh_final_values", "fhh_sim_eq_count", "fhh_sim_ot_sums", "fhh_sim_crawl",
-    "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench", "fhh_microbench_gather", "fhh_microbench_hybrid", "fhh_debug_aes_ps", "fhh_sketch_set_impl", "fhh_sketch_plan",
+    "fhh_get_stats", "fhh_reset_stats", "fhh_set_timing", "fhh_device_info", "fhh_microbench", "fhh_microbench_gather", "fhh_microbench_hybrid", "fhh_sketch_set_impl", "fhh_sketch_plan",
     "fhh_debug_launch_gaps", "fhh_wave_profile_arm", "fhh_wave_profile_launches",
     "fhh_set_variant", "fhh_variant_info",
     "fhh_rccl_load", "fhh_comm_unique_id", "fhh_comm_create", "fhh_comm_destroy", "fhh_comm_allreduce_u64",
@@ -109,7 +110,7 @@ class FhhSimConfig(ctypes.Structure):
     ]
 
 
-SOURCES = ("fhh_kernels.hip", "fhh_expand_bs.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_ot.hip", "fhh_loop.hip",
+SOURCES = ("fhh_kernels.hip", "fhh_sketch.hip", "fhh_gc.hip", "fhh_ot.hip", "fhh_loop.hip",
            "fhh_microbench.hip", "fhh_host.cpp", "fhh_gcot.cpp", "fhh_group.cpp", "fhh_comm.cpp", "fhh_base_ot.cpp")
 
 
@@ -223,10 +224,14 @@ def build(verbose: bool = False) -> str:
     objdir = os.path.join(_HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall"]
-    if os.environ.get("FHH_AB_VARIANTS"):   # A/B builds: the measured-negative k_expand variants too
-        flags.append("-DFHH_AB_VARIANTS")
-    if os.environ.get("FHH_EXTRA_DEFINES"):   # A/B builds only (tools/ab_builds.sh)
-        flags += ["-D" + d for d in os.environ["FHH_EXTRA_DEFINES"].split()]
+    # kernel tuning defines are honoured only in an explicit A/B build (tools/ab_builds.sh sets both),
+    # and announced, so a stray environment variable cannot change the product kernels silently
+    extra = os.environ.get("FHH_EXTRA_DEFINES", "").split()
+    if extra and os.environ.get("FHH_AB_BUILD") == "1":
+        flags += ["-D" + d for d in extra]
+        print(f"fhh build: A/B defines {extra}", file=sys.stderr)
+    elif extra:
+        print("fhh build: FHH_EXTRA_DEFINES ignored (set FHH_AB_BUILD=1 for an A/B build)", file=sys.stderr)
 
     def compile_one(f):
         obj = os.path.join(objdir, f + ".o")
@@ -325,7 +330,6 @@ def lib():
         "fhh_microbench": (i, [i, i, P(ctypes.c_double)]),
         "fhh_microbench_gather": (i, [i, i, ctypes.c_uint32, P(ctypes.c_double)]),
         "fhh_microbench_hybrid": (i, [i, i, P(ctypes.c_double)]),
-        "fhh_debug_aes_ps": (i, [i, u8p, u8p]),
         "fhh_sketch_set_impl": (i, [i]),
         "fhh_sketch_plan": (i, [u64, u32, u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int)]),

@@ -1,5 +1,5 @@
-// Bitslice transposition helpers shared by the device kernels (fhh_expand_bs.hip) and the
-// host self-test (tests/host/aes_bs_host_test.cpp).
+// The 32 x 32 bit transpose of the OT kernels (fhh_ot.hip) and the garbled-table kernels (fhh_gc.hip),
+// which read the tile-major IKNP matrices as row words; host self-test tests/host/transpose_host_test.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

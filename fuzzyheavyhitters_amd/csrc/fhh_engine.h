@@ -121,8 +121,6 @@ struct fhh_ctx {
     std::vector<uint8_t> h_key_idx, h_root, h_cws, h_cwb;
     uint64_t h_n = 0;
     bool dev_keys = false;        // keys resident on the device (uploaded or generated)
-    bool keys_bs = false;         // cw_seed / root_seed rows in the bitsliced layout
-    bool tab_bs = false;          // prefix tables (since the last tree_init) in the bitsliced layout
 
     DevBuf cw_seed, cw_bits, root_seed, key_idx, valid;
     DimTable tab[kMaxDims];

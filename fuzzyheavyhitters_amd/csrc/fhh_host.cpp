@@ -184,7 +184,6 @@ int upload_staged_keys(fhh_ctx* ctx) {
     rc = sync(ctx);
     if (rc) return rc;
     ctx->dev_keys = true;
-    ctx->keys_bs = false;
     ctx->h_key_idx.clear();
     ctx->h_root.clear();
     ctx->h_cws.clear();
@@ -248,50 +247,8 @@ int upload_lists(fhh_ctx* ctx) {
     return FHH_OK;
 }
 
-// Convert the device keys' 16-byte seed rows (CW seeds [L][K], root seeds [K]) to the layout
-// the selected k_expand variant reads (bitsliced for kBsVariant, client-major otherwise).
-int ensure_key_layout(fhh_ctx* ctx) {
-    const bool want = variant_is_bs(ctx->variant);
-    if (ctx->keys_bs == want) return FHH_OK;
-    DevBuf* bufs[2] = {&ctx->cw_seed, &ctx->root_seed};
-    const uint64_t rows[2] = {(uint64_t)ctx->L * ctx->K, (uint64_t)ctx->K};
-    for (int b = 0; b < 2; b++) {
-        DevBuf tmp;
-        HIP_TRY(ctx, tmp.ensure(rows[b] * ctx->npad * 16));
-        HIP_TRY(ctx, launch_bitslice(bufs[b]->as<uint4>(), tmp.as<uint4>(), rows[b], (uint32_t)ctx->npad, want ? 1 : 0,
-                                     ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        std::swap(bufs[b]->p, tmp.p);
-        std::swap(bufs[b]->bytes, tmp.bytes);
-    }
-    ctx->keys_bs = want;
-    return FHH_OK;
-}
-
-// bitsliced rows [rows][32][ng] uint4 -> client-major [rows][npad] uint4 (host; export paths)
-void host_unbitslice(std::vector<uint8_t>& buf, size_t rows, size_t npad) {
-    const size_t ng = npad / 32;
-    std::vector<uint8_t> out(buf.size());
-    const uint32_t* in = reinterpret_cast<const uint32_t*>(buf.data());
-    uint32_t* o = reinterpret_cast<uint32_t*>(out.data());
-    for (size_t r = 0; r < rows; r++)
-        for (size_t g = 0; g < ng; g++) {
-            uint32_t w[128];
-            for (int i = 0; i < 128; i++) w[i] = in[((r * 32 + i / 4) * ng + g) * 4 + i % 4];
-            for (int j = 0; j < 32; j++)
-                for (int k = 0; k < 4; k++) {
-                    uint32_t v = 0;
-                    for (int b = 0; b < 32; b++) v |= ((w[32 * k + b] >> j) & 1u) << b;
-                    o[(r * npad + 32 * g + j) * 4 + k] = v;
-                }
-        }
-    buf.swap(out);
-}
-
 // Prepare expansion jobs for one ctx (dst buffers sized; lists already on the device).
 int prepare_expand(fhh_ctx* ctx, ExpandJob* jobs, uint32_t* njobs) {
-    if (ctx->tab_bs != variant_is_bs(ctx->variant))
-        return ctx->fail(FHH_E_STATE, "k_expand variant changed seed layout mid-crawl; call tree_init");
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         const int src = T.cur, dst = 1 - T.cur;
@@ -331,7 +288,7 @@ void finalize_launch(ExpandLaunch& L, int grid, int variant) {
     uint32_t n_live[kMaxJobs] = {};
     for (uint32_t k = 0; k < L.njobs; k++) n_live[k] = L.job[k].n_live;
     ItemLayout lay;
-    item_layout(n_live, L.njobs, expand_unit(variant, L.job[0].nw), expand_max_group(variant), waves,
+    item_layout(n_live, L.njobs, L.job[0].nw, expand_max_group(variant), waves,
                 expand_tail_split(variant), lay, expand_max_wpi(variant));
     L.wpi = lay.wpi;
     for (uint32_t k = 0; k < L.njobs; k++) {
@@ -577,8 +534,8 @@ int sim_ot_sums_impl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, uint64
     HIP_TRY(c0, c0->scratch2.ensure(std::max<uint64_t>(C, 1) * 8 * 16));
     ChildArgs a = child_args(c0, c1);
     a.prf_seed = seed;
-    if (last) HIP_TRY(c0, launch_sim_ot_fe255(a, c0->scratch2.as<uint64_t>(), c0->stream));
-    else HIP_TRY(c0, launch_sim_ot_fe(a, c0->scratch2.as<uint64_t>(), c0->stream, true));
+    if (last) HIP_TRY(c0, launch_child_sums_fe255(a, c0->scratch2.as<uint64_t>(), c0->stream));
+    else HIP_TRY(c0, launch_child_sums_fe(a, c0->scratch2.as<uint64_t>(), c0->stream, true));
     std::vector<uint64_t> h(C * per);
     rc = fetch_partials(c0, cfg, c0->scratch2.as<uint64_t>(), C * per, h.data());
     if (rc) return rc;
@@ -712,7 +669,6 @@ int add_keys_bincode_records(fhh_ctx* ctx, uint64_t n, const uint8_t* recs) {
                                         ((herr & 4) ? "dims per client" : "") + ")");
     }
     ctx->dev_keys = true;
-    ctx->keys_bs = false;
     return FHH_OK;
 }
 }  // namespace eng
@@ -1048,7 +1004,7 @@ int loop_resize(fhh_ctx* c0, LoopBuffers& B, uint32_t E_cap, uint32_t F_cap, uin
         // a resumed prune reads the (reduced) partials of `level`
         DevBuf npart, nred;
         HIP_TRY(c0, npart.ensure(C_new * 16 * 8));
-        // FE levels add into the partials (k_sim_ot_fe client chunks); k_prune re-zeroes them
+        // FE levels add into the partials (k_child_sums_fe client chunks); k_prune re-zeroes them
         HIP_TRY(c0, hipMemsetAsync(npart.p, 0, C_new * 16 * 8, c0->stream));
         if (B.distributed) HIP_TRY(c0, nred.ensure(C_new * 16 * 8));
         // ... and, multi-rank, the local partials too: the all-reduces of the no-op levels
@@ -1137,7 +1093,6 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         if (cfg->probe_n_levels > LoopBuffers::kMaxProbe || !cfg->probe_levels || !cfg->probe_n_clients ||
             !cfg->probe_clients || !cfg->probe_seeds || !cfg->probe_ty || !cfg->probe_children)
             return c0->fail(FHH_E_ARG, "sim_crawl: bad probe arguments");
-        if (c0->tab_bs) return c0->fail(FHH_E_ARG, "sim_crawl: the probe reads the T-table variants' layout");
         for (uint32_t i = 0; i < cfg->probe_n_clients; i++)
             if (cfg->probe_clients[i] >= c0->n) return c0->fail(FHH_E_ARG, "sim_crawl: probe client out of range");
         HIP_TRY(c0, B.probe_C.ensure((size_t)cfg->probe_n_levels * 4));
@@ -1151,7 +1106,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         uint32_t* l0[kMaxDims] = {nullptr, nullptr, nullptr, nullptr};
         for (uint32_t j = 0; j < d; j++) l0[j] = B.live[0].as<uint32_t>() + (size_t)j * B.E_cap;
         for (uint32_t j = d; j < kMaxDims; j++) l0[j] = l0[0];
-        HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, expand_unit(variant, c0->nw), expand_max_group(variant),
+        HIP_TRY(c0, launch_loop_init(B.ctl.as<LoopCtl>(), d, (uint32_t)c0->nw, expand_max_group(variant),
                                      expand_max_wpi(variant),
                                      d, 2, grid_waves, B.pos[0].as<uint32_t>(), l0, c0->stream));
     }
@@ -1424,16 +1379,16 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     }
                     // the chunk's children's sums (FE: atomics into the partials k_prune zeroed;
                     // FE255: one store per child)
-                    if (pmode == 1) HIP_TRY(c0, launch_sim_ot_fe(ca, part, c0->stream, false));
-                    else HIP_TRY(c0, launch_sim_ot_fe255(ca, part, c0->stream));
+                    if (pmode == 1) HIP_TRY(c0, launch_child_sums_fe(ca, part, c0->stream, false));
+                    else HIP_TRY(c0, launch_child_sums_fe255(ca, part, c0->stream));
                 }
                 if (timed) HIP_TRY(c0, timing_end(c0, gc_slot, kGcotTag));
             } else if (pmode == 0) {
                 HIP_TRY(c0, launch_eq_count(a, part, c0->stream));
             } else if (pmode == 1) {
-                HIP_TRY(c0, launch_sim_ot_fe(a, part, c0->stream, false));
+                HIP_TRY(c0, launch_child_sums_fe(a, part, c0->stream, false));
             } else {
-                HIP_TRY(c0, launch_sim_ot_fe255(a, part, c0->stream));
+                HIP_TRY(c0, launch_child_sums_fe255(a, part, c0->stream));
             }
             // -- cross-rank sum (client-sharded multi-GPU)
             // (the count is the capacity bound: entries past C are never read)
@@ -1501,7 +1456,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.njobs_per_ctx = d;
         pa.nctx = 2;
         pa.grid_waves = grid_waves;
-        pa.unit = expand_unit(variant, c0->nw);
+        pa.unit = (uint32_t)c0->nw;
         pa.max_group = expand_max_group(variant);
         pa.tail_split = expand_tail_split(variant) ? 1u : 0u;
         pa.max_wpi = expand_max_wpi(variant);
@@ -1780,7 +1735,6 @@ int fhh_reset(fhh_ctx* ctx) {
     ctx->h_cwb.clear();
     ctx->h_n = 0;
     ctx->dev_keys = false;
-    ctx->keys_bs = false;
     ctx->n = ctx->npad = ctx->nw = 0;
     ctx->phase = Phase::kNoInit;
     ctx->frontier.clear();
@@ -1873,7 +1827,6 @@ int fhh_gen_keys_pair(fhh_ctx* c0, fhh_ctx* c1, uint64_t n, const uint8_t* left_
     if (rc) return rc;
     c0->stats.keygen_ms += ms;
     c0->dev_keys = c1->dev_keys = true;
-    c0->keys_bs = c1->keys_bs = false;
     return FHH_OK;
 }
 
@@ -1901,15 +1854,11 @@ int fhh_export_keys(fhh_ctx* ctx, uint8_t* key_idx, uint8_t* root_seed, uint8_t*
     const size_t n = ctx->n, K = ctx->K, L = ctx->L, npad = ctx->npad, nw = ctx->nw;
     std::vector<uint8_t> cws(L * K * npad * 16), roots(K * npad * 16);
     std::vector<uint64_t> cwb(L * K * 4 * nw), kidx(K * nw);
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // uploads / keygen / bitslicing are async
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // uploads / keygen are async
     HIP_TRY(ctx, hipMemcpy(cws.data(), ctx->cw_seed.p, cws.size(), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(roots.data(), ctx->root_seed.p, roots.size(), hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(cwb.data(), ctx->cw_bits.p, cwb.size() * 8, hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(kidx.data(), ctx->key_idx.p, kidx.size() * 8, hipMemcpyDeviceToHost));
-    if (ctx->keys_bs) {
-        host_unbitslice(cws, L * K, npad);
-        host_unbitslice(roots, K, npad);
-    }
     for (size_t c = 0; c < n; c++)
         for (size_t kk = 0; kk < K; kk++) {
             const size_t w = c / 64, bit = c % 64;
@@ -1952,9 +1901,6 @@ int fhh_tree_init(fhh_ctx* ctx) {
     rc = upload_staged_keys(ctx);
     if (rc) return rc;
     if (!ctx->dev_keys || ctx->n == 0) return ctx->fail(FHH_E_STATE, "tree_init with no keys (collect.rs:83)");
-    rc = ensure_key_layout(ctx);
-    if (rc) return rc;
-    ctx->tab_bs = ctx->keys_bs;
     for (uint32_t j = 0; j < ctx->d; j++) {
         DimTable& T = ctx->tab[j];
         T.cur = 0;
@@ -2135,7 +2081,6 @@ int fhh_export_states(fhh_ctx* ctx, uint64_t* n_nodes, uint8_t* seeds, uint8_t* 
         HIP_TRY(ctx, hipMemcpy(hs.data(), T.seed[buf].p, hs.size(), hipMemcpyDeviceToHost));
         HIP_TRY(ctx, hipMemcpy(ht.data(), T.t[buf].p, ht.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(ctx, hipMemcpy(hy.data(), T.y[buf].p, hy.size() * 8, hipMemcpyDeviceToHost));
-        if (ctx->tab_bs) host_unbitslice(hs, T.cap[buf] * 2, npad);
         for (uint64_t node = 0; node < F; node++) {
             uint32_t e;
             if (pending) {
@@ -2340,12 +2285,7 @@ int fhh_set_variant(fhh_ctx* ctx, int variant) {
     if (variant < 0 || variant >= expand_variant_count()) return ctx->fail(FHH_E_ARG, "set_variant: no such variant");
     if (!expand_threads(variant))
         return ctx->fail(FHH_E_ARG, "set_variant: variant " + std::to_string(variant) +
-                                        " is not in this build (the A/B variants build with FHH_AB_VARIANTS=1)");
-    // 43 / 44 store no / only the dir-0 child seeds (HBM-write A/B): their states are incomplete,
-    // so they are refused unless the caller asks for diagnostics explicitly
-    if ((variant == 43 || variant == 44) && !std::getenv("FHH_DIAGNOSTIC_VARIANTS"))
-        return ctx->fail(FHH_E_ARG, "set_variant: variants 43/44 are diagnostic (incomplete child states); "
-                                    "set FHH_DIAGNOSTIC_VARIANTS=1 to select them");
+                                        " is not in this build (it holds 52 and 33; the r01-r03 A/B forms were removed)");
     ctx->variant = variant;
     ctx->grid = expand_grid(ctx->device, variant);
     return FHH_OK;

@@ -154,7 +154,7 @@ __host__ __device__ inline void item_layout(const uint32_t* n_live, uint32_t njo
 // k_expand's dynamic work heads inside fhh_ctx::work_counter (kWorkCounterBytes): two sets of
 // kExpandHeads per-XCD heads (one 64-B line each) by launch parity (the kernel zeroes the next
 // launch's set), then the wave-timeline exit count of the profiling variant; words 0-1 belong to the
-// A/B bitsliced kernels' re-armed counter (FHH_AB_VARIANTS)
+// r01 A/B kernels' re-armed counter (unused since r06)
 constexpr uint32_t kExpandHeads = 8, kExpandSlot0 = 16, kExpandSlotStride = 16;
 constexpr uint32_t kExpandProfSlot = kExpandSlot0 + 2 * kExpandHeads * kExpandSlotStride;
 constexpr size_t kWorkCounterBytes = 2048;
@@ -275,11 +275,11 @@ struct PruneArgs {
     uint32_t njobs_per_ctx;     // = d
     uint32_t nctx;              // 2 (pair)
     uint64_t grid_waves;        // persistent k_expand waves (for the group size)
-    uint32_t unit;              // k_expand items per entry group (nw; bitsliced: 4 * ceil(nw / 32))
-    uint32_t max_group;         // entries per item cap (8; bitsliced: 1)
+    uint32_t unit;              // k_expand items per entry group (nw)
+    uint32_t max_group;         // entries per item cap
     uint32_t tail_split;        // item_layout end phase (expand_tail_split)
     uint32_t max_wpi;           // item_layout words-per-item cap (expand_max_wpi)
-    // FE levels: k_sim_ot_fe adds its client chunks into the partials by atomics, so a prune that
+    // FE levels: k_child_sums_fe adds its client chunks into the partials by atomics, so a prune that
     // completes zeroes them for the next level (a memset node would also run after a sticky
     // abort and wipe the sums the resumed prune re-reads)
     uint64_t* zero_partials;
@@ -308,8 +308,8 @@ int expand_threads(int variant);
 hipError_t launch_eq_count(const ChildArgs& a, uint64_t* counts, hipStream_t stream);
 hipError_t launch_share_planes(const ChildArgs& a, uint64_t* out, hipStream_t stream);
 // zero: clear partials first (host-driven launches); the device loop's k_prune clears them instead
-hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream, bool zero);
-hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials /*[C][16]*/, hipStream_t stream);
+hipError_t launch_child_sums_fe(const ChildArgs& a, uint64_t* partials /*[C][4]*/, hipStream_t stream, bool zero);
+hipError_t launch_child_sums_fe255(const ChildArgs& a, uint64_t* partials /*[C][16]*/, hipStream_t stream);
 // per-child limb partials of values [C][ld] (n per row) in format fmt (FHH_VALS_*): FE -> [C][2],
 // FE255 -> [C][8]
 hipError_t launch_sum_vals(const void* vals, uint32_t fmt, uint64_t C, uint64_t n, uint64_t ld, uint64_t* partials,
@@ -510,28 +510,6 @@ hipError_t launch_sketch_fe255(const Sketch255Args& a, hipStream_t stream);
 hipError_t launch_mul_fe255(const Mul255Args& a, hipStream_t stream);
 hipError_t launch_verify_fe255(const Verify255Args& a, hipStream_t stream);
 
-// ---- bitsliced k_expand (fhh_expand_bs.hip) -------------------------------------------------
-// Variant kBsVariant selects it; seeds (CW, root, prefix tables) are then stored per key row as
-// [32 quads][npad / 32] uint4 bitsliced words (see fhh_expand_bs.hip). Work item = one
-// (entry, side, dir) x 2048 clients (pair mode: (entry, side) x 2048 clients, both dirs), one
-// entry per item.
-constexpr int kBsVariant = 14;   // first bitsliced variant
-constexpr int kBsCount = 13;     // bitsliced variants 14..26; T-table variants 0..13 and 27..
-hipError_t launch_expand_bs(const ExpandLaunch& a, int which, int grid, uint32_t* work_counter, hipStream_t stream);
-const void* expand_bs_fn(int which);
-int expand_bs_count();
-int expand_bs_threads(int which);
-size_t expand_bs_dyn_lds(int which);   // dynamic LDS bytes a variant launches with
-// pair mode (which >= 2): one 2-wave workgroup per (entry, side, chunk), both dirs
-inline bool bs_pair_mode(int which) { return which != 0 && which != 1 && which != 5; }
-// to_bs = 1: client-major [rows][npad] uint4 -> bitsliced; 0: inverse (out-of-place)
-hipError_t launch_bitslice(const uint4* in, uint4* out, uint64_t rows, uint32_t npad, int to_bs, hipStream_t stream);
-inline bool variant_is_bs(int variant) { return variant >= kBsVariant && variant < kBsVariant + kBsCount; }
-inline uint32_t expand_unit(int variant, uint64_t nw) {
-    if (!variant_is_bs(variant)) return (uint32_t)nw;
-    const uint32_t per_chunk = bs_pair_mode(variant - kBsVariant) ? 2 : 4;   // (side[, dir]) per chunk
-    return (uint32_t)(per_chunk * ((nw + 31) / 32));
-}
 // entries per work item (CW reuse and counter traffic vs. end-of-level tail): variant 29 is
 // variant 3 drawing the next item one entry ahead; 30 / 31 are variant 3 with up to 16 / 32
 // entries per item; 32 / 33 store child seeds nontemporally with up to 8 / 16 entries per item;
@@ -547,7 +525,6 @@ inline uint32_t expand_unit(int variant, uint64_t nw) {
 // pins expand_item_ps: in 45-48 which items the VALU waves take depends on timing); 50 is 34 with
 // ordinary (write-back) child-seed stores instead of nontemporal ones (the power-bound A/B)
 inline uint32_t expand_max_group(int variant) {
-    if (variant_is_bs(variant)) return 1u;
     return (variant == 30 || variant == 33 || variant == 34 || (variant >= 36 && variant <= 52))
                ? 16u : variant == 31 ? 32u : 8u;
 }

@@ -6,7 +6,9 @@
 //   k_eq_count      plaintext stand-in for the GC equality test: clients whose two share
 //                   strings agree, per child (collect.rs:393-482 replaced)
 //   k_share_planes  share-bit planes for the GC (collect.rs:393-418)
-//   k_sim_ot_fe*    simulated OT share values summed per child (collect.rs:439-501, 846-905)
+//   k_child_sums_fe* per-child sums of the share values: the in-process harness's simulated OT
+//                   shares, or (ot_val set) the real protocol's garbled-table / C-OT outputs
+//                   (collect.rs:439-501, 846-905; named k_sim_ot_fe before r06)
 //   k_sum_fe*       per-child sums of host-provided FE / FE255 values (collect.rs:487-501)
 //   k_keygen        batched gen_interval keygen (ibDCF.rs:84-173)
 //   k_init_table    eval_init for every key (ibDCF.rs:229-236, collect.rs:67-92)
@@ -14,18 +16,11 @@
 #include "fhh_internal.h"
 #include "expand_kernel.h"
 #include "../../include/fhh.h"
-// The measured-negative k_expand variants (hybrid T-table + pair-sliced VALU waves 45-49, the bitsliced
-// 14-26 in fhh_expand_bs.hip, the r01-r02 T-table forms) and their generated AES programs
-// (aes_ps_gen.h, aes_bs_gen.h) build only with -DFHH_AB_VARIANTS (FHH_AB_VARIANTS=1 for
-// _lib.build(): A/B builds, tools/ab_builds.sh); the default build holds the product variant 52 and the
-// generic-AES variant 33 the parity suite compares it with.
-#ifdef FHH_AB_VARIANTS
-#include "expand_ps.h"
-#else
-namespace fhh {
-__device__ __forceinline__ void expand_item_ps(const ExpandJob&, uint64_t, uint32_t) {}   // no hybrid variant built
-}  // namespace fhh
-#endif
+// The measured-negative k_expand forms of r01-r03 (bitsliced VALU AES, the T-table + pair-sliced
+// hybrid, the earlier T-table variants) and their generated AES programs were removed in r06; they are
+// in git history at commit 78c7ebe (fhh_expand_bs.hip, expand_ps.h, aes_bs_gen.h, aes_ps_gen.h,
+// tools/gen_aes_bs.py, tools/gen_aes_ps.py). The build holds the product
+// variant 52 and the generic-AES variant 33 the parity suite compares it with.
 
 namespace fhh {
 
@@ -253,8 +248,8 @@ __device__ uint32_t g_wprof_launch = 0;
 // FLAGS: bit 0 = draw the next item one entry ahead, bit 1 = nontemporal child-seed stores,
 // bit 2 = sibling-pair AES (dir 0 / dir 1 share rounds 1-2, aes0_mmo_pair), bit 3 = wave timeline,
 // bit 4 = decode the end-phase items of item_layout (only the variants that lay them out:
-// the extra decode state made the 1024-thread kernel spill), bits 7-11 = NBS: the last NBS waves
-// of every workgroup are VALU waves (expand_item_ps, pair-sliced AES) — the hybrid variants,
+// the extra decode state made the 1024-thread kernel spill), bits 7-11 were the r02 hybrid's VALU
+// waves (removed in r06),
 // bit 12 = MW: a bulk item may span wpi consecutive words (item_layout, narrow levels), and each
 // wave's first item is its wave index instead of a counter draw (the counter then hands out items
 // from nwaves on: 4 096 simultaneous first draws cost ≈ 46 µs at the counter's 88 per µs)
@@ -266,11 +261,10 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     constexpr bool PROF = (FLAGS & 8) != 0;
     constexpr bool TAIL = (FLAGS & 16) != 0;
     constexpr int STORE = (FLAGS >> 5) & 3;   // diagnostic variants 43 / 44 only
-    constexpr int NBS = (FLAGS >> 7) & 31;
     constexpr bool MW = (FLAGS & 4096) != 0;
     constexpr bool NTL = (FLAGS & 8192) != 0;   // bit 13: nontemporal parent-seed loads (MW path)
-    static_assert(!(MW && (AHEAD || TAIL || NBS > 0 || PF)), "MW: plain dynamic items only");
-    static_assert(NBS <= THR / 64, "hybrid: NBS VALU waves out of THR / 64");
+    static_assert(!(MW && (AHEAD || TAIL || PF)), "MW: plain dynamic items only");
+    static_assert(((FLAGS >> 7) & 31) == 0, "the hybrid VALU waves were removed in r06");
     __shared__ uint32_t tbl[Tab::kWords];
     __shared__ uint32_t s_drained;   // bit h: a wave of this workgroup found head h dry
     for (int i = threadIdx.x; i < Tab::kWords; i += THR) tbl[i] = Tab::word(c_T0.v, i);
@@ -282,7 +276,6 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     const uint32_t lane = threadIdx.x & 63;
     uint32_t b0, b1;
     Tab::bases(lane, b0, b1);
-    const bool valu_wave = NBS > 0 && wave_id_uniform() >= (uint32_t)(THR / 64 - NBS);
     const uint64_t wpb = THR / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     // sizes: kernel arguments (host-driven crawl) or LoopCtl (device-resident loop)
@@ -369,8 +362,7 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
             const uint32_t grp = (uint32_t)(local / nwi), w0 = (uint32_t)(local % nwi) * wpi, w1 = min(J.nw, w0 + wpi);
             for (uint32_t w = w0; w < w1; w++)
                 expand_item_wg<Tab, NB, NT, PAIR, STORE, NTL>(J, w, grp, tbl, lane, b0, b1);
-        } else if (NBS > 0 && valu_wave) expand_item_ps(J, item - J.item_begin, lane);
-        else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
+        } else if constexpr (PF) expand_item_pf<Tab, NT, PAIR>(J, item - J.item_begin, tbl, lane, b0, b1);
         else if constexpr (AHEAD) expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1, heads, &nxt);
         else expand_item<Tab, NB, NT, PAIR, STORE>(J, item - J.item_begin, tbl, lane, b0, b1);
         if (heads) {
@@ -401,32 +393,6 @@ __global__ __launch_bounds__(THR, MINW) void k_expand(ExpandLaunch a, uint32_t* 
     }
 }
 
-// test hook: AES_0 of 1024 blocks through the hybrid's pair-sliced data path (k_debug_aes_ps);
-// in / out are host arrays of 1024 x 16 bytes
-#ifdef FHH_AB_VARIANTS
-extern "C" int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out) {
-    if (!in || !out) return FHH_E_ARG;
-    if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
-    uint4 *din = nullptr, *dout = nullptr;
-    if (hipMalloc(&din, 16384) != hipSuccess) return FHH_E_NOMEM;
-    if (hipMalloc(&dout, 16384) != hipSuccess) {
-        (void)hipFree(din);
-        return FHH_E_NOMEM;
-    }
-    hipError_t e = hipMemcpy(din, in, 16384, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_debug_aes_ps, dim3(1), dim3(64), 0, 0, din, dout);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) e = hipMemcpy(out, dout, 16384, hipMemcpyDeviceToHost);
-    (void)hipFree(din);
-    (void)hipFree(dout);
-    return e == hipSuccess ? FHH_OK : FHH_E_HIP;
-}
-#else
-extern "C" int fhh_debug_aes_ps(int, const uint8_t*, uint8_t*) { return FHH_E_ARG; }   // FHH_AB_VARIANTS only
-#endif
-
 // arm the wave timeline: buf = device buffer of cap launches x grid waves x 3 u64 (NULL disarms)
 extern "C" int fhh_wave_profile_arm(int device, uint64_t* buf, uint32_t cap) {
     if (hipSetDevice(device) != hipSuccess) return FHH_E_HIP;
@@ -444,55 +410,11 @@ extern "C" int fhh_wave_profile_launches(int device, uint32_t* launches) {
 }
 
 // Variant table (fhh_set_variant): id, table layout, blocks per lane, threads, min waves, dynamic
-// items, [prefetch, FLAGS]. The default build holds 33 and 52 (the product default); the rest are
-// the A/B forms of r01-r03, built with -DFHH_AB_VARIANTS.
-#ifndef FHH_AB_VARIANTS
+// items, [prefetch, FLAGS]: 52 is the product default, 33 the generic-AES form the parity suite
+// compares it with (the other ids of r01-r03 were removed in r06).
 #define FHH_EXPAND_VARIANTS(X)                                   \
     X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)            \
     X(52, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096 | 8192)
-#else
-#define FHH_EXPAND_VARIANTS(X)                          \
-    X(0, TabT0R64<DevOpsX>, 4, 512, 1, false)           \
-    X(1, TabT0R64<DevOpsX>, 4, 512, 1, true)            \
-    X(2, Tab4T32<DevOpsX>, 4, 1024, 1, false)           \
-    X(3, Tab4T32<DevOpsX>, 4, 1024, 1, true)            \
-    X(4, TabT0R32<DevOpsX>, 2, 256, 1, false)           \
-    X(5, TabT01R32<DevOpsX>, 4, 512, 1, false)          \
-    X(6, TabT0R64<DevOpsX>, 2, 768, 1, false)           \
-    X(7, Tab4T32<DevOpsX>, 2, 1024, 1, false)           \
-    X(8, TabT0R32<DevOpsX>, 2, 384, 1, false)           \
-    X(9, TabT0R32<DevOpsX>, 2, 512, 8, false)           \
-    X(10, TabT0R64<DevOpsX>, 2, 1024, 8, false)         \
-    X(11, TabT0R64<DevOpsX>, 2, 768, 1, true)          \
-    X(12, Tab4T32<DevOpsX>, 4, 1024, 1, true, true)     \
-    X(13, Tab4T32<DevOpsX>, 4, 1024, 1, false, true)   \
-    X(27, Tab4T32<DevOpsX>, 4, 512, 1, true)            \
-    X(28, Tab4T32<DevOpsX>, 4, 512, 1, true, true)      \
-    X(29, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 1)    \
-    X(30, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
-    X(31, Tab4T32<DevOpsX>, 4, 1024, 1, true)              \
-    X(32, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
-    X(33, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 2)    \
-    X(34, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
-    X(35, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6)    \
-    X(36, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 14)   \
-    X(37, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 22)   \
-    X(38, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 30)   \
-    X(39, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 6)     \
-    X(40, Tab4T32<DevOpsX>, 4, 512, 1, true, false, 6)     \
-    X(41, Tab4T32<DevOpsX>, 4, 768, 1, true, false, 7)     \
-    X(42, Tab4T32<DevOpsX>, 4, 1024, 1, true, true, 6)      \
-    X(43, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 38)    \
-    X(44, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 70)   \
-    X(45, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (2 << 7)) \
-    X(46, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (4 << 7)) \
-    X(47, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (6 << 7)) \
-    X(48, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (8 << 7)) \
-    X(49, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | (16 << 7)) \
-    X(50, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 4)      \
-    X(51, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096) \
-    X(52, Tab4T32<DevOpsX>, 4, 1024, 1, true, false, 6 | 4096 | 8192)
-#endif
 
 struct VariantInfo {
     const void* fn;
@@ -502,18 +424,6 @@ struct VariantInfo {
 };
 
 static VariantInfo variant_info(int v) {
-    if (variant_is_bs(v)) {
-        static const char* names[] = {"bitsliced/2 waves/fence2", "bitsliced/3 waves/fence1",
-                                      "bitsliced pair+LDS/2 waves", "bitsliced pair+LDS/3 waves",
-                                      "bitsliced pair+LDS/rolled", "bitsliced/2 waves/rolled",
-                                      "bitsliced pair+LDS/rolled/PROFILE", "bitsliced pair2/rolled",
-                                      "bitsliced pair2/rolled/PROFILE", "bitsliced pair2/unrolled",
-                                      "bitsliced pair2/rolled/carry4 (slow-path test)",
-                                      "bitsliced pair2/rolled/3 waves", "bitsliced pair2/unrolled/3 waves"};
-        const int w = v - kBsVariant;
-        if (w >= expand_bs_count()) return VariantInfo{nullptr, 0, false, ""};   // 0 without FHH_AB_VARIANTS
-        return VariantInfo{expand_bs_fn(w), expand_bs_threads(w), true, names[w]};
-    }
     switch (v) {
 #define FHH_CASE(id, TAB, NB, THR, MINW, DYN, ...) \
     case id: return VariantInfo{reinterpret_cast<const void*>(&k_expand<TAB, NB, THR, MINW, ##__VA_ARGS__>), THR, DYN, TAB::kName};
@@ -523,16 +433,18 @@ static VariantInfo variant_info(int v) {
     }
 }
 
-int expand_variant_count() { return kBsVariant + kBsCount + 26; }
+int expand_variant_count() { return 53; }   // ids 0..52; this build holds 33 and 52
 
 const char* expand_variant_name(int v) { return variant_info(v).name; }
 
 hipError_t launch_expand(const ExpandLaunch& a0, int variant, int grid, uint32_t* work_counter, uint32_t* seq,
                          hipStream_t stream) {
     if (a0.total_items == 0) return hipSuccess;
-    if (variant_is_bs(variant)) return launch_expand_bs(a0, variant - kBsVariant, grid, work_counter, stream);
     ExpandLaunch a = a0;
-    a.seq = (*seq)++;
+    // the head set of this launch is chosen by the sequence's parity, and the launch zeroes the other
+    // set for the next one: the sequence advances only once a dynamic launch has been enqueued, so a
+    // refused or failed launch cannot make the next one draw from a set the launch before used up
+    a.seq = *seq;
     const VariantInfo vi = variant_info(variant);
     if (!vi.fn) return hipErrorInvalidValue;
     const uint64_t wpb = vi.threads / 64;
@@ -549,7 +461,9 @@ hipError_t launch_expand(const ExpandLaunch& a0, int variant, int grid, uint32_t
 #undef FHH_CASE
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess && ctr) ++*seq;
+    return e;
 }
 
 int expand_grid(int device, int variant) {
@@ -557,7 +471,7 @@ int expand_grid(int device, int variant) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     const VariantInfo vi = variant_info(variant);
     int per_cu = 0;
-    const size_t dyn = variant_is_bs(variant) ? expand_bs_dyn_lds(variant - kBsVariant) : 0;
+    const size_t dyn = 0;
     if (!vi.fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vi.fn, vi.threads, dyn) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
@@ -714,7 +628,7 @@ __device__ __forceinline__ bool sim_eq_bit(const ChildArgs& a, const uint32_t (&
 // at ~3 waves per CU for the usual few hundred children (255 µs per level at configs[1]); the
 // chunks' limb sums meet in partials by 64-bit atomics (zeroed by the launcher)
 constexpr uint32_t kSimOtChunk = 16 * kReduceThreads;
-__global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint64_t* partials) {
+__global__ __launch_bounds__(kReduceThreads) void k_child_sums_fe(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[4 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
     const uint64_t C_ = child_end(a);
@@ -748,14 +662,14 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe(ChildArgs a, uint6
     }
 }
 
-hipError_t launch_sim_ot_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream, bool zero) {
+hipError_t launch_child_sums_fe(const ChildArgs& a, uint64_t* partials, hipStream_t stream, bool zero) {
     if (a.C == 0) return hipSuccess;
     if (zero) {
         const hipError_t e = hipMemsetAsync(partials, 0, (size_t)a.C * 4 * sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
     }
     const uint32_t chunks = a.n ? (a.n + kSimOtChunk - 1) / kSimOtChunk : 1;
-    hipLaunchKernelGGL(k_sim_ot_fe, dim3(child_grid(window_cap(a)), chunks), dim3(kReduceThreads), 0, stream, a,
+    hipLaunchKernelGGL(k_child_sums_fe, dim3(child_grid(window_cap(a)), chunks), dim3(kReduceThreads), 0, stream, a,
                        partials);
     return hipGetLastError();
 }
@@ -794,7 +708,7 @@ __device__ __forceinline__ void blockpair_to_limbs(uint4 b0, uint4 b1, uint64_t 
     r[0] = ((uint64_t)__builtin_bswap32(b1.z) << 32) | __builtin_bswap32(b1.w);
 }
 
-__global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, uint64_t* partials) {
+__global__ __launch_bounds__(kReduceThreads) void k_child_sums_fe255(ChildArgs a, uint64_t* partials) {
     __shared__ uint64_t red[16 * (kReduceThreads / 64)];
     const uint64_t base = mix64(a.prf_seed ^ a.level);
     const uint64_t C_ = child_end(a);
@@ -849,9 +763,9 @@ __global__ __launch_bounds__(kReduceThreads) void k_sim_ot_fe255(ChildArgs a, ui
     }
 }
 
-hipError_t launch_sim_ot_fe255(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
+hipError_t launch_child_sums_fe255(const ChildArgs& a, uint64_t* partials, hipStream_t stream) {
     if (a.C == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sim_ot_fe255, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, partials);
+    hipLaunchKernelGGL(k_child_sums_fe255, dim3(child_grid(window_cap(a))), dim3(kReduceThreads), 0, stream, a, partials);
     return hipGetLastError();
 }
 

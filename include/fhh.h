@@ -689,10 +689,9 @@ typedef struct fhh_stats {
 } fhh_stats;
 
 int fhh_get_stats(const fhh_ctx* ctx, fhh_stats* out);
-/* Select the k_expand variant (LDS table layout / blocks per lane / workgroup size / work
- * distribution). All variants are bit-identical; they differ in speed. The default
- * build holds the product variant 52 and the generic-AES variant 33; the measured-negative A/B
- * variants (0-51) build only with FHH_AB_VARIANTS=1 — FHH_E_ARG for a variant not in this build. */
+/* Select the k_expand variant: the product variant 52 (sibling-pair AES, multi-word
+ * items) or the generic-AES variant 33; both are bit-identical. The measured-negative A/B forms of
+ * r01-r03 were removed in r06: FHH_E_ARG for any other id. */
 int fhh_set_variant(fhh_ctx* ctx, int variant);
 /* Describe variant: layout name, workgroup size, persistent grid on the current device.
  * Returns FHH_E_ARG for an id not in this build. */
@@ -713,9 +712,6 @@ int fhh_microbench_gather(int device, int combo, uint32_t gbytes, double* rate);
 // k_hybrid_mix: nb (0, 2, 4, 6, 8) of a 16-wave workgroup's waves run v_bitop3 chains while
 // the others run LDS lookup chains; rates[0] = lookups/s, rates[1] = bitop3 lane-ops/s.
 int fhh_microbench_hybrid(int device, int nb, double* rates);
-// Test hook of the hybrid k_expand's VALU waves: AES-128 (zero key, no feed-forward) of 1024
-// blocks (in / out: 1024 x 16 B host arrays) through the pair-sliced data path of expand_ps.h.
-int fhh_debug_aes_ps(int device, const uint8_t* in, uint8_t* out);
 /* Device time per kernel of `reps` back-to-back launches of an empty kernel on one stream
  * (launch-overhead probe for the level loop): which = 0 -> 256 x 1024 threads, 4 KiB LDS;
  * 1 -> 256 x 1024, 128 KiB LDS (k_expand's footprint); 2 -> alternating 256 x 1024 / 128 KiB and

@@ -41,14 +41,10 @@ def test_device_loop_equals_host_loop(path, cap):
     assert [r.path for r in r1] == [r.path for r in dev.final]
 
 
-@pytest.mark.parametrize("variant", [None, 14], ids=["default", "bitsliced"])
+@pytest.mark.parametrize("variant", [None, 33], ids=["default", "generic-aes"])
 def test_device_loop_large_with_growth(oracle, variant):
     """data_len 512, frontier well past the initial capacity: several grow-and-resume cycles."""
     from fuzzyheavyhitters_amd import sim_crawl, workload
-    if variant is not None:
-        from fuzzyheavyhitters_amd import lib
-        if lib().fhh_variant_info(variant, None, 0, None, None) != 0:
-            pytest.skip("the bitsliced k_expand is an A/B variant (FHH_AB_VARIANTS=1 builds it)")
     wl = workload.zipf_workload(4000, 512, 1, num_sites=60, seed=99)
     c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
     if variant is not None:

@@ -66,30 +66,19 @@ def test_keygen_ragged_and_tiny(kc, oracle):
         assert np.array_equal(cs, k1.cw_seed) and np.array_equal(cb, k1.cw_bits)
 
 
-BS_VARIANT = 14   # bitsliced k_expand (csrc/fhh_expand_bs.hip): seeds stored bitsliced
-
-
-DIAGNOSTIC_VARIANTS = (43, 44)   # store no / half of the child seeds (HBM A/B only, fhh_internal.h)
-
 GENERIC_AES_VARIANT = 33   # T-table k_expand with the generic AES (the default, 52, shares rounds 1-2 of sibling pairs)
+# (the r01-r03 A/B forms — bitsliced, hybrid, pair-sliced — were removed in r06; git history at 78c7ebe)
 
 
 def _need_variant(v):
-    """The A/B variants (bitsliced, hybrid, pair-sliced, r01-r03 T-table forms) build only with
-    FHH_AB_VARIANTS=1; the default build holds 52 and 33."""
+    """Every variant id the tests name is in the build (52 and 33)."""
     if v is None:
         return
     from fuzzyheavyhitters_amd import lib
-    if lib().fhh_variant_info(v, None, 0, None, None) != 0:
-        pytest.skip(f"k_expand variant {v} is an A/B variant, not in this build (FHH_AB_VARIANTS=1 builds it)")
-HYBRID_VARIANT = 46        # T-table waves + 4 pair-sliced VALU waves per workgroup (expand_ps.h)
-VALU_ONLY_VARIANT = 49     # every wave a pair-sliced VALU wave: pins expand_item_ps deterministically
+    assert lib().fhh_variant_info(v, None, 0, None, None) == 0, f"k_expand variant {v} not in this build"
 
 
-@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT, BS_VARIANT + 2, BS_VARIANT + 7,
-                                     BS_VARIANT + 10, HYBRID_VARIANT, VALU_ONLY_VARIANT],
-                         ids=["default", "generic-aes", "bitsliced", "bitsliced-pair", "bitsliced-pair2", "pair2-carry4",
-                              "hybrid", "pair-sliced-only"])
+@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT], ids=["default", "generic-aes"])
 @pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
 def test_level_states_bit_exact(kc, oracle, path, variant):
     """Every level: EvalState seeds/t/y of all children, share planes and equality counts
@@ -105,7 +94,7 @@ def test_level_states_bit_exact(kc, oracle, path, variant):
             c1.set_variant(variant)
         c0.tree_init()
         c1.tree_init()
-        if variant is not None:   # keys now live in the variant's layout; the export undoes it
+        if variant is not None:   # the keys export unchanged after a variant switch
             _, rs, cs, cb = c1.export_keys()
             assert np.array_equal(rs, k1.root_seed) and np.array_equal(cs, k1.cw_seed)
             assert np.array_equal(cb, k1.cw_bits)
@@ -143,13 +132,12 @@ def test_level_states_bit_exact(kc, oracle, path, variant):
                 break
 
 
-@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT, BS_VARIANT + 7, VALU_ONLY_VARIANT],
-                         ids=["default-pair-aes", "generic-aes", "bitsliced-pair2", "pair-sliced-only"])
+@pytest.mark.parametrize("variant", [None, GENERIC_AES_VARIANT], ids=["default-pair-aes", "generic-aes"])
 @pytest.mark.parametrize("d", [1, 2])
 def test_prg_counter_carry_seeds(kc, oracle, variant, d):
     """Root seeds whose byte 8 is 0xFF: the right child's counter (+1 in the upper u64 lane,
     prg.rs:273-276) carries into byte 9, 11 or wraps bytes 8..15 — the carry fallback of the
-    sibling-pair AES and the bitsliced kernels' carry path — at level 0, every client pattern
+    sibling-pair AES — at level 0, every client pattern
     in every wave. Seeds / t / y of the first levels equal the oracle's."""
     _need_variant(variant)
     from fuzzyheavyhitters_amd import workload
@@ -388,11 +376,13 @@ def test_sim_crawl_matches_oracle_crawl(kc, oracle, d, n, L, sites, thr):
 
 
 def test_every_expand_variant_bit_exact(kc, oracle):
-    """All compiled k_expand variants (LDS layout / blocks per lane / workgroup size /
-    static or dynamic items) give the oracle's crawl, twice in a row (the dynamic-item
-    counter re-arms itself between launches), and the oracle's final-level EvalStates."""
+    """Both compiled k_expand variants give the oracle's crawl and the oracle's final-level EvalStates,
+    alternated an odd number of times on one ctx pair with refused selections in between: the dynamic
+    heads alternate by launch parity, and a refused variant must not advance the launch sequence
+    (a sequence step without a launch left the next launch on a used-up head set)."""
     import ctypes
     from fuzzyheavyhitters_amd import lib, sim_crawl, workload
+    from fuzzyheavyhitters_amd._lib import FhhError
     wl = workload.zipf_workload(700, 64, 1, num_sites=9, seed=5)
     k0, k1 = oracle.gen_keys(wl.left, wl.right, wl.root_seeds)
     ores = oracle.crawl(k0, k1, 0.01, mode="count", keep_levels=[62])
@@ -405,68 +395,23 @@ def test_every_expand_variant_bit_exact(kc, oracle):
     buf = ctypes.create_string_buffer(64)
     first = None
     built = [v for v in range(64) if lib().fhh_variant_info(v, buf, 64, None, None) == 0]
-    for v in built:
-        if v in DIAGNOSTIC_VARIANTS:
-            continue
+    assert built == [33, 52]
+    for v in (52, 33, 52, 33, 52):
+        for bad in (0, 14, 46):
+            with pytest.raises(FhhError, match="not in this build"):
+                c0.set_variant(bad)
         c0.set_variant(v)
         c1.set_variant(v)
-        for _ in range(2):
-            res = sim_crawl(c0, c1, 0.01, mode="count")
-            assert np.array_equal(np.concatenate(res.counts), exp_counts), f"variant {v} ({buf.value})"
+        res = sim_crawl(c0, c1, 0.01, mode="count")
+        assert np.array_equal(np.concatenate(res.counts), exp_counts), f"variant {v}"
         # the counts do not depend on the AES (the control bits are constant): the
         # final frontier's seeds must equal the oracle's
         st = [c.export_states() for c in (c0, c1)]
         for (gs, gt, gy), o in zip(st, (last0, last1)):
-            assert gs.shape[0] == kept.size, f"variant {v} ({buf.value}) frontier size"
+            assert gs.shape[0] == kept.size, f"variant {v} frontier size"
             assert np.array_equal(gs, o.seed[kept]) and np.array_equal(gt, o.t[kept]) and \
-                np.array_equal(gy, o.y[kept]), f"variant {v} ({buf.value}) states vs oracle"
-
+                np.array_equal(gy, o.y[kept]), f"variant {v} states vs oracle"
         if first is None:
             first = st
         for (sa, ta, ya), (sb, tb, yb) in zip(first, st):
-            assert np.array_equal(sa, sb) and np.array_equal(ta, tb) and np.array_equal(ya, yb), \
-                f"variant {v} ({buf.value}) states"
-    assert 33 in built and 52 in built
-
-
-def test_diagnostic_variants_refused(monkeypatch):
-    """Variants 43 / 44 store no / half of the child seeds (HBM-write A/B): selecting one without
-    FHH_DIAGNOSTIC_VARIANTS fails loudly instead of crawling with incomplete states."""
-    import fuzzyheavyhitters_amd as fhh
-    from fuzzyheavyhitters_amd._lib import FhhError
-    monkeypatch.delenv("FHH_DIAGNOSTIC_VARIANTS", raising=False)
-    _need_variant(43)
-    c = fhh.KeyCollection(8, 1)
-    for v in DIAGNOSTIC_VARIANTS:
-        with pytest.raises(FhhError, match="diagnostic"):
-            c.set_variant(v)
-    c.set_variant(52)
-    monkeypatch.setenv("FHH_DIAGNOSTIC_VARIANTS", "1")
-    c.set_variant(43)
-
-
-def test_pair_sliced_aes_data_path(oracle):
-    """The hybrid k_expand's VALU waves (expand_ps.h): 1024 blocks through the ballot /
-    v_writelane scatter, the generated pair-sliced AES (DPP swaps, lane-parity round keys) and
-    the two 32x32 transposes equal AES-128 under the zero key (no feed-forward) block by block.
-    Dir-1 units carry the dir-0 block + 1 in the upper u64 lane, as PRG counters do, plus
-    the all-ones / carry patterns."""
-    import ctypes
-    from fuzzyheavyhitters_amd import lib
-    _need_variant(49)   # the pair-sliced data path exists only in an FHH_AB_VARIANTS build
-    rng = np.random.default_rng(11)
-    blk = rng.integers(0, 256, (16, 64, 16), dtype=np.uint8)
-    blk[0, :4] = 0
-    blk[0, 4:8] = 0xFF
-    blk[2, :8, 8:] = 0xFF                 # upper lane wraps for the dir-1 unit
-    for u in range(1, 16, 2):             # dir-1 unit: same bytes 0..7, upper u64 + 1
-        hi = blk[u - 1, :, 8:].copy().view("<u8")[:, 0] + np.uint64(1)
-        blk[u] = blk[u - 1]
-        blk[u, :, 8:] = hi.reshape(-1, 1).view(np.uint8)
-    inp = np.ascontiguousarray(blk.reshape(1024, 16))
-    out = np.zeros_like(inp)
-    u8p = ctypes.POINTER(ctypes.c_uint8)
-    assert lib().fhh_debug_aes_ps(0, inp.ctypes.data_as(u8p), out.ctypes.data_as(u8p)) == 0
-    exp = np.array([np.frombuffer(oracle.aes0(bytes(b)), np.uint8) for b in inp])
-    bad = np.nonzero(np.any(out != exp, axis=1))[0]
-    assert bad.size == 0, f"{bad.size} blocks differ, first {bad[:8].tolist()}"
+            assert np.array_equal(sa, sb) and np.array_equal(ta, tb) and np.array_equal(ya, yb), f"variant {v} states"

@@ -19,24 +19,15 @@ def test_aes_ttable_host(tmp_path):
     assert out.returncode == 0 and out.stdout.strip() == "OK", out.stdout + out.stderr
 
 
-def test_aes_bitsliced_host(tmp_path):
-    """Generated bitsliced AES (csrc/aes_bs_gen.h) + bitslice transposition, emulated bitop3."""
+def test_transpose32_host(tmp_path):
+    """The 32 x 32 bit transpose (csrc/bitslice.h) of the OT hashes and the garbled-table kernels."""
     if not shutil.which("hipcc"):
         pytest.skip("hipcc not available")
-    exe = tmp_path / "aes_bs_host"
-    # -O0: the 15k-op straight-line function takes the optimiser minutes on the host
-    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O0", "-std=c++17",
-                    os.path.join(ROOT, "tests", "host", "aes_bs_host_test.cpp"), "-o", str(exe)], check=True)
+    exe = tmp_path / "transpose_host"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O1", "-std=c++17",
+                    os.path.join(ROOT, "tests", "host", "transpose_host_test.cpp"), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.strip() == "OK", out.stdout + out.stderr
-
-
-def test_aes_bs_generator_check():
-    """tools/gen_aes_bs.py re-derives the LUT program and checks it against AES in Python."""
-    import sys
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_aes_bs.py"), "--check-only"],
-                       capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr
 
 
 def test_item_layout_host(tmp_path):

@@ -419,7 +419,9 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",
         "channel_bytes_per_crawl": bytes_d, "channel_bytes_total": sum(bytes_d.values()),
         "heavy_hitters": hh,
-        "dropin_material": "each server its own (os.urandom: Delta and mask per chunk, CO15 seeds and s); every "
+        "dropin_material": "each server its own (os.urandom: mask per chunk; Delta = the labels base-OT run's s, one "
+                           "per level, the chunks kept apart by disjoint row-PRG ranges and the gate tweaks; CO15 "
+                           "seeds and s); every "
                            "level's labels OT extension on Chou-Orlandi base OTs between the servers over the "
                            "channel (1 CO15 run per level, 2 at the FieldElm level: its share OT; the FE levels' "
                            "shares come from one garbled table per test)",

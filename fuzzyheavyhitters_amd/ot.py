@@ -57,7 +57,9 @@ def cot_extend(kc, mode: int, choices, base_seeds, base_choice, delta=None, mask
     sender values / out [m] u64 (the garbler's r1 = v + mask, the receiver's share); mode 3 (FieldElm,
     OT pairs with one choice): sender values / out [m/2][32] BlockPairs; mode 4 (FHH_COT_RAW, the labels
     OT since r05b): sender_out = q [m][16], out = t [m][16] = q ^ r s, no y (zeros)."""
-    from ._lib import FHH_COT_FE, FHH_COT_FE255
+    from ._lib import FHH_COT_FE, FHH_COT_FE255, FHH_COT_LABELS
+    if mode == FHH_COT_LABELS and delta is None:
+        raise ValueError("cot_extend: the labels mode needs delta (x1 = x0 ^ delta)")
     ch = np.ascontiguousarray(np.asarray(choices).astype(np.uint8) & 1)
     m = ch.size
     seeds = np.ascontiguousarray(base_seeds, np.uint8).reshape(128, 2, 16)

@@ -255,7 +255,10 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     (fhh_party_node_sums), keep_values on the leader, prune both.
 
     material "fresh" (the default, a deployment's behaviour): each party draws its own secrets —
-    the garbler a Delta and mask per chunk — and every level's two OT extensions start
+    the garbler a mask per chunk; its Delta is the labels base-OT run's s (per base-OT run: one per
+    level, or one per crawl with base_ot_every "crawl"), so the chunks sharing a Delta stay independent
+    through their disjoint row-PRG ranges of the run (ctr_off, party_session) and the level and test
+    index in every gate tweak — and every level's two OT extensions start
     from real Chou–Orlandi base OTs run between the parties over the channel (base_ot_every "level",
     as the reference inits per level, collect.rs:454,460; "crawl": one run per OT kind for the whole
     crawl, the library extending it from a running counter). The runs are computed `base_ot_ahead`

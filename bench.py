@@ -620,7 +620,83 @@ def collective_after_init(errs, rehearse_rccl: bool):
     return ("hosted" if rehearse_rccl else "fail"), err
 
 
-def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot"):
+def crawl_sig(res):
+    """What a crawl recovers (leader.rs:417-440, collect.rs:945-1029): every level's child count and counts
+    (count mode: counts; fe mode: v0 - v1, the same integers) and the sorted (path, value) heavy hitters."""
+    import numpy as np
+    counts = np.concatenate([np.asarray(c, np.uint64) for c in res.counts]) if res.counts else np.zeros(0, np.uint64)
+    final = sorted((tuple(tuple(int(b) for b in dim) for dim in r.path), int(r.value)) for r in res.final)
+    return {"level_children": [int(x) for x in res.level_children], "counts": counts, "final": final}
+
+
+def sig_equal(a, b):
+    import numpy as np
+    return (a["level_children"] == b["level_children"] and np.array_equal(a["counts"], b["counts"])
+            and a["final"] == b["final"])
+
+
+def golden_sig(args, n_total):
+    """tests/golden/zipf_1m_L512.npz (tests/golden/make_zipf_1m.py: the plaintext recount of the metric's
+    workload) as a crawl signature, when this run's workload is that one; else None."""
+    import numpy as np
+    if not (args.workload == "zipf" and n_total == 1_000_000 and args.data_len == 512 and args.dims == 1 and
+            args.num_sites == 10_000 and args.zipf == 1.03 and args.ball == 1 and args.seed == 0x5EED and
+            args.threshold == 0.001):
+        return None
+    g = np.load(os.path.join(ROOT, "tests", "golden", "zipf_1m_L512.npz"), allow_pickle=False)
+    L = int(g["data_len"])
+    paths = np.unpackbits(g["paths"], axis=1, bitorder="big")[:, :L]
+    return {"level_children": [int(x) for x in g["level_children"]], "counts": g["counts"].astype(np.uint64),
+            "final": sorted(((tuple(int(b) for b in p),), int(v)) for p, v in zip(paths, g["values"]))}
+
+
+def protocol_aes_blocks(level_children, n: int, d: int, circuit: bool = False):
+    """Executed AES blocks of one real-protocol crawl on this rank (n clients), by phase, from the kernels'
+    work decomposition (fhh_host.cpp level loop; fhh_gc.hip, fhh_ot.hip): FE levels with b = 2d <= 2 run the
+    labels OT's expands (receiver 2, sender 1 AES per OT, OT index over 512-client tiles) and the tile-major
+    garbled table (2^b rows per test garbled, 1 evaluated, padding tests included); b = 4 the row-major table
+    (64-client words) after k_ot_rows_out; the FieldElm level the half-gates circuit (TCCR: 8 AES per AND
+    gate garbled, 4 evaluated) + the share C-OT (2 OTs per test: expands 2 + 1, hashes 2 + 1 per OT) and the
+    labels OT's two row transposes (32 B of HBM per OT and party). circuit: the half-gates circuit + the
+    output-label share (2 AES garbled, 1 evaluated per test) at the FE levels too (gc "ot-circuit")."""
+    b = 2 * d
+    npad64 = (n + 63) // 64 * 64
+    npad_tm = (n + 511) // 512 * 512
+    ph = {"ot_recv_expand": 0, "ot_send_expand": 0, "table_garble": 0, "table_eval": 0, "circuit_garble": 0,
+          "circuit_eval": 0, "share_ot": 0}
+    transpose_bytes = 0
+    L = len(level_children)
+    for lv, C in enumerate(int(x) for x in level_children):
+        if lv + 1 < L and circuit:
+            m1 = C * b * npad64
+            ph["ot_recv_expand"] += 2 * m1
+            ph["ot_send_expand"] += m1
+            ph["circuit_garble"] += (8 * (b - 1) + 2) * C * n
+            ph["circuit_eval"] += (4 * (b - 1) + 1) * C * n
+            transpose_bytes += 2 * 32 * m1
+        elif lv + 1 < L:
+            tm = b <= 2
+            npad = npad_tm if tm else npad64
+            m1 = C * b * npad
+            ph["ot_recv_expand"] += 2 * m1
+            ph["ot_send_expand"] += m1
+            ph["table_garble"] += (1 << b) * C * (npad if tm else n)
+            ph["table_eval"] += C * (npad if tm else n)
+            if not tm:
+                transpose_bytes += 2 * 32 * m1
+        else:
+            m1 = C * b * npad64
+            ph["ot_recv_expand"] += 2 * m1
+            ph["ot_send_expand"] += m1
+            ph["circuit_garble"] += 8 * (b - 1) * C * n
+            ph["circuit_eval"] += 4 * (b - 1) * C * n
+            m2 = 2 * C * n
+            ph["share_ot"] += 2 * m2 + m2 + 2 * m2 + m2
+            transpose_bytes += 2 * 32 * m1
+    return ph, transpose_bytes
+
+
+def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None):
     """The real protocol's crawl on the headline's keys (tree_crawl with gc_sender per level,
     collect.rs:419-482, with OtSender/OtReceiver::init per channel and level, :454-471; the leader's
     loop leader.rs:422-440): the GPU garbled-circuit equality test and both OT extensions in every
@@ -631,7 +707,8 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot"):
     import fuzzyheavyhitters_amd as fhh
 
     def run(levels=None):
-        return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=False,
+        # record: every level's v0 - v1 comes back to the host (a few KB per level) for the output check
+        return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=True,
                              comm=comm, gc=gc, base_ot=True, levels=levels)
 
     def barrier():
@@ -653,10 +730,35 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     hh = len(res.final)
+    sig = crawl_sig(res)
+    ph, tr_bytes = protocol_aes_blocks(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit")
+    total = sum(ph.values())
+    gpu_s = s0["gcot_ms"] / 1e3
+    rate = total / gpu_s if gpu_s > 0 else 0.0
+    roof = {
+        "executed_aes_blocks": total,
+        "executed_aes_blocks_by_phase": ph,
+        "aes_blocks_note": ("executed blocks on this rank from the kernels' work decomposition "
+                            "(bench.protocol_aes_blocks): padding tests of the 512-client tiles included"),
+        "gcot_gpu_s": gpu_s,
+        "blocks_per_s": rate,
+        "valu_tops": rate * VALU_OPS_PER_BLOCK / 1e12,
+        "frac": rate * VALU_OPS_PER_BLOCK / 1e12 / VALU_PEAK_TOPS,
+        "frac_basis": (f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d) x blocks / the GC + OT steps' GPU "
+                       f"time (HIP events) over {VALU_PEAK_TOPS} T ops/s"),
+        "vs_k_expand_in_kernel": rate / expand_rate if expand_rate else None,
+        "transpose_hbm_bytes": tr_bytes,
+        "transpose_note": ("k_ot_rows_out's bytes (32 B per OT and party): since r06 only the FieldElm level's "
+                           "circuit (and d = 2's table) transposes; d = 1's FE levels read Q / T tile-major"),
+    }
     return {
         "wall_s": wall,
         "heavy_hitters": hh,
-        "heavy_hitters_equal_headline": hh == headline_hh,
+        "heavy_hitters_equal_headline": sig_equal(sig, headline_sig) if headline_sig else None,
+        "output_check": ("every level's child count and v0 - v1 per child, and the sorted (path, value) heavy "
+                         "hitters, equal the headline crawl's (recorded in its untimed warm-up)"),
+        "roofline": roof,
+        "sig": sig,
         "base_ot": "chou-orlandi over P-256 (host threads, a fresh instance per level for the labels OT and one "
                    "for the FieldElm level's share OT; chunks on disjoint row-PRG counters)",
         "base_ot_instances": s0["base_ot_instances"],
@@ -875,9 +977,9 @@ def main():
                           "comm_ranks": nr, "comm_rank": rk}
             log(f"[rank {rank}] RCCL communicator: {nr} ranks, rank {rk}")
 
-    def step():
+    def step(record=False):
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
-                             record=False, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc],
+                             record=record, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc],
                              base_ot=args.base_ot)
 
     def barrier():
@@ -885,8 +987,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # the warm-up crawls record every level's counts (D2H per level; untimed): the output the timed steps
+    # and the protocol crawl are checked against
+    res_ref = None
     for _ in range(args.warmup):
-        res = step()
+        res_ref = step(record=True)
     barrier()
     c0.reset_stats()
     c1.reset_stats()
@@ -911,16 +1016,31 @@ def main():
         a = torch.tensor([ar_us or 0.0], dtype=torch.float64)
         dist.all_reduce(a, op=dist.ReduceOp.MAX)
         ar_us_max = float(a.item()) if ar_us is not None else None
-    headline_hh = len(res.final)
+    run_proto = args.workload == "zipf" and args.gc == "none" and not args.no_protocol_crawl
+    if res_ref is None and run_proto:   # no warm-up: one recorded crawl after the timed region
+        res_ref = step(record=True)
+    ref_sig = crawl_sig(res_ref) if res_ref is not None else None
+    gold = golden_sig(args, n_total)
+    checks = None if ref_sig is None else {
+        "timed_final_equal_reference": sorted((tuple(tuple(int(b) for b in d) for d in r.path), int(r.value))
+                                              for r in res.final) == ref_sig["final"],
+        "reference_equal_golden": sig_equal(ref_sig, gold) if gold else None,
+        "golden": "tests/golden/zipf_1m_L512.npz (plaintext recount of the metric's workload)" if gold else None,
+        "note": ("the headline's recorded warm-up crawl: every level's child count and counts and the sorted "
+                 "(path, value) heavy hitters; the timed steps' heavy hitters equal it"),
+    }
+    launches0 = max(1, s0["expand_launches_timed"])
+    expand_rate = (s0["expand_blocks_timed"] / launches0) / (s0["expand_ms"] / launches0 / 1e3) if s0["expand_ms"] else None
     proto = None
-    if args.workload == "zipf" and args.gc == "none" and not args.no_protocol_crawl:
-        proto = protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh)
+    if run_proto:
+        proto = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate)
+        proto["output_equal_golden"] = sig_equal(proto.pop("sig"), gold) if gold else None
         if not args.no_protocol_circuit:
             # the same crawl with the half-gates circuit at every level (the reference's construction,
             # r05c form) beside the default garbled table: what the table buys, on the same box
-            circ = protocol_crawl(args, c0, c1, n_total, comm, dist, headline_hh, gc="ot-circuit")
+            circ = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, gc="ot-circuit", expand_rate=expand_rate)
             proto["circuit_form"] = {k: circ[k] for k in ("wall_s", "heavy_hitters", "heavy_hitters_equal_headline",
-                                                          "gcot_gpu_ms", "expand_gpu_ms", "protocol")}
+                                                          "gcot_gpu_ms", "expand_gpu_ms", "protocol", "roofline")}
 
     if rank == 0:
         launches = max(1, s0["expand_launches_timed"])
@@ -1001,6 +1121,7 @@ def main():
             "protocol_crawl_wall_s": proto["wall_s"] if proto else None,
             "protocol_crawl": proto,
             "final_heavy_hitters": len(res.final),
+            "output_checks": checks,
             "levels": int(len(res.level_children)),
             "children_total": int(res.level_children.sum()),
             "roofline": {

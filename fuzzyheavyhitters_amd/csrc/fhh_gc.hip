@@ -20,6 +20,7 @@
 #include "fhh_internal.h"
 #include "aes_keyed.h"
 #include "cot_fe.h"
+#include "bitslice.h"
 
 namespace fhh {
 
@@ -605,6 +606,285 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval(GcArgs a) {
     }
 }
 
+// ---- r06: the garbled table on the labels OT's tile-major matrices ------------------------------
+// k_gt_garble / k_gt_eval read one row-major 16-B label per (test, bit), which k_ot_rows_out produced
+// from the tile-major Q / T the OT expands write: 32 B of HBM per OT and party (read + write) and a
+// launch, ~12 % of the 1M protocol crawl. Here the table kernels read Q / T tile-major
+// themselves. With the OT index (g b + k) Npad + i and Npad a multiple of 512 (the level loop pads the
+// share planes to 8-word rows), test i's b labels sit at the same position p = i % 512 of the b tiles
+// ((g b + k) Npad / 512 + i / 512), so a wave takes one 512-test tile: its lanes load the b tiles' row
+// words (whole 128-B lines), fold the labels into the tests' row keys in the row domain (gt_tile_rows), make
+// ONE in-register transpose (transpose32) and deal the keys to the lanes through 2 KiB of LDS, as the OT
+// hashes do (ot_tile_load / ot_tile_round) — no label is stored. Lane l takes tests p = 256 u + 32 (l >> 3) +
+// 8 r + (l & 7) (u < 2, exchange round r < 4): 8 consecutive lanes hold 8 consecutive tests, so the
+// messages and node values move in 64-B runs. Each round's two tests go to the AES at once (garbler: the
+// 2^b rows of one test per pass, as k_gt_garble; evaluator: two rounds' 4 tests per pass). Identical
+// outputs to k_ot_rows_out + k_gt_garble / k_gt_eval (oracle orc_gt_garble / orc_gt_eval).
+constexpr int kGtWaves = kGcThreads / 64;
+constexpr uint32_t kGtTileWords = 128 * 16;   // one 512-OT tile of Q / T: 128 rows x 16 words
+
+// exchange round r (x[0..7] = the tile's x[8 r .. 8 r + 7]): lane l receives OTs 32 qq + 8 r + (l & 7),
+// qq = (l >> 3) + 8 u, u < 2; then x moves down by 8 (a rolled round loop keeps x in registers). Stage
+// word of (kk, writer lane l') = 64 kk + (l' ^ 8 kk): the writes are lane-linear per kk, and the 16 lanes
+// of a ds_read_b128 group hit 16 distinct bank quads (4 qq ^ 8 kk = 8 (kk ^ (qq >> 1)) + 4 (qq & 1)).
+__device__ __forceinline__ void gt_tile_round(uint32_t* st, uint32_t (&x)[32], uint32_t lane, uint32_t (&o)[2][4]) {
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) st[64 * kk + (lane ^ (8 * kk))] = x[kk];
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t kk = lane & 7;
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const uint32_t qq = (lane >> 3) + 8 * u;
+        const uint4 v = *reinterpret_cast<const uint4*>(st + 64 * kk + ((4 * qq) ^ (8 * kk)));
+        o[u][0] = v.x;
+        o[u][1] = v.y;
+        o[u][2] = v.z;
+        o[u][3] = v.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 24; i++) x[i] = x[i + 8];
+}
+
+// the lane's test of round r, u within its 512-test tile
+__device__ __forceinline__ uint32_t gt_tile_test(uint32_t lane, int r, int u) {
+    return 256 * u + 32 * (lane >> 3) + 8 * r + (lane & 7);
+}
+
+// The tile's raw row keys, S = e_0 ^ sigma(e_1) over the labels OT's matrix (Horner at b = 2; b = 1:
+// S = e_0), built in the ROW domain before the one transpose: row r of sigma(e) is row r - 1 of e, plus
+// row 127 into rows 0, 1, 2, 7 (x^128 = x^7 + x^2 + x + 1; row r = bit r of the LE u128 label), so lane
+// (q, rg) loads e_1's rows shifted by one — its first load is row 32 rg - 1, or for rg = 0 row 127, which
+// is also the reduction term. One transpose per tile instead of one per label. (The garbler's labels are
+// Z_k = E_k ^ (x_k ? 0 : Delta); being linear, its Delta terms are added per test after the exchange.)
+// On return x[k] = word rg of S for test 32 q + k, lane (q, rg) = (lane >> 2, lane & 3).
+template <int B>
+__device__ __forceinline__ void gt_tile_rows(const GcArgs& a, uint64_t g, uint32_t iw, uint32_t Npt, uint32_t lane,
+                                             uint32_t (&x)[32]) {
+    static_assert(B == 1 || B == 2, "gt_tile_rows: b <= 2");
+    const uint32_t q = lane >> 2, rg = lane & 3;
+    const uint32_t* t0 = reinterpret_cast<const uint32_t*>(a.ev_labels) + (((uint64_t)g * B) * Npt + iw) * kGtTileWords + q;
+#pragma unroll
+    for (int i = 0; i < 32; i++) x[i] = __builtin_nontemporal_load(t0 + (32 * rg + i) * 16);
+    if constexpr (B == 2) {
+        const uint32_t* t1 = t0 + (uint64_t)Npt * kGtTileWords;   // bit 1's tile
+        const uint32_t y0 = __builtin_nontemporal_load(t1 + (rg ? 32 * rg - 1 : 127) * 16);
+        x[0] ^= y0;
+#pragma unroll
+        for (int i = 1; i < 32; i++) x[i] ^= __builtin_nontemporal_load(t1 + (32 * rg + i - 1) * 16);
+        if (rg == 0) {   // e_1's row 127: the reduction into rows 1, 2, 7 (row 0 took it above)
+            x[1] ^= y0;
+            x[2] ^= y0;
+            x[7] ^= y0;
+        }
+    }
+    transpose32(x);
+}
+
+// the colours of the lane's tests (r, u): bit 8 r + (lane & 7) of cw[u] = row 0 word (lane >> 3) + 8 u of
+// the tile, packed as the test's row index bits (b = 2: colour of z_1 << 1 | colour of z_0)
+template <int B>
+__device__ __forceinline__ void gt_tile_colours(const GcArgs& a, uint64_t g, uint32_t iw, uint32_t Npt, uint32_t lane,
+                                                uint32_t (&cw)[B][2]) {
+    const uint32_t* lab = reinterpret_cast<const uint32_t*>(a.ev_labels);
+#pragma unroll
+    for (int k = 0; k < B; k++)
+#pragma unroll
+        for (int u = 0; u < 2; u++)   // row 0 (cached: the tile was just read)
+            cw[k][u] = lab[(((uint64_t)g * B + k) * Npt + iw) * kGtTileWords + (lane >> 3) + 8 * u];
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t gt_row_of(const uint32_t (&cw)[B][2], int r, int u, uint32_t lane) {
+    const uint32_t sh = 8 * r + (lane & 7);
+    uint32_t row = 0;
+#pragma unroll
+    for (int k = 0; k < B; k++) row |= ((cw[k][u] >> sh) & 1u) << k;
+    return row;
+}
+
+// the lane's 8 tests' row keys S[j] (j = 2 r + u, without the tweak) and row indices (4 bits per test, test
+// j at bits 4 j of col): gt_tile_rows, then the 4 exchange rounds; each round's two keys rotate to the end
+// of S (a rolled round loop keeps S and x in registers), so after 4 rounds S is in order. The tile's words
+// are dead before the AES phase starts (live beside the AES they spilled the 128-VGPR budget).
+template <int B, bool GARBLER>
+__device__ __forceinline__ void gt_tile_keys(const GcArgs& a, uint64_t g, uint32_t iw, uint32_t Npt, uint32_t* st,
+                                             uint32_t lane, const uint32_t (&Dk)[B][4], uint32_t (&S)[8][4],
+                                             uint32_t& col) {
+    uint32_t x[32], cw[B][2], nx[B][2];
+    gt_tile_rows<B>(a, g, iw, Npt, lane, x);
+    gt_tile_colours<B>(a, g, iw, Npt, lane, cw);
+    if constexpr (GARBLER) {   // ~x_k of the lane's tests (plane words (lane >> 3) + 8 u of the tile)
+#pragma unroll
+        for (int k = 0; k < B; k++)
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                nx[k][u] = ~reinterpret_cast<const uint32_t*>(a.gb_planes)[((a.g_off + g) * B + k) * (2 * (uint64_t)a.nw) +
+                                                                          16 * iw + (lane >> 3) + 8 * u];
+                cw[k][u] ^= nx[k][u];   // Z_k's colour: Delta's colour bit is 1
+            }
+    }
+    col = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int u = 0; u < 2; u++) col |= gt_row_of<B>(cw, r, u, lane) << (4 * (2 * r + u));
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) {
+        uint32_t o[2][4];
+        gt_tile_round(st, x, lane, o);
+        if constexpr (GARBLER) {   // S ^= XOR_k (x_k ? 0 : sigma^k(Delta))
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int k = 0; k < B; k++) {
+                    const uint32_t f = (nx[k][u] >> (8 * r + (lane & 7))) & 1u;
+#pragma unroll
+                    for (int c = 0; c < 4; c++) o[u][c] ^= f ? Dk[k][c] : 0u;
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) S[j][c] = S[j + 2][c];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            S[6][c] = o[0][c];
+            S[7][c] = o[1][c];
+        }
+    }
+}
+
+// (b <= 2, the d = 1 tests of the metric's configuration; d = 2 keeps k_ot_rows_out + the row-major kernels)
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
+    static_assert(B <= 2, "the tile-major garbler takes b <= 2");
+    __shared__ uint32_t tbl_gc[GcTab::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kGtWaves][512];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t n_act = gc_active(a);
+    const uint32_t Npt = a.nw / 8;   // 512-test tiles per group
+    const uint64_t tiles = (n_act / a.N) * Npt;
+    if ((uint64_t)blockIdx.x * kGtWaves >= tiles) return;   // no tiles for this workgroup: skip the table fill
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(lane, b0, b1);
+    constexpr uint32_t R = 1u << B;   // rows per test: one AES pass
+    const uint64_t n = a.G * a.N;
+    uint32_t Dk[B][4];   // sigma^k(Delta)
+#pragma unroll
+    for (int c = 0; c < 4; c++) Dk[0][c] = a.delta[c];
+#pragma unroll
+    for (int k = 1; k < B; k++) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) Dk[k][c] = Dk[k - 1][c];
+        gf_dbl(Dk[k]);
+    }
+    for (uint64_t wt = (uint64_t)blockIdx.x * kGtWaves + wv; wt < tiles; wt += (uint64_t)gridDim.x * kGtWaves) {
+        const uint64_t g = wt / Npt;
+        const uint32_t iw = (uint32_t)(wt - g * Npt);
+        uint32_t S[8][4], col;
+        gt_tile_keys<B, true>(a, g, iw, Npt, stage[wv], lane, Dk, S, col);
+#pragma unroll 1
+        for (int j = 0; j < 8; j++) {   // test j = (r, u) = (j >> 1, j & 1); S and col rotate by one test
+            const uint32_t i = 512 * iw + gt_tile_test(lane, j >> 1, j & 1);
+            const bool live = i < a.N;
+            const uint64_t t = g * a.N + i;
+            const uint64_t tw = a.gate_base + a.g_off * a.N + t;   // the test's index in the whole level
+            const uint32_t K[4] = {S[0][0] ^ (uint32_t)tw, S[0][1] ^ (uint32_t)(tw >> 32), S[0][2], S[0][3]};
+            const uint32_t cl = col & (R - 1);
+            const uint32_t rstar = ~cl & (R - 1);   // the row whose z are all 1 (eq = 1)
+            uint32_t h[R][4];
+#pragma unroll
+            for (uint32_t q = 0; q < R; q++) {
+                const uint32_t flip = q ^ cl;   // z_k of the row = bit k of r ^ col
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    uint32_t w = K[c];
+#pragma unroll
+                    for (int k = 0; k < B; k++) w ^= ((flip >> k) & 1u) ? Dk[k][c] : 0u;
+                    h[q][c] = w;
+                }
+            }
+            aes0_mmo_tab<DevOpsX, GcTab, R>(h, tbl_gc, b0, b1);   // cr_hash: pi(K) ^ K
+            uint64_t p0 = 0, p1 = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < R; q++) {
+                const uint32_t o_r = (uint32_t)(q == rstar) ^ a.mask;
+                const uint64_t hl = (uint64_t)h[q][0] | ((uint64_t)h[q][1] << 32);
+                if (q == 0) {   // row 0's value pair[o_0] is H(K_0) mod p: it fixes v
+                    const uint64_t hv = ot_fe_of_u128(hl, (uint64_t)h[q][2] | ((uint64_t)h[q][3] << 32));
+                    const uint64_t v = o_r == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
+                    p0 = v;
+                    p1 = a.mask ? fe_inc(v) : fe_dec(v);
+                    if (live) a.sh_gb[t] = a.mask ? fe_inc(v) : v;   // r1 = v + mask
+                } else if (live) {
+                    a.gt_msgs[(uint64_t)(q - 1) * n + t] = hl ^ (o_r ? p1 : p0);
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < 7; jj++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 1][c];
+            col >>= 4;
+        }
+    }
+}
+
+template <int B>
+__global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
+    static_assert(B <= 2, "the tile-major evaluator takes b <= 2");
+    __shared__ uint32_t tbl_gc[GcTab::kWords];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kGtWaves][512];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t n_act = gc_active(a);
+    const uint32_t Npt = a.nw / 8;
+    const uint64_t tiles = (n_act / a.N) * Npt;
+    if ((uint64_t)blockIdx.x * kGtWaves >= tiles) return;
+    gc_fill(tbl_gc);
+    uint32_t b0, b1;
+    GcTab::bases(lane, b0, b1);
+    const uint64_t n = a.G * a.N;
+    for (uint64_t wt = (uint64_t)blockIdx.x * kGtWaves + wv; wt < tiles; wt += (uint64_t)gridDim.x * kGtWaves) {
+        const uint64_t g = wt / Npt;
+        const uint32_t iw = (uint32_t)(wt - g * Npt);
+        uint32_t S[8][4], col;
+        const uint32_t nod[B][4] = {};
+        gt_tile_keys<B, false>(a, g, iw, Npt, stage[wv], lane, nod, S, col);
+#pragma unroll 1
+        for (int r = 0; r < 4; r++) {   // round r's 2 tests: 2 AES blocks in lockstep (4 spilled 6 VGPRs)
+            uint32_t h[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t i = 512 * iw + gt_tile_test(lane, r, u);
+                const uint64_t tw = a.gate_base + a.g_off * a.N + g * a.N + i;
+                h[u][0] = S[u][0] ^ (uint32_t)tw;
+                h[u][1] = S[u][1] ^ (uint32_t)(tw >> 32);
+                h[u][2] = S[u][2];
+                h[u][3] = S[u][3];
+            }
+            aes0_mmo_tab<DevOpsX, GcTab, 2>(h, tbl_gc, b0, b1);
+            // (the row messages are loaded after the AES: r05 measured the early load neutral,
+            // profiles/r05/table/ab_gt_eval_msg.json)
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t i = 512 * iw + gt_tile_test(lane, r, u);
+                if (i >= a.N) continue;
+                const uint64_t t = g * a.N + i;
+                const uint32_t row = (col >> (4 * u)) & 0xFu;
+                const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
+                a.sh_ev[t] = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
+                                 : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
+            }
+#pragma unroll
+            for (int jj = 0; jj < 6; jj++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 2][c];
+            col >>= 8;
+        }
+    }
+}
+
 template <int B>
 static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     int dev = 0, cus = 0;
@@ -613,6 +893,13 @@ static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     const uint64_t n = a.G * a.N;
+    if constexpr (B <= 2) if (a.lab_tm) {   // r06: one wave per 512-test tile, one 160 KiB workgroup per CU
+        const uint64_t tiles = a.G * (a.nw / 8), need = (tiles + kGtWaves - 1) / kGtWaves;
+        const int grid = (int)(need < (uint64_t)cus ? (need ? need : 1) : (uint64_t)cus);
+        if (garble) hipLaunchKernelGGL(k_gt_garble_tm<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+        else hipLaunchKernelGGL(k_gt_eval_tm<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+        return hipGetLastError();
+    }
     const uint64_t need = (n + kGcThreads - 1) / kGcThreads;
     const int grid = (int)(need < (uint64_t)cus * 8 ? (need ? need : 1) : (uint64_t)cus * 8);
     if (garble) hipLaunchKernelGGL(k_gt_garble<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
@@ -623,6 +910,8 @@ static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
 static hipError_t gt_dispatch(const GcArgs& a, bool garble, hipStream_t stream) {
     if (a.G * a.N == 0) return hipSuccess;
     if (!a.gt_msgs || !(garble ? a.sh_gb : a.sh_ev) || !a.ev_labels) return hipErrorInvalidValue;
+    // r06 tile-major labels: 512-test tiles per group, b <= 2 (gt_tm_bits)
+    if (a.lab_tm && (a.nw % 8 != 0 || a.bits > (uint32_t)kGtTmMaxBits)) return hipErrorInvalidValue;
     switch (a.bits) {
         case 1: return gt_launch<1>(a, garble, stream);
         case 2: return gt_launch<2>(a, garble, stream);

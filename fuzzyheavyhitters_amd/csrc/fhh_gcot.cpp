@@ -161,18 +161,19 @@ int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
     const uint64_t mp = ot_padded(m);
     const size_t rows = (size_t)128 * (mp / 128) * 16;   // = 16 mp bytes
     for (int k = 0; k < 3; k++) HIP_TRY(ctx, ctx->ot_buf[k].ensure(rows));
-    if (a.mode != 4) HIP_TRY(ctx, ctx->ot_buf[5].ensure(m * 16));
+    if (a.mode < 4) HIP_TRY(ctx, ctx->ot_buf[5].ensure(m * 16));
     if (a.mode == 0) HIP_TRY(ctx, ctx->ot_buf[6].ensure(m * 16));
     a.m = m;
     a.mp = mp;
     a.T = ctx->ot_buf[0].as<uint4>();
     a.U = ctx->ot_buf[1].as<uint4>();
     a.Q = ctx->ot_buf[2].as<uint4>();
-    a.Y0 = a.mode != 4 ? ctx->ot_buf[5].as<uint4>() : nullptr;
+    a.Y0 = a.mode < 4 ? ctx->ot_buf[5].as<uint4>() : nullptr;
     a.Y1 = a.mode == 0 ? ctx->ot_buf[6].as<uint4>() : nullptr;
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
-    if (a.mode == 4) {   // the correlation itself: q_j, t_j (no hash, no y)
+    if (a.mode == 5) {   // the correlation, left tile-major in Q / T for the r06 garbled table
+    } else if (a.mode == 4) {   // the correlation itself: q_j, t_j (no hash, no y)
         HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));
         HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));
     } else {
@@ -535,7 +536,11 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
         return ctx->fail(FHH_E_ARG, "gt_cot: NULL argument");
     if (!(base_choice[0] & 1)) return ctx->fail(FHH_E_ARG, "gt_cot: s is the free-XOR Delta: its bit 0 must be 1");
     if (n > 0xFFFFFFFFull) return ctx->fail(FHH_E_ARG, "gt_cot: n must fit 32 bits");
-    const uint64_t nw = (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad, R = 1ull << bits;
+    // r06: b <= 2 runs the tile-major table kernels on Q / T (the level loop's form), whose OT index wants
+    // plane rows of whole 512-client tiles; b = 3, 4 the row-major labels of k_ot_rows_out
+    const bool tm = bits <= (uint32_t)kGtTmMaxBits;
+    const uint64_t nw = tm ? (n + 511) / 512 * 8 : (n + 63) / 64, npad = 64 * nw, m = (uint64_t)bits * npad;
+    const uint64_t R = 1ull << bits;
     std::vector<uint64_t> planes[2];
     const uint8_t* src[2] = {gb_bits, ev_bits};
     for (int s = 0; s < 2; s++) {
@@ -556,9 +561,9 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     const uint32_t* rk = nullptr;
     rc = ot_host_keys(ctx, base_seeds, base_choice, &rk);
     if (rc) return rc;
-    // 1. the labels OT (mode 4), as fhh_gc_cot_host
+    // 1. the labels OT (mode 4, as fhh_gc_cot_host; b <= 2: mode 5, Q / T left tile-major)
     OtArgs a{};
-    a.mode = 4;
+    a.mode = tm ? 5 : 4;
     a.rk = rk;
     words_from_bytes(base_choice, a.s);
     a.choices = dp[1].as<uint32_t>();
@@ -578,15 +583,24 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     g.mask = mask & 1u;
     words_from_bytes(base_choice, g.delta);
     g.gate_base = gate_base;
-    g.ev_labels = de.as<uint4>();
+    g.ev_labels = tm ? ctx->ot_buf[2].as<uint4>() : de.as<uint4>();
+    g.lab_tm = tm ? 1u : 0u;
     g.ev_ot = 1;
     g.gt_msgs = dm.as<uint64_t>();
     g.sh_gb = dsh.as<uint64_t>();
     HIP_TRY(ctx, launch_gt_garble(g, ctx->stream));
-    g.ev_labels = da.as<uint4>();
+    g.ev_labels = tm ? ctx->ot_buf[0].as<uint4>() : da.as<uint4>();
     g.sh_gb = nullptr;
     g.sh_ev = dsh.as<uint64_t>() + n;
     HIP_TRY(ctx, launch_gt_eval(g, ctx->stream));
+    if (tm && (ev_zero || ev_active)) {   // the transcript's row-major labels, after the fact (tests only)
+        a.m = m;
+        a.mp = ot_padded(m);
+        a.T = ctx->ot_buf[0].as<uint4>();
+        a.Q = ctx->ot_buf[2].as<uint4>();
+        HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));
+        HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));
+    }
     rc = ctx_sync(ctx);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(gb_share, dsh.p, n * 8, hipMemcpyDeviceToHost));
@@ -643,6 +657,8 @@ struct PartyState {
     bool last = false;          // tree_crawl_last: FieldElm shares (BlockPair = 2 OTs per test)
     bool lshare = false;        // r05c (FE levels): the share from the GC output labels, no OT 2
     bool ltable = false;        // r05d (FE levels, bits <= kGtMaxBits): one garbled table per test
+    bool ltm = false;           // r06 (ltable, bits <= kGtTmMaxBits): the table kernels read the labels OT's
+                                // tile-major Q / T (no row transposes); npad / nw = whole 512-client tiles
     // C = this instance's children: the chunk [c_off, c_off + C) of the level's level_C children
     // (child_begin / child_count); covered = children whose OTs are finished
     uint64_t c_off = 0, level_C = 0, covered = 0;
@@ -709,13 +725,18 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
     P.c_off = b;
     P.C = child_count ? std::min<uint64_t>(child_count, LC - b) : LC;
     P.n = ctx->n;
-    P.npad = ctx->npad;
+    P.npad = ctx->npad;   // (r06 tile-major table: whole 512-client tiles, set below)
     P.nw = ctx->nw;
     P.bits = 2 * ctx->d;
     P.tests = P.C * P.n;
     P.per2 = P.last ? 2 : 1;
     P.lshare = !P.last;
     P.ltable = P.lshare && P.bits <= (uint32_t)kGtMaxBits && form == 0;   // form 1: the circuit (r05c)
+    P.ltm = P.ltable && P.bits <= (uint32_t)kGtTmMaxBits;
+    if (P.ltm) {   // plane rows and the OT index over whole 512-client tiles (both parties alike: n is public)
+        P.nw = (ctx->nw + 7) / 8 * 8;
+        P.npad = 64 * P.nw;
+    }
     P.m1 = P.C * P.bits * P.npad;   // OT index (g bits + j) npad + i: the share planes as choice bits
     P.m2 = P.lshare ? 0 : P.tests * P.per2;   // OT 2 (the share OT) at the FieldElm level only
     if (b == 0) P.bytes_sent = 0;   // the level's outgoing bytes, over its chunks
@@ -728,6 +749,7 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
         ChildArgs a = ctx_child_args(ctx);
         a.c_off = P.c_off;
         a.c_cnt = P.C;
+        a.plane_nw = (uint32_t)P.nw;
         HIP_TRY(ctx, launch_share_planes(a, P.planes.as<uint64_t>(), ctx->stream));
     }
     // the level's node values, one row of n per child (u64 FE, or a BlockPair at the last level)
@@ -852,14 +874,15 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
     if (rc) return rc;
     rc = party_ot_buffers(ctx, P, P.m1, true);
     if (rc) return rc;
-    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
+    if (!P.ltm) HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
     if (P.m1) {   // OT 1's receiver: choice bits = this server's share planes as they stand
         OtArgs a = party_ot(P, 0, P.m1);
-        a.mode = 4;
+        a.mode = P.ltm ? 5 : 4;
         a.choices = P.planes.as<uint32_t>();
-        a.out = P.labels.as<uint4>();
+        a.out = P.ltm ? nullptr : P.labels.as<uint4>();
         HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));        // T, U
-        HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));    // its active labels t_j
+        // its active labels t_j: row-major for the circuit; the r06 table reads T tile-major
+        if (!P.ltm) HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));
     }
     rc = ctx_sync(ctx);
     if (rc) return rc;
@@ -897,7 +920,9 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     // the garbling arguments of the chunk (multiple_gb_equality_test, equalitytest.rs:25-65); the
     // evaluator's zero labels are OT 1's sender messages, at the OT index of its choice bits
     HIP_TRY(ctx, P.gc.ensure(std::max<uint64_t>(gc_bytes(P), 1)));
-    HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
+    if (!P.ltm) HIP_TRY(ctx, P.labels.ensure(std::max<uint64_t>(P.m1, 1) * 16));
+    rc = party_ot_buffers(ctx, P, P.m1, false, false);
+    if (rc) return rc;
     fhh_gc_batch gb{};
     gb.groups = P.C;
     gb.clients = (uint32_t)P.n;
@@ -910,28 +935,27 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     gb.ev_planes_dev = P.planes.as<uint64_t>();   // not read: the evaluator's labels go by OT
     gb.tables_dev = P.gc.as<uint8_t>();
     gb.gb_labels_dev = P.gc.as<uint8_t>();
-    gb.ev_labels_dev = P.labels.as<uint8_t>();
+    gb.ev_labels_dev = P.ltm ? P.Q.as<uint8_t>() : P.labels.as<uint8_t>();   // r06: the tile-major Q itself
     gb.decode_dev = P.gc.as<uint8_t>();
     gb.out_dev = P.gc.as<uint8_t>();
     rc = gc_args(ctx, &gb, P.g);
     if (rc) return rc;
     gc_layout(P, P.gc.as<uint8_t>(), P.g);
     P.g.ev_ot = 1;
+    P.g.lab_tm = P.ltm ? 1u : 0u;
     P.g.out = nullptr;
     // r05c: the garbler's node values r1 straight into the level's rows (the y it forms travels in gc)
     P.g.sh_gb = P.lshare ? reinterpret_cast<uint64_t*>(party_vals(P)) : nullptr;
     // OT 1 as the IKNP correlation (gb_set_fancy_inputs, equalitytest.rs:67-82): q_j is the evaluator's
     // zero label of its share bit j, q_j ^ s its one label, and s = Delta: nothing to send back
-    rc = party_ot_buffers(ctx, P, P.m1, false, false);
-    if (rc) return rc;
     if (P.m1) {
         OtArgs a = party_ot(P, 0, P.m1);
-        a.mode = 4;
+        a.mode = P.ltm ? 5 : 4;
         a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
         for (int c = 0; c < 4; c++) a.s[c] = P.s[0][c];
-        a.sx = P.labels.p;
+        a.sx = P.ltm ? nullptr : P.labels.p;
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
-        HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));   // the zero labels q_j
+        if (!P.ltm) HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));   // the zero labels q_j (the circuit)
     }
     rc = ctx_sync(ctx);
     if (rc) return rc;
@@ -986,7 +1010,8 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     g.bits = P.bits;
     g.gate_base = party_gate_base(P);
     gc_layout(P, const_cast<uint8_t*>(gc_msg_dev), g);
-    g.ev_labels = P.labels.as<uint4>();
+    g.ev_labels = P.ltm ? P.T.as<uint4>() : P.labels.as<uint4>();   // r06: the tile-major T itself
+    g.lab_tm = P.ltm ? 1u : 0u;
     g.ev_ot = 1;
     g.out = P.out.as<uint8_t>();
     if (P.lshare) {

@@ -1046,12 +1046,17 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
     // GC + OT chunk: children per protocol instance, so the level's GC and OT buffers (~400 B per
     // test at d = 1) stay within FHH_GC_CHUNK_BYTES (default 64 GiB): one chunk per level at
     // configs[1], ~160 children per chunk at 1M clients
-    uint64_t gc_groups = ~0ull;
+    uint64_t gc_groups = ~0ull, gc_groups_last = ~0ull;
     if (cfg->gc) {
         uint64_t budget = 64ull << 30;
         if (const char* e = std::getenv("FHH_GC_CHUNK_BYTES")) budget = std::strtoull(e, nullptr, 10);
-        const uint64_t per_test = 200ull * 2 * d + 2;
+        // r06: the d = 1 garbled table on the tile-major labels holds ~140 B per test (T, U, Q 96, rows 24,
+        // node values 16), not the circuit's ~400: larger chunks, one per level at 1M clients
+        const bool tm_table = cfg->gc == 2 && 2 * d <= (uint32_t)kGtTmMaxBits;
+        const uint64_t per_test = tm_table ? 150ull : 200ull * 2 * d + 2;
         gc_groups = std::max<uint64_t>(1, budget / (per_test * std::max<uint64_t>(c0->npad, 1)));
+        // the FieldElm level runs the circuit + share C-OT whatever the FE levels run
+        gc_groups_last = std::max<uint64_t>(1, budget / ((200ull * 2 * d + 2) * std::max<uint64_t>(c0->npad, 1)));
     }
     PhaseClock pc;
     LoopBuffers B;
@@ -1206,20 +1211,29 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 // chunk a fresh protocol instance: its own garbler key / Delta / mask, and its own
                 // row-PRG range of the level's base-OT sessions
                 const uint32_t bits = 2 * d;
-                const size_t plane_bytes = (size_t)C_cap * bits * c0->nw * 8;
+                const bool real_ot = cfg->gc >= 2;
+                // r05c / r05d: at the FE levels the share comes from the circuit's output labels, or (d <= 2,
+                // gc 2) from ONE garbled table per test; r06: for b <= 2 (d = 1) the table kernels read the
+                // labels OT's tile-major Q / T themselves (no k_ot_rows_out), which wants plane rows of
+                // whole 512-client tiles: the planes and the OT index take nw_gc = nw rounded up to 8 words
+                const bool lshare = real_ot && pmode == 1;
+                const bool ltable = lshare && bits <= (uint32_t)kGtMaxBits && cfg->gc == 2;   // gc 3: the circuit
+                const bool ltm = ltable && bits <= (uint32_t)kGtTmMaxBits;
+                const uint64_t nw_gc = ltm ? (c0->nw + 7) / 8 * 8 : c0->nw, npad_gc = 64 * nw_gc;
+                const size_t plane_bytes = (size_t)C_cap * bits * nw_gc * 8;
                 for (int s = 0; s < 2; s++) HIP_TRY(c0, B.gc_planes[s].ensure(plane_bytes));
                 size_t gc_slot = 0;
                 if (timed) HIP_TRY(c0, timing_begin(c0, &gc_slot));
                 ChildArgs pa = a;
+                pa.plane_nw = (uint32_t)nw_gc;
                 HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[0].as<uint64_t>(), c0->stream));
                 pa.s0 = a.s1;
                 HIP_TRY(c0, launch_share_planes(pa, B.gc_planes[1].as<uint64_t>(), c0->stream));
-                const uint64_t Gc = std::min<uint64_t>(C_cap, gc_groups);
+                const uint64_t Gc = std::min<uint64_t>(C_cap, pmode == 2 ? gc_groups_last : gc_groups);
                 const uint64_t chunks = (C_cap + Gc - 1) / Gc;
-                const bool real_ot = cfg->gc >= 2;
                 const uint64_t tests = Gc * c0->n;
                 const uint32_t per2 = pmode == 1 ? 1 : 2;   // OTs per test of the share conversion
-                const uint64_t m1 = Gc * bits * c0->npad, m2 = tests * per2;
+                const uint64_t m1 = Gc * bits * npad_gc, m2 = tests * per2;
                 // the level's two base-OT sessions (OtSender / OtReceiver::init per level and kind,
                 // collect.rs:454,460): kind 0 the labels OT, kind 1 the share OT; chunk k extends them
                 // from row-PRG block k x (the chunk's blocks), so no two chunks share a pad
@@ -1249,20 +1263,22 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         }
                     }
                 }
-                HIP_TRY(c0, B.gc_tables.ensure((size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
+                // (the garbled table writes no half-gate tables, decoding bits or output bytes)
+                HIP_TRY(c0, B.gc_tables.ensure(ltable ? 16 : (size_t)std::max(bits - 1, 1u) * 2 * tests * 16));
                 // garbler labels: the ideal-OT garbler's only (the r05 garbler folds its string in)
                 HIP_TRY(c0, B.gc_gbl.ensure(real_ot ? 16 : (size_t)(bits + 1) * tests * 16));
                 // ideal OT: the evaluator's active labels [bits][tests]; OT mode: its zero labels (the
-                // labels C-OT's sender messages) at OT index (g bits + j) npad + i
-                HIP_TRY(c0, B.gc_evl.ensure(std::max<size_t>((size_t)bits * tests, real_ot ? m1 : 0) * 16));
-                HIP_TRY(c0, B.gc_decode.ensure(tests));
-                HIP_TRY(c0, B.gc_out.ensure(tests));
+                // labels C-OT's sender messages) at OT index (g bits + j) npad + i (r06 tile-major table: none,
+                // the kernels read Q / T)
+                HIP_TRY(c0, B.gc_evl.ensure(std::max<size_t>((size_t)bits * tests, real_ot && !ltm ? m1 : 0) * 16));
+                HIP_TRY(c0, B.gc_decode.ensure(ltable ? 1 : tests));
+                HIP_TRY(c0, B.gc_out.ensure(ltable ? 1 : tests));
                 for (uint64_t k = 0; k < chunks; k++) {
                     const uint64_t g_off = k * Gc;
                     fhh_gc_batch gb{};
                     gb.groups = Gc;
                     gb.clients = (uint32_t)c0->n;
-                    gb.words = (uint32_t)c0->nw;
+                    gb.words = (uint32_t)nw_gc;
                     gb.bits = bits;
                     gc_chunk_material(cfg->prf_seed, lv, k, gb.label_key, gb.delta, &gb.mask);
                     gb.gate_base = (uint64_t)lv << 40;   // the level in the gate tweaks (party_gate_base)
@@ -1287,37 +1303,39 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         // q_j ^ r_j s the active one, with the labels session's s (colour bit set) as the
                         // circuit's Delta; server 0's string and mask fold into the circuit
                         // (k_gc_garble_cot: no label is drawn, no reply is sent)
-                        HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
+                        if (!ltm) HIP_TRY(c0, B.gc_evact.ensure(m1 * 16));
                         for (int c = 0; c < 4; c++) g.delta[c] = sw_ot[0][c];
                         OtArgs a1{};
-                        a1.mode = 4;
+                        a1.mode = ltm ? 5 : 4;
                         a1.rk = rk_ot[0];
                         for (int c = 0; c < 4; c++) a1.s[c] = sw_ot[0][c];
-                        a1.choices = B.gc_planes[1].as<uint32_t>() + g_off * bits * c0->nw * 2;
+                        a1.choices = B.gc_planes[1].as<uint32_t>() + g_off * bits * nw_gc * 2;
                         a1.ctr_off = k * ot_session_blocks(m1);
-                        a1.sx = B.gc_evl.p;
-                        a1.out = B.gc_evact.as<uint4>();
+                        a1.sx = ltm ? nullptr : B.gc_evl.p;
+                        a1.out = ltm ? nullptr : B.gc_evact.as<uint4>();
                         a1.ctl = B.ctl.as<LoopCtl>();
-                        a1.per_group = (uint64_t)c0->npad * bits;
+                        a1.per_group = npad_gc * bits;
                         a1.g_off = g_off;
                         rc = ot_run(c0, a1, m1, nullptr);
                         if (rc) return rc;
                         g.ev_ot = 1;
+                        if (ltm) {   // the table kernels on the tile-major Q (garbler) / T (evaluator)
+                            g.lab_tm = 1;
+                            g.ev_labels = c0->ot_buf[2].as<uint4>();
+                        }
                     }
                     // r05c: at the FE levels the share comes from the circuit's output labels (W_0 and
                     // W_0 ^ Delta of o = eq ^ mask in the share C-OT's roles): server 0's node value r1 and
-                    // the 8-B y from k_gc_garble_cot, server 1's value from k_gc_eval — no second OT
-                    const bool lshare = real_ot && pmode == 1;
+                    // the 8-B y from k_gc_garble_cot, server 1's value from k_gc_eval — no second OT.
                     // r05d: tests of <= kGtMaxBits bits (d <= 2) take the share from ONE garbled table per
                     // test (k_gt_garble / k_gt_eval: 2^bits + 1 AES instead of the half-gates chain's)
-                    const bool ltable = lshare && bits <= (uint32_t)kGtMaxBits && cfg->gc == 2;   // gc 3: the circuit
                     if (ltable) {
                         for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
                         HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
                         g.gt_msgs = B.gc_msgs.as<uint64_t>();
                         g.sh_gb = B.gc_val[0].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_garble(g, c0->stream));
-                        g.ev_labels = B.gc_evact.as<uint4>();
+                        g.ev_labels = ltm ? c0->ot_buf[0].as<uint4>() : B.gc_evact.as<uint4>();
                         g.sh_gb = nullptr;
                         g.sh_ev = B.gc_val[1].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_eval(g, c0->stream));

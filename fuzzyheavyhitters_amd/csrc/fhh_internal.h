@@ -205,6 +205,9 @@ struct ChildArgs {
     // gc_out / ot_recv / OT messages indexed (c - c_off) * gc_N + i; c_cnt = 0: every child
     uint64_t c_off;
     uint64_t c_cnt;
+    // k_share_planes' row stride in words (0: nw); words nw .. plane_nw - 1 are written as zero (r06: the
+    // tile-major garbled table wants rows of whole 512-client tiles, plane_nw a multiple of 8)
+    uint32_t plane_nw;
 };
 
 // Garbled-circuit equality tests (row f1, equalitytest.rs:25-219): tests t = g * N + i for
@@ -251,8 +254,13 @@ struct GcArgs {
     // k_gt_garble writes rows 1 .. 2^bits - 1's messages SoA [2^bits - 1][G N] and the garbler's node
     // values to sh_gb, k_gt_eval reads them and writes the evaluator's to sh_ev
     uint64_t* gt_msgs;
+    // r06: 1 = ev_labels is the labels OT's tile-major matrix itself (Q for k_gt_garble, T for k_gt_eval;
+    // fhh_ot.hip ot_tmaj) instead of one row-major label per OT (k_ot_rows_out); needs nw % 8 == 0 (the OT
+    // index (g bits + k) 64 nw + i puts a test's labels at one position of 512-OT tiles)
+    uint32_t lab_tm;
 };
 constexpr int kGtMaxBits = 4;   // 16 rows (d = 2); wider tests keep the half-gates chain
+constexpr int kGtTmMaxBits = 2;   // r06: the table kernels read the tile-major labels (lab_tm) for b <= 2 (d = 1)
 
 struct PruneArgs {
     LoopCtl* ctl;
@@ -371,7 +379,8 @@ struct OtArgs {
     const LoopCtl* ctl;
     uint64_t per_group;
     uint64_t g_off;              // level loop chunk: OTs of groups [g_off, ctl->C) only
-    uint32_t mode;               // 0..4 above
+    uint32_t mode;               // 0..4 above; 5 = 4 left tile-major (expands only: the r06 garbled table
+                                 // reads Q / T itself, GcArgs::lab_tm)
     uint32_t mask;               // modes 2, 3: the garbler's mask bit
     uint64_t ctr_off;            // the row PRG's first block (a multiple of 256): a base-OT session's
                                  // running counter, so batches extending one session never repeat pads

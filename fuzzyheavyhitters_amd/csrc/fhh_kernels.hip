@@ -585,15 +585,16 @@ __global__ __launch_bounds__(kReduceThreads) void k_share_planes(ChildArgs a, ui
     for (uint64_t c = a.c_off + blockIdx.x; c < C_; c += gridDim.x) {
         uint32_t e[kMaxDims];
         child_entries(a, c, e);
-        for (uint32_t w = threadIdx.x; w < a.nw; w += blockDim.x) {
+        const uint32_t pnw = a.plane_nw ? a.plane_nw : a.nw;
+        for (uint32_t w = threadIdx.x; w < pnw; w += blockDim.x) {
 #pragma unroll
             for (int s = 0; s < 2; s++)
 #pragma unroll
                 for (int j = 0; j < kMaxDims; j++)
                     if (j < (int)a.d) {
                         const size_t idx = ((size_t)e[j] * 2 + s) * a.nw + w;
-                        out[((size_t)(c - a.c_off) * 2 * a.d + (size_t)s * a.d + j) * a.nw + w] =
-                            (a.s0.t[j][idx] ^ a.s0.y[j][idx]) & a.valid[w];
+                        out[((size_t)(c - a.c_off) * 2 * a.d + (size_t)s * a.d + j) * pnw + w] =
+                            w < a.nw ? (a.s0.t[j][idx] ^ a.s0.y[j][idx]) & a.valid[w] : 0ull;
                     }
         }
     }

@@ -562,7 +562,9 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
  * value r1 = v + mask) with pair[o_r], o_r = eq_r ^ mask; row 0's value is its hash mod p (no
  * message), rows 1 .. 2^b - 1 send lo64(hash) ^ pair[o_r]. Outputs: msgs [n][2^bits - 1] u64 (may be
  * NULL), gb_share / ev_share [n] (r1 and the evaluator's value: gb - ev = eq mod p), ev_zero /
- * ev_active [n][bits][16] (may be NULL). Garbler 2^b AES per test, evaluator 1. */
+ * ev_active [n][bits][16] (may be NULL). Garbler 2^b AES per test, evaluator 1. The labels OT's index
+ * is k npad + i with npad = n rounded up to 64 (b = 3, 4) or, since r06, to 512 (b <= 2: the table kernels
+ * read the OT's tile-major matrices, whose 512-OT tiles must hold one client range per bit). */
 int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
                     uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,

@@ -330,9 +330,11 @@ def test_gpu_output_label_share_bit_exact(oracle, n, bits):
 # ---- r05d: the FE levels' garbled table (one b-input garbled gate per test) ------------------------
 def _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
     """The labels OT (the IKNP correlation), then the garbled table on its zero labels and the
-    evaluator's row on its t_j — all in the oracle."""
+    evaluator's row on its t_j — all in the oracle. OT index k npad + i: npad = n rounded up to 512 for
+    b <= 2 (r06: the GPU's table kernels read the tile-major Q / T, one client range per 512-OT tile), to 64
+    for b = 3, 4."""
     n, bits = g.shape
-    npad = (n + 63) // 64 * 64
+    npad = (n + 511) // 512 * 512 if bits <= 2 else (n + 63) // 64 * 64
     ch = np.zeros(bits * npad, np.uint8)
     for k in range(bits):
         ch[k * npad: k * npad + n] = e[:, k]

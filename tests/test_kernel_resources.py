@@ -77,6 +77,9 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     # r05d: the FE levels' garbled table, b = 1..4
     names += [f"_ZN3fhh11k_gt_garbleILi{b}EEEvNS_6GcArgsE" for b in range(1, 5)]
     names += [f"_ZN3fhh9k_gt_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 5)]
+    # r06: the table kernels on the labels OT's tile-major Q / T (b <= 2)
+    names += [f"_ZN3fhh14k_gt_garble_tmILi{b}EEEvNS_6GcArgsE" for b in (1, 2)]
+    names += [f"_ZN3fhh12k_gt_eval_tmILi{b}EEEvNS_6GcArgsE" for b in (1, 2)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
     names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE",

@@ -55,7 +55,8 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     # message sizes (the bytes that would cross the servers' channel)
     lb = got.level_bytes[0]
     C0, bits = int(got.level_children[0]), 2 * d
-    npad = (n + 63) // 64 * 64
+    # r06: d = 1 runs the tile-major table (OT index over whole 512-client tiles), d = 2 the row-major one
+    npad = (n + 511) // 512 * 512 if bits <= 2 else (n + 63) // 64 * 64
     # r05d: the FE levels' gc message is the garbled table's rows 1 .. 2^bits - 1, 8 B each
     assert lb["gc"] == C0 * n * ((1 << bits) - 1) * 8
     # r05b: the labels OT is the IKNP correlation itself (no reply); r05c: no share OT at the FE levels

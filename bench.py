@@ -86,6 +86,17 @@ def cpu_baseline(args):
     dt = time.perf_counter() - t0
     done = len(res.n_children)
     protocol = cpu_protocol_baseline(args, O, res, n_cpu, threads, L)
+    if protocol:   # the configs[0] keys of r05's line
+        protocol["configs0_crawl_s_extrapolated"] = protocol["crawl_s_extrapolated"]
+    # the CPU path at 1 000 / 100 000 / 1 000 000 clients (the larger two sampled)
+    import numpy as np
+    sizes = {"1000": {"value": res.aes_blocks / dt, "crawl_s": dt if done == L else None,
+                      "crawl_s_extrapolated": (protocol or {}).get("crawl_s_extrapolated"), "kind": "full crawl"}}
+    gold = {100_000: "oracle_zipf_100k_L512.npz", 1_000_000: "zipf_1m_L512.npz"}
+    if not args.no_cpu_sizes:
+        for n_s, fx in gold.items():
+            lc = np.load(os.path.join(ROOT, "tests", "golden", fx), allow_pickle=False)["level_children"]
+            sizes[str(n_s)] = cpu_size_sample(args, O, n_s, threads, int(lc.sum()), budget=max(4.0, args.cpu_baseline_seconds / 15))
     return {
         "value": res.aes_blocks / dt,
         "unit": "AES blocks/s",
@@ -102,10 +113,15 @@ def cpu_baseline(args):
                    f"(oracle/fhh_oracle.c: AES-NI single block per eval_bit, reference child order, OpenMP "
                    f"{threads} threads on {cpu_model()})"),
         "protocol": protocol,
+        "sizes": sizes,
+        "sizes_note": ("the oracle's eval crawl (AES blocks/s) and the reference-form protocol at each client count "
+                       "of BASELINE.md; 1000 = configs[0] crawled in full, 100000 / 1000000 sampled over their first "
+                       "levels and extrapolated (cpu_size_sample)"),
     }
 
 
-def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int):
+def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int, crawl_tests: int | None = None,
+                          budget: float | None = None, what: str = "configs[0]"):
     """The reference's dominant per-level cost on the host cores: tree_crawl's GC equality test + OTs
     (collect.rs:419-482, equalitytest.rs:25-106) in the REFERENCE's protocol form — the garbler labels
     every wire (2 bits + 1 AES-CTR labels), the evaluator's labels and the FE shares go by plain OT
@@ -115,7 +131,8 @@ def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int):
     ~cpu_baseline_seconds / 6 of protocol time; tests/s extrapolated to the configs[0] crawl's tests.
     Every sampled level's v0 - v1 equals the plaintext count (checked)."""
     import numpy as np
-    budget = max(5.0, args.cpu_baseline_seconds / 6)
+    if budget is None:
+        budget = max(5.0, args.cpu_baseline_seconds / 6)
     rng = np.random.default_rng(args.seed)
     FE_P = O.FE_P
     tests = 0
@@ -146,12 +163,12 @@ def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int):
         tables, gbl, evl, dec = O.gc_garble_eq(gb, ev, mask, key, delta)
         zero = evl ^ (ev[:, :, None] * D)          # the OT sender's x0: the evaluator's zero labels
         # the labels OT (plain OT of (x0, x0 ^ Delta), gb_set_fancy_inputs, equalitytest.rs:67-82)
-        lab = O.ot_extend(ev.reshape(-1), zero.reshape(-1, 16), None, delta, seeds[0], sch[0])
+        lab = O.ot_extend(ev.reshape(-1), zero.reshape(-1, 16), None, delta, seeds[0], sch[0], prg="aes")
         out = O.gc_eval_eq(tables, gbl, lab.reshape(T, bits, 16), dec)
         # the share OT (collect.rs:439-471): (r0, r1) if mask else (r1, r0), choice = the GC output
         blk = lambda v: np.concatenate([v.view(np.uint8).reshape(T, 8), np.zeros((T, 8), np.uint8)], axis=1)
         m0, m1 = (r0, r1) if mask else (r1, r0)
-        got = O.ot_extend(out, blk(m0), blk(m1), None, seeds[1], sch[1])
+        got = O.ot_extend(out, blk(m0), blk(m1), None, seeds[1], sch[1], prg="aes")
         dt = time.perf_counter() - t0
         v1 = np.ascontiguousarray(got[:, :8]).view(np.uint64).reshape(C, n)
         diff = (r1.reshape(C, n).astype(object).sum(axis=1) - v1.astype(object).sum(axis=1)) % FE_P
@@ -164,20 +181,63 @@ def cpu_protocol_baseline(args, O, res, n_cpu: int, threads: int, L: int):
     if not tests:
         return None
     rate = tests / spent
-    full = len(res.n_children) == L   # the crawl above finished inside its time bound
-    crawl_tests = int(sum(res.n_children)) * n_cpu
+    full = crawl_tests is not None or len(res.n_children) == L   # the crawl above finished inside its time bound
+    if crawl_tests is None:
+        crawl_tests = int(sum(res.n_children)) * n_cpu
     aes = (2 * bits + 1) + 8 * (bits - 1) + 4 * (bits - 1) + 6 * bits + 6
     return {
         "value": rate, "unit": "GC equality tests + OTs per s", "cores": threads, "kind": "port",
         "aes_blocks_per_test": aes,
-        "configs0_crawl_tests": crawl_tests if full else None,
-        "configs0_crawl_s_extrapolated": crawl_tests / rate if full else None,
-        "tests_in_levels_crawled": crawl_tests, "levels_crawled": len(res.n_children),
-        "sample": (f"configs[0] levels {levels} ({tests} tests, {spent:.2f} s): the reference's protocol form "
+        "crawl_tests": crawl_tests if full else None,
+        "crawl_s_extrapolated": crawl_tests / rate if full else None,
+        "levels_crawled": len(res.n_children),
+        "sample": (f"{what} levels {levels} ({tests} tests, {spent:.2f} s): the reference's protocol form "
                    f"(garbler labels all {2 * bits + 1} wires, half-gates + TCCR, plain ALSZ OT for the labels and "
                    f"the FE share; {aes} AES per test) on oracle/fhh_oracle.c with AES-NI, OpenMP {threads} "
                    f"threads; v0 - v1 per child = the plaintext count at every sampled level; extrapolated to the "
                    f"crawl's {crawl_tests} tests"),
+    }
+
+
+def cpu_size_sample(args, O, n: int, threads: int, crawl_children: int, budget: float):
+    """BASELINE.md's CPU crawl at a larger client count (100k = configs[1], 1M = the metric's), sampled: the
+    metric's Zipf workload at n clients (seed args.seed), its first 32 levels (the strings' first 32 bits:
+    the same children as the full crawl's first levels) keyed by the oracle's keygen and crawled by the
+    oracle (AES-NI single-block eval_bit, reference child order, OpenMP) until `budget` seconds, in count
+    mode with the plaintext equality — the eval path the GPU headline runs. AES blocks/s of that sample,
+    extrapolated to the full crawl's children (`crawl_children`: the committed golden's level_children sum)
+    and labelled as such; then the reference-form protocol on the sampled levels' share strings
+    (cpu_protocol_baseline), extrapolated the same way."""
+    from fuzzyheavyhitters_amd import workload
+    t0 = time.perf_counter()
+    wl = workload.zipf_workload(n, 512, 1, num_sites=10_000, zipf_s=1.03, ball_size=1, seed=args.seed)
+    K = 32
+    left, right = wl.left[:, :, :K].copy(), wl.right[:, :, :K].copy()
+    roots = wl.root_seeds
+    del wl
+    k0, k1 = O.gen_keys(left, right, roots, nthreads=threads)
+    del left, right
+    t_setup = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    # at most 6 (1M) / 9 (100k) levels: a level's States are ~36 B per (child, client) and server
+    res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=budget, keep_levels=[1, 2, 3],
+                  levels=6 if n >= 1_000_000 else 9)
+    dt = time.perf_counter() - t0
+    done = len(res.n_children)
+    per_child_client = res.aes_blocks / (sum(res.n_children) * n)
+    full_blocks = per_child_client * crawl_children * n
+    rate = res.aes_blocks / dt
+    proto = cpu_protocol_baseline(args, O, res, n, threads, K, crawl_tests=crawl_children * n,
+                                  budget=budget / 2, what=f"{n} clients")
+    return {
+        "clients": n, "value": rate, "unit": "AES blocks/s", "cores": threads, "kind": "port",
+        "levels_sampled": done, "children_sampled": int(sum(res.n_children)), "aes_blocks_sampled": int(res.aes_blocks),
+        "sample_s": dt, "setup_s": t_setup,
+        "crawl_aes_blocks": int(full_blocks), "crawl_s_extrapolated": full_blocks / rate,
+        "extrapolation": (f"sampled levels 0..{done - 1} ({sum(res.n_children)} children); the full crawl's "
+                          f"{crawl_children} children from the committed golden level counts x {n} clients x "
+                          f"{per_child_client:.0f} AES per (child, client) at the sampled rate"),
+        "protocol": proto,
     }
 
 
@@ -843,6 +903,7 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=150.0,
                     help="upper bound on the configs[0] CPU crawl (it normally completes well inside)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-sizes", action="store_true", help="cpu_baseline: configs[0] only (no 100k / 1M samples)")
     ap.add_argument("--microbench", action="store_true", help="measure VALU/LDS peaks on this device")
     ap.add_argument("--variant", type=int, default=-1, help="k_expand variant (-1 = library default)")
     ap.add_argument("--rehearse", action="store_true",

@@ -7,13 +7,14 @@
 //   sender   (base choice s):  q_i = G(k_i^{s_i}) ^ s_i u_i  =>  q_j = t_j ^ r_j s (columns)
 //   sender:    y_j^b = x_j^b ^ H(j, q_j ^ b s)        receiver:  x_j^{r_j} = y_j^{r_j} ^ H(j, t_j)
 //
-// G = AES-128-CTR under the row key (block c -> OTs 128 c .. 128 c + 127), H(j, x) = scuttlebutt's
+// G = ChaCha12 under the row key since r06 (one 64-B block -> OTs 512 j .. 512 j + 511 of a row; AES-128-CTR,
+// block c -> OTs 128 c .. 128 c + 127, in r01-r05 as ocelot's AesRng), H(j, x) = scuttlebutt's
 // AesHash::cr_hash(j, x) = pi(x) ^ x (the correlation-robust hash ocelot's ALSZ applies to q_j,
 // q_j ^ s and t_j; j is not an input), pi = AES-128 under the zero key (as fhh_gc.hip): the
 // fixed-key AES + feed-forward of k_expand (aes0_mmo_tab, round keys as immediates). The 128 base OTs are
 // ideal (the host hands the sender k_i^{s_i}).
 //
-//   k_ot_recv_expand / k_ot_send_expand        one lane per (row, 128-OT block): 2 / 1 AES
+//   k_ot_recv_expand_cc / k_ot_send_expand_cc  one lane per (row, 512-OT tile): 2 / 1 ChaCha12 blocks
 //   k_ot_send_hash_rows / k_ot_recv_hash_rows  one wave per 512 OTs, the 128 x 512 bit tile of T / Q
 //                                              transposed in registers + LDS: 2 / 1 cr_hash per OT
 #include "fhh_internal.h"
@@ -29,7 +30,6 @@ namespace fhh {
 
 __constant__ WordTable c_T0_ot = T0;
 using OtTab = Tab4T32<DevOpsX>;
-constexpr int kOtThreads = 1024;
 
 __device__ __forceinline__ void ot_fill(uint32_t* tbl) {
     for (int i = threadIdx.x; i < OtTab::kWords; i += blockDim.x) tbl[i] = OtTab::word(c_T0_ot.v, i);
@@ -57,151 +57,140 @@ __device__ __forceinline__ uint64_t ot_tmaj(uint32_t i, uint64_t c) {
     return (c >> 2) * 512 + (uint64_t)i * 4 + (c & 3);
 }
 
-__device__ __forceinline__ void ld_rk(const uint32_t* base, uint32_t (&rk)[11][4]) {
-#pragma unroll
-    for (int r = 0; r < 11; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) rk[r][c] = base[4 * r + c];
+// ---- r06: the row PRG G = ChaCha12 (VALU only) ------------------------------------------------
+// The expands were T-table AES-CTR under the row keys (r01-r05: k_ot_expand<true> 2 blocks per OT
+// and row, k_ot_send_expand_pair 1, both bound by LDS issue beside the garbled table's AES). G is now
+// the ChaCha block function with 12 rounds (rand_chacha's StdRng; fhh_oracle.c orc_chacha_block /
+// ot_prg_block, pinned for 20 rounds against RFC 8439 and OpenSSL), key = row seed || row seed, 64-bit
+// block counter = ctr_off / 4 + tile, nonce 0: one 64-byte block is exactly one row of a 512-OT tile of
+// the tile-major T / Q (ot_tmaj), so a lane stores 64 contiguous bytes. 4 adds + 4 xors + 4 rotates
+// (v_alignbit) per quarter round, ~600 VALU per 64 B against ~250 VALU + 144-160 ds_read_b32 per 16 B of
+// AES: no LDS at all, so the expands leave the LDS to the table kernels' cr_hash. The row seed is words
+// 0..3 of the row's key schedule in rk (the schedules the AES form used; unchanged on the host).
+constexpr int kOtChachaRounds = 12;
+
+__device__ __forceinline__ uint32_t cc_rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+
+__device__ __forceinline__ void cc_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    a += b; d ^= a; d = cc_rotl(d, 16);
+    c += d; b ^= c; b = cc_rotl(b, 12);
+    a += b; d ^= a; d = cc_rotl(d, 8);
+    c += d; b ^= c; b = cc_rotl(b, 7);
 }
 
-// one wave per (row i, kOtSlices consecutive 64-block slices): lane l computes blocks
-// c = c0 + 64 q + l, q < kOtSlices, in lockstep. nblk = mp / 128 is a multiple of 64, so a slice
-// is wholly inside or outside the row and the row's key schedules are uniform (scalar loads)
-// The receiver's expand (the sender's is k_ot_send_expand_pair below; the template parameter keeps
-// the kernel's name, k_ot_expand<true>, that every profile since r01 reports)
-template <bool RECV>
-__global__ __launch_bounds__(kOtThreads) void k_ot_expand(OtArgs a) {
-    static_assert(RECV, "the sender's expand is k_ot_send_expand_pair");
-    // 4 slices per wave (4 blocks per lane in lockstep). The receiver runs its two row keys one
-    // after the other over the same 4 blocks (T = G(k0) is stored, U = T ^ G(k1) ^ r): only one
-    // 44-word schedule is live in SGPRs at a time (both at once spilled it into VGPRs: 128 VGPRs
-    // plus scratch)
-    constexpr int kOtSlices = 4;
-    // a lane's blocks c0 + 64 q + lane (c0 a multiple of 256) differ only in byte 0: aes_rk_ctr
-    // shares rounds 1-2 of blocks 1..3 with block 0 (559 instead of 640 lookups per lane and key)
-    static_assert(64 * kOtSlices <= 256, "the slices' counters must differ in byte 0 alone");
-    __shared__ uint32_t tbl_ot[OtTab::kWords];   // static: a dynamic base costs an add per lookup
+// NB independent ChaCha blocks (key k[q] = seed || seed, counter ctr[q], nonce 0) in lockstep
+template <int NB>
+__device__ __forceinline__ void cc_blocks(const uint32_t (&k)[NB][4], const uint64_t (&ctr)[NB], uint32_t (&x)[NB][16]) {
+#pragma unroll
+    for (int q = 0; q < NB; q++) {
+        x[q][0] = 0x61707865u; x[q][1] = 0x3320646eu; x[q][2] = 0x79622d32u; x[q][3] = 0x6b206574u;
+#pragma unroll
+        for (int w = 0; w < 4; w++) x[q][4 + w] = x[q][8 + w] = k[q][w];
+        x[q][12] = (uint32_t)ctr[q];
+        x[q][13] = (uint32_t)(ctr[q] >> 32);
+        x[q][14] = 0u;
+        x[q][15] = 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kOtChachaRounds; r += 2) {
+#pragma unroll
+        for (int q = 0; q < NB; q++) {
+            cc_qr(x[q][0], x[q][4], x[q][8], x[q][12]);
+            cc_qr(x[q][1], x[q][5], x[q][9], x[q][13]);
+            cc_qr(x[q][2], x[q][6], x[q][10], x[q][14]);
+            cc_qr(x[q][3], x[q][7], x[q][11], x[q][15]);
+            cc_qr(x[q][0], x[q][5], x[q][10], x[q][15]);
+            cc_qr(x[q][1], x[q][6], x[q][11], x[q][12]);
+            cc_qr(x[q][2], x[q][7], x[q][8], x[q][13]);
+            cc_qr(x[q][3], x[q][4], x[q][9], x[q][14]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NB; q++) {   // feed-forward
+        x[q][0] += 0x61707865u; x[q][1] += 0x3320646eu; x[q][2] += 0x79622d32u; x[q][3] += 0x6b206574u;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            x[q][4 + w] += k[q][w];
+            x[q][8 + w] += k[q][w];
+        }
+        x[q][12] += (uint32_t)ctr[q];
+        x[q][13] += (uint32_t)(ctr[q] >> 32);
+    }
+}
+
+__device__ __forceinline__ void ld_seed(const uint32_t* rk, uint32_t row, uint32_t (&k)[4]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rk + (size_t)row * 44);   // words 0..3 of the schedule = the key
+    k[0] = v.x;
+    k[1] = v.y;
+    k[2] = v.z;
+    k[3] = v.w;
+}
+
+constexpr int kOtCcThreads = 256;
+
+// The receiver: work item = (512-OT tile j, row half h); lane l = row i = 64 h + l computes G(k_i^0) and
+// G(k_i^1) for tile j (2 ChaCha blocks in lockstep), stores T's row i of the tile (64 B, tile-major) and
+// U = T ^ G(k_i^1) ^ r (row form [128][mp / 128]: 64 B per lane). The tile's choice words r are the same
+// for every lane (a broadcast load); 128-OT blocks past the active OTs get no choice bits.
+__global__ __launch_bounds__(kOtCcThreads) void k_ot_recv_expand_cc(OtArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
-    // the active tiles (rows x 64 kOtSlices blocks) in contiguous runs per wave: consecutive tiles
-    // of a wave share a row, so its key schedules (scalar loads, re-issued per tile to keep the
-    // SGPR budget) hit the scalar cache instead of going to L2 as grid-strided tiles did
-    const uint64_t tiles_per_row = (nblk_act + 64 * kOtSlices - 1) / (64 * kOtSlices);
-    const uint64_t tiles = 128 * tiles_per_row;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
-    const uint64_t wave = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6);
-    const uint64_t run = (tiles + nwaves - 1) / nwaves;
-    // a workgroup whose waves have no tiles (an empty chunk of the level loop) skips the table fill
-    if ((uint64_t)blockIdx.x * (kOtThreads / 64) * run >= tiles) return;
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
-    const uint64_t t_end = min(tiles, (wave + 1) * run);
-    for (uint64_t t = wave * run; t < t_end; t++) {
-        const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_row));
-        const uint64_t c0 = (t - (uint64_t)i * tiles_per_row) * 64 * kOtSlices;
-        if (c0 >= nblk_act) continue;   // wave-uniform
-        uint32_t g[kOtSlices][4];
+    const uint64_t items = 2 * ((nblk_act + 3) / 4);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtCcThreads / 64);
+    for (uint64_t it = (uint64_t)blockIdx.x * (kOtCcThreads / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+        const uint64_t j = it >> 1;
+        const uint32_t i = 64 * (uint32_t)(it & 1) + lane;
+        uint32_t k[2][4];
+        ld_seed(a.rk, i, k[0]);
+        ld_seed(a.rk, 128 + i, k[1]);
+        const uint64_t ctr[2] = {a.ctr_off / 4 + j, a.ctr_off / 4 + j};
+        uint32_t g[2][16];
+        cc_blocks<2>(k, ctr, g);
+        const uint4* ch = reinterpret_cast<const uint4*>(a.choices);
 #pragma unroll
-        for (int q = 0; q < kOtSlices; q++) {
-            const uint64_t c = a.ctr_off + c0 + 64 * q + lane;   // the session's running counter
-            g[q][0] = (uint32_t)c;
-            g[q][1] = (uint32_t)(c >> 32);
-            g[q][2] = 0u;
-            g[q][3] = 0u;
-        }
-        {
-            uint32_t rk[11][4];
-            ld_rk(a.rk + (size_t)i * 44, rk);
-            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g, tbl_ot, b0, b1, rk);   // G(k_i^0)
-        }
-        {
-            uint32_t g1[kOtSlices][4];
-#pragma unroll
-            for (int q = 0; q < kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * q + lane, cc = a.ctr_off + c;
-                if (c0 + 64 * q < nblk_act) a.T[ot_tmaj(i, c)] = make_uint4(g[q][0], g[q][1], g[q][2], g[q][3]);
-                g1[q][0] = (uint32_t)cc;
-                g1[q][1] = (uint32_t)(cc >> 32);
-                g1[q][2] = 0u;
-                g1[q][3] = 0u;
-            }
-            uint32_t rk[11][4];
-            ld_rk(a.rk + (size_t)(128 + i) * 44, rk);
-            aes_rk_ctr<OtTab, kOtSlices, 0, 0>(g1, tbl_ot, b0, b1, rk);   // G(k_i^1)
-#pragma unroll
-            for (int q = 0; q < kOtSlices; q++) {
-                const uint64_t c = c0 + 64 * q + lane;
-                if (c0 + 64 * q >= nblk_act) break;   // wave-uniform
-                const uint4 r = reinterpret_cast<const uint4*>(a.choices)[c];
-                a.U[(uint64_t)i * nblk + c] = make_uint4(g[q][0] ^ g1[q][0] ^ r.x, g[q][1] ^ g1[q][1] ^ r.y,
-                                                         g[q][2] ^ g1[q][2] ^ r.z, g[q][3] ^ g1[q][3] ^ r.w);
-            }
+        for (int w = 0; w < 4; w++) {
+            const uint64_t c = 4 * j + w;
+            const uint4 r = c < nblk_act ? ch[c] : make_uint4(0, 0, 0, 0);
+            a.T[ot_tmaj(i, c)] = make_uint4(g[0][4 * w], g[0][4 * w + 1], g[0][4 * w + 2], g[0][4 * w + 3]);
+            a.U[(uint64_t)i * nblk + c] = make_uint4(g[0][4 * w] ^ g[1][4 * w] ^ r.x, g[0][4 * w + 1] ^ g[1][4 * w + 1] ^ r.y,
+                                                     g[0][4 * w + 2] ^ g[1][4 * w + 2] ^ r.z,
+                                                     g[0][4 * w + 3] ^ g[1][4 * w + 3] ^ r.w);
         }
     }
 }
 
-// The sender's expand in row pairs (r04): a wave takes rows 2 p (lanes 0-31) and 2 p + 1 (lanes
-// 32-63) over the same 128 blocks, lane l computing blocks c0 + 32 q + (l & 31), q < 4 (c0 a multiple
-// of 128: the four counters differ in byte 0 alone, as aes_rk_ctr needs). Both rows' schedules are
-// staged in LDS per row pair and read as one ds_read_b128 per round (-5.7 % against per-half-wave
-// global key loads, profiles/r04/ab_ot_expand_pair/). In the tile-major Q (ot_tmaj) rows 2 p and 2 p + 1
-// of a tile are adjacent, so each store instruction writes 8 whole 128-B lines instead of 16 half
-// lines: 263 -> 246 us per configs[1] launch against k_ot_expand<false> (the receiver's pair form
-// measured +0.8 %: its two keys per block keep the one-row form; profiles/r04/ab_ot_expand_pair/).
-__global__ __launch_bounds__(kOtThreads) void k_ot_send_expand_pair(OtArgs a) {
-    constexpr int kSlices = 4;
-    __shared__ uint32_t tbl_ot[OtTab::kWords];
-    // the wave's two row schedules, staged once per row pair: a per-half-wave key read by global
-    // loads put an L2 round trip on every round (vmcnt waits in the AES)
-    __shared__ __attribute__((aligned(16))) uint32_t rk_pair[kOtThreads / 64][2][44];
-    const uint32_t lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31, wv = threadIdx.x >> 6;
-    uint32_t cur_p = ~0u;
+// The sender: work item = (2 tiles j, j + 1, row half h); lane row i computes G(k_i^{s_i}) for both tiles
+// (2 ChaCha blocks in lockstep) and stores Q = G ^ s_i U tile-major.
+__global__ __launch_bounds__(kOtCcThreads) void k_ot_send_expand_cc(OtArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t nblk = a.mp / 128;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
-    const uint64_t tiles_per_pair = (nblk_act + 32 * kSlices - 1) / (32 * kSlices);
-    const uint64_t tiles = 64 * tiles_per_pair;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtThreads / 64);
-    const uint64_t wave = (uint64_t)blockIdx.x * (kOtThreads / 64) + (threadIdx.x >> 6);
-    const uint64_t run = (tiles + nwaves - 1) / nwaves;
-    if ((uint64_t)blockIdx.x * (kOtThreads / 64) * run >= tiles) return;
-    ot_fill(tbl_ot);
-    uint32_t b0, b1;
-    OtTab::bases(lane, b0, b1);
-    const uint64_t t_end = min(tiles, (wave + 1) * run);
-    for (uint64_t t = wave * run; t < t_end; t++) {
-        const uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(t / tiles_per_pair));
-        const uint64_t c0 = (t - (uint64_t)p * tiles_per_pair) * 32 * kSlices;
-        if (c0 >= nblk_act) continue;   // wave-uniform
-        const uint32_t i = 2 * p + half;
-        if (p != cur_p) {   // wave-uniform: the wave's tiles run in contiguous order, mostly one pair
-            if (lane < 44) {
-                rk_pair[wv][0][lane] = a.rk[(size_t)(256 + 2 * p) * 44 + lane];
-                rk_pair[wv][1][lane] = a.rk[(size_t)(257 + 2 * p) * 44 + lane];
-            }
-            cur_p = p;
-            __builtin_amdgcn_wave_barrier();   // one wave's LDS accesses retire in order
-        }
-        uint32_t g[kSlices][4];
-#pragma unroll
-        for (int q = 0; q < kSlices; q++) {
-            const uint64_t c = a.ctr_off + c0 + 32 * q + l;   // the session's running counter
-            g[q][0] = (uint32_t)c;
-            g[q][1] = (uint32_t)(c >> 32);
-            g[q][2] = 0u;
-            g[q][3] = 0u;
-        }
-        aes_lds_rk_ctr<OtTab, kSlices, 0, 0>(g, tbl_ot, b0, b1,
-                                             reinterpret_cast<const uint4*>(&rk_pair[wv][half][0]));   // G(k_i^{s_i})
+    const uint64_t tiles = (nblk_act + 3) / 4;
+    const uint64_t items = 2 * ((tiles + 1) / 2);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtCcThreads / 64);
+    for (uint64_t it = (uint64_t)blockIdx.x * (kOtCcThreads / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+        const uint64_t j0 = 2 * (it >> 1);
+        const uint32_t i = 64 * (uint32_t)(it & 1) + lane;
         const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
+        uint32_t k[2][4];
+        ld_seed(a.rk, 256 + i, k[0]);
 #pragma unroll
-        for (int q = 0; q < kSlices; q++) {
-            const uint64_t c = c0 + 32 * q + l;
-            if (c0 + 32 * q >= nblk_act) break;   // wave-uniform
-            uint4 u = make_uint4(0, 0, 0, 0);
-            if (si) u = a.U[(uint64_t)i * nblk + c];
-            a.Q[ot_tmaj(i, c)] = make_uint4(g[q][0] ^ u.x, g[q][1] ^ u.y, g[q][2] ^ u.z, g[q][3] ^ u.w);
+        for (int w = 0; w < 4; w++) k[1][w] = k[0][w];
+        const uint64_t ctr[2] = {a.ctr_off / 4 + j0, a.ctr_off / 4 + j0 + 1};
+        uint32_t g[2][16];
+        cc_blocks<2>(k, ctr, g);
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            if (j0 + q >= tiles) break;   // wave-uniform
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint64_t c = 4 * (j0 + q) + w;
+                uint4 u = make_uint4(0, 0, 0, 0);
+                if (si) u = a.U[(uint64_t)i * nblk + c];
+                a.Q[ot_tmaj(i, c)] = make_uint4(g[q][4 * w] ^ u.x, g[q][4 * w + 1] ^ u.y, g[q][4 * w + 2] ^ u.z,
+                                                g[q][4 * w + 3] ^ u.w);
+            }
         }
     }
 }
@@ -606,23 +595,22 @@ static int device_cus() {
     return cus;
 }
 
-static int ot_grid(uint64_t items, int threads) {
-    const uint64_t need = (items + threads - 1) / threads;
-    // 1024-thread workgroups: 4 per CU (one per CU measured -3.1 % for the receiver expand at
-    // configs[1] but +6 % at 1M clients, where the longer per-wave tile runs balance worse; r03)
-    const uint64_t cap = (uint64_t)device_cus() * (threads >= 1024 ? 4 : 16);
+
+// the ChaCha expands: 256-thread workgroups (no LDS, ~70 VGPRs), 8 per CU, waves stride over the items
+static int ot_cc_grid(uint64_t items) {
+    const uint64_t wpb = kOtCcThreads / 64, need = (items + wpb - 1) / wpb, cap = (uint64_t)device_cus() * 8;
     return (int)(need < cap ? (need ? need : 1) : cap);
 }
 
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_expand<true>, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
-                       stream, a);
+    if (a.ctr_off % 4) return hipErrorInvalidValue;   // ChaCha counters per 512-OT tile
+    hipLaunchKernelGGL(k_ot_recv_expand_cc, dim3(ot_cc_grid(2 * (a.mp / 512))), dim3(kOtCcThreads), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ot_send_expand_pair, dim3(ot_grid(128 * (a.mp / 128) / 4, kOtThreads)), dim3(kOtThreads), 0,
-                       stream, a);
+    if (a.ctr_off % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ot_send_expand_cc, dim3(ot_cc_grid(a.mp / 512)), dim3(kOtCcThreads), 0, stream, a);
     return hipGetLastError();
 }
 

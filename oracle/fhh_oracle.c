@@ -1315,15 +1315,75 @@ void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint
 /* not vendored) used at equalitytest.rs:67-82 (evaluator labels) and */
 /* collect.rs:437-471 (FE shares). Published scheme restated: kappa = */
 /* 128 base OTs (ideal here: the sender is handed k_i^{s_i}), G =     */
-/* AES-128-CTR under k (block c = LE128(c) gives OT bits 128c..+127),  */
+/* ChaCha12 under k (r06; prg 0: AES-128-CTR, block c = LE128(c) gives */
+/* OT bits 128c..+127 — ot_prg_block),                                 */
 /* H(j, x) = cr_hash(j, x) = pi(x) ^ x (ot_cr_hash; tweak_base is    */
 /* not an input of it). Parity: functional (out_j = x_j^{r_j}); wire  */
 /* format unpinned.                                                   */
 /* ------------------------------------------------------------------ */
-static void ot_prg_block(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
+static void ot_prg_block_aes(const uint8_t rk[176], uint64_t c, uint8_t out[16]) {
     uint8_t ctr[16] = {0};
     for (int k = 0; k < 8; k++) ctr[k] = (uint8_t)(c >> (8 * k));
     gc_aes_rk(rk, ctr, out);
+}
+
+/* ChaCha block function (RFC 8439 2.3 with the original 64-bit block counter in state words 12-13 and a
+ * 64-bit nonce in 14-15; "expand 32-byte k"), `rounds` = 20 / 12 / 8: out = the 64-byte block. Pinned for
+ * rounds = 20 against RFC 8439 2.3.2's vector and OpenSSL's EVP_chacha20 (tests/test_oracle_kat.py). */
+static inline uint32_t cc_rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+#define CC_QR(a, b, c, d)                                                                             \
+    a += b; d ^= a; d = cc_rotl(d, 16); c += d; b ^= c; b = cc_rotl(b, 12);                            \
+    a += b; d ^= a; d = cc_rotl(d, 8); c += d; b ^= c; b = cc_rotl(b, 7);
+void orc_chacha_block(uint32_t rounds, const uint8_t key[32], uint64_t ctr, uint64_t nonce, uint8_t out[64]) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int k = 0; k < 8; k++)
+        st[4 + k] = (uint32_t)key[4 * k] | ((uint32_t)key[4 * k + 1] << 8) | ((uint32_t)key[4 * k + 2] << 16) |
+                    ((uint32_t)key[4 * k + 3] << 24);
+    st[12] = (uint32_t)ctr;
+    st[13] = (uint32_t)(ctr >> 32);
+    st[14] = (uint32_t)nonce;
+    st[15] = (uint32_t)(nonce >> 32);
+    uint32_t x[16];
+    memcpy(x, st, sizeof x);
+    for (uint32_t r = 0; r < rounds; r += 2) {
+        CC_QR(x[0], x[4], x[8], x[12]) CC_QR(x[1], x[5], x[9], x[13]) CC_QR(x[2], x[6], x[10], x[14])
+        CC_QR(x[3], x[7], x[11], x[15])
+        CC_QR(x[0], x[5], x[10], x[15]) CC_QR(x[1], x[6], x[11], x[12]) CC_QR(x[2], x[7], x[8], x[13])
+        CC_QR(x[3], x[4], x[9], x[14])
+    }
+    for (int k = 0; k < 16; k++) {
+        const uint32_t v = x[k] + st[k];
+        for (int b = 0; b < 4; b++) out[4 * k + b] = (uint8_t)(v >> (8 * b));
+    }
+}
+
+/* r06: the OT extension's row PRG G is ChaCha12 (the block function above, 12 rounds — rand_chacha's
+ * StdRng) keyed by the row's base-OT seed k (key = k || k, nonce 0): 128-OT block c (the row's bits
+ * 128 c .. 128 c + 127) = bytes 16 (c % 4) .. 16 (c % 4) + 15 of the ChaCha block at counter c / 4 — one
+ * ChaCha block = one row of a 512-OT tile of the GPU's tile-major matrices. It replaces AES-128-CTR
+ * (r01-r05, ocelot's AesRng): a VALU-only PRG, no T-table lookups. prg 0 keeps the
+ * AES-CTR form (the reference-form CPU baseline, bench.py cpu_protocol_baseline). */
+#define OT_CHACHA_ROUNDS 12
+typedef struct {   /* the last ChaCha block of one row key (the row loops walk c upwards) */
+    uint64_t ctr;
+    int valid;
+    uint8_t blk[64];
+} ot_cc_cache;
+static void ot_prg_block(int prg, const uint8_t seed[16], const uint8_t rk[176], uint64_t c, uint8_t out[16],
+                         ot_cc_cache* cache) {
+    if (prg == 0) {
+        ot_prg_block_aes(rk, c, out);
+        return;
+    }
+    if (!cache->valid || cache->ctr != c / 4) {
+        uint8_t key[32];
+        memcpy(key, seed, 16);
+        memcpy(key + 16, seed, 16);
+        orc_chacha_block(OT_CHACHA_ROUNDS, key, c / 4, 0, cache->blk);
+        cache->ctr = c / 4;
+        cache->valid = 1;
+    }
+    memcpy(out, cache->blk + 16 * (c % 4), 16);
 }
 
 /* Correlation-robust hash of the OT extension: scuttlebutt AesHash::cr_hash(i, x) = pi(x) ^ x,
@@ -1339,7 +1399,7 @@ static void ot_cr_hash(const uint8_t x[16], uint8_t out[16]) {
  * u_out [128][nblk][16] (nblk = ceil(m / 128)), y0_out / y1_out [m][16]. */
 void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const uint8_t* x1, const uint8_t delta[16],
                    const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t tweak_base, uint8_t* out,
-                   uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out) {
+                   uint8_t* u_out, uint8_t* y0_out, uint8_t* y1_out, int prg) {
     oracle_init();
     const uint64_t nblk = (m + 127) / 128;
     uint8_t* T = (uint8_t*)calloc(128 * nblk * 16, 1);
@@ -1352,10 +1412,11 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
         key_expand(seeds + (i * 2 + 1) * 16, rk1);
         const int si = (s[i / 8] >> (i % 8)) & 1;
         key_expand(seeds + (i * 2 + si) * 16, rks);   /* ideal base OT: the sender holds k_i^{s_i} */
+        ot_cc_cache cc[3] = {{0, 0, {0}}, {0, 0, {0}}, {0, 0, {0}}};
         for (uint64_t c = 0; c < nblk; c++) {
             uint8_t g0[16], g1[16], gs[16];
-            ot_prg_block(rk0, c, g0);
-            ot_prg_block(rk1, c, g1);
+            ot_prg_block(prg, seeds + (i * 2 + 0) * 16, rk0, c, g0, &cc[0]);
+            ot_prg_block(prg, seeds + (i * 2 + 1) * 16, rk1, c, g1, &cc[1]);
             uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
             uint8_t* u = U + ((uint64_t)i * nblk + c) * 16;
             for (int k = 0; k < 16; k++) {
@@ -1367,7 +1428,7 @@ void orc_ot_extend(uint64_t m, const uint8_t* choices, const uint8_t* x0, const 
                 t[k] = g0[k];
                 u[k] = g0[k] ^ g1[k] ^ r;                 /* receiver -> sender */
             }
-            ot_prg_block(rks, c, gs);                     /* sender: q_i = G(k_i^{s_i}) ^ s_i u_i */
+            ot_prg_block(prg, seeds + (i * 2 + si) * 16, rks, c, gs, &cc[2]);   /* sender: q_i = G(k_i^{s_i}) ^ s_i u_i */
             uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
             for (int k = 0; k < 16; k++) q[k] = gs[k] ^ (si ? u[k] : 0);
         }
@@ -1485,10 +1546,11 @@ void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uin
         key_expand(seeds + (i * 2 + 1) * 16, rk1);
         const int si = (s[i / 8] >> (i % 8)) & 1;
         key_expand(seeds + (i * 2 + si) * 16, rks);
+        ot_cc_cache cc[3] = {{0, 0, {0}}, {0, 0, {0}}, {0, 0, {0}}};
         for (uint64_t c = 0; c < nblk; c++) {
             uint8_t g0[16], g1[16], gs[16];
-            ot_prg_block(rk0, ctr_off + c, g0);
-            ot_prg_block(rk1, ctr_off + c, g1);
+            ot_prg_block(1, seeds + (i * 2 + 0) * 16, rk0, ctr_off + c, g0, &cc[0]);
+            ot_prg_block(1, seeds + (i * 2 + 1) * 16, rk1, ctr_off + c, g1, &cc[1]);
             uint8_t* t = T + ((uint64_t)i * nblk + c) * 16;
             uint8_t* u = U + ((uint64_t)i * nblk + c) * 16;
             for (int k = 0; k < 16; k++) {
@@ -1500,7 +1562,7 @@ void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uin
                 t[k] = g0[k];
                 u[k] = g0[k] ^ g1[k] ^ r;
             }
-            ot_prg_block(rks, ctr_off + c, gs);
+            ot_prg_block(1, seeds + (i * 2 + si) * 16, rks, ctr_off + c, gs, &cc[2]);
             uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
             for (int k = 0; k < 16; k++) q[k] = gs[k] ^ (si ? u[k] : 0);
         }

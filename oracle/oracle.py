@@ -692,10 +692,12 @@ def gc_eval_eq(tables, gb_labels, ev_labels, decode, gate_base: int = 0) -> np.n
 
 
 def ot_extend(choices: np.ndarray, x0: np.ndarray, x1, delta: bytes, seeds: np.ndarray, s: bytes,
-              tweak_base: int = 0, transcript: bool = False):
+              tweak_base: int = 0, transcript: bool = False, prg: str = "chacha12"):
     """IKNP/ALSZ OT extension (see fhh_oracle.c): choices [m] 0/1, x0 / x1 [m][16] (x1 None:
     x1 = x0 ^ delta), seeds [128][2][16], s 16 bytes. Returns out [m][16] (and U [128][nblk][16],
-    Y0, Y1 [m][16] if transcript)."""
+    Y0, Y1 [m][16] if transcript). prg: the row PRG — "chacha12" (the GPU's since r06) or "aes"
+    (AES-128-CTR, the reference's ocelot AesRng form; bench.py's reference-form CPU baseline)."""
+    prg_id = {"aes": 0, "chacha12": 1}[prg]
     ch = np.packbits(np.asarray(choices, np.uint8) & 1, bitorder="little")
     m = len(choices)
     a0 = np.ascontiguousarray(x0, np.uint8)
@@ -711,8 +713,17 @@ def ot_extend(choices: np.ndarray, x0: np.ndarray, x1, delta: bytes, seeds: np.n
     lib().orc_ot_extend(ctypes.c_uint64(m), _p(np.ascontiguousarray(ch)), _p(a0), None if a1 is None else _p(a1),
                         _p(dl), _p(sd), _p(sv), ctypes.c_uint64(tweak_base), _p(out),
                         None if u is None else _p(u), None if y0 is None else _p(y0),
-                        None if y1 is None else _p(y1))
+                        None if y1 is None else _p(y1), ctypes.c_int(prg_id))
     return (out, u, y0, y1) if transcript else out
+
+
+def chacha_block(rounds: int, key: bytes, ctr: int, nonce: int = 0) -> bytes:
+    """The ChaCha block function of the OT row PRG (fhh_oracle.c orc_chacha_block): 64 bytes."""
+    out = np.zeros(64, np.uint8)
+    k = np.frombuffer(key, np.uint8).copy()
+    assert k.size == 32
+    lib().orc_chacha_block(ctypes.c_uint32(rounds), _p(k), ctypes.c_uint64(ctr), ctypes.c_uint64(nonce), _p(out))
+    return out.tobytes()
 
 
 def gc_set_ni(on: bool) -> None:

@@ -63,9 +63,8 @@ def test_ot_hash_rows_do_not_spill(tmp_path):
 
 
 def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
-    """k_gc_garble / k_gc_eval at every share-string width b = 1..8 and both OT expands (the receiver's
-    one-row form, the sender's row-pair form) stay
-    in registers at 4 waves per SIMD."""
+    """k_gc_garble / k_gc_eval at every share-string width b = 1..8, the garbled-table kernels and both
+    OT expands (ChaCha12 since r06) stay in registers at >= 4 waves per SIMD."""
     if not shutil.which("hipcc"):
         pytest.skip("hipcc not available")
     u = _resource_usage("fhh_gc.hip", tmp_path)
@@ -82,8 +81,9 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     names += [f"_ZN3fhh12k_gt_eval_tmILi{b}EEEvNS_6GcArgsE" for b in (1, 2)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
-    names += ["_ZN3fhh11k_ot_expandILb1EEEvNS_6OtArgsE", "_ZN3fhh21k_ot_send_expand_pairENS_6OtArgsE",
-              "_ZN3fhh13k_ot_rows_outENS_6OtArgsEi"]   # r05b: the labels OT's row transpose (mode 4)
+    # r06: the ChaCha12 row-PRG expands (no LDS), and the labels OT's row transpose (mode 4, r05b)
+    names += ["_ZN3fhh19k_ot_recv_expand_ccENS_6OtArgsE", "_ZN3fhh19k_ot_send_expand_ccENS_6OtArgsE",
+              "_ZN3fhh13k_ot_rows_outENS_6OtArgsEi"]
     for name in names:
         assert name in u, f"{name} not found"
         k = u[name]

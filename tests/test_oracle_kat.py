@@ -41,6 +41,42 @@ def test_against_openssl(oracle):
             assert oracle.aes0(blk, ni=True) == out.raw
 
 
+def test_chacha20_rfc8439_vector(oracle):
+    """The OT row PRG's block function (r06, fhh_oracle.c orc_chacha_block) at 20 rounds: RFC 8439
+    2.3.2's test vector (key 00..1f, nonce 00:00:00:09:00:00:00:4a:00:00:00:00, block counter 1) — in the
+    64-bit-counter layout: counter word 13 = nonce bytes 0-3, nonce words 14-15 = nonce bytes 4-11."""
+    key = bytes(range(32))
+    nonce = bytes.fromhex("000000090000004a00000000")
+    ctr = 1 | (int.from_bytes(nonce[:4], "little") << 32)
+    out = oracle.chacha_block(20, key, ctr, int.from_bytes(nonce[4:], "little"))
+    assert out.hex() == ("10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+                         "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+
+
+def test_chacha20_against_openssl(oracle):
+    """orc_chacha_block(20, ...) = OpenSSL's EVP_chacha20 keystream (IV = 32-bit counter LE || 96-bit
+    nonce) for random keys, counters past 2^32 and the key = seed || seed form the OT rows use."""
+    L = _openssl()
+    L.EVP_chacha20.restype = ctypes.c_void_p
+    L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+
+    def ossl(key, iv):
+        ctx = ctypes.c_void_p(L.EVP_CIPHER_CTX_new())
+        assert L.EVP_EncryptInit_ex(ctx, ctypes.c_void_p(L.EVP_chacha20()), None, key, iv) == 1
+        out, ol = ctypes.create_string_buffer(64), ctypes.c_int()
+        assert L.EVP_EncryptUpdate(ctx, out, ctypes.byref(ol), bytes(64), 64) == 1
+        L.EVP_CIPHER_CTX_free(ctx)
+        return out.raw[:ol.value]
+
+    rng = np.random.default_rng(8439)
+    for k in range(64):
+        seed = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        key = seed + seed if k % 2 else rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        ctr = int(rng.integers(0, 1 << 63)) if k % 3 else k
+        iv = (ctr & 0xFFFFFFFF).to_bytes(4, "little") + (ctr >> 32).to_bytes(4, "little") + bytes(8)
+        assert oracle.chacha_block(20, key, ctr, 0) == ossl(key, iv)
+
+
 def test_mmo_prg_kat(oracle):
     # SURVEY §8c (ii): expand of the zero seed; right block uses ctr + 1 in the upper u64 lane
     left, b = oracle.expand_dir(bytes(16), 0)

@@ -81,9 +81,11 @@ def cpu_baseline(args):
     threads, why = host_threads()
     sample_levels = list(range(1, L, 64))   # the protocol sample's levels (states kept for these)
     t0 = time.perf_counter()
+    log("cpu baseline: configs[0] crawl")
     res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=args.cpu_baseline_seconds,
                   keep_levels=sample_levels)
     dt = time.perf_counter() - t0
+    log(f"cpu baseline: configs[0] crawl {dt:.1f} s")
     done = len(res.n_children)
     protocol = cpu_protocol_baseline(args, O, res, n_cpu, threads, L)
     if protocol:   # the configs[0] keys of r05's line
@@ -218,12 +220,14 @@ def cpu_size_sample(args, O, n: int, threads: int, crawl_children: int, budget: 
     k0, k1 = O.gen_keys(left, right, roots, nthreads=threads)
     del left, right
     t_setup = time.perf_counter() - t0
+    log(f"cpu baseline: {n} clients, workload + keys {t_setup:.1f} s")
     t0 = time.perf_counter()
     # at most 6 (1M) / 9 (100k) levels: a level's States are ~36 B per (child, client) and server
     res = O.crawl(k0, k1, 0.001, mode="count", nthreads=threads, max_seconds=budget, keep_levels=[1, 2, 3],
                   levels=6 if n >= 1_000_000 else 9)
     dt = time.perf_counter() - t0
     done = len(res.n_children)
+    log(f"cpu baseline: {n} clients, {done} levels in {dt:.1f} s")
     per_child_client = res.aes_blocks / (sum(res.n_children) * n)
     full_blocks = per_child_client * crawl_children * n
     rate = res.aes_blocks / dt
@@ -778,12 +782,14 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
 
     run(levels=min(32, args.data_len))
     barrier()
+    log(f"protocol crawl ({gc}): warm-up done")
     c0.reset_stats()
     c1.reset_stats()
     t0 = time.perf_counter()
     res = run()
     barrier()
     wall = time.perf_counter() - t0
+    log(f"protocol crawl ({gc}): {wall:.2f} s, {len(res.final)} heavy hitters")
     s0 = c0.stats()
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
@@ -1054,6 +1060,7 @@ def main():
     for _ in range(args.warmup):
         res_ref = step(record=True)
     barrier()
+    log(f"[rank {rank}] warm-up done ({args.warmup} recorded crawls)")
     c0.reset_stats()
     c1.reset_stats()
     t0 = time.perf_counter()
@@ -1061,6 +1068,7 @@ def main():
         res = step()
     barrier()
     elapsed = time.perf_counter() - t0
+    log(f"[rank {rank}] timed: {args.steps} crawls in {elapsed:.2f} s")
     s0, s1 = c0.stats(), c1.stats()
     blocks = s0["aes_blocks"] + s1["aes_blocks"]
     ref_evals = s0["ref_evals"] + s1["ref_evals"]

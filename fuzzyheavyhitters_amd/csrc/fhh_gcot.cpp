@@ -190,6 +190,18 @@ int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
     return FHH_OK;
 }
 
+// the transcript's U [128][ceil(m / 128)][16] (row form) from the device's tile-major U (r06, fhh_ot.hip ot_tmaj:
+// 128-OT block c of row i at uint4 (c / 4) 512 + 4 i + c % 4)
+int u_transcript(fhh_ctx* ctx, const OtOut& tr, uint64_t m, uint8_t* u_out) {
+    const uint64_t nb = (m + 127) / 128;
+    std::vector<uint8_t> h(tr.nblk * 128 * 16);
+    HIP_TRY(ctx, hipMemcpy(h.data(), tr.U, h.size(), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < 128; i++)
+        for (uint64_t c = 0; c < nb; c++)
+            std::memcpy(u_out + (i * nb + c) * 16, h.data() + ((c / 4) * 512 + 4 * i + c % 4) * 16, 16);
+    return FHH_OK;
+}
+
 // row-PRG blocks one batch of m OTs takes from its base-OT session (a multiple of 256, the expand
 // kernels' shared-rounds alignment)
 uint64_t ot_session_blocks(uint64_t m) { return (ot_padded(m) / 128 + 255) / 256 * 256; }
@@ -356,9 +368,9 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
     HIP_TRY(ctx, hipMemcpy(out, dout.p, m * 16, hipMemcpyDeviceToHost));
     if (y0_out) HIP_TRY(ctx, hipMemcpy(y0_out, tr.Y0, m * 16, hipMemcpyDeviceToHost));
     if (y1_out) HIP_TRY(ctx, hipMemcpy(y1_out, tr.Y1, m * 16, hipMemcpyDeviceToHost));
-    if (u_out) {   // rows [128][ceil(m / 128)] of the padded [128][mp / 128] matrix
-        const uint64_t nb = (m + 127) / 128;
-        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
+    if (u_out) {   // rows [128][ceil(m / 128)] of the padded tile-major matrix
+        rc = u_transcript(ctx, tr, m, u_out);
+        if (rc) return rc;
     }
     return FHH_OK;
 }
@@ -411,8 +423,8 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
     if (sender_out) HIP_TRY(ctx, hipMemcpy(sender_out, dsx.p, m * per, hipMemcpyDeviceToHost));
     if (y_out && mode != FHH_COT_RAW) HIP_TRY(ctx, hipMemcpy(y_out, tr.Y0, m * per, hipMemcpyDeviceToHost));
     if (u_out) {
-        const uint64_t nb = (m + 127) / 128;
-        HIP_TRY(ctx, hipMemcpy2D(u_out, nb * 16, tr.U, tr.nblk * 16, nb * 16, 128, hipMemcpyDeviceToHost));
+        rc = u_transcript(ctx, tr, m, u_out);
+        if (rc) return rc;
     }
     return FHH_OK;
 }

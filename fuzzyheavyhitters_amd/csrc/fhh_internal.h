@@ -371,7 +371,7 @@ struct OtArgs {
     const uint32_t* rk;          // [3][128][44]: receiver k_i^0, k_i^1, sender k_i^{s_i}
     uint32_t s[4];               // sender's base choice bits
     const uint32_t* choices;     // [mp / 32] receiver's choice bits (0 past m)
-    uint4 *T, *U, *Q;            // U [128][mp / 128] (row form, the wire); T, Q tile-major (fhh_ot.hip ot_tmaj)
+    uint4 *T, *U, *Q;            // tile-major (fhh_ot.hip ot_tmaj): T, Q, and since r06 U (the wire) too
     const uint4 *x0, *x1;        // mode 0: [m]; x1 == nullptr: x1 = x0 ^ delta (correlated messages)
     uint32_t delta[4];           // modes 0 (x1 == nullptr) and 1
     uint4 *Y0, *Y1, *out;        // mode 0: Y0, Y1 [m]; modes 1-3: y in Y0 (mode 2: 8 B per OT); out [m]

@@ -49,7 +49,8 @@ __device__ __forceinline__ uint64_t ot_active(const OtArgs& a) {
 // T and Q (internal to the parties, never on the wire) are stored tile-major: a hash's 512-OT tile
 // (4 blocks x 128 rows = 8 KiB) is one contiguous run, row r at words 16 r .. 16 r + 15, so its 32
 // row loads per lane read whole 128 B lines (rows r, r + 1) instead of 64 B from each of 128 rows
-// mp / 8 bytes apart. U, the receiver's message to the sender, stays in row form [128][mp / 128].
+// mp / 8 bytes apart. U, the receiver's message to the sender, was in row form [128][mp / 128] until r06;
+// the ChaCha expands write (and read) it tile-major as well (the transcript exports convert it back).
 // Same-box A/B at configs[1] (profiles/r04/ab_ot_tmaj/): receive hash -11 %, send hash -3 %, the
 // sender's expand +12 % (one row per wave: its Q stores are 64 B runs), all kernels -0.9 / -1.6 %;
 // T alone tile-major -0.2 %; 8-block (128 B per row) runs: hashes as before.
@@ -127,20 +128,64 @@ __device__ __forceinline__ void ld_seed(const uint32_t* rk, uint32_t row, uint32
 }
 
 constexpr int kOtCcThreads = 256;
+constexpr int kOtCcWaves = kOtCcThreads / 64;
+constexpr int kOtCcRowWords = 20;   // LDS words per staged 64-B row (80 B: 16 lanes of a b128 access hit distinct banks)
+
+// A wave's 64 rows x 64 B of one tile — rows 64 h .. 64 h + 63 of tile j, one contiguous 4 KiB run of a
+// tile-major matrix (ot_tmaj) — moved through LDS so that every store instruction writes 1 KiB of whole
+// 128-B lines: lane l stages its row at 80 l, then store k writes bytes 1024 k + 16 l (row 16 k + l / 4,
+// chunk l % 4). Lane-row stores (16 B into each of 64 rows per instruction) left partial lines in the L2
+// and cost 2.2-2.5x the algorithmic bytes in HBM writes (WRITE_SIZE, profiles/r06/ot_pmc/).
+typedef uint32_t cc_v4 __attribute__((ext_vector_type(4)));   // for the nontemporal builtins
+
+__device__ __forceinline__ void cc_store_rows(uint32_t* st, uint32_t lane, const uint32_t (&v)[16], uint4* run) {
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+        *reinterpret_cast<uint4*>(st + kOtCcRowWords * lane + 4 * w) = make_uint4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t r = 16 * k + (lane >> 2), w = lane & 3;
+        __builtin_nontemporal_store(*reinterpret_cast<const cc_v4*>(st + kOtCcRowWords * r + 4 * w),
+                                    reinterpret_cast<cc_v4*>(run + 64 * k + lane));
+    }
+    __builtin_amdgcn_wave_barrier();   // the reads precede the next item's stage writes
+}
+
+// the inverse: the 4 KiB run read by whole lines (load k = bytes 1024 k + 16 l) and dealt to the lanes by row
+__device__ __forceinline__ void cc_load_rows(uint32_t* st, uint32_t lane, const uint4* run, uint32_t (&v)[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t r = 16 * k + (lane >> 2), w = lane & 3;
+        *reinterpret_cast<cc_v4*>(st + kOtCcRowWords * r + 4 * w) =
+            __builtin_nontemporal_load(reinterpret_cast<const cc_v4*>(run + 64 * k + lane));
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint4 x = *reinterpret_cast<const uint4*>(st + kOtCcRowWords * lane + 4 * w);
+        v[4 * w] = x.x;
+        v[4 * w + 1] = x.y;
+        v[4 * w + 2] = x.z;
+        v[4 * w + 3] = x.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
 
 // The receiver: work item = (512-OT tile j, row half h); lane l = row i = 64 h + l computes G(k_i^0) and
-// G(k_i^1) for tile j (2 ChaCha blocks in lockstep), stores T's row i of the tile (64 B, tile-major) and
-// U = T ^ G(k_i^1) ^ r (row form [128][mp / 128]: 64 B per lane). The tile's choice words r are the same
-// for every lane (a broadcast load); 128-OT blocks past the active OTs get no choice bits.
+// G(k_i^1) for tile j (2 ChaCha blocks in lockstep); T = G(k_i^0) and U = T ^ G(k_i^1) ^ r are both stored
+// tile-major (r06: U, the message to the sender, in the same layout as T — row i's 64 B of tile j at
+// ot_tmaj(i, 4 j)), each as the wave's contiguous 4 KiB run. The tile's choice words r are the same for
+// every lane (a broadcast load); 128-OT blocks past the active OTs get no choice bits.
 __global__ __launch_bounds__(kOtCcThreads) void k_ot_recv_expand_cc(OtArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nblk = a.mp / 128;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kOtCcWaves][64 * kOtCcRowWords];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
     const uint64_t items = 2 * ((nblk_act + 3) / 4);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtCcThreads / 64);
-    for (uint64_t it = (uint64_t)blockIdx.x * (kOtCcThreads / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtCcWaves;
+    for (uint64_t it = (uint64_t)blockIdx.x * kOtCcWaves + wv; it < items; it += nwaves) {
         const uint64_t j = it >> 1;
-        const uint32_t i = 64 * (uint32_t)(it & 1) + lane;
+        const uint32_t h = (uint32_t)(it & 1), i = 64 * h + lane;
         uint32_t k[2][4];
         ld_seed(a.rk, i, k[0]);
         ld_seed(a.rk, 128 + i, k[1]);
@@ -152,26 +197,29 @@ __global__ __launch_bounds__(kOtCcThreads) void k_ot_recv_expand_cc(OtArgs a) {
         for (int w = 0; w < 4; w++) {
             const uint64_t c = 4 * j + w;
             const uint4 r = c < nblk_act ? ch[c] : make_uint4(0, 0, 0, 0);
-            a.T[ot_tmaj(i, c)] = make_uint4(g[0][4 * w], g[0][4 * w + 1], g[0][4 * w + 2], g[0][4 * w + 3]);
-            a.U[(uint64_t)i * nblk + c] = make_uint4(g[0][4 * w] ^ g[1][4 * w] ^ r.x, g[0][4 * w + 1] ^ g[1][4 * w + 1] ^ r.y,
-                                                     g[0][4 * w + 2] ^ g[1][4 * w + 2] ^ r.z,
-                                                     g[0][4 * w + 3] ^ g[1][4 * w + 3] ^ r.w);
+            g[1][4 * w] ^= g[0][4 * w] ^ r.x;
+            g[1][4 * w + 1] ^= g[0][4 * w + 1] ^ r.y;
+            g[1][4 * w + 2] ^= g[0][4 * w + 2] ^ r.z;
+            g[1][4 * w + 3] ^= g[0][4 * w + 3] ^ r.w;
         }
+        const uint64_t run = ot_tmaj(64 * h, 4 * j);   // the wave's 4 KiB of tile j
+        cc_store_rows(stage[wv], lane, g[0], a.T + run);
+        cc_store_rows(stage[wv], lane, g[1], a.U + run);
     }
 }
 
 // The sender: work item = (2 tiles j, j + 1, row half h); lane row i computes G(k_i^{s_i}) for both tiles
-// (2 ChaCha blocks in lockstep) and stores Q = G ^ s_i U tile-major.
+// (2 ChaCha blocks in lockstep) and stores Q = G ^ s_i U tile-major (U read, Q written as whole-line runs).
 __global__ __launch_bounds__(kOtCcThreads) void k_ot_send_expand_cc(OtArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nblk = a.mp / 128;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kOtCcWaves][64 * kOtCcRowWords];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
     const uint64_t tiles = (nblk_act + 3) / 4;
     const uint64_t items = 2 * ((tiles + 1) / 2);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (kOtCcThreads / 64);
-    for (uint64_t it = (uint64_t)blockIdx.x * (kOtCcThreads / 64) + (threadIdx.x >> 6); it < items; it += nwaves) {
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtCcWaves;
+    for (uint64_t it = (uint64_t)blockIdx.x * kOtCcWaves + wv; it < items; it += nwaves) {
         const uint64_t j0 = 2 * (it >> 1);
-        const uint32_t i = 64 * (uint32_t)(it & 1) + lane;
+        const uint32_t h = (uint32_t)(it & 1), i = 64 * h + lane;
         const uint32_t si = (a.s[i >> 5] >> (i & 31)) & 1u;
         uint32_t k[2][4];
         ld_seed(a.rk, 256 + i, k[0]);
@@ -183,14 +231,12 @@ __global__ __launch_bounds__(kOtCcThreads) void k_ot_send_expand_cc(OtArgs a) {
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             if (j0 + q >= tiles) break;   // wave-uniform
+            const uint64_t run = ot_tmaj(64 * h, 4 * (j0 + q));
+            uint32_t u[16];
+            cc_load_rows(stage[wv], lane, a.U + run, u);
 #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint64_t c = 4 * (j0 + q) + w;
-                uint4 u = make_uint4(0, 0, 0, 0);
-                if (si) u = a.U[(uint64_t)i * nblk + c];
-                a.Q[ot_tmaj(i, c)] = make_uint4(g[q][4 * w] ^ u.x, g[q][4 * w + 1] ^ u.y, g[q][4 * w + 2] ^ u.z,
-                                                g[q][4 * w + 3] ^ u.w);
-            }
+            for (int w = 0; w < 16; w++) g[q][w] ^= si ? u[w] : 0u;
+            cc_store_rows(stage[wv], lane, g[q], a.Q + run);
         }
     }
 }
@@ -596,7 +642,7 @@ static int device_cus() {
 }
 
 
-// the ChaCha expands: 256-thread workgroups (no LDS, ~70 VGPRs), 8 per CU, waves stride over the items
+// the ChaCha expands: 256-thread workgroups (20 KiB of LDS staging, ~70 VGPRs), 8 per CU, waves stride over the items
 static int ot_cc_grid(uint64_t items) {
     const uint64_t wpb = kOtCcThreads / 64, need = (items + wpb - 1) / wpb, cap = (uint64_t)device_cus() * 8;
     return (int)(need < cap ? (need ? need : 1) : cap);

@@ -714,50 +714,58 @@ def golden_sig(args, n_total):
             "final": sorted(((tuple(int(b) for b in p),), int(v)) for p, v in zip(paths, g["values"]))}
 
 
-def protocol_aes_blocks(level_children, n: int, d: int, circuit: bool = False):
-    """Executed AES blocks of one real-protocol crawl on this rank (n clients), by phase, from the kernels'
-    work decomposition (fhh_host.cpp level loop; fhh_gc.hip, fhh_ot.hip): FE levels with b = 2d <= 2 run the
-    labels OT's expands (receiver 2, sender 1 AES per OT, OT index over 512-client tiles) and the tile-major
-    garbled table (2^b rows per test garbled, 1 evaluated, padding tests included); b = 4 the row-major table
-    (64-client words) after k_ot_rows_out; the FieldElm level the half-gates circuit (TCCR: 8 AES per AND
-    gate garbled, 4 evaluated) + the share C-OT (2 OTs per test: expands 2 + 1, hashes 2 + 1 per OT) and the
-    labels OT's two row transposes (32 B of HBM per OT and party). circuit: the half-gates circuit + the
-    output-label share (2 AES garbled, 1 evaluated per test) at the FE levels too (gc "ot-circuit")."""
+CHACHA12_OPS_PER_BLOCK = 608   # 6 double rounds x 8 quarter rounds x 12 add/xor/rotate + 32 (state, feed-forward)
+
+
+def protocol_work(level_children, n: int, d: int, circuit: bool = False):
+    """Executed work of one real-protocol crawl on this rank (n clients), by phase, from the kernels' work
+    decomposition (fhh_host.cpp level loop; fhh_gc.hip, fhh_ot.hip). Returns (aes, chacha, transpose_bytes):
+    AES blocks per phase — FE levels with b = 2d <= 2 run the tile-major garbled table (2^b rows per test
+    garbled, 1 evaluated, padding tests of the 512-client tiles included), b = 4 the row-major table (64-client
+    words) after k_ot_rows_out, the FieldElm level the half-gates circuit (TCCR: 8 AES per AND gate garbled, 4
+    evaluated) + the share C-OT's hashes (2 OTs per test: 2 + 1 per OT); circuit = the half-gates circuit + the
+    output-label share (2 AES garbled, 1 evaluated per test) at the FE levels too — and ChaCha12 blocks of the
+    labels / share OTs' row PRG (since r06: 64 B per row and 512-OT tile; receiver 2, sender 1 per row), and the
+    bytes of the remaining row transposes (32 B per OT and party)."""
     b = 2 * d
     npad64 = (n + 63) // 64 * 64
     npad_tm = (n + 511) // 512 * 512
-    ph = {"ot_recv_expand": 0, "ot_send_expand": 0, "table_garble": 0, "table_eval": 0, "circuit_garble": 0,
-          "circuit_eval": 0, "share_ot": 0}
+    aes = {"table_garble": 0, "table_eval": 0, "circuit_garble": 0, "circuit_eval": 0, "share_ot_hash": 0}
+    cc = {"ot_recv_expand": 0, "ot_send_expand": 0}
     transpose_bytes = 0
     L = len(level_children)
+
+    def expands(m):   # m OTs: 128 rows x ceil(m / 512) tiles, 2 blocks (receiver) + 1 (sender) each
+        tiles = (m + 511) // 512
+        cc["ot_recv_expand"] += 2 * 128 * tiles
+        cc["ot_send_expand"] += 128 * tiles
+
     for lv, C in enumerate(int(x) for x in level_children):
         if lv + 1 < L and circuit:
             m1 = C * b * npad64
-            ph["ot_recv_expand"] += 2 * m1
-            ph["ot_send_expand"] += m1
-            ph["circuit_garble"] += (8 * (b - 1) + 2) * C * n
-            ph["circuit_eval"] += (4 * (b - 1) + 1) * C * n
+            expands(m1)
+            aes["circuit_garble"] += (8 * (b - 1) + 2) * C * n
+            aes["circuit_eval"] += (4 * (b - 1) + 1) * C * n
             transpose_bytes += 2 * 32 * m1
         elif lv + 1 < L:
             tm = b <= 2
             npad = npad_tm if tm else npad64
             m1 = C * b * npad
-            ph["ot_recv_expand"] += 2 * m1
-            ph["ot_send_expand"] += m1
-            ph["table_garble"] += (1 << b) * C * (npad if tm else n)
-            ph["table_eval"] += C * (npad if tm else n)
+            expands(m1)
+            aes["table_garble"] += (1 << b) * C * (npad if tm else n)
+            aes["table_eval"] += C * (npad if tm else n)
             if not tm:
                 transpose_bytes += 2 * 32 * m1
         else:
             m1 = C * b * npad64
-            ph["ot_recv_expand"] += 2 * m1
-            ph["ot_send_expand"] += m1
-            ph["circuit_garble"] += 8 * (b - 1) * C * n
-            ph["circuit_eval"] += 4 * (b - 1) * C * n
+            expands(m1)
+            aes["circuit_garble"] += 8 * (b - 1) * C * n
+            aes["circuit_eval"] += 4 * (b - 1) * C * n
             m2 = 2 * C * n
-            ph["share_ot"] += 2 * m2 + m2 + 2 * m2 + m2
+            expands(m2)
+            aes["share_ot_hash"] += 2 * m2 + m2
             transpose_bytes += 2 * 32 * m1
-    return ph, transpose_bytes
+    return aes, cc, transpose_bytes
 
 
 def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None):
@@ -797,22 +805,27 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
         wall = float(t.item())
     hh = len(res.final)
     sig = crawl_sig(res)
-    ph, tr_bytes = protocol_aes_blocks(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit")
-    total = sum(ph.values())
+    aes, cc, tr_bytes = protocol_work(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit")
+    n_aes, n_cc = sum(aes.values()), sum(cc.values())
     gpu_s = s0["gcot_ms"] / 1e3
-    rate = total / gpu_s if gpu_s > 0 else 0.0
+    ops = n_aes * VALU_OPS_PER_BLOCK + n_cc * CHACHA12_OPS_PER_BLOCK
+    tops = ops / gpu_s / 1e12 if gpu_s > 0 else 0.0
     roof = {
-        "executed_aes_blocks": total,
-        "executed_aes_blocks_by_phase": ph,
-        "aes_blocks_note": ("executed blocks on this rank from the kernels' work decomposition "
-                            "(bench.protocol_aes_blocks): padding tests of the 512-client tiles included"),
+        "executed_aes_blocks": n_aes,
+        "executed_aes_blocks_by_phase": aes,
+        "executed_chacha12_blocks": n_cc,
+        "executed_chacha12_blocks_by_phase": cc,
+        "work_note": ("executed on this rank, from the kernels' work decomposition (bench.protocol_work): padding "
+                      "tests of the 512-client tiles included; the OT row PRG is ChaCha12 since r06 (64-B blocks)"),
         "gcot_gpu_s": gpu_s,
-        "blocks_per_s": rate,
-        "valu_tops": rate * VALU_OPS_PER_BLOCK / 1e12,
-        "frac": rate * VALU_OPS_PER_BLOCK / 1e12 / VALU_PEAK_TOPS,
-        "frac_basis": (f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d) x blocks / the GC + OT steps' GPU "
-                       f"time (HIP events) over {VALU_PEAK_TOPS} T ops/s"),
-        "vs_k_expand_in_kernel": rate / expand_rate if expand_rate else None,
+        "aes_blocks_per_s_if_alone": n_aes / gpu_s if gpu_s > 0 else 0.0,
+        "valu_tops": tops,
+        "frac": tops / VALU_PEAK_TOPS,
+        "frac_basis": (f"{VALU_OPS_PER_BLOCK} int32 ops per AES block (SURVEY 8d) + {CHACHA12_OPS_PER_BLOCK} per "
+                       f"ChaCha12 block (add/xor/rotate) / the GC + OT steps' GPU time (HIP events) over "
+                       f"{VALU_PEAK_TOPS} T ops/s"),
+        "vs_k_expand_in_kernel": (ops / VALU_OPS_PER_BLOCK / gpu_s) / expand_rate if expand_rate and gpu_s > 0 else None,
+        "vs_k_expand_note": "the steps' work in AES-block equivalents (ops / 400) per s over k_expand's in-kernel blocks/s",
         "transpose_hbm_bytes": tr_bytes,
         "transpose_note": ("k_ot_rows_out's bytes (32 B per OT and party): since r06 only the FieldElm level's "
                            "circuit (and d = 2's table) transposes; d = 1's FE levels read Q / T tile-major"),
@@ -835,14 +848,15 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
         "protocol": ("the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); every "
                      "level: half-gates GC (TCCR; the garbler's string and mask folded in); FE levels: the share "
                      "from the circuit's output labels (cr_hash of W_0, W_0 ^ Delta); the FieldElm level: ALSZ "
-                     "correlated OT for the share (21 AES blocks per d=1 FE-level test: garble 8 + 2, evaluate "
-                     "4 + 1, labels OT expands 2 x 3)") if gc == "ot-circuit" else
+                     "correlated OT for the share (15 AES blocks per d=1 FE-level test: garble 8 + 2, evaluate "
+                     "4 + 1; the labels OT's row PRG ChaCha12, 3 blocks of 64 B per row and 512 OTs)") if gc == "ot-circuit" else
                     "the evaluator's labels as the IKNP correlation (Delta = the labels OT's s, no reply); FE "
                     "levels: equality + share as one garbled table per test (Yao's garbled gate with "
                     "point-and-permute over the 2d input labels, rows keyed by cr_hash, 8 B per row; the "
                     "garbler's string and mask folded in); the FieldElm level: half-gates GC (TCCR) + ALSZ "
-                    "correlated OT for the share (11 AES blocks per d=1 FE-level test: table 4 + 1, labels OT "
-                    "expands 2 x 3)",
+                    "correlated OT for the share (5 AES blocks per d=1 FE-level test: table 4 + 1; the labels OT's "
+                    "row PRG ChaCha12 (r06), 3 blocks of 64 B per row and 512 OTs; the table kernels read the OT's "
+                    "tile-major matrices, no row transposes)",
         "gcot_gpu_ms": s0["gcot_ms"], "gcot_levels_timed": s0["gcot_timed"],
         "expand_gpu_ms": s0["expand_ms"],
         "allreduce_ms": s0["allreduce_ms"] if comm is not None else None,

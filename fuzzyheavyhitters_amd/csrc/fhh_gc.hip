@@ -646,6 +646,20 @@ __device__ __forceinline__ void gt_tile_round(uint32_t* st, uint32_t (&x)[32], u
     for (int i = 0; i < 24; i++) x[i] = x[i + 8];
 }
 
+// the wave's sum of lo / hi 32-bit limbs of its live values, added to node_partials[child][k0], [k0 + 1]
+__device__ __forceinline__ void gt_add_partials(uint64_t* partials, uint64_t child, int k0, uint64_t lo, uint64_t hi,
+                                                uint32_t lane) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo += __shfl_xor(lo, off, 64);
+        hi += __shfl_xor(hi, off, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(partials + child * 4 + k0), (unsigned long long)lo);
+        atomicAdd(reinterpret_cast<unsigned long long*>(partials + child * 4 + k0 + 1), (unsigned long long)hi);
+    }
+}
+
 // the lane's test of round r, u within its 512-test tile
 __device__ __forceinline__ uint32_t gt_tile_test(uint32_t lane, int r, int u) {
     return 256 * u + 32 * (lane >> 3) + 8 * r + (lane & 7);
@@ -785,6 +799,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
         const uint32_t iw = (uint32_t)(wt - g * Npt);
         uint32_t S[8][4], col;
         gt_tile_keys<B, true>(a, g, iw, Npt, stage[wv], lane, Dk, S, col);
+        uint64_t acc_lo = 0, acc_hi = 0;   // node_partials: this lane's live node values' limbs
 #pragma unroll 1
         for (int j = 0; j < 8; j++) {   // test j = (r, u) = (j >> 1, j & 1); S and col rotate by one test
             const uint32_t i = 512 * iw + gt_tile_test(lane, j >> 1, j & 1);
@@ -817,7 +832,13 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
                     const uint64_t v = o_r == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
                     p0 = v;
                     p1 = a.mask ? fe_inc(v) : fe_dec(v);
-                    if (live) a.sh_gb[t] = a.mask ? fe_inc(v) : v;   // r1 = v + mask
+                    const uint64_t r1 = a.mask ? fe_inc(v) : v;   // r1 = v + mask
+                    if (live && a.node_partials) {
+                        acc_lo += r1 & 0xFFFFFFFFull;
+                        acc_hi += r1 >> 32;
+                    } else if (live) {
+                        a.sh_gb[t] = r1;
+                    }
                 } else if (live) {
                     a.gt_msgs[(uint64_t)(q - 1) * n + t] = hl ^ (o_r ? p1 : p0);
                 }
@@ -828,6 +849,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
                 for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 1][c];
             col >>= 4;
         }
+        if (a.node_partials) gt_add_partials(a.node_partials, a.g_off + g, 0, acc_lo, acc_hi, lane);
     }
 }
 
@@ -851,6 +873,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
         uint32_t S[8][4], col;
         const uint32_t nod[B][4] = {};
         gt_tile_keys<B, false>(a, g, iw, Npt, stage[wv], lane, nod, S, col);
+        uint64_t acc_lo = 0, acc_hi = 0;
 #pragma unroll 1
         for (int r = 0; r < 4; r++) {   // round r's 2 tests: 2 AES blocks in lockstep (4 spilled 6 VGPRs)
             uint32_t h[2][4];
@@ -873,8 +896,14 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 const uint64_t t = g * a.N + i;
                 const uint32_t row = (col >> (4 * u)) & 0xFu;
                 const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
-                a.sh_ev[t] = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
-                                 : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
+                const uint64_t val = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
+                                         : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
+                if (a.node_partials) {
+                    acc_lo += val & 0xFFFFFFFFull;
+                    acc_hi += val >> 32;
+                } else {
+                    a.sh_ev[t] = val;
+                }
             }
 #pragma unroll
             for (int jj = 0; jj < 6; jj++)
@@ -882,6 +911,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 2][c];
             col >>= 8;
         }
+        if (a.node_partials) gt_add_partials(a.node_partials, a.g_off + g, 2, acc_lo, acc_hi, lane);
     }
 }
 
@@ -909,7 +939,8 @@ static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
 
 static hipError_t gt_dispatch(const GcArgs& a, bool garble, hipStream_t stream) {
     if (a.G * a.N == 0) return hipSuccess;
-    if (!a.gt_msgs || !(garble ? a.sh_gb : a.sh_ev) || !a.ev_labels) return hipErrorInvalidValue;
+    if (!a.gt_msgs || (!(garble ? a.sh_gb : a.sh_ev) && !(a.lab_tm && a.node_partials)) || !a.ev_labels)
+        return hipErrorInvalidValue;
     // r06 tile-major labels: 512-test tiles per group, b <= 2 (gt_tm_bits)
     if (a.lab_tm && (a.nw % 8 != 0 || a.bits > (uint32_t)kGtTmMaxBits)) return hipErrorInvalidValue;
     switch (a.bits) {

@@ -1330,14 +1330,17 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     // r05d: tests of <= kGtMaxBits bits (d <= 2) take the share from ONE garbled table per
                     // test (k_gt_garble / k_gt_eval: 2^bits + 1 AES instead of the half-gates chain's)
                     if (ltable) {
-                        for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
+                        // r06 (tile-major table): the kernels add the node values per child into the level's
+                        // partials themselves (no stored values, no k_child_sums_fe pass)
+                        if (!ltm) for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
                         HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
                         g.gt_msgs = B.gc_msgs.as<uint64_t>();
-                        g.sh_gb = B.gc_val[0].as<uint64_t>();
+                        g.node_partials = ltm ? part : nullptr;
+                        g.sh_gb = ltm ? nullptr : B.gc_val[0].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_garble(g, c0->stream));
                         g.ev_labels = ltm ? c0->ot_buf[0].as<uint4>() : B.gc_evact.as<uint4>();
                         g.sh_gb = nullptr;
-                        g.sh_ev = B.gc_val[1].as<uint64_t>();
+                        g.sh_ev = ltm ? nullptr : B.gc_val[1].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_eval(g, c0->stream));
                     } else if (lshare) {
                         for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
@@ -1397,7 +1400,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     }
                     // the chunk's children's sums (FE: atomics into the partials k_prune zeroed;
                     // FE255: one store per child)
-                    if (pmode == 1) HIP_TRY(c0, launch_child_sums_fe(ca, part, c0->stream, false));
+                    if (pmode == 1 && !ltm) HIP_TRY(c0, launch_child_sums_fe(ca, part, c0->stream, false));
                     else HIP_TRY(c0, launch_child_sums_fe255(ca, part, c0->stream));
                 }
                 if (timed) HIP_TRY(c0, timing_end(c0, gc_slot, kGcotTag));

@@ -258,6 +258,10 @@ struct GcArgs {
     // fhh_ot.hip ot_tmaj) instead of one row-major label per OT (k_ot_rows_out); needs nw % 8 == 0 (the OT
     // index (g bits + k) 64 nw + i puts a test's labels at one position of 512-OT tiles)
     uint32_t lab_tm;
+    // r06 (lab_tm): non-null = the table kernels add their node values' 32-bit limbs per child into
+    // node_partials [C][4] u64 (k_child_sums_fe's layout: garbler lo, hi; evaluator lo, hi) by one wave sum
+    // and atomic per 512-test tile, instead of storing them for k_child_sums_fe (sh_gb / sh_ev may be null)
+    uint64_t* node_partials;
 };
 constexpr int kGtMaxBits = 4;   // 16 rows (d = 2); wider tests keep the half-gates chain
 constexpr int kGtTmMaxBits = 2;   // r06: the table kernels read the tile-major labels (lab_tm) for b <= 2 (d = 1)

@@ -70,7 +70,20 @@ __device__ __forceinline__ uint64_t ot_tmaj(uint32_t i, uint64_t c) {
 // 0..3 of the row's key schedule in rk (the schedules the AES form used; unchanged on the host).
 constexpr int kOtChachaRounds = 12;
 
-__device__ __forceinline__ uint32_t cc_rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+#ifndef FHH_CC_PERM
+#define FHH_CC_PERM 0   // A/B knob: 1 = the byte rotations (16, 8) as v_perm_b32
+#endif
+#ifndef FHH_CC_TPI
+#define FHH_CC_TPI 2    // tiles per receiver work item (2 TPI ChaCha blocks per lane in lockstep; 1: +4 %, profiles/r06/ab_ot_cc/)
+#endif
+#ifndef FHH_CC_THREADS
+#define FHH_CC_THREADS 256
+#endif
+__device__ __forceinline__ uint32_t cc_rotl(uint32_t x, int n) {
+    if (FHH_CC_PERM && n == 16) return __builtin_amdgcn_perm(x, x, 0x01000302u);
+    if (FHH_CC_PERM && n == 8) return __builtin_amdgcn_perm(x, x, 0x02010003u);
+    return __builtin_amdgcn_alignbit(x, x, 32 - n);
+}
 
 __device__ __forceinline__ void cc_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
     a += b; d ^= a; d = cc_rotl(d, 16);
@@ -127,7 +140,7 @@ __device__ __forceinline__ void ld_seed(const uint32_t* rk, uint32_t row, uint32
     k[3] = v.w;
 }
 
-constexpr int kOtCcThreads = 256;
+constexpr int kOtCcThreads = FHH_CC_THREADS;
 constexpr int kOtCcWaves = kOtCcThreads / 64;
 constexpr int kOtCcRowWords = 20;   // LDS words per staged 64-B row (80 B: 16 lanes of a b128 access hit distinct banks)
 
@@ -178,33 +191,49 @@ __device__ __forceinline__ void cc_load_rows(uint32_t* st, uint32_t lane, const 
 // ot_tmaj(i, 4 j)), each as the wave's contiguous 4 KiB run. The tile's choice words r are the same for
 // every lane (a broadcast load); 128-OT blocks past the active OTs get no choice bits.
 __global__ __launch_bounds__(kOtCcThreads) void k_ot_recv_expand_cc(OtArgs a) {
+    constexpr int TPI = FHH_CC_TPI;
     __shared__ __attribute__((aligned(16))) uint32_t stage[kOtCcWaves][64 * kOtCcRowWords];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t nblk_act = (ot_active(a) + 127) / 128;
-    const uint64_t items = 2 * ((nblk_act + 3) / 4);
+    const uint64_t tiles = (nblk_act + 3) / 4;
+    const uint64_t items = 2 * ((tiles + TPI - 1) / TPI);
     const uint64_t nwaves = (uint64_t)gridDim.x * kOtCcWaves;
     for (uint64_t it = (uint64_t)blockIdx.x * kOtCcWaves + wv; it < items; it += nwaves) {
-        const uint64_t j = it >> 1;
+        const uint64_t j0 = TPI * (it >> 1);
         const uint32_t h = (uint32_t)(it & 1), i = 64 * h + lane;
-        uint32_t k[2][4];
+        uint32_t k[2 * TPI][4];
         ld_seed(a.rk, i, k[0]);
         ld_seed(a.rk, 128 + i, k[1]);
-        const uint64_t ctr[2] = {a.ctr_off / 4 + j, a.ctr_off / 4 + j};
-        uint32_t g[2][16];
-        cc_blocks<2>(k, ctr, g);
+        uint64_t ctr[2 * TPI];
+#pragma unroll
+        for (int q = 0; q < TPI; q++) {
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                k[2 * q][w] = k[0][w];
+                k[2 * q + 1][w] = k[1][w];
+            }
+            ctr[2 * q] = ctr[2 * q + 1] = a.ctr_off / 4 + j0 + q;
+        }
+        uint32_t g[2 * TPI][16];
+        cc_blocks<2 * TPI>(k, ctr, g);
         const uint4* ch = reinterpret_cast<const uint4*>(a.choices);
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint64_t c = 4 * j + w;
-            const uint4 r = c < nblk_act ? ch[c] : make_uint4(0, 0, 0, 0);
-            g[1][4 * w] ^= g[0][4 * w] ^ r.x;
-            g[1][4 * w + 1] ^= g[0][4 * w + 1] ^ r.y;
-            g[1][4 * w + 2] ^= g[0][4 * w + 2] ^ r.z;
-            g[1][4 * w + 3] ^= g[0][4 * w + 3] ^ r.w;
+        for (int q = 0; q < TPI; q++) {
+            const uint64_t j = j0 + q;
+            if (j >= tiles) break;   // wave-uniform
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint64_t c = 4 * j + w;
+                const uint4 r = c < nblk_act ? ch[c] : make_uint4(0, 0, 0, 0);
+                g[2 * q + 1][4 * w] ^= g[2 * q][4 * w] ^ r.x;
+                g[2 * q + 1][4 * w + 1] ^= g[2 * q][4 * w + 1] ^ r.y;
+                g[2 * q + 1][4 * w + 2] ^= g[2 * q][4 * w + 2] ^ r.z;
+                g[2 * q + 1][4 * w + 3] ^= g[2 * q][4 * w + 3] ^ r.w;
+            }
+            const uint64_t run = ot_tmaj(64 * h, 4 * j);   // the wave's 4 KiB of tile j
+            cc_store_rows(stage[wv], lane, g[2 * q], a.T + run);
+            cc_store_rows(stage[wv], lane, g[2 * q + 1], a.U + run);
         }
-        const uint64_t run = ot_tmaj(64 * h, 4 * j);   // the wave's 4 KiB of tile j
-        cc_store_rows(stage[wv], lane, g[0], a.T + run);
-        cc_store_rows(stage[wv], lane, g[1], a.U + run);
     }
 }
 

@@ -8,6 +8,10 @@
 // on the host and never moves state (the reference does O(F) Vec::remove of whole nodes,
 // collect.rs:918-929).
 #include "fhh_engine.h"
+
+#ifndef FHH_GT_FUSED_SUMS
+#define FHH_GT_FUSED_SUMS 1   // r06: the tile-major table kernels add the node values per child themselves
+#endif
 #include "aes_tables.h"
 
 #include <hip/hip_runtime.h>
@@ -1332,15 +1336,16 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     if (ltable) {
                         // r06 (tile-major table): the kernels add the node values per child into the level's
                         // partials themselves (no stored values, no k_child_sums_fe pass)
-                        if (!ltm) for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
+                        const bool fused = ltm && FHH_GT_FUSED_SUMS;
+                        if (!fused) for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
                         HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
                         g.gt_msgs = B.gc_msgs.as<uint64_t>();
-                        g.node_partials = ltm ? part : nullptr;
-                        g.sh_gb = ltm ? nullptr : B.gc_val[0].as<uint64_t>();
+                        g.node_partials = ltm && FHH_GT_FUSED_SUMS ? part : nullptr;
+                        g.sh_gb = fused ? nullptr : B.gc_val[0].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_garble(g, c0->stream));
                         g.ev_labels = ltm ? c0->ot_buf[0].as<uint4>() : B.gc_evact.as<uint4>();
                         g.sh_gb = nullptr;
-                        g.sh_ev = ltm ? nullptr : B.gc_val[1].as<uint64_t>();
+                        g.sh_ev = fused ? nullptr : B.gc_val[1].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_eval(g, c0->stream));
                     } else if (lshare) {
                         for (int sv = 0; sv < 2; sv++) HIP_TRY(c0, B.gc_val[sv].ensure(tests * 8));
@@ -1400,8 +1405,11 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                     }
                     // the chunk's children's sums (FE: atomics into the partials k_prune zeroed;
                     // FE255: one store per child)
-                    if (pmode == 1 && !ltm) HIP_TRY(c0, launch_child_sums_fe(ca, part, c0->stream, false));
-                    else HIP_TRY(c0, launch_child_sums_fe255(ca, part, c0->stream));
+                    if (pmode == 1) {
+                        if (!(ltm && FHH_GT_FUSED_SUMS)) HIP_TRY(c0, launch_child_sums_fe(ca, part, c0->stream, false));
+                    } else {
+                        HIP_TRY(c0, launch_child_sums_fe255(ca, part, c0->stream));
+                    }
                 }
                 if (timed) HIP_TRY(c0, timing_end(c0, gc_slot, kGcotTag));
             } else if (pmode == 0) {

@@ -717,7 +717,7 @@ def golden_sig(args, n_total):
 CHACHA12_OPS_PER_BLOCK = 608   # 6 double rounds x 8 quarter rounds x 12 add/xor/rotate + 32 (state, feed-forward)
 
 
-def protocol_work(level_children, n: int, d: int, circuit: bool = False):
+def protocol_work(level_children, n: int, d: int, circuit: bool = False, ss_k: int = 1):
     """Executed work of one real-protocol crawl on this rank (n clients), by phase, from the kernels' work
     decomposition (fhh_host.cpp level loop; fhh_gc.hip, fhh_ot.hip). Returns (aes, chacha, transpose_bytes):
     AES blocks per phase — FE levels with b = 2d <= 2 run the tile-major garbled table (2^b rows per test
@@ -737,6 +737,10 @@ def protocol_work(level_children, n: int, d: int, circuit: bool = False):
 
     def expands(m):   # m OTs: 128 rows x ceil(m / 512) tiles, 2 blocks (receiver) + 1 (sender) each
         tiles = (m + 511) // 512
+        if ss_k > 1:   # SoftSpoken: 128 / k chunks, 2^k blocks (receiver) and 2^k - 1 (sender) per tile
+            cc["ot_recv_expand"] += (128 // ss_k) * (1 << ss_k) * tiles
+            cc["ot_send_expand"] += (128 // ss_k) * ((1 << ss_k) - 1) * tiles
+            return
         cc["ot_recv_expand"] += 2 * 128 * tiles
         cc["ot_send_expand"] += 128 * tiles
 
@@ -768,7 +772,44 @@ def protocol_work(level_children, n: int, d: int, circuit: bool = False):
     return aes, cc, transpose_bytes
 
 
-def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None):
+def protocol_bytes(level_children, n: int, d: int, circuit: bool = False, ss_k: int = 1):
+    """Server-to-server bytes of one real-protocol crawl on this rank (n clients), by message, as the party ABI
+    counts them (fhh_gcot.cpp u_bytes / gc_bytes / y2_bytes; the base OTs' CO15 messages excluded): the labels
+    OT's U (16 / ss_k B per OT: 128 / ss_k rows; SoftSpoken adds 4 KiB of GGM corrections per base-OT session),
+    the FE levels' garbled table (2^b - 1 rows of 8 B per test) or circuit (2 (b - 1) blocks + decode + the 8-B
+    share per test), the FieldElm level's circuit and its share OT (U and 16 B of y per OT, 2 OTs per test)."""
+    b = 2 * d
+    npad64 = (n + 63) // 64 * 64
+    npad_tm = (n + 511) // 512 * 512
+    L = len(level_children)
+    out = {"u_labels": 0, "u_shares": 0, "ggm_corrections": 0, "table": 0, "circuit": 0, "y_shares": 0}
+    corr = 4096 if ss_k > 1 else 0
+    for lv, C in enumerate(int(x) for x in level_children):
+        if C == 0:
+            continue
+        tests = C * n
+        if lv + 1 < L:
+            tm = (not circuit) and b <= 2
+            m1 = C * b * (npad_tm if tm else npad64)
+            out["u_labels"] += 16 * m1 // ss_k
+            out["ggm_corrections"] += corr
+            if circuit:
+                out["circuit"] += tests * (2 * (b - 1) * 16 + 1 + 8)
+            else:
+                out["table"] += tests * ((1 << b) - 1) * 8
+        else:
+            m1 = C * b * npad64
+            m2 = 2 * tests
+            out["u_labels"] += 16 * m1 // ss_k
+            out["u_shares"] += 16 * m2 // ss_k
+            out["ggm_corrections"] += 2 * corr
+            out["circuit"] += tests * (2 * (b - 1) * 16 + 1)
+            out["y_shares"] += 16 * m2
+    out["total"] = sum(out.values())
+    return out
+
+
+def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None, ot_ss_k=1):
     """The real protocol's crawl on the headline's keys (tree_crawl with gc_sender per level,
     collect.rs:419-482, with OtSender/OtReceiver::init per channel and level, :454-471; the leader's
     loop leader.rs:422-440): the GPU garbled-circuit equality test and both OT extensions in every
@@ -781,23 +822,24 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
     def run(levels=None):
         # record: every level's v0 - v1 comes back to the host (a few KB per level) for the output check
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=True,
-                             comm=comm, gc=gc, base_ot=True, levels=levels)
+                             comm=comm, gc=gc, base_ot=True, levels=levels, ot_ss_k=ot_ss_k)
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
+    tag = gc if ot_ss_k == 1 else f"{gc}, SoftSpoken k={ot_ss_k}"
     run(levels=min(32, args.data_len))
     barrier()
-    log(f"protocol crawl ({gc}): warm-up done")
+    log(f"protocol crawl ({tag}): warm-up done")
     c0.reset_stats()
     c1.reset_stats()
     t0 = time.perf_counter()
     res = run()
     barrier()
     wall = time.perf_counter() - t0
-    log(f"protocol crawl ({gc}): {wall:.2f} s, {len(res.final)} heavy hitters")
+    log(f"protocol crawl ({tag}): {wall:.2f} s, {len(res.final)} heavy hitters")
     s0 = c0.stats()
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
@@ -805,7 +847,9 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
         wall = float(t.item())
     hh = len(res.final)
     sig = crawl_sig(res)
-    aes, cc, tr_bytes = protocol_work(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit")
+    aes, cc, tr_bytes = protocol_work(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit",
+                                      ss_k=ot_ss_k)
+    wire = protocol_bytes(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit", ss_k=ot_ss_k)
     n_aes, n_cc = sum(aes.values()), sum(cc.values())
     gpu_s = s0["gcot_ms"] / 1e3
     ops = n_aes * VALU_OPS_PER_BLOCK + n_cc * CHACHA12_OPS_PER_BLOCK
@@ -834,6 +878,11 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
         "wall_s": wall,
         "heavy_hitters": hh,
         "heavy_hitters_equal_headline": sig_equal(sig, headline_sig) if headline_sig else None,
+        "ot_extension": "IKNP (128 rows of U)" if ot_ss_k == 1 else
+                        f"SoftSpoken k={ot_ss_k} ({128 // ot_ss_k} rows of U, GGM trees from the base OTs)",
+        "channel_bytes": wire,
+        "channel_bytes_note": ("server-to-server bytes of this crawl on this rank by message, as the party ABI "
+                               "counts them (bench.protocol_bytes; CO15 base-OT messages excluded)"),
         "output_check": ("every level's child count and v0 - v1 per child, and the sorted (path, value) heavy "
                          "hitters, equal the headline crawl's (recorded in its untimed warm-up)"),
         "roofline": roof,
@@ -939,6 +988,10 @@ def main():
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
     ap.add_argument("--no-protocol-circuit", action="store_true",
                     help="skip the second protocol crawl with the half-gates circuit at every level")
+    ap.add_argument("--ot-ss-k", type=int, default=1, choices=(1, 2, 4),
+                    help="--gc ot: the OT extension of the timed crawl (1 IKNP, 2 / 4 SoftSpoken)")
+    ap.add_argument("--protocol-ss-k", default="4",
+                    help="comma list of SoftSpoken k (2, 4) to run the protocol crawl with beside IKNP ('' = none)")
     ap.add_argument("--no-protocol-crawl", action="store_true",
                     help="skip the real protocol's crawl (GC + OT + real base OTs every level) that follows the "
                          "headline's timed region on the zipf workload")
@@ -1061,7 +1114,7 @@ def main():
     def step(record=False):
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
                              record=record, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc],
-                             base_ot=args.base_ot)
+                             base_ot=args.base_ot, ot_ss_k=args.ot_ss_k if args.gc == "ot" else 1)
 
     def barrier():
         if dist is not None:
@@ -1123,7 +1176,16 @@ def main():
             # r05c form) beside the default garbled table: what the table buys, on the same box
             circ = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, gc="ot-circuit", expand_rate=expand_rate)
             proto["circuit_form"] = {k: circ[k] for k in ("wall_s", "heavy_hitters", "heavy_hitters_equal_headline",
-                                                          "gcot_gpu_ms", "expand_gpu_ms", "protocol", "roofline")}
+                                                          "gcot_gpu_ms", "expand_gpu_ms", "protocol", "roofline",
+                                                          "channel_bytes")}
+        # r06: the same crawl on SoftSpoken OT extension (fewer rows of U on the wire, more ChaCha work)
+        proto["softspoken"] = {}
+        for k in [int(x) for x in args.protocol_ss_k.split(",") if x.strip()]:
+            ss = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate, ot_ss_k=k)
+            proto["softspoken"][f"k{k}"] = {key: ss[key] for key in (
+                "wall_s", "heavy_hitters", "heavy_hitters_equal_headline", "gcot_gpu_ms", "ot_extension",
+                "channel_bytes", "roofline")}
+            proto["softspoken"][f"k{k}"]["output_equal_golden"] = sig_equal(ss["sig"], gold) if gold else None
 
     if rank == 0:
         launches = max(1, s0["expand_launches_timed"])
@@ -1187,6 +1249,7 @@ def main():
                 "clients_total": n_total, "clients_per_gpu": n_local, "data_len": args.data_len,
                 "n_dims": args.dims, "num_sites": args.num_sites, "zipf_s": args.zipf, "ball_size": args.ball,
                 "threshold": args.threshold, "mode": args.mode, "gc": args.gc,
+                "ot_extension": None if args.gc != "ot" else ("IKNP" if args.ot_ss_k == 1 else f"SoftSpoken k={args.ot_ss_k}"),
                 "base_ot": "chou-orlandi (host)" if args.base_ot else ("ideal" if args.gc == "ot" else None),
                 "parallelism": f"client-shard x{world}", "collective": collective,
                 "variant": args.variant if args.variant >= 0 else "default",

@@ -54,7 +54,7 @@ EXPORTS = [
     "fhh_create_multi", "fhh_shard_info", "fhh_shard_ctx", "fhh_node_sums_fe_device", "fhh_node_sums_fe255_device",
     "fhh_gb_garble", "fhh_gb_ot_labels", "fhh_gb_ot_shares", "fhh_ev_ot_labels", "fhh_ev_evaluate", "fhh_ev_ot_shares",
     "fhh_party_node_sums", "fhh_party_bytes_sent", "fhh_gc_party_test_cfgs", "fhh_memcpy_device",
-    "fhh_cot_extend_host", "fhh_gc_cot_host", "fhh_gt_cot_host",
+    "fhh_cot_extend_host", "fhh_cot_extend_ss_host", "fhh_gc_cot_host", "fhh_gt_cot_host",
     "fhh_shard_plan",
 ]
 
@@ -107,6 +107,7 @@ class FhhSimConfig(ctypes.Structure):
         ("probe_ty", u8p),
         ("probe_children", u64p),
         ("base_ot", ctypes.c_uint32),
+        ("ot_ss_k", ctypes.c_uint32),
     ]
 
 
@@ -199,6 +200,8 @@ class FhhGbCfg(ctypes.Structure):
         ("base_choice", ctypes.c_uint8 * (2 * 16)),
         ("child_begin", ctypes.c_uint64),
         ("child_count", ctypes.c_uint64),
+        ("ot_ss_k", ctypes.c_uint32),   # r06: 0 / 1 IKNP, 2 / 4 SoftSpoken (as the evaluator's)
+        ("pad_", ctypes.c_uint32),
     ]
 
 
@@ -207,7 +210,7 @@ class FhhEvCfg(ctypes.Structure):
     _fields_ = [
         ("base_pairs", ctypes.c_uint8 * (2 * 128 * 2 * 16)),
         ("form", ctypes.c_uint32),   # as FhhGbCfg.form (public)
-        ("pad_", ctypes.c_uint32),
+        ("ot_ss_k", ctypes.c_uint32),   # r06: 0 / 1 IKNP, 2 / 4 SoftSpoken
         ("child_begin", ctypes.c_uint64),
         ("child_count", ctypes.c_uint64),
     ]
@@ -293,6 +296,7 @@ def lib():
         "fhh_party_bytes_sent": (i, [vp, u64p]),
         "fhh_gc_party_test_cfgs": (i, [u64, u32, P(FhhGbCfg), P(FhhEvCfg)]),
         "fhh_cot_extend_host": (i, [vp, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p]),
+        "fhh_cot_extend_ss_host": (i, [vp, u32, u64, u32, u8p, u8p, u32, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p]),
         "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
                                 u64p]),
         "fhh_gt_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u64p, u64p, u64p]),

@@ -254,6 +254,8 @@ struct OtOut {            // optional transcript (device pointers into the scrat
     const uint4* Y0 = nullptr;
     const uint4* Y1 = nullptr;
     uint64_t nblk = 0;
+    uint32_t u_rows = 128;            // 128 / ss_k (SoftSpoken)
+    const uint4* corr = nullptr;      // SoftSpoken: the GGM corrections [u_rows][ss_k][2]
 };
 int ot_host_keys(fhh_ctx* ctx, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], const uint32_t** rk_dev);
 // m OTs of OtArgs a's mode on ctx's stream (fhh_gcot.cpp): sizes, scratch matrices and messages are

@@ -170,6 +170,14 @@ int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
     a.Q = ctx->ot_buf[2].as<uint4>();
     a.Y0 = a.mode < 4 ? ctx->ot_buf[5].as<uint4>() : nullptr;
     a.Y1 = a.mode == 0 ? ctx->ot_buf[6].as<uint4>() : nullptr;
+    if (a.ss_k > 1) {   // SoftSpoken: both GGM trees (the receiver's corrections are its first message)
+        if (a.ss_k != 2 && a.ss_k != 4) return ctx->fail(FHH_E_ARG, "ot: SoftSpoken k must be 2 or 4");
+        HIP_TRY(ctx, ctx->ot_buf[3].ensure((size_t)2 * 128 * 16 * 16 / a.ss_k));
+        HIP_TRY(ctx, ctx->ot_buf[4].ensure((size_t)128 * 2 * 16));
+        a.ss_leaf = ctx->ot_buf[3].as<uint4>();
+        a.ss_corr = ctx->ot_buf[4].as<uint4>();
+        HIP_TRY(ctx, launch_ss_ggm(a, ctx->stream));
+    }
     HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));     // receiver -> sender: U
     HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));     // sender: Q
     if (a.mode == 5) {   // the correlation, left tile-major in Q / T for the r06 garbled table
@@ -186,6 +194,8 @@ int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
         tr->Y0 = a.Y0;
         tr->Y1 = a.Y1;
         tr->nblk = mp / 128;
+        tr->u_rows = a.ss_k > 1 ? 128 / a.ss_k : 128;
+        tr->corr = a.ss_k > 1 ? a.ss_corr : nullptr;
     }
     return FHH_OK;
 }
@@ -193,12 +203,12 @@ int ot_run(fhh_ctx* ctx, OtArgs a, uint64_t m, OtOut* tr) {
 // the transcript's U [128][ceil(m / 128)][16] (row form) from the device's tile-major U (r06, fhh_ot.hip ot_tmaj:
 // 128-OT block c of row i at uint4 (c / 4) 512 + 4 i + c % 4)
 int u_transcript(fhh_ctx* ctx, const OtOut& tr, uint64_t m, uint8_t* u_out) {
-    const uint64_t nb = (m + 127) / 128;
-    std::vector<uint8_t> h(tr.nblk * 128 * 16);
+    const uint64_t nb = (m + 127) / 128, R = tr.u_rows;   // SoftSpoken: R = 128 / k rows, tile stride R rows
+    std::vector<uint8_t> h(tr.nblk * R * 16);
     HIP_TRY(ctx, hipMemcpy(h.data(), tr.U, h.size(), hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < 128; i++)
+    for (uint64_t i = 0; i < R; i++)
         for (uint64_t c = 0; c < nb; c++)
-            std::memcpy(u_out + (i * nb + c) * 16, h.data() + ((c / 4) * 512 + 4 * i + c % 4) * 16, 16);
+            std::memcpy(u_out + (i * nb + c) * 16, h.data() + ((c / 4) * 4 * R + 4 * i + c % 4) * 16, 16);
     return FHH_OK;
 }
 
@@ -375,12 +385,14 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
     return FHH_OK;
 }
 
-int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
-                        uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
-                        uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
+int fhh_cot_extend_ss_host(fhh_ctx* ctx, uint32_t ss_k, uint64_t m, uint32_t mode, const uint8_t* choices,
+                           const uint8_t delta[16], uint32_t mask, const uint8_t base_seeds[128 * 2 * 16],
+                           const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* sender_out, uint8_t* out,
+                           uint8_t* u_out, uint8_t* y_out, uint8_t* corr_out) {
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
+    if (ss_k != 1 && ss_k != 2 && ss_k != 4) return ctx->fail(FHH_E_ARG, "cot_extend: ss_k must be 1, 2 or 4");
     if (mode < FHH_COT_LABELS || mode > FHH_COT_RAW) return ctx->fail(FHH_E_ARG, "cot_extend: mode must be 1..4");
     if (m == 0) return FHH_OK;
     if (!choices || !out || !base_seeds || !base_choice || (mode == FHH_COT_LABELS && !delta))
@@ -414,6 +426,7 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
     a.ctr_off = ctr_off;
     a.sx = dsx.p;
     a.out = dout.as<uint4>();
+    a.ss_k = ss_k;
     OtOut tr;
     rc = ot_run(ctx, a, m, &tr);
     if (rc) return rc;
@@ -426,7 +439,15 @@ int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* 
         rc = u_transcript(ctx, tr, m, u_out);
         if (rc) return rc;
     }
+    if (corr_out && ss_k > 1) HIP_TRY(ctx, hipMemcpy(corr_out, tr.corr, (size_t)128 * 2 * 16, hipMemcpyDeviceToHost));
     return FHH_OK;
+}
+
+int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
+                        uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
+                        uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
+    return fhh_cot_extend_ss_host(ctx, 1, m, mode, choices, delta, mask, base_seeds, base_choice, ctr_off, sender_out,
+                                  out, u_out, y_out, nullptr);
 }
 
 int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
@@ -694,6 +715,8 @@ struct PartyState {
     DevBuf vals;                // the level's node values [level_C][n] (u64, or a BlockPair at the last level)
     std::vector<uint32_t> rk_host;
     uint64_t bytes_sent = 0;    // this ctx's outgoing message bytes for the level
+    uint32_t ss_k = 1;          // r06: 1 IKNP, 2 / 4 SoftSpoken (both OT kinds; fhh_ev_cfg / fhh_gb_cfg.ot_ss_k)
+    DevBuf ss_leaf;             // SoftSpoken: this party's GGM leaves
 };
 
 void party_destroy(fhh_ctx* ctx) {
@@ -812,19 +835,32 @@ OtArgs party_ot(PartyState& P, int w, uint64_t m) {
     a.U = P.U.as<uint4>();
     a.Q = P.Q.as<uint4>();
     a.ctr_off = P.ctr[w];
+    a.ss_k = P.ss_k > 1 ? P.ss_k : 0;
     return a;
 }
+
+// SoftSpoken (P.ss_k > 1): this party's half of the GGM trees before its expand — the receiver's corrections
+// go after U in its message, the sender reads them there (a.U = the received message)
+hipError_t party_ggm(PartyState& P, OtArgs& a, bool receiver, hipStream_t stream) {
+    if (P.ss_k < 2) return hipSuccess;
+    a.ss_leaf = P.ss_leaf.as<uint4>();
+    a.ss_corr = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(a.U) + 16 * a.mp / P.ss_k);
+    a.ss_role = receiver ? 1 : 2;
+    return launch_ss_ggm(a, stream);
+}
+
+// message sizes: U = 128 / k rows of the padded OTs (+ SoftSpoken's GGM corrections, 4 KiB)
+uint64_t u_bytes(uint64_t m, uint32_t k) { return 16 * ot_padded(m) / k + (k > 1 ? 128 * 2 * 16 : 0); }
 
 int party_ot_buffers(fhh_ctx* ctx, PartyState& P, uint64_t m, bool receiver, bool reply = true) {
     const uint64_t rows = 16 * ot_padded(m);   // [128][mp / 128] blocks
     HIP_TRY(ctx, (receiver ? P.T : P.Q).ensure(rows));
-    if (receiver) HIP_TRY(ctx, P.U.ensure(rows));
+    if (receiver) HIP_TRY(ctx, P.U.ensure(u_bytes(m, P.ss_k)));
     else if (reply) HIP_TRY(ctx, P.Y.ensure(std::max<uint64_t>(m, 1) * 16));
+    if (P.ss_k > 1) HIP_TRY(ctx, P.ss_leaf.ensure((size_t)2 * 128 * 16 * 16 / P.ss_k));
     return FHH_OK;
 }
 
-// message sizes
-uint64_t u_bytes(uint64_t m) { return 16 * ot_padded(m); }
 uint64_t gc_bytes(const PartyState& P) {
     if (P.ltable) return P.tests * (((uint64_t)1 << P.bits) - 1) * 8;   // rows 1 .. 2^bits - 1, 8 B each
     return P.tests * ((uint64_t)2 * (P.bits - 1) * 16 + 1 + (P.lshare ? 8 : 0));
@@ -872,9 +908,12 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
     CTX_CHECK(ctx);
     if (!cfg || !u_dev || !u_len) return ctx->fail(FHH_E_ARG, "ev_ot_labels: NULL argument");
     if (cfg->form > 1) return ctx->fail(FHH_E_ARG, "ev_ot_labels: form must be 0 (table) or 1 (circuit)");
+    if (cfg->ot_ss_k > 1 && cfg->ot_ss_k != 2 && cfg->ot_ss_k != 4)
+        return ctx->fail(FHH_E_ARG, "ev_ot_labels: ot_ss_k must be 0 / 1 (IKNP), 2 or 4 (SoftSpoken)");
     int rc = party_begin(ctx, 1, cfg->child_begin, cfg->child_count, cfg->form);
     if (rc) return rc;
     PartyState& P = *ctx->party;
+    P.ss_k = cfg->ot_ss_k > 1 ? cfg->ot_ss_k : 1;
     // both OT kinds' receiver schedules and session counters (OtReceiver::init, collect.rs:460)
     // (kind 1, the share OT, at the FieldElm level only: the FE levels' share rides on the GC, r05c)
     party_session(P, 0, &cfg->base_pairs[0][0][0][0], 128 * 32, P.m1);
@@ -892,6 +931,7 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
         a.mode = P.ltm ? 5 : 4;
         a.choices = P.planes.as<uint32_t>();
         a.out = P.ltm ? nullptr : P.labels.as<uint4>();
+        HIP_TRY(ctx, party_ggm(P, a, true, ctx->stream));
         HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));        // T, U
         // its active labels t_j: row-major for the circuit; the r06 table reads T tile-major
         if (!P.ltm) HIP_TRY(ctx, launch_ot_rows_out(a, false, ctx->stream));
@@ -900,7 +940,7 @@ int fhh_ev_ot_labels(fhh_ctx* ctx, const fhh_ev_cfg* cfg, const uint8_t** u_dev,
     if (rc) return rc;
     P.step = 1;
     *u_dev = P.U.as<uint8_t>();
-    *u_len = P.m1 ? u_bytes(P.m1) : 0;
+    *u_len = P.m1 ? u_bytes(P.m1, P.ss_k) : 0;
     P.bytes_sent += *u_len;
     return FHH_OK;
 }
@@ -910,10 +950,13 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     CTX_CHECK(ctx);
     if (!cfg || !y_dev || !y_len) return ctx->fail(FHH_E_ARG, "gb_ot_labels: NULL argument");
     if (cfg->form > 1) return ctx->fail(FHH_E_ARG, "gb_ot_labels: form must be 0 (table) or 1 (circuit)");
+    if (cfg->ot_ss_k > 1 && cfg->ot_ss_k != 2 && cfg->ot_ss_k != 4)
+        return ctx->fail(FHH_E_ARG, "gb_ot_labels: ot_ss_k must be 0 / 1 (IKNP), 2 or 4 (SoftSpoken)");
     int rc = party_begin(ctx, 0, cfg->child_begin, cfg->child_count, cfg->form);
     if (rc) return rc;
     PartyState& P = *ctx->party;
-    rc = check_in(ctx, u_dev, u_len, P.m1 ? u_bytes(P.m1) : 0, "U (labels OT)");
+    P.ss_k = cfg->ot_ss_k > 1 ? cfg->ot_ss_k : 1;
+    rc = check_in(ctx, u_dev, u_len, P.m1 ? u_bytes(P.m1, P.ss_k) : 0, "U (labels OT)");
     if (rc) return rc;
     P.mask = cfg->mask & 1u;
     if (!(cfg->base_choice[0][0] & 1))
@@ -966,6 +1009,7 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
         a.U = const_cast<uint4*>(reinterpret_cast<const uint4*>(u_dev));
         for (int c = 0; c < 4; c++) a.s[c] = P.s[0][c];
         a.sx = P.ltm ? nullptr : P.labels.p;
+        HIP_TRY(ctx, party_ggm(P, a, false, ctx->stream));
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));      // Q from U
         if (!P.ltm) HIP_TRY(ctx, launch_ot_rows_out(a, true, ctx->stream));   // the zero labels q_j (the circuit)
     }
@@ -1040,13 +1084,14 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     if (P.m2) {
         OtArgs a = party_ot(P, 1, P.m2);
         a.choices = P.choices2.as<uint32_t>();
+        HIP_TRY(ctx, party_ggm(P, a, true, ctx->stream));
         HIP_TRY(ctx, launch_ot_recv_expand(a, ctx->stream));
     }
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 2;
     *u_dev = P.U.as<uint8_t>();
-    *u_len = P.m2 ? u_bytes(P.m2) : 0;
+    *u_len = P.m2 ? u_bytes(P.m2, P.ss_k) : 0;
     P.bytes_sent += *u_len;
     return FHH_OK;
 }
@@ -1059,7 +1104,7 @@ int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const u
     PartyState* Pp = ctx->party;
     if (!Pp || Pp->role != 0 || Pp->step != 2) return ctx->fail(FHH_E_STATE, "gb_ot_shares: call after fhh_gb_garble");
     PartyState& P = *Pp;
-    rc = check_in(ctx, u_dev, u_len, P.m2 ? u_bytes(P.m2) : 0, "U (shares OT)");
+    rc = check_in(ctx, u_dev, u_len, P.m2 ? u_bytes(P.m2, P.ss_k) : 0, "U (shares OT)");
     if (rc) return rc;
     rc = party_ot_buffers(ctx, P, P.m2, false);
     if (rc) return rc;
@@ -1074,6 +1119,7 @@ int fhh_gb_ot_shares(fhh_ctx* ctx, const uint8_t* u_dev, uint64_t u_len, const u
         for (int c = 0; c < 4; c++) a.s[c] = P.s[1][c];
         a.sx = party_vals(P);
         a.Y0 = P.Y.as<uint4>();
+        HIP_TRY(ctx, party_ggm(P, a, false, ctx->stream));
         HIP_TRY(ctx, launch_ot_send_expand(a, ctx->stream));
         HIP_TRY(ctx, launch_ot_send_hash_rows(a, ctx->stream));
         if (P.last) HIP_TRY(ctx, launch_cot_fe255_finish(a, ctx->stream));

@@ -1320,6 +1320,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         a1.ctl = B.ctl.as<LoopCtl>();
                         a1.per_group = npad_gc * bits;
                         a1.g_off = g_off;
+                        a1.ss_k = cfg->ot_ss_k;
                         rc = ot_run(c0, a1, m1, nullptr);
                         if (rc) return rc;
                         g.ev_ot = 1;
@@ -1398,6 +1399,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         a2.ctl = B.ctl.as<LoopCtl>();
                         a2.per_group = (uint64_t)c0->n * per2;
                         a2.g_off = g_off;
+                        a2.ss_k = cfg->ot_ss_k;
                         rc = ot_run(c0, a2, m2, nullptr);
                         if (rc) return rc;
                         ca.ot_val[0] = B.gc_val[0].p;
@@ -2215,6 +2217,8 @@ int fhh_sim_crawl(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg) {
     if (cfg->gc && (cfg->mode != 1 || cfg->host_loop))
         return c0->fail(FHH_E_ARG, "sim_crawl: gc needs mode 1 (OT share values) and the device loop");
     if (cfg->gc && 2 * c0->d > (uint32_t)kGcMaxBits) return c0->fail(FHH_E_ARG, "sim_crawl: gc supports d <= 4");
+    if (cfg->ot_ss_k > 1 && cfg->ot_ss_k != 2 && cfg->ot_ss_k != 4)
+        return c0->fail(FHH_E_ARG, "sim_crawl: ot_ss_k must be 0 / 1 (IKNP), 2 or 4 (SoftSpoken)");
     if (cfg->probe_n_levels && cfg->host_loop)
         return c0->fail(FHH_E_ARG, "sim_crawl: the probe instruments the device loop (host_loop = 0)");
     if (c0->device != c1->device) return c0->fail(FHH_E_ARG, "sim_crawl: ctxs on different devices");

@@ -389,7 +389,17 @@ struct OtArgs {
     uint64_t ctr_off;            // the row PRG's first block (a multiple of 256): a base-OT session's
                                  // running counter, so batches extending one session never repeat pads
     void* sx;                    // modes 1, 3, 4: uint4 [m]; mode 2: u64 [m] (the sender's node values)
+    // r06: 0 / 1 = IKNP; 2, 4 = SoftSpoken with k = ss_k (fhh_ot.hip k_ss_*): U is then 128 / k rows
+    // (tile-major, tile stride 128 / k rows), ss_leaf [2][128 / k][2^k] the GGM leaves (receiver, sender),
+    // ss_corr [128 / k][k][2] the receiver's GGM corrections (the wire)
+    uint32_t ss_k;
+    uint32_t ss_role;            // k_ss_ggm: 0 both parties (the level loop), 1 the receiver (leaves + corrections),
+                                 // 2 the sender (its leaves from ss_corr, the received corrections) — the party ABI
+    uint4* ss_leaf;
+    uint4* ss_corr;
 };
+// SoftSpoken GGM trees of both parties from rk / s (one workgroup; before the expands)
+hipError_t launch_ss_ggm(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream);
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream);
 // the hashes reading T / Q in row form with the transpose fused in (no Tt / Qt pass)

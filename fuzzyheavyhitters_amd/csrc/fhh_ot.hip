@@ -270,6 +270,308 @@ __global__ __launch_bounds__(kOtCcThreads) void k_ot_send_expand_cc(OtArgs a) {
     }
 }
 
+// ---- r06: SoftSpoken OT extension (OtArgs::ss_k = 2, 4; oracle/fhh_oracle.c cot_rows / ss_ggm) ---------
+// L. Roy, "SoftSpoken OT" (CRYPTO 2022), semi-honest small-field VOLE with the repetition code: the 128 base
+// OTs in n_c = 128 / k chunks of k; chunk c's GGM tree gives the receiver 2^k leaf seeds and the sender every
+// leaf but x = Delta_c (Delta_c bit b = s bit b n_c + c). Receiver: u_c = XOR_x G(leaf_x), t row b n_c + c =
+// XOR_{x_b = 1} G(leaf_x), U_c = u_c ^ r on the wire; sender: q row b n_c + c = XOR_{y != 0, y_b = 1}
+// G(leaf_{y ^ Delta_c}) ^ (Delta_c)_b U_c. Then q_j = t_j ^ r_j s exactly as IKNP, so every mode after the
+// expands is unchanged — and U is 128 / k rows: 16 / k bytes per OT on the wire instead of 16. The price is
+// ChaCha work: 2^k blocks per (chunk, tile) at the receiver (2 per row at k = 1: k = 2 the same, k = 4 2x) and
+// 2^k - 1 at the sender (1 per row at k = 1: k = 2 1.5x, k = 4 3.75x). G is the IKNP row PRG (ChaCha12, key
+// leaf || leaf, counter ctr_off / 4 + tile, nonce 0); the GGM tree's PRG and masks use nonces 1, 2, its root 3.
+
+// one ChaCha12 block of a general 256-bit key, 64-bit counter and nonce (the GGM tree: one thread per chunk)
+__device__ void cc_block_key8(const uint32_t (&key)[8], uint64_t ctr, uint32_t nonce, uint32_t (&x)[16]) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                       key[4], key[5], key[6], key[7], (uint32_t)ctr, (uint32_t)(ctr >> 32), nonce, 0u};
+#pragma unroll
+    for (int w = 0; w < 16; w++) x[w] = st[w];
+    for (int r = 0; r < kOtChachaRounds; r += 2) {
+        cc_qr(x[0], x[4], x[8], x[12]);
+        cc_qr(x[1], x[5], x[9], x[13]);
+        cc_qr(x[2], x[6], x[10], x[14]);
+        cc_qr(x[3], x[7], x[11], x[15]);
+        cc_qr(x[0], x[5], x[10], x[15]);
+        cc_qr(x[1], x[6], x[11], x[12]);
+        cc_qr(x[2], x[7], x[8], x[13]);
+        cc_qr(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int w = 0; w < 16; w++) x[w] += st[w];
+}
+
+__device__ __forceinline__ uint4 ss_key_row(const uint32_t* rk, uint32_t row) {
+    return *reinterpret_cast<const uint4*>(rk + (size_t)row * 44);
+}
+
+// ChaCha12(a || b, ctr, nonce): the first 8 words (two 16-B seeds)
+__device__ __forceinline__ void ss_cc(uint4 a, uint4 b, uint64_t ctr, uint32_t nonce, uint4& o0, uint4& o1) {
+    const uint32_t key[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t x[16];
+    cc_block_key8(key, ctr, nonce, x);
+    o0 = make_uint4(x[0], x[1], x[2], x[3]);
+    o1 = make_uint4(x[4], x[5], x[6], x[7]);
+}
+
+__device__ __forceinline__ uint4 x4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+
+// Both parties' GGM trees (the level loop runs both servers): thread c = chunk c. Receiver: the root from its
+// pair k_c^0 || k_c^1, every level's two side sums masked under k_i^{1 - beta} (ss_corr [n_c][K][2], the
+// wire); sender: unmasks side 1 - s_i with k_i^{s_i} and rebuilds every leaf but Delta_c. ss_leaf = receiver
+// [n_c][2^K] then sender [n_c][2^K] (its x = Delta_c entry zero).
+template <int K>
+__global__ __launch_bounds__(64) void k_ss_ggm(OtArgs a) {
+    constexpr uint32_t NC = 128 / K, NL = 1u << K;
+    const uint32_t c = threadIdx.x;
+    if (c >= NC) return;
+    // every loop is unrolled (K is a template argument) so node / nxt stay in registers (no scratch)
+    uint4 node[NL], nxt[NL];
+    uint4 dummy;
+    uint4* corr = a.ss_corr + (size_t)c * K * 2;
+    if (a.ss_role != 2) {   // the receiver
+        ss_cc(ss_key_row(a.rk, c), ss_key_row(a.rk, 128 + c), c, 3, node[0], dummy);
+#pragma unroll
+        for (uint32_t l = 1; l <= K; l++) {
+            const uint32_t half = 1u << (l - 1), i = (l - 1) * NC + c;
+            uint4 ks[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+#pragma unroll
+            for (uint32_t z = 0; z < half; z++) {
+                uint4 lft, rgt;
+                ss_cc(node[z], node[z], 0, 1, lft, rgt);
+                nxt[z] = lft;
+                nxt[z | half] = rgt;
+                ks[0] = x4(ks[0], lft);
+                ks[1] = x4(ks[1], rgt);
+            }
+#pragma unroll
+            for (uint32_t beta = 0; beta < 2; beta++) {
+                const uint4 kk = ss_key_row(a.rk, (1 - beta) * 128 + i);
+                uint4 msk;
+                ss_cc(kk, kk, 0, 2, msk, dummy);
+                corr[(l - 1) * 2 + beta] = x4(ks[beta], msk);
+            }
+#pragma unroll
+            for (uint32_t z = 0; z < 2 * half; z++) node[z] = nxt[z];
+        }
+        uint4* leaf_r = a.ss_leaf + (size_t)c * NL;
+#pragma unroll
+        for (uint32_t x = 0; x < NL; x++) leaf_r[x] = node[x];
+    }
+    if (a.ss_role == 1) return;
+    // the sender
+    uint32_t dc = 0;
+    for (uint32_t b = 0; b < (uint32_t)K; b++) {
+        const uint32_t i = b * NC + c;
+        dc |= ((a.s[i >> 5] >> (i & 31)) & 1u) << b;
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < NL; x++) node[x] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t l = 1; l <= K; l++) {
+        const uint32_t half = 1u << (l - 1), i = (l - 1) * NC + c, db = (dc >> (l - 1)) & 1u;
+        const uint32_t path = dc & (half - 1);
+        const uint4 kk = ss_key_row(a.rk, 256 + i);   // k_i^{s_i}
+        uint4 msk;
+        ss_cc(kk, kk, 0, 2, msk, dummy);
+        uint4 sib = x4(corr[(l - 1) * 2 + (1 - db)], msk);
+#pragma unroll
+        for (uint32_t x = 0; x < NL; x++) nxt[x] = make_uint4(0, 0, 0, 0);
+        if (l > 1) {
+#pragma unroll
+            for (uint32_t z = 0; z < half; z++) {
+                if (z == path) continue;   // the unknown node on the path (its children stay zero)
+                uint4 lft, rgt;
+                ss_cc(node[z], node[z], 0, 1, lft, rgt);
+                nxt[z] = lft;
+                nxt[z | half] = rgt;
+                sib = x4(sib, db ? lft : rgt);
+            }
+        }
+        const uint32_t at = path | ((1 - db) << (l - 1));   // the path's sibling
+#pragma unroll
+        for (uint32_t z = 0; z < 2 * half; z++)
+            if (z == at) nxt[z] = sib;
+#pragma unroll
+        for (uint32_t z = 0; z < 2 * half; z++) node[z] = nxt[z];
+    }
+    uint4* leaf_s = a.ss_leaf + (size_t)(NC + c) * NL;
+#pragma unroll
+    for (uint32_t x = 0; x < NL; x++) leaf_s[x] = x == dc ? make_uint4(0, 0, 0, 0) : node[x];
+}
+
+// the staging store of cc_store_rows with the wave's 64 rows in two runs: stage rows 0..31 -> run_lo, 32..63
+// -> run_hi (k = 4: two tiles per wave), the high half skipped when hi_ok is false
+__device__ __forceinline__ void cc_store_rows2(uint32_t* st, uint32_t lane, const uint32_t (&v)[16], uint4* run_lo,
+                                               uint4* run_hi, bool hi_ok) {
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+        *reinterpret_cast<uint4*>(st + kOtCcRowWords * lane + 4 * w) = make_uint4(v[4 * w], v[4 * w + 1], v[4 * w + 2], v[4 * w + 3]);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t r = 16 * k + (lane >> 2), w = lane & 3;
+        if (k >= 2 && !hi_ok) break;   // wave-uniform
+        uint4* dst = (k < 2 ? run_lo + 64 * k : run_hi + 64 * (k - 2)) + lane;
+        __builtin_nontemporal_store(*reinterpret_cast<const cc_v4*>(st + kOtCcRowWords * r + 4 * w),
+                                    reinterpret_cast<cc_v4*>(dst));
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Receiver: one wave = 64 (chunk, tile) lanes — k = 2: tile j, lane = chunk; k = 4: tiles j0, j0 + 1, lane =
+// 32 (tile - j0) + chunk. 2^K blocks per lane, 2 in lockstep; t rows b n_c + c and U row c stored tile-major
+// through the LDS stage (the wave's rows are whole-line runs: T rows b n_c .. b n_c + n_c - 1 of its tiles,
+// U rows 0 .. n_c - 1 of its tiles — one contiguous 4 KiB, U's tile stride being n_c rows).
+template <int K>
+__global__ __launch_bounds__(kOtCcThreads) void k_ss_recv_expand(OtArgs a) {
+    constexpr uint32_t NC = 128 / K, NL = 1u << K, TPW = 64 / NC;   // tiles per wave
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kOtCcWaves][64 * kOtCcRowWords];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t c = lane % NC, tq = lane / NC;
+    const uint64_t nblk_act = (ot_active(a) + 127) / 128;
+    const uint64_t tiles = (nblk_act + 3) / 4;
+    const uint64_t items = (tiles + TPW - 1) / TPW;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtCcWaves;
+    const uint4* leaf = a.ss_leaf + (size_t)c * NL;
+    for (uint64_t it = (uint64_t)blockIdx.x * kOtCcWaves + wv; it < items; it += nwaves) {
+        const uint64_t j0 = TPW * it, j = j0 + tq;
+        const bool hi_ok = TPW == 1 || j0 + 1 < tiles;
+        uint32_t u[16], v[K][16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            u[w] = 0;
+#pragma unroll
+            for (int b = 0; b < K; b++) v[b][w] = 0;
+        }
+#pragma unroll
+        for (uint32_t x = 0; x < NL; x += 2) {
+            uint32_t kk[2][4];
+            const uint4 l0 = leaf[x], l1 = leaf[x + 1];
+            kk[0][0] = l0.x; kk[0][1] = l0.y; kk[0][2] = l0.z; kk[0][3] = l0.w;
+            kk[1][0] = l1.x; kk[1][1] = l1.y; kk[1][2] = l1.z; kk[1][3] = l1.w;
+            const uint64_t ctr[2] = {a.ctr_off / 4 + j, a.ctr_off / 4 + j};
+            uint32_t g[2][16];
+            cc_blocks<2>(kk, ctr, g);
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+#pragma unroll
+                for (int w = 0; w < 16; w++) {
+                    u[w] ^= g[q][w];
+#pragma unroll
+                    for (int b = 0; b < K; b++)
+                        if (((x + q) >> b) & 1) v[b][w] ^= g[q][w];
+                }
+            }
+        }
+        const uint4* ch = reinterpret_cast<const uint4*>(a.choices);
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint64_t cb = 4 * j + w;
+            const uint4 r = cb < nblk_act ? ch[cb] : make_uint4(0, 0, 0, 0);
+            u[4 * w] ^= r.x;
+            u[4 * w + 1] ^= r.y;
+            u[4 * w + 2] ^= r.z;
+            u[4 * w + 3] ^= r.w;
+        }
+        // U: tile j0's rows 0 .. n_c - 1 onwards, contiguous for the wave (tile stride 4 n_c uint4)
+        uint4* urun = a.U + j0 * (4 * NC);
+        cc_store_rows2(stage[wv], lane, u, urun, urun + 128, hi_ok);
+#pragma unroll
+        for (int b = 0; b < K; b++)
+            cc_store_rows2(stage[wv], lane, v[b], a.T + ot_tmaj(b * NC, 4 * j0),
+                           a.T + ot_tmaj(b * NC + (TPW == 1 ? 32 : 0), 4 * (j0 + TPW - 1)), hi_ok);
+    }
+}
+
+// Sender: the same lanes; y = 1 .. 2^K - 1 walks the leaves x = y ^ Delta_c (the coefficient (x ^ Delta_c)_b
+// = y_b is the same for every lane), then q rows = w_b ^ (Delta_c)_b U_c.
+template <int K>
+__global__ __launch_bounds__(kOtCcThreads) void k_ss_send_expand(OtArgs a) {
+    constexpr uint32_t NC = 128 / K, NL = 1u << K, TPW = 64 / NC;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kOtCcWaves][64 * kOtCcRowWords];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t c = lane % NC, tq = lane / NC;
+    const uint64_t nblk_act = (ot_active(a) + 127) / 128;
+    const uint64_t tiles = (nblk_act + 3) / 4;
+    const uint64_t items = (tiles + TPW - 1) / TPW;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kOtCcWaves;
+    uint32_t dc = 0;
+#pragma unroll
+    for (int b = 0; b < K; b++) {
+        const uint32_t i = b * NC + c;
+        dc |= ((a.s[i >> 5] >> (i & 31)) & 1u) << b;
+    }
+    const uint4* leaf = a.ss_leaf + (size_t)(NC + c) * NL;
+    for (uint64_t it = (uint64_t)blockIdx.x * kOtCcWaves + wv; it < items; it += nwaves) {
+        const uint64_t j0 = TPW * it, j = j0 + tq;
+        const bool hi_ok = TPW == 1 || j0 + 1 < tiles;
+        uint32_t wr[K][16];
+#pragma unroll
+        for (int w = 0; w < 16; w++)
+#pragma unroll
+            for (int b = 0; b < K; b++) wr[b][w] = 0;
+#pragma unroll
+        for (uint32_t y = 1; y < NL; y += 2) {   // pairs (y, y + 1); y = NL - 1 alone
+            const bool two = y + 1 < NL;
+            uint32_t kk[2][4];
+            const uint4 l0 = leaf[y ^ dc], l1 = two ? leaf[(y + 1) ^ dc] : l0;
+            kk[0][0] = l0.x; kk[0][1] = l0.y; kk[0][2] = l0.z; kk[0][3] = l0.w;
+            kk[1][0] = l1.x; kk[1][1] = l1.y; kk[1][2] = l1.z; kk[1][3] = l1.w;
+            const uint64_t ctr[2] = {a.ctr_off / 4 + j, a.ctr_off / 4 + j};
+            uint32_t g[2][16];
+            if (two) {
+                cc_blocks<2>(kk, ctr, g);
+            } else {
+                uint32_t k1[1][4] = {{kk[0][0], kk[0][1], kk[0][2], kk[0][3]}};
+                const uint64_t c1[1] = {ctr[0]};
+                uint32_t g1[1][16];
+                cc_blocks<1>(k1, c1, g1);
+#pragma unroll
+                for (int w = 0; w < 16; w++) g[0][w] = g1[0][w];
+            }
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                if (q == 1 && !two) break;
+#pragma unroll
+                for (int w = 0; w < 16; w++)
+#pragma unroll
+                    for (int b = 0; b < K; b++)
+                        if (((y + q) >> b) & 1) wr[b][w] ^= g[q][w];
+            }
+        }
+        uint32_t u[16];
+        {   // U rows of the wave's tiles (contiguous), dealt to the lanes through the stage
+            const uint4* urun = a.U + j0 * (4 * NC);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t r = 16 * k + (lane >> 2), w = lane & 3;
+                if (k >= 2 && !hi_ok) break;
+                *reinterpret_cast<cc_v4*>(stage[wv] + kOtCcRowWords * r + 4 * w) =
+                    __builtin_nontemporal_load(reinterpret_cast<const cc_v4*>(urun + 64 * k + lane));
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint4 x = *reinterpret_cast<const uint4*>(stage[wv] + kOtCcRowWords * lane + 4 * w);
+                u[4 * w] = x.x;
+                u[4 * w + 1] = x.y;
+                u[4 * w + 2] = x.z;
+                u[4 * w + 3] = x.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int b = 0; b < K; b++) {
+            const uint32_t db = (dc >> b) & 1u;
+#pragma unroll
+            for (int w = 0; w < 16; w++) wr[b][w] ^= db ? u[w] : 0u;
+            cc_store_rows2(stage[wv], lane, wr[b], a.Q + ot_tmaj(b * NC, 4 * j0),
+                           a.Q + ot_tmaj(b * NC + (TPW == 1 ? 32 : 0), 4 * (j0 + TPW - 1)), hi_ok);
+        }
+    }
+}
+
 // ---- transpose-fused hashes (r02) ------------------------------------------------------------
 // The hashes read the 128 x m bit matrices (T, Q; tile-major) as row words and transpose on the fly, so
 // the separate transpose pass of r01 (k_ot_transpose: an HBM round trip of 32 B per OT, 7 % of the
@@ -679,13 +981,36 @@ static int ot_cc_grid(uint64_t items) {
 
 hipError_t launch_ot_recv_expand(const OtArgs& a, hipStream_t stream) {
     if (a.ctr_off % 4) return hipErrorInvalidValue;   // ChaCha counters per 512-OT tile
+    if (a.ss_k == 2 || a.ss_k == 4) {   // SoftSpoken: one wave per tile (k = 2) or tile pair (k = 4)
+        const uint64_t tiles = a.mp / 512;
+        if (a.ss_k == 2) hipLaunchKernelGGL(k_ss_recv_expand<2>, dim3(ot_cc_grid(tiles)), dim3(kOtCcThreads), 0, stream, a);
+        else hipLaunchKernelGGL(k_ss_recv_expand<4>, dim3(ot_cc_grid((tiles + 1) / 2)), dim3(kOtCcThreads), 0, stream, a);
+        return hipGetLastError();
+    }
+    if (a.ss_k > 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ot_recv_expand_cc, dim3(ot_cc_grid(2 * (a.mp / 512))), dim3(kOtCcThreads), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_ot_send_expand(const OtArgs& a, hipStream_t stream) {
     if (a.ctr_off % 4) return hipErrorInvalidValue;
+    if (a.ss_k == 2 || a.ss_k == 4) {
+        const uint64_t tiles = a.mp / 512;
+        if (a.ss_k == 2) hipLaunchKernelGGL(k_ss_send_expand<2>, dim3(ot_cc_grid(tiles)), dim3(kOtCcThreads), 0, stream, a);
+        else hipLaunchKernelGGL(k_ss_send_expand<4>, dim3(ot_cc_grid((tiles + 1) / 2)), dim3(kOtCcThreads), 0, stream, a);
+        return hipGetLastError();
+    }
+    if (a.ss_k > 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ot_send_expand_cc, dim3(ot_cc_grid(a.mp / 512)), dim3(kOtCcThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_ss_ggm(const OtArgs& a, hipStream_t stream) {
+    switch (a.ss_k) {
+        case 2: hipLaunchKernelGGL(k_ss_ggm<2>, dim3(1), dim3(64), 0, stream, a); break;
+        case 4: hipLaunchKernelGGL(k_ss_ggm<4>, dim3(1), dim3(64), 0, stream, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -50,13 +50,17 @@ def ot_extend(kc, choices, x0, x1=None, delta=None, base_seeds=None, base_choice
 
 
 def cot_extend(kc, mode: int, choices, base_seeds, base_choice, delta=None, mask: int = 0, ctr_off: int = 0,
-               transcript: bool = False):
+               transcript: bool = False, ss_k: int = 1):
     """Correlated OT extension on the GPU (fhh_cot_extend_host; the r05 protocol's two OTs, see
-    include/fhh.h FHH_COT_*): returns (sender_out, out) and, with transcript, (U, y).
+    include/fhh.h FHH_COT_*): returns (sender_out, out) and, with transcript, (U, y) — and with ss_k > 1
+    (r06, SoftSpoken OT extension with k = ss_k: fhh_cot_extend_ss_host) also the GGM corrections,
+    (U [128 / ss_k][ceil(m / 128)][16], y, corr [128 / ss_k][ss_k][2][16]).
     mode 1 (labels): sender_out = x0 [m][16] (x1 = x0 ^ delta), out [m][16]; mode 2 (FE share):
     sender values / out [m] u64 (the garbler's r1 = v + mask, the receiver's share); mode 3 (FieldElm,
     OT pairs with one choice): sender values / out [m/2][32] BlockPairs; mode 4 (FHH_COT_RAW, the labels
     OT since r05b): sender_out = q [m][16], out = t [m][16] = q ^ r s, no y (zeros)."""
+    if ss_k not in (1, 2, 4):
+        raise ValueError("cot_extend: ss_k must be 1, 2 or 4")
     from ._lib import FHH_COT_FE, FHH_COT_FE255, FHH_COT_LABELS
     if mode == FHH_COT_LABELS and delta is None:
         raise ValueError("cot_extend: the labels mode needs delta (x1 = x0 ^ delta)")
@@ -71,9 +75,15 @@ def cot_extend(kc, mode: int, choices, base_seeds, base_choice, delta=None, mask
         sx, out, y = np.zeros((m // 2, 32), np.uint8), np.zeros((m // 2, 32), np.uint8), np.zeros((m, 16), np.uint8)
     else:
         sx, out, y = np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8)
-    u = np.zeros((128, (m + 127) // 128, 16), np.uint8) if transcript else None
+    u = np.zeros((128 // ss_k, (m + 127) // 128, 16), np.uint8) if transcript else None
     u8 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
-    check(lib().fhh_cot_extend_host(kc.handle, m, mode, ptr(ch), ptr(d), int(mask) & 1, ptr(seeds), ptr(s), ctr_off,
-                                    u8(sx), u8(out), ptr(u) if transcript else None, u8(y) if transcript else None),
-          kc.handle)
-    return (sx, out, u, y) if transcript else (sx, out)
+    if ss_k == 1:
+        check(lib().fhh_cot_extend_host(kc.handle, m, mode, ptr(ch), ptr(d), int(mask) & 1, ptr(seeds), ptr(s),
+                                        ctr_off, u8(sx), u8(out), ptr(u) if transcript else None,
+                                        u8(y) if transcript else None), kc.handle)
+        return (sx, out, u, y) if transcript else (sx, out)
+    corr = np.zeros((128 // ss_k, ss_k, 2, 16), np.uint8) if transcript else None
+    check(lib().fhh_cot_extend_ss_host(kc.handle, ss_k, m, mode, ptr(ch), ptr(d), int(mask) & 1, ptr(seeds), ptr(s),
+                                       ctr_off, u8(sx), u8(out), ptr(u) if transcript else None,
+                                       u8(y) if transcript else None, ptr(corr) if transcript else None), kc.handle)
+    return (sx, out, u, y, corr) if transcript else (sx, out)

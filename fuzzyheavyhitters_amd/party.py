@@ -248,7 +248,7 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
                     chunk_children: int | None = None, chunk_bytes: int = 64 << 30,
                     level_log: list | None = None, base_ot_every: str = "level",
                     base_ot_workers: int | None = None, base_ot_ahead: int = 8,
-                    form: str = "table") -> TwoPartyResult:
+                    form: str = "table", ot_ss_k: int = 1) -> TwoPartyResult:
     """The leader's level loop (leader.rs:417-440) with the GC + OT of every level split between the
     two servers' ctxs (server 0 garbles / sends, server 1 evaluates / receives): crawl both, run the
     level's protocol through the channel, take each server's node sums from its own device
@@ -275,7 +275,10 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
     whole level), one protocol instance per chunk. `level_log` (a list) receives one (level, children,
     crawl_s, gcot_s, node_sums_s) tuple per level. `form`: "table" (the FE levels' test as one garbled
     table where 2d <= 4, r05d) or "circuit" (the half-gates circuit at every level, r05c) — a public
-    protocol choice both parties make alike."""
+    protocol choice both parties make alike. `ot_ss_k` (r06, public like form): 1 = IKNP OT extension, 2 / 4 =
+    SoftSpoken with k = ot_ss_k (the U messages carry 128 / k rows + the GGM corrections)."""
+    if ot_ss_k not in (1, 2, 4):
+        raise ValueError(f"two_party_crawl: ot_ss_k {ot_ss_k!r}")
     if material not in ("fresh", "test"):
         raise ValueError(f"two_party_crawl: material {material!r}")
     if form not in ("table", "circuit"):
@@ -362,6 +365,7 @@ def two_party_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, ncli
                         cfg_gb.child_begin, cfg_gb.child_count = cb, cc
                         cfg_ev.child_begin, cfg_ev.child_count = cb, cc
                         cfg_gb.form = cfg_ev.form = form_id
+                    cfg_gb.ot_ss_k = cfg_ev.ot_ss_k = ot_ss_k
                     for name, v in run_chunk(a, b, cfg_gb, cfg_ev, to_gb, to_ev).items():
                         sizes[name] = sizes.get(name, 0) + v
             res.level_bytes.append(sizes)

@@ -62,7 +62,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
               init_capacity: int = 0, comm=None, gc=False, probe: dict | None = None,
-              base_ot: bool = False) -> SimResult:
+              base_ot: bool = False, ot_ss_k: int = 1) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
@@ -71,11 +71,14 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     test (server 0 garbles, server 1 evaluates) instead of comparing shares: `True` / "ot" with
     the evaluator's labels and the FE shares moved by the GPU OT extension (base OTs ideal),
     "ideal" with both OTs ideal; "ot-circuit" as "ot" but the half-gates circuit (+ the output-label
-    share) at every level instead of the FE levels' garbled table.
+    share) at every level instead of the FE levels' garbled table. `ot_ss_k` (gc "ot" / "ot-circuit", r06):
+    1 = IKNP OT extension, 2 / 4 = SoftSpoken with k = ot_ss_k (128 / k rows of U on the wire).
 
     `probe` (parity tests) = {"levels": [...], "clients": [...], "capacity": C_max}: the device
     loop gathers those clients' EvalStates of every pending child right after each listed
     level's k_expand (res.probe)."""
+    if ot_ss_k not in (1, 2, 4):
+        raise ValueError("sim_crawl: ot_ss_k must be 1 (IKNP), 2 or 4 (SoftSpoken)")
     L = levels or c0.depth
     n_local = c0.num_clients()
     cfg = FhhSimConfig()
@@ -88,6 +91,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.init_capacity = init_capacity
     cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2, "ot-circuit": 3}[gc]
     cfg.base_ot = 1 if base_ot else 0   # gc = "ot": Chou–Orlandi base OTs on the host (else ideal)
+    cfg.ot_ss_k = ot_ss_k
     ar = None
     if comm is not None:
         cfg.comm = comm.handle

@@ -305,6 +305,10 @@ typedef struct fhh_sim_config {
      * time; base_ot_stall_ms: the time the loop waited for them) and uploaded as key schedules
      * before the level's OTs. */
     uint32_t base_ot;
+    /* gc >= 2 (r06): the OT extension of both OT kinds — 0 or 1 = IKNP (128 rows of U: 16 B per OT on the
+     * wire), 2 or 4 = SoftSpoken with k = ot_ss_k (fhh_cot_extend_ss_host: 128 / k rows, 16 / k B per OT,
+     * 2^k - 1 ChaCha12 blocks per chunk and tile at the sender). Same sums. */
+    uint32_t ot_ss_k;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x
@@ -530,6 +534,17 @@ int fhh_ot_extend_host(fhh_ctx* ctx, uint64_t m, const uint8_t* choices, const u
 int fhh_cot_extend_host(fhh_ctx* ctx, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
                         uint32_t mask, const uint8_t base_seeds[128 * 2 * 16], const uint8_t base_choice[16],
                         uint64_t ctr_off, uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out);
+/* r06: the same on SoftSpoken OT extension (Roy, CRYPTO 2022; semi-honest small-field VOLE, repetition code)
+ * with k = ss_k base OTs per chunk (1 = IKNP, exactly fhh_cot_extend_host; 2, 4): chunk c's k base OTs
+ * become a (2^k - 1)-out-of-2^k OT of GGM leaf seeds, and the receiver's message U has 128 / k rows
+ * (u_out [128 / ss_k][ceil(m / 128)][16]: 16 / k bytes per OT instead of 16) plus the GGM corrections
+ * corr_out [128 / ss_k][ss_k][2][16] (4 KiB per base-OT session). The correlation q_j = t_j ^ r_j s with
+ * s = base_choice is IKNP's, so the modes are unchanged. Restated in oracle/fhh_oracle.c cot_rows / ss_ggm
+ * (tree PRG, masks and root derivation there). */
+int fhh_cot_extend_ss_host(fhh_ctx* ctx, uint32_t ss_k, uint64_t m, uint32_t mode, const uint8_t* choices,
+                           const uint8_t delta[16], uint32_t mask, const uint8_t base_seeds[128 * 2 * 16],
+                           const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* sender_out, uint8_t* out,
+                           uint8_t* u_out, uint8_t* y_out, uint8_t* corr_out);
 /* The labels step of one batch on host buffers: the labels OT (FHH_COT_RAW since r05b: choice bits =
  * the evaluator's bits at OT index j npad + i, npad = n rounded up to 64; the evaluator's zero labels
  * E_j = q_j, its active labels t_j, Delta = the sender's s, whose bit 0 must be 1), garbling with the
@@ -621,12 +636,17 @@ typedef struct fhh_gb_cfg {
                                             kind's s is the free-XOR Delta: its bit 0 must be 1   */
     uint64_t child_begin;
     uint64_t child_count;
+    uint32_t ot_ss_k;                    /* r06: the OT extension of both kinds, as the evaluator's:
+                                            0 / 1 IKNP, 2 / 4 SoftSpoken (fhh_cot_extend_ss_host) */
+    uint32_t pad_;
 } fhh_gb_cfg;
 typedef struct fhh_ev_cfg {
     uint8_t base_pairs[2][128][2][16];   /* per OT kind: both base-OT keys of every base OT (kind 1
                                             read at tree_crawl_last only, r05c)                    */
     uint32_t form;                       /* as fhh_gb_cfg.form (the public protocol choice)       */
-    uint32_t pad_;
+    uint32_t ot_ss_k;                    /* r06: 0 / 1 IKNP, 2 / 4 SoftSpoken with k = ot_ss_k: the
+                                            U messages carry 128 / k rows + 4 KiB of GGM
+                                            corrections (u_bytes = 16 mp / k + 4096)              */
     uint64_t child_begin;
     uint64_t child_count;
 } fhh_ev_cfg;

@@ -1527,18 +1527,158 @@ static void limbs_to_be32(const uint32_t v[8], uint8_t* be) {
     }
 }
 
-void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16], uint32_t mask,
-                    const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t ctr_off, uint8_t* sender_out,
-                    uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
-    oracle_init();
-    mask &= 1;
+/* ------------------------------------------------------------------ */
+/* r06: SoftSpoken OT extension (L. Roy, "SoftSpoken OT", CRYPTO     */
+/* 2022: small-field subspace VOLE with the repetition code, the      */
+/* semi-honest form, no consistency check). The 128 base OTs are cut  */
+/* into n_c = 128 / k chunks of k; chunk c turns its k OTs into a     */
+/* (2^k - 1)-out-of-2^k OT of leaf seeds by a GGM tree, and the row   */
+/* matrices come from the 2^k leaves:                                 */
+/*   receiver: u_c = XOR_x G(leaf_x),  v_c[b] = XOR_{x: x_b = 1}      */
+/*             G(leaf_x) (b < k);  U_c = u_c ^ r on the wire          */
+/*   sender (Delta_c, every leaf but x = Delta_c):                    */
+/*             w_c[b] = XOR_{x != Delta_c} (x ^ Delta_c)_b G(leaf_x)  */
+/*                      ^ (Delta_c)_b U_c  =  v_c[b] ^ (Delta_c)_b r  */
+/* so with t row i = v_c[b], q row i = w_c[b] for i = b n_c + c (row  */
+/* order bit-major) and s bit i = (Delta_c)_b, q_j = t_j ^ r_j s: the */
+/* IKNP correlation every mode below consumes, for 128 / k rows of U  */
+/* (16 / k bytes per OT on the wire instead of 16). k = 1 is IKNP.    */
+/* GGM (one per chunk): root = ChaCha12(k_c^0 || k_c^1, ctr c, nonce  */
+/* 3)[0..15] (the receiver holds both, the sender one); node -> (left, */
+/* right) = ChaCha12(node || node, ctr 0, nonce 1)[0..31]; the leaf   */
+/* index x takes bit l - 1 at level l. Level l's correction of side   */
+/* beta = XOR of the level's nodes with bit l - 1 = beta, masked with */
+/* ChaCha12(k || k, 0, nonce 2)[0..15] of k = k_i^{1 - beta},         */
+/* i = (l - 1) n_c + c: the sender (k_i^{s_i}) unmasks side 1 - s_i,  */
+/* the sibling of its path, and rebuilds every leaf but Delta_c.      */
+/* Rows: G(leaf) = ChaCha12 as IKNP's row PRG (key leaf || leaf,      */
+/* counter ctr_off / 4 + tile, nonce 0). corr [n_c][k][2][16].        */
+/* Parity: functional (q = t ^ r s; the GPU's matrices bit-exact);    */
+/* the scheme is restated from the paper, no reference code.          */
+/* ------------------------------------------------------------------ */
+static void ss_cc16(const uint8_t a[16], const uint8_t b[16], uint64_t ctr, uint64_t nonce, uint8_t* out, size_t n) {
+    uint8_t key[32], blk[64];
+    memcpy(key, a, 16);
+    memcpy(key + 16, b, 16);
+    orc_chacha_block(OT_CHACHA_ROUNDS, key, ctr, nonce, blk);
+    memcpy(out, blk, n);
+}
+
+/* chunk c's GGM: leaf_r [2^k][16] (receiver), leaf_s [2^k][16] (sender; x = Delta_c zero), corr [k][2][16] */
+static void ss_ggm(uint32_t k, uint32_t c, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint8_t* leaf_r,
+                   uint8_t* leaf_s, uint8_t* corr) {
+    const uint32_t nc = 128 / k, nl = 1u << k;
+    uint8_t node[16 * 16], nxt[16 * 16];
+    ss_cc16(seeds + (c * 2 + 0) * 16, seeds + (c * 2 + 1) * 16, c, 3, node, 16);
+    for (uint32_t l = 1; l <= k; l++) {
+        const uint32_t half = 1u << (l - 1), i = (l - 1) * nc + c;
+        uint8_t K[2][16] = {{0}};
+        for (uint32_t z = 0; z < half; z++) {
+            uint8_t lr[32];
+            ss_cc16(node + 16 * z, node + 16 * z, 0, 1, lr, 32);
+            memcpy(nxt + 16 * z, lr, 16);
+            memcpy(nxt + 16 * (z | half), lr + 16, 16);
+            for (int q = 0; q < 16; q++) {
+                K[0][q] ^= lr[q];
+                K[1][q] ^= lr[16 + q];
+            }
+        }
+        for (int beta = 0; beta < 2; beta++) {
+            uint8_t msk[16];
+            ss_cc16(seeds + (i * 2 + (1 - beta)) * 16, seeds + (i * 2 + (1 - beta)) * 16, 0, 2, msk, 16);
+            for (int q = 0; q < 16; q++) corr[((l - 1) * 2 + beta) * 16 + q] = K[beta][q] ^ msk[q];
+        }
+        memcpy(node, nxt, 16 * 2 * half);
+    }
+    memcpy(leaf_r, node, 16 * nl);
+    /* the sender: path Delta_c, knows k_i^{s_i} of every level */
+    uint32_t dc = 0;
+    for (uint32_t b = 0; b < k; b++) dc |= (uint32_t)((s[(b * nc + c) / 8] >> ((b * nc + c) % 8)) & 1) << b;
+    uint8_t kn[16 * 16];
+    memset(kn, 0, sizeof kn);
+    for (uint32_t l = 1; l <= k; l++) {
+        const uint32_t half = 1u << (l - 1), i = (l - 1) * nc + c, db = (dc >> (l - 1)) & 1;
+        const uint32_t path = dc & (half - 1);   /* the level-(l-1) node on the path (unknown) */
+        uint8_t nk[16 * 16];
+        memset(nk, 0, sizeof nk);
+        uint8_t K[16], msk[16];
+        const uint8_t* ks = seeds + (i * 2 + db) * 16;   /* k_i^{s_i} */
+        ss_cc16(ks, ks, 0, 2, msk, 16);
+        for (int q = 0; q < 16; q++) K[q] = corr[((l - 1) * 2 + (1 - db)) * 16 + q] ^ msk[q];
+        for (uint32_t z = 0; z < half; z++) {
+            if (l > 1 && z == path) continue;
+            uint8_t lr[32];
+            if (l == 1) continue;
+            ss_cc16(kn + 16 * z, kn + 16 * z, 0, 1, lr, 32);
+            memcpy(nk + 16 * z, lr, 16);
+            memcpy(nk + 16 * (z | half), lr + 16, 16);
+            const uint8_t* side = (1 - db) ? lr + 16 : lr;
+            for (int q = 0; q < 16; q++) K[q] ^= side[q];
+        }
+        memcpy(nk + 16 * (path | ((1 - db) << (l - 1))), K, 16);   /* the sibling of the path */
+        memcpy(kn, nk, 16 * 2 * half);
+    }
+    memcpy(leaf_s, kn, 16 * nl);
+    memset(leaf_s + 16 * dc, 0, 16);
+}
+
+/* the row matrices T, Q [128][nblk][16] and U [128 / k][nblk][16] (row form) of m OTs; corr (k > 1)
+ * [n_c][k][2][16] */
+static void cot_rows(uint32_t k, uint64_t m, const uint8_t* choices, const uint8_t seeds[128 * 2 * 16],
+                     const uint8_t s[16], uint64_t ctr_off, uint8_t* T, uint8_t* Q, uint8_t* U, uint8_t* corr) {
     const uint64_t nblk = (m + 127) / 128;
-    uint8_t* T = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
-    uint8_t* Q = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
-    uint8_t* U = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
-    uint8_t* H0 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j) */
-    uint8_t* H1 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j ^ s) */
-    uint8_t* HT = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(t_j) */
+    if (k > 1) {
+        const uint32_t nc = 128 / k, nl = 1u << k;
+        const uint64_t tiles = (nblk + 3) / 4;
+#pragma omp parallel for schedule(static)
+        for (int c = 0; c < (int)nc; c++) {
+            uint8_t leaf_r[16 * 16], leaf_s[16 * 16];
+            ss_ggm(k, (uint32_t)c, seeds, s, leaf_r, leaf_s, corr + (size_t)c * k * 32);
+            uint32_t dc = 0;
+            for (uint32_t b = 0; b < k; b++) dc |= (uint32_t)((s[(b * nc + c) / 8] >> ((b * nc + c) % 8)) & 1) << b;
+            for (uint64_t J = 0; J < tiles; J++) {
+                uint8_t g[64], u[64] = {0}, v[4][64], w[4][64];
+                memset(v, 0, sizeof v);
+                memset(w, 0, sizeof w);
+                for (uint32_t x = 0; x < nl; x++) {
+                    ss_cc16(leaf_r + 16 * x, leaf_r + 16 * x, ctr_off / 4 + J, 0, g, 64);
+                    for (int q = 0; q < 64; q++) u[q] ^= g[q];
+                    for (uint32_t b = 0; b < k; b++)
+                        if ((x >> b) & 1)
+                            for (int q = 0; q < 64; q++) v[b][q] ^= g[q];
+                    if (x == dc) continue;
+                    ss_cc16(leaf_s + 16 * x, leaf_s + 16 * x, ctr_off / 4 + J, 0, g, 64);
+                    for (uint32_t b = 0; b < k; b++)
+                        if (((x ^ dc) >> b) & 1)
+                            for (int q = 0; q < 64; q++) w[b][q] ^= g[q];
+                }
+                for (uint32_t wd = 0; wd < 4; wd++) {
+                    const uint64_t cb = 4 * J + wd;
+                    if (cb >= nblk) break;
+                    uint8_t r[16];
+                    for (int q = 0; q < 16; q++) {
+                        r[q] = 0;
+                        for (int bt = 0; bt < 8; bt++) {
+                            const uint64_t j = cb * 128 + (uint64_t)q * 8 + bt;
+                            if (j < m && ((choices[j / 8] >> (j % 8)) & 1)) r[q] |= (uint8_t)(1u << bt);
+                        }
+                    }
+                    uint8_t* uc = U + ((uint64_t)c * nblk + cb) * 16;
+                    for (int q = 0; q < 16; q++) uc[q] = u[16 * wd + q] ^ r[q];
+                    for (uint32_t b = 0; b < k; b++) {
+                        const uint64_t i = (uint64_t)b * nc + c;
+                        uint8_t* t = T + (i * nblk + cb) * 16;
+                        uint8_t* qq = Q + (i * nblk + cb) * 16;
+                        for (int q = 0; q < 16; q++) {
+                            t[q] = v[b][16 * wd + q];
+                            qq[q] = w[b][16 * wd + q] ^ (((dc >> b) & 1) ? uc[q] : 0);
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < 128; i++) {
         uint8_t rk0[176], rk1[176], rks[176];
@@ -1564,9 +1704,28 @@ void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uin
             }
             ot_prg_block(1, seeds + (i * 2 + si) * 16, rks, ctr_off + c, gs, &cc[2]);
             uint8_t* q = Q + ((uint64_t)i * nblk + c) * 16;
-            for (int k = 0; k < 16; k++) q[k] = gs[k] ^ (si ? u[k] : 0);
+            for (int kk = 0; kk < 16; kk++) q[kk] = gs[kk] ^ (si ? u[kk] : 0);
         }
     }
+}
+
+/* ss_k = 1: IKNP (orc_cot_extend); 2 / 4: SoftSpoken (cot_rows), u_out [128 / ss_k][nblk][16], corr_out
+ * [128 / ss_k][ss_k][2][16] (ss_k > 1) */
+void orc_cot_extend_ss(uint32_t ss_k, uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16],
+                       uint32_t mask, const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t ctr_off,
+                       uint8_t* sender_out, uint8_t* out, uint8_t* u_out, uint8_t* y_out, uint8_t* corr_out) {
+    oracle_init();
+    mask &= 1;
+    const uint64_t nblk = (m + 127) / 128;
+    uint8_t* T = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* Q = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* U = (uint8_t*)calloc(128 * nblk * 16 + 16, 1);
+    uint8_t* H0 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j) */
+    uint8_t* H1 = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(q_j ^ s) */
+    uint8_t* HT = (uint8_t*)calloc(m * 16 + 16, 1);   /* H(t_j) */
+    uint8_t corr[128 * 2 * 16];
+    cot_rows(ss_k, m, choices, seeds, s, ctr_off, T, Q, U, corr);
+    if (corr_out && ss_k > 1) memcpy(corr_out, corr, (size_t)128 * 2 * 16);
 #pragma omp parallel for schedule(static)
     for (int64_t j = 0; j < (int64_t)m; j++) {
         uint8_t qj[16] = {0}, tj[16] = {0}, qs[16];
@@ -1632,11 +1791,17 @@ void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uin
             for (int k = 0; k < 32; k++) out[t * 32 + k] = (rj ? y[k] : 0) ^ HT[2 * t * 16 + k];
         }
     }
-    if (u_out) memcpy(u_out, U, 128 * nblk * 16);
+    if (u_out) memcpy(u_out, U, (128 / ss_k) * nblk * 16);
     free(T);
     free(Q);
     free(U);
     free(H0);
     free(H1);
     free(HT);
+}
+
+void orc_cot_extend(uint64_t m, uint32_t mode, const uint8_t* choices, const uint8_t delta[16], uint32_t mask,
+                    const uint8_t seeds[128 * 2 * 16], const uint8_t s[16], uint64_t ctr_off, uint8_t* sender_out,
+                    uint8_t* out, uint8_t* u_out, uint8_t* y_out) {
+    orc_cot_extend_ss(1, m, mode, choices, delta, mask, seeds, s, ctr_off, sender_out, out, u_out, y_out, NULL);
 }

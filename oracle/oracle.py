@@ -830,3 +830,30 @@ def cot_extend(mode: int, choices: np.ndarray, seeds: np.ndarray, s: bytes, delt
                          ctypes.c_uint32(mask & 1), _p(sd), _p(sv), ctypes.c_uint64(ctr_off),
                          sx.ctypes.data_as(u8p), out.ctypes.data_as(u8p), _p(u), y.ctypes.data_as(u8p))
     return sx, out, u, y
+
+
+def cot_extend_ss(ss_k: int, mode: int, choices: np.ndarray, seeds: np.ndarray, s: bytes, delta: bytes | None = None,
+                  mask: int = 0, ctr_off: int = 0):
+    """cot_extend on SoftSpoken OT extension with k = ss_k bits per chunk (fhh_oracle.c cot_rows / ss_ggm;
+    ss_k = 1 is IKNP). Returns (sender_out, out, U [128 / ss_k][nblk][16], y, corr [128 / ss_k][ss_k][2][16]):
+    U and the GGM corrections are the receiver's messages."""
+    assert ss_k in (1, 2, 4)
+    ch = np.packbits(np.asarray(choices, np.uint8) & 1, bitorder="little")
+    m = len(choices)
+    sd = np.ascontiguousarray(seeds, np.uint8)
+    sv = np.frombuffer(s, np.uint8).copy()
+    dl = np.frombuffer(delta if delta is not None else bytes(16), np.uint8).copy()
+    nblk = (m + 127) // 128
+    u = np.zeros((128 // ss_k, nblk, 16), np.uint8)
+    corr = np.zeros((128 // ss_k, ss_k, 2, 16), np.uint8)
+    if mode == COT_FE:
+        sx, out, y = np.zeros(m, np.uint64), np.zeros(m, np.uint64), np.zeros(m, np.uint64)
+    elif mode == COT_FE255:
+        sx, out, y = np.zeros((m // 2, 32), np.uint8), np.zeros((m // 2, 32), np.uint8), np.zeros((m, 16), np.uint8)
+    else:
+        sx, out, y = np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8), np.zeros((m, 16), np.uint8)
+    lib().orc_cot_extend_ss(ctypes.c_uint32(ss_k), ctypes.c_uint64(m), ctypes.c_uint32(mode),
+                            _p(np.ascontiguousarray(ch)), _p(dl), ctypes.c_uint32(mask & 1), _p(sd), _p(sv),
+                            ctypes.c_uint64(ctr_off), sx.ctypes.data_as(u8p), out.ctypes.data_as(u8p), _p(u),
+                            y.ctypes.data_as(u8p), _p(corr))
+    return sx, out, u, y, corr

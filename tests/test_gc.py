@@ -172,6 +172,33 @@ def test_gpu_crawl_with_gc_equals_plain(kind, gc_mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ss_k", [2, 4])
+@pytest.mark.parametrize("gc_mode", ["ot", "ot+co15", "ot-circuit"])
+@pytest.mark.parametrize("kind", ["zipf_d1", "coords_d2"])
+def test_gpu_crawl_with_softspoken_equals_plain(kind, gc_mode, ss_k):
+    """r06: both OT kinds of every level on SoftSpoken OT extension (k = 2, 4: 128 / k rows of U) give the
+    same sums, keep decisions and heavy hitters as the plaintext harness, with ideal and with real
+    Chou-Orlandi base OTs, the garbled table (d = 1: tile-major, d = 2: row form) and the circuit."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    if kind == "zipf_d1":
+        wl = workload.zipf_workload(3000, 64, 1, num_sites=40, seed=5)
+    else:
+        wl = workload.coords_workload(1500, ball_size=3, num_centroids=40, side_km=4.0)
+    c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    plain = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=9)
+    got = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=9, gc=gc_mode.split("+")[0], init_capacity=2,
+                    base_ot=gc_mode.endswith("co15"), ot_ss_k=ss_k)
+    assert _sig(got) == _sig(plain)
+    assert len(got.final) > 0
+
+
+def test_sim_crawl_rejects_bad_ss_k():
+    from fuzzyheavyhitters_amd import sim_crawl
+    with pytest.raises(ValueError):
+        sim_crawl(None, None, 0.01, mode="fe", gc="ot", ot_ss_k=3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("gc_mode", ["ideal", "ot", "ot+co15", "ot-circuit"])
 def test_gpu_crawl_with_gc_in_chunks(monkeypatch, gc_mode):
     """A level's GC + OT split into chunks of children, each a fresh protocol instance (the

@@ -90,3 +90,12 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
         assert k["ScratchSize [bytes/lane]"] == "0", (name, k)
         assert k["VGPRs Spill"] == "0", (name, k)
         assert int(k["Occupancy [waves/SIMD]"]) >= 4, (name, k)
+    # r06 SoftSpoken (k = 2, 4): the GGM trees and both expands stay in registers; k = 4 keeps 4 / 3 row sums
+    # of 16 words beside two ChaCha blocks (occupancy 2-3 at 256-thread workgroups, VALU-bound)
+    for name in [f"_ZN3fhh{len(f'k_ss_{r}')}k_ss_{r}ILi{k}EEEvNS_6OtArgsE" for r in ("ggm", "recv_expand", "send_expand")
+                 for k in (2, 4)]:
+        assert name in u, f"{name} not found"
+        k = u[name]
+        assert k["ScratchSize [bytes/lane]"] == "0", (name, k)
+        assert k["VGPRs Spill"] == "0", (name, k)
+        assert int(k["Occupancy [waves/SIMD]"]) >= 2, (name, k)

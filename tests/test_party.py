@@ -67,6 +67,36 @@ def test_two_party_equals_in_process_gc_ot(d, n, L, thr, channel, material):
     assert lbl["gc"] == Cl * n * (2 * (bits - 1) * 16 + 1) and lbl["y2"] == Cl * n * 2 * 16
 
 
+@pytest.mark.parametrize("ss_k", [2, 4])
+@pytest.mark.parametrize("form", ["table", "circuit"])
+@pytest.mark.parametrize("d,n,L,thr", [(1, 300, 20, 0.02), (2, 200, 12, 0.05)], ids=["d1", "d2"])
+def test_two_party_softspoken(d, n, L, thr, form, ss_k):
+    """r06: both parties on SoftSpoken OT extension (ot_ss_k = 2, 4; each its own material and CO15 base
+    OTs over the channel) equal the in-process SoftSpoken crawl and the IKNP run level by level; the U
+    messages shrink to 128 / k rows plus 4 KiB of GGM corrections."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import workload
+    wl = workload.zipf_workload(n, 32, d, num_sites=5, seed=60 + d)
+    wl.left, wl.right = wl.left[:, :, :L].copy(), wl.right[:, :, :L].copy()
+    gc = "ot" if form == "table" else "ot-circuit"
+    c0, c1 = _keys(wl, L, d)
+    ref = fhh.sim_crawl(c0, c1, thr, mode="fe", prf_seed=5, gc=gc, ot_ss_k=ss_k)
+    p0, p1 = _keys(wl, L, d)
+    got = fhh.two_party_crawl(p0, p1, thr, form=form, ot_ss_k=ss_k)
+    _assert_same_crawl(ref, got)
+    t0, t1 = _keys(wl, L, d)
+    iknp = fhh.two_party_crawl(t0, t1, thr, form=form)
+    _assert_same_crawl(iknp, got)
+    bits = 2 * d
+    for lv, (a, b) in enumerate(zip(got.level_bytes, iknp.level_bytes)):
+        C = int(got.level_children[lv])
+        for key in ("u1", "u2"):
+            if b.get(key, 0):
+                assert a[key] == b[key] // ss_k + 4096, (lv, key)
+        assert a["gc"] == b["gc"] and a["y2"] == b["y2"]
+    assert len(got.final) > 0
+
+
 @pytest.mark.parametrize("d,n,L,thr", [(1, 300, 20, 0.02), (2, 200, 12, 0.05)], ids=["d1", "d2"])
 def test_two_party_circuit_form(d, n, L, thr):
     """form="circuit" (both parties: the half-gates circuit + output-label share at every FE level,

@@ -21,13 +21,14 @@ def test_chunk_windows_cover_the_level_in_order(C, chunk):
 
 def test_party_cfg_layouts_match_header():
     """fhh_gb_cfg / fhh_ev_cfg (include/fhh.h): the ctypes mirrors have the C layout (no padding on
-    x86-64: every field is naturally aligned), the chunk window last."""
+    x86-64: every field is naturally aligned), the chunk window last (the garbler's: before r06's ot_ss_k)."""
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
-    gb = 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8
+    gb = 4 + 4 + 2 * 128 * 16 + 2 * 16 + 8 + 8 + 4 + 4
     ev = 2 * 128 * 2 * 16 + 4 + 4 + 8 + 8
     assert ctypes.sizeof(FhhGbCfg) == gb and ctypes.sizeof(FhhEvCfg) == ev
-    for T, size in ((FhhGbCfg, gb), (FhhEvCfg, ev)):
-        assert T.child_begin.offset == size - 16 and T.child_count.offset == size - 8
+    assert FhhGbCfg.ot_ss_k.offset == gb - 8 and FhhEvCfg.ot_ss_k.offset == ev - 20
+    for T, end in ((FhhGbCfg, gb - 8), (FhhEvCfg, ev)):
+        assert T.child_begin.offset == end - 16 and T.child_count.offset == end - 8
         cfg = T()
         assert cfg.child_begin == 0 and cfg.child_count == 0   # zero-initialised: the whole level
 
@@ -41,7 +42,8 @@ def test_evaluator_cfg_carries_no_garbler_secret():
     from fuzzyheavyhitters_amd._lib import FhhEvCfg, FhhGbCfg
     ev_fields = {f for f, _ in FhhEvCfg._fields_}
     gb_fields = {f for f, _ in FhhGbCfg._fields_}
-    assert ev_fields == {"base_pairs", "form", "pad_", "child_begin", "child_count"}   # form: public
+    # form, ot_ss_k: public protocol choices
+    assert ev_fields == {"base_pairs", "form", "ot_ss_k", "child_begin", "child_count"}
     for secret in ("mask", "base_chosen", "base_choice"):
         assert secret in gb_fields and secret not in ev_fields
     assert "delta" not in gb_fields | ev_fields

@@ -412,11 +412,18 @@ def dropin_bench(args, world, rank, local_rank, dist):
 
     runs = {}
 
+    cold = {}
+
     def timed(fn, reps, warm=1):
-        for _ in range(warm):
+        for w in range(warm):
+            torch.cuda.synchronize()
             t0 = time.perf_counter()
             fn()
-            print(f"dropin:   warm-up run {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if w == 0:
+                cold[id(fn)] = dt   # the first crawl on fresh collections: every buffer allocated on the way
+            print(f"dropin:   warm-up run {dt:.2f} s", file=sys.stderr, flush=True)
         times, out = [], None
         for _ in range(reps):
             torch.cuda.synchronize()
@@ -443,7 +450,9 @@ def dropin_bench(args, world, rank, local_rank, dist):
                                "base OTs", "parallelism": "single GPU"},
     }
     c0, c1 = pair()
-    fused_fn = lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False)  # noqa: E731
+    ssk = args.protocol_ot_ss_k
+    fused_fn = lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False,  # noqa: E731
+                                     ot_ss_k=ssk)
     t_fused, res = timed(fused_fn, reps, warm)
     fused_runs = runs[id(fused_fn)]
     hh = len(res.final)
@@ -451,6 +460,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
     print(f"dropin: fused protocol crawl {t_fused:.2f} s, {hh} heavy hitters", file=sys.stderr, flush=True)
 
     leg_runs = {}
+    leg_cold = {}
 
     def dropin_leg(devices=None, channel="inplace"):
         p0, p1 = pair(devices)
@@ -460,11 +470,12 @@ def dropin_bench(args, world, rank, local_rank, dist):
         def run():
             tm.clear()
             r = fhh.two_party_crawl(p0, p1, args.threshold, channel=channel, timing=tm, record=False,
-                                    material="fresh")
+                                    material="fresh", ot_ss_k=ssk)
             last["r"] = r
             return r
         t, r = timed(run, reps, warm)
         leg_runs[(tuple(devices) if devices else None, channel)] = runs[id(run)]
+        leg_cold[(tuple(devices) if devices else None, channel)] = cold.get(id(run))
         assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
         tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
         tot["base_ot"] = r.base_ot_bytes
@@ -478,10 +489,14 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "fused_protocol_crawl_s": t_fused, "dropin_crawl_s": t_d, "dropin_over_fused": t_d / t_fused,
         "timing_stat": "median of the timed runs per leg (every run listed in *_runs_s)",
         "fused_runs_s": fused_runs, "dropin_runs_s": leg_runs[(None, "inplace")],
+        "fused_cold_crawl_s": cold.get(id(fused_fn)), "dropin_cold_crawl_s": leg_cold[(None, "inplace")],
+        "dropin_cold_over_warm": (leg_cold[(None, "inplace")] / t_d) if leg_cold[(None, "inplace")] else None,
+        "cold_note": "cold = the first (warm-up) crawl on freshly built collections, buffers allocated as the crawl grows",
         "dropin_ms_per_level": per_d,
         "dropin_overhead_ms_per_level": (t_d - t_fused) / L * 1e3,
         "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",
         "channel_bytes_per_crawl": bytes_d, "channel_bytes_total": sum(bytes_d.values()),
+        "ot_extension": "IKNP" if ssk == 1 else f"SoftSpoken k={ssk} (--protocol-ot-ss-k)",
         "heavy_hitters": hh,
         "dropin_material": "each server its own (os.urandom: mask per chunk; Delta = the labels base-OT run's s, one "
                            "per level, the chunks kept apart by disjoint row-PRG ranges and the gate tweaks; CO15 "
@@ -990,8 +1005,12 @@ def main():
                     help="skip the second protocol crawl with the half-gates circuit at every level")
     ap.add_argument("--ot-ss-k", type=int, default=1, choices=(1, 2, 4),
                     help="--gc ot: the OT extension of the timed crawl (1 IKNP, 2 / 4 SoftSpoken)")
-    ap.add_argument("--protocol-ss-k", default="4",
-                    help="comma list of SoftSpoken k (2, 4) to run the protocol crawl with beside IKNP ('' = none)")
+    ap.add_argument("--protocol-ot-ss-k", type=int, default=2, choices=(1, 2, 4),
+                    help="the protocol crawl's OT extension: 1 IKNP, 2 / 4 SoftSpoken (default 2: half of IKNP's U "
+                         "bytes for ~1.5x the sender's ChaCha work, profiles/r06/softspoken/)")
+    ap.add_argument("--protocol-ss-k", default="1,4",
+                    help="comma list of further OT extensions (1 IKNP, 2 / 4 SoftSpoken) to run the protocol crawl "
+                         "with beside it ('' = none)")
     ap.add_argument("--no-protocol-crawl", action="store_true",
                     help="skip the real protocol's crawl (GC + OT + real base OTs every level) that follows the "
                          "headline's timed region on the zipf workload")
@@ -1169,23 +1188,28 @@ def main():
     expand_rate = (s0["expand_blocks_timed"] / launches0) / (s0["expand_ms"] / launches0 / 1e3) if s0["expand_ms"] else None
     proto = None
     if run_proto:
-        proto = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate)
+        proto = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate,
+                               ot_ss_k=args.protocol_ot_ss_k)
         proto["output_equal_golden"] = sig_equal(proto.pop("sig"), gold) if gold else None
         if not args.no_protocol_circuit:
             # the same crawl with the half-gates circuit at every level (the reference's construction,
             # r05c form) beside the default garbled table: what the table buys, on the same box
-            circ = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, gc="ot-circuit", expand_rate=expand_rate)
+            circ = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, gc="ot-circuit", expand_rate=expand_rate,
+                                  ot_ss_k=args.protocol_ot_ss_k)
             proto["circuit_form"] = {k: circ[k] for k in ("wall_s", "heavy_hitters", "heavy_hitters_equal_headline",
                                                           "gcot_gpu_ms", "expand_gpu_ms", "protocol", "roofline",
                                                           "channel_bytes")}
-        # r06: the same crawl on SoftSpoken OT extension (fewer rows of U on the wire, more ChaCha work)
-        proto["softspoken"] = {}
+        # r06: the same crawl on the other OT extensions (IKNP: 128 rows of U; SoftSpoken k: 128 / k rows of U,
+        # 2^k ChaCha12 blocks per chunk and tile) — the wire bytes against the GPU time
+        proto["ot_extension_forms"] = {}
         for k in [int(x) for x in args.protocol_ss_k.split(",") if x.strip()]:
+            if k == args.protocol_ot_ss_k:
+                continue
             ss = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate, ot_ss_k=k)
-            proto["softspoken"][f"k{k}"] = {key: ss[key] for key in (
+            proto["ot_extension_forms"][f"k{k}"] = {key: ss[key] for key in (
                 "wall_s", "heavy_hitters", "heavy_hitters_equal_headline", "gcot_gpu_ms", "ot_extension",
                 "channel_bytes", "roofline")}
-            proto["softspoken"][f"k{k}"]["output_equal_golden"] = sig_equal(ss["sig"], gold) if gold else None
+            proto["ot_extension_forms"][f"k{k}"]["output_equal_golden"] = sig_equal(ss["sig"], gold) if gold else None
 
     if rank == 0:
         launches = max(1, s0["expand_launches_timed"])

@@ -5,6 +5,9 @@
 //              bank-conflict free, data-dependent byte index)
 //   which = 5: v_mad_u64_u32 lane-ops/s (the 32 x 32 + 64 -> 64 multiply-add of the FE products of
 //              k_sketch_fe), 8 waves/SIMD, independent chains; 6: the same at 4 waves/SIMD
+//   which = 7 / 8: v_alignbit_b32 / v_add_u32 lane-ops/s (r06: the ChaCha12 row PRG's rotate and add),
+//              8 waves/SIMD; 9: ChaCha double rounds over 2 independent states per lane (12 ops per
+//              quarter round counted), 8 waves/SIMD; 10: the same at 2 waves/SIMD
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/fhh.h"
@@ -64,6 +67,64 @@ __global__ __launch_bounds__(256) void k_mad64_peak(uint32_t* out, uint32_t iter
 #pragma unroll
     for (int k = 0; k < 16; k++) acc ^= x[k];
     if (acc == 0x12345678u) out[0] = (uint32_t)acc;   // keep live
+}
+
+// v_alignbit_b32 (OP 0) / v_add_u32 (OP 1) over 16 independent words, as k_valu_peak
+template <int OP>
+__global__ __launch_bounds__(256) void k_valu_op_peak(uint32_t* out, uint32_t iters, uint32_t seed) {
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = seed * (threadIdx.x + 1) + k * 0x9e3779b9u + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if constexpr (OP == 0) x[k] = __builtin_amdgcn_alignbit(x[(k + 1 + r) & 15], x[k], 7 + r);
+                else x[k] += x[(k + 1 + r) & 15];
+            }
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) acc ^= x[k];
+    if (acc == 0x12345678u) out[0] = acc;   // keep live
+}
+
+__device__ __forceinline__ uint32_t mb_rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ void mb_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+    a += b; d ^= a; d = mb_rotl(d, 16);
+    c += d; b ^= c; b = mb_rotl(b, 12);
+    a += b; d ^= a; d = mb_rotl(d, 8);
+    c += d; b ^= c; b = mb_rotl(b, 7);
+}
+
+// ChaCha double rounds over 2 independent 16-word states per lane (the expands' ILP)
+__global__ __launch_bounds__(256) void k_chacha_peak(uint32_t* out, uint32_t iters, uint32_t seed) {
+    uint32_t x[2][16];
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int k = 0; k < 16; k++) x[q][k] = seed * (threadIdx.x + 1) + (16 * q + k) * 0x9e3779b9u + blockIdx.x;
+    for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            mb_qr(x[q][0], x[q][4], x[q][8], x[q][12]);
+            mb_qr(x[q][1], x[q][5], x[q][9], x[q][13]);
+            mb_qr(x[q][2], x[q][6], x[q][10], x[q][14]);
+            mb_qr(x[q][3], x[q][7], x[q][11], x[q][15]);
+            mb_qr(x[q][0], x[q][5], x[q][10], x[q][15]);
+            mb_qr(x[q][1], x[q][6], x[q][11], x[q][12]);
+            mb_qr(x[q][2], x[q][7], x[q][8], x[q][13]);
+            mb_qr(x[q][3], x[q][4], x[q][9], x[q][14]);
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc ^= x[q][k];
+    if (acc == 0x12345678u) out[0] = acc;   // keep live
 }
 
 __global__ __launch_bounds__(512) void k_lds_peak(uint32_t* out, uint32_t iters) {
@@ -291,11 +352,17 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
         if (which == 0 || which >= 2) {
             // 0: v_xor_b32, 8 waves/SIMD; 2: v_bitop3_b32, 8 waves/SIMD;
             // 3: v_bitop3_b32, 2 waves/SIMD; 4: v_xor_b32, 2 waves/SIMD
-            const int wps = (which == 3 || which == 4) ? 2 : (which == 6 ? 4 : 8);
+            const int wps = (which == 3 || which == 4 || which == 10) ? 2 : (which == 6 ? 4 : 8);
             const int blocks = cus * wps;   // 256-thread blocks = 4 waves = one per SIMD
             const uint32_t iters = 4096;
             (void)hipEventRecord(a, 0);
-            if (which == 0 || which == 4)
+            if (which == 7)
+                hipLaunchKernelGGL(fhh::k_valu_op_peak<0>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else if (which == 8)
+                hipLaunchKernelGGL(fhh::k_valu_op_peak<1>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else if (which == 9 || which == 10)
+                hipLaunchKernelGGL(fhh::k_chacha_peak, dim3(blocks), dim3(threads), 0, 0, out, iters / 8, 7u);
+            else if (which == 0 || which == 4)
                 hipLaunchKernelGGL(fhh::k_valu_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             else if (which == 5 || which == 6)
                 hipLaunchKernelGGL(fhh::k_mad64_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
@@ -303,6 +370,7 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
                 hipLaunchKernelGGL(fhh::k_bitop3_peak, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             (void)hipEventRecord(b, 0);
             ops = (double)blocks * threads * iters * 8 * 16;
+            if (which == 9 || which == 10) ops = (double)blocks * threads * (iters / 8) * 2 * 8 * 12;
         } else {
             const int blocks = cus * 2;   // 64 KiB LDS -> 2 blocks/CU of 512 threads (as k_expand)
             const uint32_t iters = 8192;

@@ -1190,7 +1190,8 @@ def main():
     if run_proto:
         proto = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate,
                                ot_ss_k=args.protocol_ot_ss_k)
-        proto["output_equal_golden"] = sig_equal(proto.pop("sig"), gold) if gold else None
+        psig = proto.pop("sig")   # (not JSON: the crawl's signature arrays)
+        proto["output_equal_golden"] = sig_equal(psig, gold) if gold else None
         if not args.no_protocol_circuit:
             # the same crawl with the half-gates circuit at every level (the reference's construction,
             # r05c form) beside the default garbled table: what the table buys, on the same box

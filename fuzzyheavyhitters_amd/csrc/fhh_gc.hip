@@ -849,7 +849,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
                 for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 1][c];
             col >>= 4;
         }
-        if (a.node_partials) gt_add_partials(a.node_partials, a.g_off + g, 0, acc_lo, acc_hi, lane);
+        if (a.node_partials) gt_add_partials(a.node_partials, a.node_off + a.g_off + g, 0, acc_lo, acc_hi, lane);
     }
 }
 
@@ -911,7 +911,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 for (int c = 0; c < 4; c++) S[jj][c] = S[jj + 2][c];
             col >>= 8;
         }
-        if (a.node_partials) gt_add_partials(a.node_partials, a.g_off + g, 2, acc_lo, acc_hi, lane);
+        if (a.node_partials) gt_add_partials(a.node_partials, a.node_off + a.g_off + g, 2, acc_lo, acc_hi, lane);
     }
 }
 

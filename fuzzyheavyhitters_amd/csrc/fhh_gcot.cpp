@@ -5,6 +5,7 @@
 // runs its half on its own ctx, only the protocol messages cross).
 #include "fhh_engine.h"
 #include "aes_tables.h"
+#include "field_arith.h"
 
 #include <algorithm>
 #include <cstring>
@@ -717,6 +718,13 @@ struct PartyState {
     uint64_t bytes_sent = 0;    // this ctx's outgoing message bytes for the level
     uint32_t ss_k = 1;          // r06: 1 IKNP, 2 / 4 SoftSpoken (both OT kinds; fhh_ev_cfg / fhh_gb_cfg.ot_ss_k)
     DevBuf ss_leaf;             // SoftSpoken: this party's GGM leaves
+    // r06 (ltm): the table kernels add this party's node values per child into partials [level_C][4] (the
+    // level loop's layout: garbler slots 0, 1, evaluator 2, 3) instead of storing them in vals, and the
+    // garble / evaluate calls copy the partials to the host before they return: fhh_party_node_sums then
+    // needs no device work (no sums kernel, no values round trip, no extra synchronisation)
+    bool lfused = false;
+    DevBuf partials;
+    std::vector<uint64_t> partials_host;
 };
 
 void party_destroy(fhh_ctx* ctx) {
@@ -787,8 +795,25 @@ int party_begin(fhh_ctx* ctx, int role, uint64_t child_begin, uint64_t child_cou
         a.plane_nw = (uint32_t)P.nw;
         HIP_TRY(ctx, launch_share_planes(a, P.planes.as<uint64_t>(), ctx->stream));
     }
-    // the level's node values, one row of n per child (u64 FE, or a BlockPair at the last level)
-    if (b == 0) HIP_TRY(ctx, P.vals.ensure(std::max<uint64_t>(LC * P.n * P.per2, 1) * (P.last ? 16 : 8)));
+    // the level's node values, one row of n per child (u64 FE, or a BlockPair at the last level); with the
+    // fused sums (ltm) only the per-child partials, zeroed at the level's first chunk
+    P.lfused = P.ltm;
+    if (b == 0 && P.lfused) {
+        HIP_TRY(ctx, P.partials.ensure(std::max<uint64_t>(LC, 1) * 4 * 8));
+        HIP_TRY(ctx, hipMemsetAsync(P.partials.p, 0, std::max<uint64_t>(LC, 1) * 4 * 8, ctx->stream));
+        P.partials_host.assign(std::max<uint64_t>(LC, 1) * 4, 0);
+    } else if (b == 0) {
+        HIP_TRY(ctx, P.vals.ensure(std::max<uint64_t>(LC * P.n * P.per2, 1) * (P.last ? 16 : 8)));
+    }
+    return FHH_OK;
+}
+
+// the fused partials of the level so far, to the host (each chunk's call copies the whole accumulating
+// array; after the level's last chunk the host copy is complete)
+int party_partials_to_host(fhh_ctx* ctx, PartyState& P) {
+    if (!P.lfused || P.level_C == 0) return FHH_OK;
+    HIP_TRY(ctx, hipMemcpyAsync(P.partials_host.data(), P.partials.p, P.level_C * 4 * 8, hipMemcpyDeviceToHost,
+                                ctx->stream));
     return FHH_OK;
 }
 
@@ -999,8 +1024,11 @@ int fhh_gb_ot_labels(fhh_ctx* ctx, const fhh_gb_cfg* cfg, const uint8_t* u_dev, 
     P.g.ev_ot = 1;
     P.g.lab_tm = P.ltm ? 1u : 0u;
     P.g.out = nullptr;
-    // r05c: the garbler's node values r1 straight into the level's rows (the y it forms travels in gc)
-    P.g.sh_gb = P.lshare ? reinterpret_cast<uint64_t*>(party_vals(P)) : nullptr;
+    // r05c: the garbler's node values r1 straight into the level's rows (the y it forms travels in gc);
+    // r06 (ltm): added per child into the partials instead
+    P.g.sh_gb = P.lshare && !P.lfused ? reinterpret_cast<uint64_t*>(party_vals(P)) : nullptr;
+    P.g.node_partials = P.lfused ? P.partials.as<uint64_t>() : nullptr;
+    P.g.node_off = P.c_off;
     // OT 1 as the IKNP correlation (gb_set_fancy_inputs, equalitytest.rs:67-82): q_j is the evaluator's
     // zero label of its share bit j, q_j ^ s its one label, and s = Delta: nothing to send back
     if (P.m1) {
@@ -1030,6 +1058,8 @@ int fhh_gb_garble(fhh_ctx* ctx, const uint8_t** gc_msg_dev, uint64_t* gc_msg_byt
     if (!Pp || Pp->role != 0 || Pp->step != 1) return ctx->fail(FHH_E_STATE, "gb_garble: call after fhh_gb_ot_labels");
     PartyState& P = *Pp;
     if (P.tests) HIP_TRY(ctx, P.ltable ? launch_gt_garble(P.g, ctx->stream) : launch_gc_garble(P.g, ctx->stream));
+    rc = party_partials_to_host(ctx, P);
+    if (rc) return rc;
     rc = ctx_sync(ctx);
     if (rc) return rc;
     P.step = 2;
@@ -1070,7 +1100,10 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
     g.lab_tm = P.ltm ? 1u : 0u;
     g.ev_ot = 1;
     g.out = P.out.as<uint8_t>();
-    if (P.lshare) {
+    if (P.lfused) {   // r06: added per child into the partials
+        g.node_partials = P.partials.as<uint64_t>();
+        g.node_off = P.c_off;
+    } else if (P.lshare) {
         // r05c: its node value from its output label and the gc message's y, straight into the rows
         g.sh_ev = reinterpret_cast<uint64_t*>(party_vals(P));
     } else {
@@ -1078,6 +1111,8 @@ int fhh_ev_evaluate(fhh_ctx* ctx, const uint8_t* gc_msg_dev, uint64_t gc_len, co
         g.out_dup = P.per2;
     }
     if (P.tests) HIP_TRY(ctx, P.ltable ? launch_gt_eval(g, ctx->stream) : launch_gc_eval(g, ctx->stream));
+    rc = party_partials_to_host(ctx, P);
+    if (rc) return rc;
     // 3. OT 2's receiver: choice = the GC output (collect.rs:461-471); T and U reused
     rc = party_ot_buffers(ctx, P, P.m2, true);
     if (rc) return rc;
@@ -1166,6 +1201,7 @@ int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
         int rc = fhh_shard_info(ctx, 0, &S, nullptr, nullptr, nullptr, nullptr);
         if (rc) return rc;
         std::vector<const void*> v((size_t)S, nullptr);
+        std::vector<PartyState*> fused_shards;
         int last = -1;
         for (int k = 0; k < S; k++) {
             fhh_ctx* sh = nullptr;
@@ -1181,8 +1217,25 @@ int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
             if (last >= 0 && last != (int)P->last) return ctx->fail(FHH_E_STATE, "party_node_sums: shards disagree");
             last = P->last;
             v[(size_t)k] = P->vals.p;
+            fused_shards.push_back(P);
         }
         if (last < 0) return ctx->fail(FHH_E_STATE, "party_node_sums: no shard holds clients");
+        if (!fused_shards.empty() && fused_shards[0]->lfused) {   // r06: the shards' host partials, summed
+            const uint64_t LC = fused_shards[0]->level_C;
+            std::vector<uint64_t> h(LC * 2, 0);
+            for (PartyState* P : fused_shards) {
+                if (!P->lfused || P->level_C != LC) return ctx->fail(FHH_E_STATE, "party_node_sums: shards disagree");
+                const int k0 = P->role == 0 ? 0 : 2;
+                for (uint64_t c = 0; c < LC; c++) {
+                    h[2 * c] += P->partials_host[4 * c + k0];
+                    h[2 * c + 1] += P->partials_host[4 * c + k0 + 1];
+                }
+            }
+            uint64_t* sums = static_cast<uint64_t*>(sums_a);
+            if (sums)
+                for (uint64_t c = 0; c < LC; c++) sums[c] = fhh::fe_canon_from_limbs(h[2 * c], h[2 * c + 1]);
+            return FHH_OK;
+        }
         const uint32_t fmt = last ? FHH_VALS_FE255_BLOCKPAIR : FHH_VALS_FE_U64;
         return group_node_sums(ctx, v.data(), false, 0, fmt, sums_a, sums_b);   // ld 0: each shard's n
     }
@@ -1190,6 +1243,14 @@ int fhh_party_node_sums(fhh_ctx* ctx, void* sums_a, void* sums_b) {
     if (!Pp || Pp->step != 3 || Pp->covered != Pp->level_C)
         return ctx->fail(FHH_E_STATE, "party_node_sums: the level's OTs are not finished for every child");
     PartyState& P = *Pp;
+    if (P.lfused) {   // r06: the partials the garble / evaluate calls copied to the host
+        const int k0 = P.role == 0 ? 0 : 2;
+        uint64_t* sums = static_cast<uint64_t*>(sums_a);
+        if (sums)
+            for (uint64_t c = 0; c < P.level_C; c++)
+                sums[c] = fhh::fe_canon_from_limbs(P.partials_host[4 * c + k0], P.partials_host[4 * c + k0 + 1]);
+        return FHH_OK;
+    }
     // the garbler's value is r1 = v + mask, the evaluator's its C-OT output (written per chunk into
     // P.vals); rows of n values: FE as u64, FieldElm as a BlockPair (2 blocks)
     const void* vv[1] = {P.vals.p};

@@ -1342,6 +1342,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         HIP_TRY(c0, B.gc_msgs.ensure(tests * (((size_t)1 << bits) - 1) * 8));
                         g.gt_msgs = B.gc_msgs.as<uint64_t>();
                         g.node_partials = ltm && FHH_GT_FUSED_SUMS ? part : nullptr;
+                        g.node_off = 0;
                         g.sh_gb = fused ? nullptr : B.gc_val[0].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_garble(g, c0->stream));
                         g.ev_labels = ltm ? c0->ot_buf[0].as<uint4>() : B.gc_evact.as<uint4>();

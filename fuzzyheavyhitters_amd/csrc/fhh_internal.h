@@ -262,6 +262,7 @@ struct GcArgs {
     // node_partials [C][4] u64 (k_child_sums_fe's layout: garbler lo, hi; evaluator lo, hi) by one wave sum
     // and atomic per 512-test tile, instead of storing them for k_child_sums_fe (sh_gb / sh_ev may be null)
     uint64_t* node_partials;
+    uint64_t node_off;   // node_partials row of the launch's group 0 beyond g_off (the party ABI: its chunk's c_off)
 };
 constexpr int kGtMaxBits = 4;   // 16 rows (d = 2); wider tests keep the half-gates chain
 constexpr int kGtTmMaxBits = 2;   // r06: the table kernels read the tile-major labels (lab_tm) for b <= 2 (d = 1)

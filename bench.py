@@ -449,16 +449,7 @@ def dropin_bench(args, world, rank, local_rank, dist):
                                "real Chou-Orlandi base OTs over the channel; fused leg: one-seed material, ideal "
                                "base OTs", "parallelism": "single GPU"},
     }
-    c0, c1 = pair()
     ssk = args.protocol_ot_ss_k
-    fused_fn = lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False,  # noqa: E731
-                                     ot_ss_k=ssk)
-    t_fused, res = timed(fused_fn, reps, warm)
-    fused_runs = runs[id(fused_fn)]
-    hh = len(res.final)
-    del c0, c1
-    print(f"dropin: fused protocol crawl {t_fused:.2f} s, {hh} heavy hitters", file=sys.stderr, flush=True)
-
     leg_runs = {}
     leg_cold = {}
 
@@ -476,14 +467,28 @@ def dropin_bench(args, world, rank, local_rank, dist):
         t, r = timed(run, reps, warm)
         leg_runs[(tuple(devices) if devices else None, channel)] = runs[id(run)]
         leg_cold[(tuple(devices) if devices else None, channel)] = cold.get(id(run))
-        assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
+        if hh is not None:
+            assert len(r.final) == hh, f"drop-in ({devices}, {channel}) found {len(r.final)} heavy hitters, fused {hh}"
         tot = {k: sum(lb.get(k, 0) for lb in r.level_bytes) for k in ("gc", "u1", "y1", "u2", "y2")}
         tot["base_ot"] = r.base_ot_bytes
         print(f"dropin: leg devices={devices} channel={channel}: {t:.2f} s ({r.base_ot_runs} CO15 runs, "
               f"crawl waited {r.base_ot_wait_s:.3f} s for them)", file=sys.stderr, flush=True)
         return t, {k: v / L * 1e3 for k, v in tm.items()}, tot, r
 
+    # the drop-in leg first: its cold crawl is a server process's first crawl. Run after the fused leg, the
+    # drop-in's first crawl paid +3.1 s at 1M for allocating over the fused pair's freed memory, against +0.03 s
+    # in a fresh process (tools/r06_cold.py, profiles/r06/cold/)
+    hh = None
     t_d, per_d, bytes_d, r_d = dropin_leg()
+    c0, c1 = pair()
+    fused_fn = lambda: fhh.sim_crawl(c0, c1, args.threshold, mode="fe", prf_seed=7, gc="ot", record=False,  # noqa: E731
+                                     ot_ss_k=ssk)
+    t_fused, res = timed(fused_fn, reps, warm)
+    fused_runs = runs[id(fused_fn)]
+    hh = len(res.final)
+    del c0, c1
+    print(f"dropin: fused protocol crawl {t_fused:.2f} s, {hh} heavy hitters", file=sys.stderr, flush=True)
+    assert len(r_d.final) == hh, f"drop-in found {len(r_d.final)} heavy hitters, fused {hh}"
     out.update({
         "value": t_d, "ms_per_step": t_d * 1e3,
         "fused_protocol_crawl_s": t_fused, "dropin_crawl_s": t_d, "dropin_over_fused": t_d / t_fused,
@@ -491,7 +496,8 @@ def dropin_bench(args, world, rank, local_rank, dist):
         "fused_runs_s": fused_runs, "dropin_runs_s": leg_runs[(None, "inplace")],
         "fused_cold_crawl_s": cold.get(id(fused_fn)), "dropin_cold_crawl_s": leg_cold[(None, "inplace")],
         "dropin_cold_over_warm": (leg_cold[(None, "inplace")] / t_d) if leg_cold[(None, "inplace")] else None,
-        "cold_note": "cold = the first (warm-up) crawl on freshly built collections, buffers allocated as the crawl grows",
+        "cold_note": ("cold = the first (warm-up) crawl on freshly built collections, buffers allocated as the crawl "
+                      "grows; the drop-in leg runs first in the process (a server's first crawl), the fused leg after it"),
         "dropin_ms_per_level": per_d,
         "dropin_overhead_ms_per_level": (t_d - t_fused) / L * 1e3,
         "channel": "in place (the receiver reads the sender's device buffer; bytes counted, not moved)",

@@ -7,7 +7,8 @@
 //              k_sketch_fe), 8 waves/SIMD, independent chains; 6: the same at 4 waves/SIMD
 //   which = 7 / 8: v_alignbit_b32 / v_add_u32 lane-ops/s (r06: the ChaCha12 row PRG's rotate and add),
 //              8 waves/SIMD; 9: ChaCha double rounds over 2 independent states per lane (12 ops per
-//              quarter round counted), 8 waves/SIMD; 10: the same at 2 waves/SIMD
+//              quarter round counted), 8 waves/SIMD; 10: the same at 2 waves/SIMD; 11 / 12: v_perm_b32 /
+//              v_lshl_or_b32
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/fhh.h"
@@ -81,6 +82,8 @@ __global__ __launch_bounds__(256) void k_valu_op_peak(uint32_t* out, uint32_t it
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 if constexpr (OP == 0) x[k] = __builtin_amdgcn_alignbit(x[(k + 1 + r) & 15], x[k], 7 + r);
+                else if constexpr (OP == 2) x[k] = __builtin_amdgcn_perm(x[(k + 1 + r) & 15], x[k], 0x05040302u + r);
+                else if constexpr (OP == 3) x[k] = (x[k] << (7 + r)) | x[(k + 1 + r) & 15];
                 else x[k] += x[(k + 1 + r) & 15];
             }
         }
@@ -360,6 +363,10 @@ extern "C" int fhh_microbench(int device, int which, double* rate) {
                 hipLaunchKernelGGL(fhh::k_valu_op_peak<0>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             else if (which == 8)
                 hipLaunchKernelGGL(fhh::k_valu_op_peak<1>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else if (which == 11)
+                hipLaunchKernelGGL(fhh::k_valu_op_peak<2>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
+            else if (which == 12)
+                hipLaunchKernelGGL(fhh::k_valu_op_peak<3>, dim3(blocks), dim3(threads), 0, 0, out, iters, 7u);
             else if (which == 9 || which == 10)
                 hipLaunchKernelGGL(fhh::k_chacha_peak, dim3(blocks), dim3(threads), 0, 0, out, iters / 8, 7u);
             else if (which == 0 || which == 4)

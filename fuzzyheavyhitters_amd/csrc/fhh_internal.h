@@ -97,7 +97,11 @@ struct LoopCtl {
 constexpr uint32_t kTailGroup = 8;
 // r05: 4 (was 2) since k_expand draws from 8 per-XCD heads on narrow levels: configs[3] k_expand
 // 0.44 -> 0.47 of the VALU roofline, the d = 1 headline unchanged (profiles/r05/expand_heads/)
-constexpr uint64_t kMwItemsPerWave = 4;
+// (r06 A/B, profiles/r06/ab_mw_ipw/: 2 -> 0.459, 8 or 16 -> 0.166 — wpi falls to 1 — against 0.478)
+#ifndef FHH_MW_IPW
+#define FHH_MW_IPW 4
+#endif
+constexpr uint64_t kMwItemsPerWave = FHH_MW_IPW;
 struct ItemLayout {
     uint32_t g, g_b, wpi;
     uint64_t items_a, total;

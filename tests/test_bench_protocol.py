@@ -1,0 +1,51 @@
+"""bench.py's protocol-crawl accounting (CPU): the executed-work and wire-byte decompositions the driver line
+reports for the real protocol's crawl (protocol_work, protocol_bytes), on the metric's golden level counts. The
+byte budget is the party ABI's own (fhh_gcot.cpp u_bytes / gc_bytes / y2_bytes; tests/test_party.py checks
+those against the messages that cross), so the SoftSpoken forms must shrink exactly U."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.fixture(scope="module")
+def golden_children():
+    g = np.load(os.path.join(ROOT, "tests", "golden", "zipf_1m_L512.npz"), allow_pickle=False)
+    return [int(x) for x in g["level_children"]]
+
+
+def test_protocol_bytes_by_ot_extension(golden_children):
+    import bench
+    n = 1_000_000
+    iknp = bench.protocol_bytes(golden_children, n, 1, ss_k=1)
+    json.dumps(iknp)   # plain ints: the driver line is JSON
+    assert iknp["total"] == sum(v for k, v in iknp.items() if k != "total")
+    assert abs(iknp["total"] / 1e12 - 5.734) < 0.01
+    for k, tb in ((2, 4.097), (4, 3.278)):
+        ss = bench.protocol_bytes(golden_children, n, 1, ss_k=k)
+        assert ss["table"] == iknp["table"] and ss["circuit"] == iknp["circuit"] and ss["y_shares"] == iknp["y_shares"]
+        assert ss["u_labels"] == iknp["u_labels"] // k and ss["u_shares"] == iknp["u_shares"] // k
+        assert ss["ggm_corrections"] == 4096 * (len(golden_children) + 1)   # one per OT session
+        assert abs(ss["total"] / 1e12 - tb) < 0.01
+    assert bench.protocol_bytes(golden_children, n, 1, ss_k=4)["total"] <= 3.5e12
+
+
+def test_protocol_work_counts_chacha_blocks(golden_children):
+    import bench
+    n = 1_000_000
+    aes, cc, tr = bench.protocol_work(golden_children, n, 1)
+    json.dumps([aes, cc, tr])
+    # d = 1: the FE levels' tile-major table (4 AES garbled + 1 evaluated per test, 512-client tiles) and no
+    # row transposes there; IKNP expands 2 + 1 ChaCha12 blocks per row and 512-OT tile
+    assert aes["table_garble"] == 4 * aes["table_eval"]
+    assert cc["ot_recv_expand"] == 2 * cc["ot_send_expand"]
+    _, cc2, _ = bench.protocol_work(golden_children, n, 1, ss_k=2)
+    _, cc4, _ = bench.protocol_work(golden_children, n, 1, ss_k=4)
+    # SoftSpoken: 2^k blocks per chunk and tile at the receiver, 2^k - 1 at the sender (128 / k chunks)
+    assert cc2["ot_recv_expand"] == cc["ot_recv_expand"] and 2 * cc2["ot_send_expand"] == 3 * cc["ot_send_expand"]
+    assert cc4["ot_recv_expand"] == 2 * cc["ot_recv_expand"] and 4 * cc4["ot_send_expand"] == 15 * cc["ot_send_expand"]

@@ -793,12 +793,13 @@ def protocol_work(level_children, n: int, d: int, circuit: bool = False, ss_k: i
     return aes, cc, transpose_bytes
 
 
-def protocol_bytes(level_children, n: int, d: int, circuit: bool = False, ss_k: int = 1):
+def protocol_bytes(level_children, n: int, d: int, circuit: bool = False, ss_k: int = 1, ring32: bool = False):
     """Server-to-server bytes of one real-protocol crawl on this rank (n clients), by message, as the party ABI
     counts them (fhh_gcot.cpp u_bytes / gc_bytes / y2_bytes; the base OTs' CO15 messages excluded): the labels
     OT's U (16 / ss_k B per OT: 128 / ss_k rows; SoftSpoken adds 4 KiB of GGM corrections per base-OT session),
     the FE levels' garbled table (2^b - 1 rows of 8 B per test) or circuit (2 (b - 1) blocks + decode + the 8-B
-    share per test), the FieldElm level's circuit and its share OT (U and 16 B of y per OT, 2 OTs per test)."""
+    share per test), the FieldElm level's circuit and its share OT (U and 16 B of y per OT, 2 OTs per test);
+    ring32 (d = 1 table): the table's rows are 4-B Z_2^32 messages."""
     b = 2 * d
     npad64 = (n + 63) // 64 * 64
     npad_tm = (n + 511) // 512 * 512
@@ -817,7 +818,7 @@ def protocol_bytes(level_children, n: int, d: int, circuit: bool = False, ss_k: 
             if circuit:
                 out["circuit"] += tests * (2 * (b - 1) * 16 + 1 + 8)
             else:
-                out["table"] += tests * ((1 << b) - 1) * 8
+                out["table"] += tests * ((1 << b) - 1) * (4 if ring32 and b <= 2 else 8)
         else:
             m1 = C * b * npad64
             m2 = 2 * tests
@@ -830,7 +831,8 @@ def protocol_bytes(level_children, n: int, d: int, circuit: bool = False, ss_k: 
     return out
 
 
-def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None, ot_ss_k=1):
+def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", expand_rate=None, ot_ss_k=1,
+                   ring32=False):
     """The real protocol's crawl on the headline's keys (tree_crawl with gc_sender per level,
     collect.rs:419-482, with OtSender/OtReceiver::init per channel and level, :454-471; the leader's
     loop leader.rs:422-440): the GPU garbled-circuit equality test and both OT extensions in every
@@ -843,14 +845,15 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
     def run(levels=None):
         # record: every level's v0 - v1 comes back to the host (a few KB per level) for the output check
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode="fe", prf_seed=7, record=True,
-                             comm=comm, gc=gc, base_ot=True, levels=levels, ot_ss_k=ot_ss_k)
+                             comm=comm, gc=gc, base_ot=True, levels=levels, ot_ss_k=ot_ss_k,
+                             table_ring32=ring32 and gc == "ot")
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    tag = gc if ot_ss_k == 1 else f"{gc}, SoftSpoken k={ot_ss_k}"
+    tag = (gc if ot_ss_k == 1 else f"{gc}, SoftSpoken k={ot_ss_k}") + (", Z_2^32 table" if ring32 and gc == "ot" else "")
     run(levels=min(32, args.data_len))
     barrier()
     log(f"protocol crawl ({tag}): warm-up done")
@@ -870,7 +873,8 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
     sig = crawl_sig(res)
     aes, cc, tr_bytes = protocol_work(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit",
                                       ss_k=ot_ss_k)
-    wire = protocol_bytes(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit", ss_k=ot_ss_k)
+    wire = protocol_bytes(res.level_children, c0.num_clients(), args.dims, circuit=gc == "ot-circuit", ss_k=ot_ss_k,
+                          ring32=ring32 and gc == "ot")
     n_aes, n_cc = sum(aes.values()), sum(cc.values())
     gpu_s = s0["gcot_ms"] / 1e3
     ops = n_aes * VALU_OPS_PER_BLOCK + n_cc * CHACHA12_OPS_PER_BLOCK
@@ -901,6 +905,8 @@ def protocol_crawl(args, c0, c1, n_total, comm, dist, headline_sig, gc="ot", exp
         "heavy_hitters_equal_headline": sig_equal(sig, headline_sig) if headline_sig else None,
         "ot_extension": "IKNP (128 rows of U)" if ot_ss_k == 1 else
                         f"SoftSpoken k={ot_ss_k} ({128 // ot_ss_k} rows of U, GGM trees from the base OTs)",
+        "table_shares": ("Z_2^32 (4-B rows)" if ring32 and gc == "ot" and args.dims == 1 else "FE (8-B rows)")
+                        if gc == "ot" else None,
         "channel_bytes": wire,
         "channel_bytes_note": ("server-to-server bytes of this crawl on this rank by message, as the party ABI "
                                "counts them (bench.protocol_bytes; CO15 base-OT messages excluded)"),
@@ -1009,11 +1015,16 @@ def main():
                     help="time every K-th k_expand launch with HIP events (roofline.avg_launch_us)")
     ap.add_argument("--no-protocol-circuit", action="store_true",
                     help="skip the second protocol crawl with the half-gates circuit at every level")
+    ap.add_argument("--table-ring32", action="store_true",
+                    help="--gc ot: the FE levels' garbled table in Z_2^32 (4-B rows) instead of FE")
     ap.add_argument("--ot-ss-k", type=int, default=1, choices=(1, 2, 4),
                     help="--gc ot: the OT extension of the timed crawl (1 IKNP, 2 / 4 SoftSpoken)")
     ap.add_argument("--protocol-ot-ss-k", type=int, default=2, choices=(1, 2, 4),
                     help="the protocol crawl's OT extension: 1 IKNP, 2 / 4 SoftSpoken (default 2: half of IKNP's U "
                          "bytes for ~1.5x the sender's ChaCha work, profiles/r06/softspoken/)")
+    ap.add_argument("--protocol-table-fe", action="store_true",
+                    help="the protocol crawl's FE-level garbled table with FE shares (8-B rows) instead of the "
+                         "default Z_2^32 shares (4-B rows; d = 1)")
     ap.add_argument("--protocol-ss-k", default="1,4",
                     help="comma list of further OT extensions (1 IKNP, 2 / 4 SoftSpoken) to run the protocol crawl "
                          "with beside it ('' = none)")
@@ -1139,7 +1150,8 @@ def main():
     def step(record=False):
         return fhh.sim_crawl(c0, c1, args.threshold, nclients_total=n_total, mode=args.mode, prf_seed=7,
                              record=record, comm=comm, gc={"none": False, "ot": "ot", "ideal": "ideal"}[args.gc],
-                             base_ot=args.base_ot, ot_ss_k=args.ot_ss_k if args.gc == "ot" else 1)
+                             base_ot=args.base_ot, ot_ss_k=args.ot_ss_k if args.gc == "ot" else 1,
+                             table_ring32=args.table_ring32 and args.gc == "ot")
 
     def barrier():
         if dist is not None:
@@ -1194,8 +1206,9 @@ def main():
     expand_rate = (s0["expand_blocks_timed"] / launches0) / (s0["expand_ms"] / launches0 / 1e3) if s0["expand_ms"] else None
     proto = None
     if run_proto:
+        ring = not args.protocol_table_fe
         proto = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate,
-                               ot_ss_k=args.protocol_ot_ss_k)
+                               ot_ss_k=args.protocol_ot_ss_k, ring32=ring)
         psig = proto.pop("sig")   # (not JSON: the crawl's signature arrays)
         proto["output_equal_golden"] = sig_equal(psig, gold) if gold else None
         if not args.no_protocol_circuit:
@@ -1212,10 +1225,11 @@ def main():
         for k in [int(x) for x in args.protocol_ss_k.split(",") if x.strip()]:
             if k == args.protocol_ot_ss_k:
                 continue
-            ss = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate, ot_ss_k=k)
+            ss = protocol_crawl(args, c0, c1, n_total, comm, dist, ref_sig, expand_rate=expand_rate, ot_ss_k=k,
+                                ring32=ring)
             proto["ot_extension_forms"][f"k{k}"] = {key: ss[key] for key in (
                 "wall_s", "heavy_hitters", "heavy_hitters_equal_headline", "gcot_gpu_ms", "ot_extension",
-                "channel_bytes", "roofline")}
+                "table_shares", "channel_bytes", "roofline")}
             proto["ot_extension_forms"][f"k{k}"]["output_equal_golden"] = sig_equal(ss["sig"], gold) if gold else None
 
     if rank == 0:

@@ -54,7 +54,7 @@ EXPORTS = [
     "fhh_create_multi", "fhh_shard_info", "fhh_shard_ctx", "fhh_node_sums_fe_device", "fhh_node_sums_fe255_device",
     "fhh_gb_garble", "fhh_gb_ot_labels", "fhh_gb_ot_shares", "fhh_ev_ot_labels", "fhh_ev_evaluate", "fhh_ev_ot_shares",
     "fhh_party_node_sums", "fhh_party_bytes_sent", "fhh_gc_party_test_cfgs", "fhh_memcpy_device",
-    "fhh_cot_extend_host", "fhh_cot_extend_ss_host", "fhh_gc_cot_host", "fhh_gt_cot_host",
+    "fhh_cot_extend_host", "fhh_cot_extend_ss_host", "fhh_gc_cot_host", "fhh_gt_cot_host", "fhh_gt_cot_ring32_host",
     "fhh_shard_plan",
 ]
 
@@ -108,6 +108,7 @@ class FhhSimConfig(ctypes.Structure):
         ("probe_children", u64p),
         ("base_ot", ctypes.c_uint32),
         ("ot_ss_k", ctypes.c_uint32),
+        ("table_ring32", ctypes.c_uint32),
     ]
 
 
@@ -300,6 +301,7 @@ def lib():
         "fhh_gc_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
                                 u64p]),
         "fhh_gt_cot_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u64p, u64p, u64p]),
+        "fhh_gt_cot_ring32_host": (i, [vp, u64, u32, u8p, u8p, u32, u64, u8p, u8p, u64, u8p, u8p, u64p, u64p, u64p]),
         "fhh_memcpy_device": (i, [i, vp, vp, u64]),
         "fhh_shard_plan": (i, [u64, i, u64p, u64p]),
         "fhh_destroy": (None, [vp]),

@@ -827,6 +827,21 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
             for (uint32_t q = 0; q < R; q++) {
                 const uint32_t o_r = (uint32_t)(q == rstar) ^ a.mask;
                 const uint64_t hl = (uint64_t)h[q][0] | ((uint64_t)h[q][1] << 32);
+                if (a.ring32) {   // r06: the same table over Z_2^32 (lo32 of the hash, 4-B messages)
+                    if (q == 0) {
+                        const uint32_t h32 = h[0][0];
+                        const uint32_t v = o_r == 0 ? h32 : (a.mask ? h32 - 1u : h32 + 1u);
+                        p0 = v;
+                        p1 = (uint32_t)(a.mask ? v + 1u : v - 1u);
+                        const uint32_t r1 = a.mask ? v + 1u : v;   // r1 = v + mask
+                        if (live && a.node_partials) acc_lo += r1;
+                        else if (live) a.sh_gb[t] = r1;
+                    } else if (live) {
+                        reinterpret_cast<uint32_t*>(a.gt_msgs)[(uint64_t)(q - 1) * n + t] =
+                            h[q][0] ^ (uint32_t)(o_r ? p1 : p0);
+                    }
+                    continue;
+                }
                 if (q == 0) {   // row 0's value pair[o_0] is H(K_0) mod p: it fixes v
                     const uint64_t hv = ot_fe_of_u128(hl, (uint64_t)h[q][2] | ((uint64_t)h[q][3] << 32));
                     const uint64_t v = o_r == 0 ? hv : (a.mask ? fe_dec(hv) : fe_inc(hv));
@@ -896,8 +911,12 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 const uint64_t t = g * a.N + i;
                 const uint32_t row = (col >> (4 * u)) & 0xFu;
                 const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
-                const uint64_t val = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
-                                         : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
+                uint64_t val;
+                if (a.ring32)   // r06: Z_2^32 shares, 4-B messages
+                    val = row ? (h[u][0] ^ reinterpret_cast<const uint32_t*>(a.gt_msgs)[(uint64_t)(row - 1) * n + t]) : h[u][0];
+                else
+                    val = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
+                              : ot_fe_of_u128(hl, (uint64_t)h[u][2] | ((uint64_t)h[u][3] << 32));
                 if (a.node_partials) {
                     acc_lo += val & 0xFFFFFFFFull;
                     acc_hi += val >> 32;
@@ -943,6 +962,7 @@ static hipError_t gt_dispatch(const GcArgs& a, bool garble, hipStream_t stream) 
         return hipErrorInvalidValue;
     // r06 tile-major labels: 512-test tiles per group, b <= 2 (gt_tm_bits)
     if (a.lab_tm && (a.nw % 8 != 0 || a.bits > (uint32_t)kGtTmMaxBits)) return hipErrorInvalidValue;
+    if (a.ring32 && !a.lab_tm) return hipErrorInvalidValue;   // Z_2^32: the tile-major kernels only
     switch (a.bits) {
         case 1: return gt_launch<1>(a, garble, stream);
         case 2: return gt_launch<2>(a, garble, stream);

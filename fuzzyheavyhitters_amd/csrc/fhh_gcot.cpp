@@ -557,14 +557,16 @@ int fhh_gc_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     return rc;
 }
 
-int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
-                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
-                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
-                    uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share) {
+static int gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                       uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                       const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                       uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share, bool ring32) {
     CTX_CHECK(ctx);
     int rc = ctx_set_device(ctx);
     if (rc) return rc;
     if (bits < 1 || bits > (uint32_t)kGtMaxBits) return ctx->fail(FHH_E_ARG, "gt_cot: bits must be in [1, 4]");
+    if (ring32 && bits > (uint32_t)kGtTmMaxBits)
+        return ctx->fail(FHH_E_ARG, "gt_cot: the Z_2^32 table runs on the tile-major kernels (bits <= 2)");
     if (n == 0) return FHH_OK;
     if (!gb_bits || !ev_bits || !base_seeds || !base_choice || !gb_share || !ev_share)
         return ctx->fail(FHH_E_ARG, "gt_cot: NULL argument");
@@ -621,6 +623,7 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     g.lab_tm = tm ? 1u : 0u;
     g.ev_ot = 1;
     g.gt_msgs = dm.as<uint64_t>();
+    g.ring32 = ring32 ? 1u : 0u;
     g.sh_gb = dsh.as<uint64_t>();
     HIP_TRY(ctx, launch_gt_garble(g, ctx->stream));
     g.ev_labels = tm ? ctx->ot_buf[0].as<uint4>() : da.as<uint4>();
@@ -639,7 +642,12 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy(gb_share, dsh.p, n * 8, hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipMemcpy(ev_share, dsh.as<uint64_t>() + n, n * 8, hipMemcpyDeviceToHost));
-    if (msgs && R > 1) {   // SoA [R-1][n] on the device -> [n][R-1]
+    if (msgs && R > 1 && ring32) {   // SoA [R-1][n] u32 on the device -> [n][R-1] (zero-extended)
+        std::vector<uint32_t> h((R - 1) * n);
+        HIP_TRY(ctx, hipMemcpy(h.data(), dm.p, h.size() * 4, hipMemcpyDeviceToHost));
+        for (uint64_t r = 0; r + 1 < R; r++)
+            for (uint64_t t = 0; t < n; t++) msgs[t * (R - 1) + r] = h[r * n + t];
+    } else if (msgs && R > 1) {   // SoA [R-1][n] on the device -> [n][R-1]
         std::vector<uint64_t> h((R - 1) * n);
         HIP_TRY(ctx, hipMemcpy(h.data(), dm.p, h.size() * 8, hipMemcpyDeviceToHost));
         for (uint64_t r = 0; r + 1 < R; r++)
@@ -657,6 +665,22 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
     rc = soa_to_aos(de, ev_zero);
     if (!rc) rc = soa_to_aos(da, ev_active);
     return rc;
+}
+
+int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                    uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                    const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                    uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share) {
+    return gt_cot_host(ctx, n, bits, gb_bits, ev_bits, mask, gate_base, base_seeds, base_choice, ctr_off, ev_zero,
+                       ev_active, msgs, gb_share, ev_share, false);
+}
+
+int fhh_gt_cot_ring32_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                           uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                           const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                           uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share) {
+    return gt_cot_host(ctx, n, bits, gb_bits, ev_bits, mask, gate_base, base_seeds, base_choice, ctr_off, ev_zero,
+                       ev_active, msgs, gb_share, ev_share, true);
 }
 
 }  // extern "C"

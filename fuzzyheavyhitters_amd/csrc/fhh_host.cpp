@@ -1062,6 +1062,9 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         // the FieldElm level runs the circuit + share C-OT whatever the FE levels run
         gc_groups_last = std::max<uint64_t>(1, budget / ((200ull * 2 * d + 2) * std::max<uint64_t>(c0->npad, 1)));
     }
+    // r06: Z_2^32 table shares at the FE levels (the tile-major table with fused sums, d = 1)
+    const bool ring32 = cfg->table_ring32 && cfg->gc == 2 && cfg->mode == 1 && 2 * d <= (uint32_t)kGtTmMaxBits &&
+                        FHH_GT_FUSED_SUMS;
     PhaseClock pc;
     LoopBuffers B;
     B.distributed = cfg->comm || cfg->allreduce;
@@ -1343,6 +1346,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                         g.gt_msgs = B.gc_msgs.as<uint64_t>();
                         g.node_partials = ltm && FHH_GT_FUSED_SUMS ? part : nullptr;
                         g.node_off = 0;
+                        g.ring32 = ring32 && ltm ? 1u : 0u;
                         g.sh_gb = fused ? nullptr : B.gc_val[0].as<uint64_t>();
                         HIP_TRY(c0, launch_gt_garble(g, c0->stream));
                         g.ev_labels = ltm ? c0->ot_buf[0].as<uint4>() : B.gc_evact.as<uint4>();
@@ -1493,6 +1497,7 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
         pa.tail_split = expand_tail_split(variant) ? 1u : 0u;
         pa.max_wpi = expand_max_wpi(variant);
         pa.zero_partials = (cfg->mode != 0 && !last) ? B.partials.as<uint64_t>() : nullptr;
+        pa.ring32 = ring32 && !last ? 1u : 0u;
         pa.zero_count = (uint64_t)C_cap * 4;
         HIP_TRY(c0, launch_prune(pa, c0->stream));
         lv++;
@@ -1648,6 +1653,8 @@ int sim_crawl_device_loop(fhh_ctx* c0, fhh_ctx* c1, const fhh_sim_config* cfg, u
                 uint64_t v;
                 if (cfg->mode == 0) {
                     v = r[c];
+                } else if (!lvl_last && ring32) {   // r06: Z_2^32 shares
+                    v = (uint32_t)(r[c * 4] - r[c * 4 + 2]);
                 } else if (!lvl_last) {
                     v = fe_sub_canon(fe_canon_from_limbs(r[c * 4], r[c * 4 + 1]), fe_canon_from_limbs(r[c * 4 + 2], r[c * 4 + 3]));
                 } else {

@@ -267,6 +267,9 @@ struct GcArgs {
     // and atomic per 512-test tile, instead of storing them for k_child_sums_fe (sh_gb / sh_ev may be null)
     uint64_t* node_partials;
     uint64_t node_off;   // node_partials row of the launch's group 0 beyond g_off (the party ABI: its chunk's c_off)
+    // r06 (lab_tm): 1 = the table's shares live in Z_2^32 instead of FE (row value lo32 of the
+    // hash, pair (v, v +- 1 mod 2^32), 4-B messages [2^b - 1][n] u32; the partials' low sums taken mod 2^32)
+    uint32_t ring32;
 };
 constexpr int kGtMaxBits = 4;   // 16 rows (d = 2); wider tests keep the half-gates chain
 constexpr int kGtTmMaxBits = 2;   // r06: the table kernels read the tile-major labels (lab_tm) for b <= 2 (d = 1)
@@ -301,6 +304,7 @@ struct PruneArgs {
     // abort and wipe the sums the resumed prune re-reads)
     uint64_t* zero_partials;
     uint64_t zero_count;
+    uint32_t ring32;            // r06, mode 1: the level's shares are in Z_2^32 (GcArgs::ring32): v0 - v1 mod 2^32
 };
 
 struct KeygenArgs {

@@ -36,6 +36,10 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 
 __device__ __forceinline__ bool keep_of(const PruneArgs& a, uint32_t c) {
     if (a.mode == 0) return a.partials[c] >= (a.last ? (uint64_t)a.thr_last : a.thr);
+    if (a.mode == 1 && a.ring32) {   // r06: Z_2^32 shares (the count is < 2^32)
+        const uint64_t* p = a.partials + (size_t)c * 4;
+        return (uint64_t)(uint32_t)(p[0] - p[2]) >= a.thr;
+    }
     if (a.mode == 1) {
         const uint64_t* p = a.partials + (size_t)c * 4;
         const uint64_t s0 = fe_canon_from_limbs(p[0], p[1]), s1 = fe_canon_from_limbs(p[2], p[3]);

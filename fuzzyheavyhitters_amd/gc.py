@@ -159,11 +159,13 @@ def equality_test_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choi
     return out, tr
 
 
-def table_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate_base: int = 0, ctr_off: int = 0):
+def table_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate_base: int = 0, ctr_off: int = 0,
+              ring32: bool = False):
     """r05d, the FE levels' form (fhh_gt_cot_host, bits <= 4): the labels OT, then one garbled table
     of 2^bits rows for "the share of eq ^ mask" (Yao's garbled gate, point-and-permute) instead of the
     half-gates chain. Returns dict: msgs [n][2^bits - 1] u64, gb_share / ev_share [n] (gb - ev = eq mod
-    p), ev_zero / ev_active [n][bits][16]."""
+    p), ev_zero / ev_active [n][bits][16]. ring32 (r06, bits <= 2; fhh_gt_cot_ring32_host): the shares in
+    Z_2^32 (4-B messages; gb - ev = eq mod 2^32), returned zero-extended in the same arrays."""
     g = np.ascontiguousarray(np.asarray(gb_inputs).astype(np.uint8) & 1)
     e = np.ascontiguousarray(np.asarray(ev_inputs).astype(np.uint8) & 1)
     if g.ndim != 2 or g.shape != e.shape:
@@ -174,7 +176,8 @@ def table_cot(kc, gb_inputs, ev_inputs, mask: int, base_seeds, base_choice, gate
     tr = {"ev_zero": np.zeros((n, bits, 16), np.uint8), "ev_active": np.zeros((n, bits, 16), np.uint8),
           "msgs": np.zeros((n, (1 << bits) - 1), np.uint64), "gb_share": np.zeros(n, np.uint64),
           "ev_share": np.zeros(n, np.uint64)}
-    check(lib().fhh_gt_cot_host(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, gate_base, ptr(seeds), ptr(s),
-                                ctr_off, ptr(tr["ev_zero"]), ptr(tr["ev_active"]), ptr(tr["msgs"], u64p),
-                                ptr(tr["gb_share"], u64p), ptr(tr["ev_share"], u64p)), kc.handle)
+    fn = lib().fhh_gt_cot_ring32_host if ring32 else lib().fhh_gt_cot_host
+    check(fn(kc.handle, n, bits, ptr(g), ptr(e), int(mask) & 1, gate_base, ptr(seeds), ptr(s),
+             ctr_off, ptr(tr["ev_zero"]), ptr(tr["ev_active"]), ptr(tr["msgs"], u64p),
+             ptr(tr["gb_share"], u64p), ptr(tr["ev_share"], u64p)), kc.handle)
     return tr

@@ -62,7 +62,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
               mode: str = "count", prf_seed: int = 0, levels: int = 0, record: bool = True,
               distributed: bool = False, xchg_capacity: int = 1 << 20, host_loop: bool = False,
               init_capacity: int = 0, comm=None, gc=False, probe: dict | None = None,
-              base_ot: bool = False, ot_ss_k: int = 1) -> SimResult:
+              base_ot: bool = False, ot_ss_k: int = 1, table_ring32: bool = False) -> SimResult:
     """Leader level loop over both servers' collections. Multi-rank runs (clients sharded)
     sum per-child partials across ranks either natively (`comm`: an RcclComm, all-reduce on
     the engine stream) or, with `distributed=True`, through torch.distributed in a host
@@ -72,7 +72,8 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     the evaluator's labels and the FE shares moved by the GPU OT extension (base OTs ideal),
     "ideal" with both OTs ideal; "ot-circuit" as "ot" but the half-gates circuit (+ the output-label
     share) at every level instead of the FE levels' garbled table. `ot_ss_k` (gc "ot" / "ot-circuit", r06):
-    1 = IKNP OT extension, 2 / 4 = SoftSpoken with k = ot_ss_k (128 / k rows of U on the wire).
+    1 = IKNP OT extension, 2 / 4 = SoftSpoken with k = ot_ss_k (128 / k rows of U on the wire). `table_ring32`
+    (gc "ot", d = 1, r06): the FE levels' garbled table carries Z_2^32 shares (4-B rows) instead of FE ones.
 
     `probe` (parity tests) = {"levels": [...], "clients": [...], "capacity": C_max}: the device
     loop gathers those clients' EvalStates of every pending child right after each listed
@@ -92,6 +93,7 @@ def sim_crawl(c0: KeyCollection, c1: KeyCollection, threshold: float, nclients_t
     cfg.gc = {False: 0, None: 0, "ideal": 1, True: 2, "ot": 2, "ot-circuit": 3}[gc]
     cfg.base_ot = 1 if base_ot else 0   # gc = "ot": Chou–Orlandi base OTs on the host (else ideal)
     cfg.ot_ss_k = ot_ss_k
+    cfg.table_ring32 = 1 if table_ring32 else 0
     ar = None
     if comm is not None:
         cfg.comm = comm.handle

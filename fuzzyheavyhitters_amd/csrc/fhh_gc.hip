@@ -868,7 +868,9 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_garble_tm(GcArgs a) {
     }
 }
 
-template <int B, bool RING = false>
+// (the Z_2^32 form is a runtime branch here: as its own instantiation the evaluator ran ~20 % slower,
+// profiles/r06/ring32/)
+template <int B>
 __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
     static_assert(B <= 2, "the tile-major evaluator takes b <= 2");
     __shared__ uint32_t tbl_gc[GcTab::kWords];
@@ -912,7 +914,7 @@ __global__ __launch_bounds__(kGcThreads) void k_gt_eval_tm(GcArgs a) {
                 const uint32_t row = (col >> (4 * u)) & 0xFu;
                 const uint64_t hl = (uint64_t)h[u][0] | ((uint64_t)h[u][1] << 32);
                 uint64_t val;
-                if constexpr (RING)   // r06: Z_2^32 shares, 4-B messages
+                if (a.ring32)   // r06: Z_2^32 shares, 4-B messages
                     val = row ? (h[u][0] ^ reinterpret_cast<const uint32_t*>(a.gt_msgs)[(uint64_t)(row - 1) * n + t]) : h[u][0];
                 else
                     val = row ? (hl ^ a.gt_msgs[(uint64_t)(row - 1) * n + t])
@@ -945,14 +947,9 @@ static hipError_t gt_launch(const GcArgs& a, bool garble, hipStream_t stream) {
     if constexpr (B <= 2) if (a.lab_tm) {   // r06: one wave per 512-test tile, one 160 KiB workgroup per CU
         const uint64_t tiles = a.G * (a.nw / 8), need = (tiles + kGtWaves - 1) / kGtWaves;
         const int grid = (int)(need < (uint64_t)cus ? (need ? need : 1) : (uint64_t)cus);
-        if (a.ring32) {
-            if (garble) hipLaunchKernelGGL((k_gt_garble_tm<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-            else hipLaunchKernelGGL((k_gt_eval_tm<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-        } else if (garble) {
-            hipLaunchKernelGGL((k_gt_garble_tm<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-        } else {
-            hipLaunchKernelGGL((k_gt_eval_tm<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
-        }
+        if (garble && a.ring32) hipLaunchKernelGGL((k_gt_garble_tm<B, true>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+        else if (garble) hipLaunchKernelGGL((k_gt_garble_tm<B, false>), dim3(grid), dim3(kGcThreads), 0, stream, a);
+        else hipLaunchKernelGGL(k_gt_eval_tm<B>, dim3(grid), dim3(kGcThreads), 0, stream, a);
         return hipGetLastError();
     }
     const uint64_t need = (n + kGcThreads - 1) / kGcThreads;

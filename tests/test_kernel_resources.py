@@ -79,7 +79,7 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     # r06: the table kernels on the labels OT's tile-major Q / T (b <= 2)
     # (r06: FE and Z_2^32 shares as separate instantiations)
     names += [f"_ZN3fhh14k_gt_garble_tmILi{b}ELb{r}EEEvNS_6GcArgsE" for b in (1, 2) for r in (0, 1)]
-    names += [f"_ZN3fhh12k_gt_eval_tmILi{b}ELb{r}EEEvNS_6GcArgsE" for b in (1, 2) for r in (0, 1)]
+    names += [f"_ZN3fhh12k_gt_eval_tmILi{b}EEEvNS_6GcArgsE" for b in (1, 2)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
     # r06: the ChaCha12 row-PRG expands (no LDS), and the labels OT's row transpose (mode 4, r05b)

@@ -16,7 +16,7 @@ fhh.gen_keys_pair(c0, c1, wl.left, wl.right, wl.root_seeds)
 out = {"fe": [], "ring32": []}
 hh = {}
 for rnd in range(3):
-    for ring in (False, True):
+    for ring in ((True, False) if "ring-first" in sys.argv else (False, True)):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         r = fhh.sim_crawl(c0, c1, 0.001, mode="fe", prf_seed=7, gc="ot", base_ot=True, ot_ss_k=2, table_ring32=ring,

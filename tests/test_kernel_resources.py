@@ -78,7 +78,8 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
     names += [f"_ZN3fhh9k_gt_evalILi{b}EEEvNS_6GcArgsE" for b in range(1, 5)]
     # r06: the table kernels on the labels OT's tile-major Q / T (b <= 2)
     # (r06: FE and Z_2^32 shares as separate instantiations)
-    names += [f"_ZN3fhh14k_gt_garble_tmILi{b}ELb{r}EEEvNS_6GcArgsE" for b in (1, 2) for r in (0, 1)]
+    names += [f"_ZN3fhh14k_gt_garble_tmILi{b}ELb{r}EEEvNS_6GcArgsE" for b in (1, 2) for r in (0, 1)
+              if (b, r) != (2, 1)]
     names += [f"_ZN3fhh12k_gt_eval_tmILi{b}EEEvNS_6GcArgsE" for b in (1, 2)]
     ot = _resource_usage("fhh_ot.hip", tmp_path)
     u.update(ot)
@@ -91,6 +92,11 @@ def test_gc_and_ot_expand_kernels_do_not_spill(tmp_path):
         assert k["ScratchSize [bytes/lane]"] == "0", (name, k)
         assert k["VGPRs Spill"] == "0", (name, k)
         assert int(k["Occupancy [waves/SIMD]"]) >= 4, (name, k)
+    # r06: the b = 2 garbler's Z_2^32 instantiation keeps the FE code beside a runtime test (RING && a.ring32):
+    # compiled that way it spills one VGPR and still ran ~11 % faster than a Z_2^32-only body (2282 vs 2553 us
+    # per launch, profiles/r06/ring32/); allow that one
+    k = u["_ZN3fhh14k_gt_garble_tmILi2ELb1EEEvNS_6GcArgsE"]
+    assert int(k["VGPRs Spill"]) <= 1 and int(k["Occupancy [waves/SIMD]"]) >= 4, k
     # r06 SoftSpoken (k = 2, 4): the GGM trees and both expands stay in registers; k = 4 keeps 4 / 3 row sums
     # of 16 words beside two ChaCha blocks (occupancy 2-3 at 256-thread workgroups, VALU-bound)
     for name in [f"_ZN3fhh{len(f'k_ss_{r}')}k_ss_{r}ILi{k}EEEvNS_6OtArgsE" for r in ("ggm", "recv_expand", "send_expand")
